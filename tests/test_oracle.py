@@ -1,0 +1,223 @@
+"""Pins the CPU oracle before anything is compared against it.
+
+- hand-derived known-answer vectors (tests/golden/spec_vectors.json);
+- pyarrow 25 reads every oracle file back value-exact (vs google.protobuf's own parse);
+- pyarrow's Snappy decodes every page the oracle compresses;
+- the reference test's record-level assertions restated (KafkaProtoParquetWriterTest.java).
+"""
+import io
+import json
+import os
+import struct
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+import pytest
+
+import oracle
+import pqwalk
+import protoutil
+import synth
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SPEC = json.load(open(os.path.join(HERE, "golden", "spec_vectors.json")))
+MiB = 1024 * 1024
+
+
+@pytest.mark.parametrize("vec", SPEC["rle_hybrid"], ids=lambda v: v["name"])
+def test_rle_known_answers(vec):
+    assert oracle.rle_encode(vec["values"], vec["bit_width"]).hex().upper() == vec["expected_hex"]
+
+
+@pytest.mark.parametrize("vec", SPEC["snappy"], ids=lambda v: v["name"])
+def test_snappy_known_answers(vec):
+    assert oracle.snappy_compress(bytes.fromhex(vec["input_hex"])).hex() == vec["expected_hex"].lower()
+
+
+@pytest.mark.parametrize("n", [1, 14, 15, 16, 100, 4096, 65535, 65536, 65537, 200000])
+def test_snappy_roundtrip_pyarrow(n):
+    rng = np.random.default_rng(n)
+    for kind in range(3):
+        if kind == 0:
+            data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 1:
+            data = (b"kafka-parquet-" * (n // 14 + 1))[:n]
+        else:
+            data = rng.integers(0, 4, n, dtype=np.uint8).tobytes()
+        c = oracle.snappy_compress(data)
+        assert pa.decompress(c, decompressed_size=n, codec="snappy", asbytes=True) == data
+
+
+def _readback(schema, recs, fb):
+    tbl = pq.read_table(io.BytesIO(fb))
+    assert tbl.num_rows == len(recs)
+    assert protoutil.table_columns(tbl, schema) == protoutil.decode_columns(schema, recs)
+
+
+CASES = [
+    (synth.KIND_SAMPLE, 0, 3000), (synth.KIND_SAMPLE, 30, 3000),
+    (synth.KIND_REC8, 0, 5000), (synth.KIND_HIGHCARD, 0, 1500),
+]
+
+
+@pytest.mark.parametrize("kind,param,n", CASES)
+@pytest.mark.parametrize("codec", [oracle.UNCOMPRESSED, oracle.SNAPPY])
+@pytest.mark.parametrize("page_size,block_size", [(128 * MiB, 128 * MiB), (MiB, 128 * MiB), (8192, 64 * 1024)])
+@pytest.mark.parametrize("dictionary", [True, False])
+def test_oracle_readback(kind, param, n, codec, page_size, block_size, dictionary):
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, 0xC0FFEE01 + kind, n, param=param)
+    props = oracle.make_props(block_size=block_size, page_size=page_size, codec=codec, enable_dictionary=dictionary)
+    fb = oracle.encode_file(schema, data, offs, props)
+    _readback(schema, synth.records(data, offs), fb)
+    # every page decodes with an independent Snappy, header sizes consistent
+    pqwalk.decompress_pages(fb, "snappy" if codec == oracle.SNAPPY else "none")
+
+
+def _sample_msg(**kw):
+    cls = protoutil.message_class(synth.SAMPLE)
+    m = cls()
+    for k, v in kw.items():
+        setattr(m, k, v)
+    return m
+
+
+def _varint(v):
+    out = bytearray()
+    v &= (1 << 64) - 1
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _tag(f, wt):
+    return _varint((f << 3) | wt)
+
+
+def test_proto_edge_cases_accepted():
+    """Unknown fields skipped, last occurrence wins, any field order, 10-byte negative
+    int32, unknown groups, known number with a foreign wire type treated as unknown
+    (protobuf-java generated switch-on-tag; TestMessage.java:85-139)."""
+    base = _sample_msg(query="q", timestamp=7).SerializeToString()
+    recs = [
+        base,
+        _sample_msg(query="a", timestamp=1, page_number=-5).SerializeToString(),   # 10-byte varint
+        base + _tag(99, 0) + _varint(12345) + _tag(98, 2) + _varint(3) + b"xyz",  # unknown fields
+        base + _tag(2, 0) + _varint(42),                                         # last wins
+        _tag(4, 0) + _varint(9) + _tag(2, 0) + _varint(3) + _tag(1, 2) + b"\x02hi",  # reordered
+        base + _tag(50, 3) + _tag(51, 0) + _varint(1) + _tag(52, 3) + _tag(53, 5) + b"wxyz" + _tag(52, 4) + _tag(50, 4),  # nested unknown groups
+        base + _tag(3, 2) + b"\x01z",                                           # page_number as LEN: unknown
+        base + _tag(60, 5) + b"abcd" + _tag(61, 1) + b"12345678",                # fixed32/fixed64 unknown
+        _sample_msg(query="", timestamp=0, page_number=0, result_per_page=-1).SerializeToString(),
+    ]
+    data, offs = synth.pack(recs)
+    fb = oracle.encode_file(synth.SAMPLE, data, offs)
+    _readback(synth.SAMPLE, recs, fb)
+
+
+@pytest.mark.parametrize("bad", [
+    _tag(2, 0) + _varint(1),                                   # missing required query
+    _tag(1, 2) + b"\x05ab",                                    # truncated length-delimited
+    _tag(1, 2) + b"\x01a" + _tag(2, 0) + b"\x80",              # truncated varint
+    _tag(1, 2) + b"\x01a" + _tag(2, 0) + b"\x80" * 10 + b"\x01",  # varint > 10 bytes
+    _tag(1, 2) + b"\x01a" + _tag(2, 0) + _varint(1) + _tag(7, 6),  # wire type 6
+    _tag(1, 2) + b"\x01a" + _tag(2, 0) + _varint(1) + b"\x00",  # field number 0
+    _tag(1, 2) + b"\x01a" + _tag(2, 0) + _varint(1) + _tag(9, 4),  # stray end-group
+    _tag(1, 2) + b"\x01a" + _tag(2, 0) + _varint(1) + _tag(9, 3) + _tag(8, 4),  # mismatched end-group
+    _tag(1, 2) + b"\x01a" + _tag(2, 1) + b"\x01\x02",          # required timestamp as fixed64: unknown -> missing
+])
+def test_proto_invalid_rejected(bad):
+    w = oracle.OracleWriter(synth.SAMPLE)
+    good = _sample_msg(query="x", timestamp=1).SerializeToString()
+    w.write(good)
+    with pytest.raises(oracle.OracleError) as e:
+        w.write(bad)
+    assert e.value.status == -3
+    assert w.num_records() == 1
+    w.close()
+    _readback(synth.SAMPLE, [good], w.file_bytes())
+
+
+def _chunk_encodings(fb):
+    fm = pqwalk.footer(fb)
+    return [[cc[3][2] for cc in rg[1]] for rg in fm[4]]
+
+
+def test_dictionary_fallback_and_satisfying():
+    # HIGHCARD: uuid/blob exceed 1 MiB of dictionary -> PLAIN; code (<=1000 values) stays dictionary
+    data, offs = synth.generate(synth.KIND_HIGHCARD, 5, 40000)
+    fb = oracle.encode_file(synth.HIGHCARD, data, offs, oracle.make_props(codec=oracle.SNAPPY))
+    enc = _chunk_encodings(fb)[0]
+    assert 2 not in enc[1] and 2 not in enc[2]  # uuid, blob: no PLAIN_DICTIONARY
+    assert 2 in enc[3]                           # code: PLAIN_DICTIONARY
+    # dictionary page only where the dictionary was used
+    kinds = [(p["col"], p["header"][1]) for p in pqwalk.pages(fb)]
+    assert (3, 2) in kinds and (1, 2) not in kinds and (2, 2) not in kinds
+
+
+def test_all_null_first_page_falls_back():
+    # every optional value null: the first page's bit width is 32, isCompressionSatisfying
+    # fails (1 byte vs 0 raw) and the chunk is PLAIN with no dictionary page.
+    recs = [_sample_msg(query="q%d" % (i % 3), timestamp=i).SerializeToString() for i in range(500)]
+    data, offs = synth.pack(recs)
+    fb = oracle.encode_file(synth.SAMPLE, data, offs)
+    enc = _chunk_encodings(fb)[0]
+    assert 2 not in enc[2] and 2 not in enc[3]
+    _readback(synth.SAMPLE, recs, fb)
+
+
+def test_max_file_size_rotation():
+    """KafkaProtoParquetWriterTest.testMaxFileSize restated (:142-174): 10 KiB row groups,
+    maxFileSize 100 KiB, the WorkerThread closes a file right after the record that makes
+    getDataSize() >= maxFileSize (KPW:281-285,306-308); every closed file satisfies
+    0.9 < maxFileSize/len < 1.01."""
+    max_file = 100 * 1024
+    props = oracle.make_props(block_size=10 * 1024)
+    data, offs = synth.generate(synth.KIND_SAMPLE, 0xC0FFEE01, 6000)
+    files, start = [], 0
+    while len(files) < 2:
+        w = oracle.OracleWriter(synth.SAMPLE, props)
+        sub = offs[start:] - offs[start]
+        st, na, full = w.write_until_full(data[int(offs[start]):], sub, max_file)
+        assert st == 0
+        if not full:
+            break
+        w.close()
+        files.append(w.file_bytes())
+        start += na
+    assert len(files) >= 2
+    for fb in files:
+        r = max_file / len(fb)
+        assert 0.9 < r < 1.01, r
+        assert pq.read_table(io.BytesIO(fb)).num_rows > 0
+
+
+def test_round_trip_multiset_sample():
+    """testMaxOpenDuration's containsInAnyOrder check restated (:136-139)."""
+    data, offs = synth.generate(synth.KIND_SAMPLE, 77, 100)
+    recs = synth.records(data, offs)
+    fb = oracle.encode_file(synth.SAMPLE, data, offs)
+    cls = protoutil.message_class(synth.SAMPLE)
+    tbl = pq.read_table(io.BytesIO(fb)).to_pylist()
+    got = sorted(cls(**{k: v for k, v in row.items() if v is not None}).SerializeToString() for row in tbl)
+    want = sorted(cls.FromString(r).SerializeToString() for r in recs)
+    assert got == want
+
+
+def test_get_data_size_tracks_file():
+    data, offs = synth.generate(synth.KIND_REC8, 3, 20000)
+    w = oracle.OracleWriter(synth.REC8, oracle.make_props(block_size=256 * 1024))
+    last = 0
+    for i in range(0, 20000, 1000):
+        st, nw = w.write_batch(data, offs[i:i + 1001])
+        assert st == 0
+        ds = w.data_size()
+        assert ds > 0
+        last = ds
+    assert w.num_row_groups() >= 2
+    w.close()
+    fb = w.file_bytes()
+    assert abs(len(fb) - last) < 0.2 * len(fb)
