@@ -1,0 +1,145 @@
+/*
+ * kpw_gpu.h — C-ABI of the MI355X-native Parquet column-chunk encoder (libkpw_gpu.so).
+ *
+ * Two layers, both plain C (pointers + sizes, integer status codes, no C++ exceptions,
+ * no torch/HIP types in any signature):
+ *
+ *  (1) kpw_writer_*  — the drop-in for the reference seam ParquetFile<T>
+ *      (src/main/java/ir/sahab/kafka/reader/ParquetFile.java:24-100): open / write /
+ *      getDataSize / getNumWrittenRecords / close, fed with the raw record values the
+ *      caller already holds (KafkaProtoParquetWriter.java:270 `record.value()`), so
+ *      parser.parseFrom + ProtoWriteSupport shredding run on the GPU (K1).  The host part
+ *      of parquet-mr that north_star keeps on the host (Thrift page headers, footer, file
+ *      bytes) is done here on the CPU side of the library.
+ *
+ *  (2) kpw_encoder_* — the flush-path primitive a JVM host binds when it keeps its own
+ *      ParquetFileWriter: device-resident record batch -> encoded pages + per-page
+ *      metadata for every row group parquet-mr would cut (replaces
+ *      InternalParquetRecordWriter.flushRowGroupToStore -> ColumnWriteStoreV1.flush ->
+ *      ColumnChunkPageWriter.writePage, parquet-mr 1.10.1).
+ *
+ * Threading: handles are independent; one handle is used by one thread at a time
+ * (ParquetFile is documented not thread-safe, ParquetFile.java:19-20).  Each handle owns
+ * its HIP streams and device buffers on the device it was opened on.
+ */
+#ifndef KPW_GPU_H
+#define KPW_GPU_H
+
+#include <stdint.h>
+#include "kpw_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ (1) ParquetFile drop-in */
+
+typedef struct kpw_writer kpw_writer;
+
+/* new ParquetFile(filePath, protoClass, properties) — ParquetFile.java:36-54.
+ * path == NULL keeps the file in memory (kpw_writer_file_bytes); otherwise the file is
+ * created/overwritten (Mode.OVERWRITE, ParquetFile.java:46).  device = HIP ordinal. */
+kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, const kpw_props *props,
+                            const char *path, int *status);
+
+/* n x { parser.parseFrom(value); ParquetFile.write(T) } — KafkaProtoParquetWriter.java:268-277,
+ * ParquetFile.java:59-62.  data/offsets are host memory; record i is
+ * data[offsets[i] .. offsets[i+1]).  On an invalid record returns KPW_ERR_INVALID_PROTO:
+ * the records before it are written, it and the rest are not (kpw_writer_failed_record). */
+int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n);
+
+/* The WorkerThread size-rotation loop (KafkaProtoParquetWriter.java:277-285,306-308):
+ * writes records in order and stops right after the first one for which
+ * getDataSize() >= max_file_size.  *n_accepted = records written, *full = 1 if the stop
+ * condition fired (the caller then closes this file and opens the next). */
+int kpw_writer_write_until_full(kpw_writer *w, const uint8_t *data, const uint64_t *offsets,
+                                uint64_t n, int64_t max_file_size, uint64_t *n_accepted, int *full);
+
+int64_t kpw_writer_data_size(kpw_writer *w);        /* getDataSize()          ParquetFile.java:77-79 */
+int64_t kpw_writer_num_records(const kpw_writer *w); /* getNumWrittenRecords() ParquetFile.java:81-83 */
+int64_t kpw_writer_creation_time_ms(const kpw_writer *w); /* getCreationDate()  ParquetFile.java:70-72 */
+int kpw_writer_close(kpw_writer *w);                 /* close() (idempotent)   ParquetFile.java:65-68 */
+int kpw_writer_file_bytes(const kpw_writer *w, const uint8_t **bytes, uint64_t *len);
+int64_t kpw_writer_failed_record(const kpw_writer *w); /* -1 if none */
+const char *kpw_writer_last_error(const kpw_writer *w);
+void kpw_writer_free(kpw_writer *w);
+
+/* ------------------------------------------------------------------ (2) flush-path encoder */
+
+typedef struct kpw_encoder kpw_encoder;
+
+kpw_encoder *kpw_encoder_create(int device, const kpw_schema *schema, const kpw_props *props, int *status);
+void kpw_encoder_destroy(kpw_encoder *e);
+const char *kpw_encoder_last_error(const kpw_encoder *e);
+
+/* Per-page metadata of one encoded page (data or dictionary). */
+typedef struct kpw_page_info {
+    int32_t page_type;          /* KPW_DATA_PAGE / KPW_DICTIONARY_PAGE */
+    int32_t num_values;         /* data: values incl. nulls; dictionary: entries */
+    int32_t encoding;           /* values encoding (data) or dictionary encoding */
+    int32_t dl_encoding;        /* KPW_ENC_RLE (optional) / KPW_ENC_BIT_PACKED (required) */
+    int32_t rl_encoding;        /* KPW_ENC_BIT_PACKED (DevNull, no repeated fields) */
+    int32_t has_stats;          /* 0 for dictionary pages */
+    int64_t uncompressed_size;
+    int64_t compressed_size;
+    uint64_t offset;            /* byte offset of the (compressed) body in the batch output */
+    int64_t null_count;
+    int32_t has_min_max;
+    int32_t min_len, max_len;   /* stats bytes (Statistics.getMinBytes/getMaxBytes) */
+    uint64_t min_off, max_off;  /* offsets into kpw_batch_info.stats_bytes */
+} kpw_page_info;
+
+typedef struct kpw_chunk_info {
+    int32_t column;
+    int32_t first_page;         /* index into kpw_batch_info.pages; dictionary page first */
+    int32_t num_pages;
+    int32_t has_dictionary;
+    int64_t num_values;
+} kpw_chunk_info;
+
+typedef struct kpw_row_group_info {
+    int64_t first_record;       /* index within the batch */
+    int64_t num_records;
+    int32_t first_chunk;        /* index into kpw_batch_info.chunks (schema order) */
+    int32_t reserved;
+} kpw_row_group_info;
+
+typedef struct kpw_batch_info {
+    int32_t num_row_groups;
+    int32_t num_chunks;
+    int32_t num_pages;
+    int32_t reserved;
+    const kpw_row_group_info *row_groups;
+    const kpw_chunk_info *chunks;
+    const kpw_page_info *pages;
+    const uint8_t *stats_bytes;         /* host memory */
+    uint64_t stats_len;
+    const uint8_t *device_pages;        /* device pointer to all page bodies (valid until next call) */
+    uint64_t device_pages_len;
+    int64_t records_consumed;           /* records covered by the returned row groups */
+    int64_t open_records;               /* records left in the open (unflushed) row group */
+    int64_t open_buffered_size;         /* columnStore.getBufferedSize() of the open row group */
+    int64_t invalid_record;             /* first invalid record index, -1 if none */
+} kpw_batch_info;
+
+/* Encode a device-resident batch of n records (d_data/d_offsets are device pointers,
+ * d_offsets has n+1 entries, offsets relative to d_data).  Cuts row groups exactly where
+ * InternalParquetRecordWriter.checkBlockSizeReached would (starting a fresh row group at
+ * record 0); if `final` the trailing open row group is flushed too (close()).  Blocking;
+ * the returned info stays valid until the next call on this encoder.  hip_stream may be
+ * NULL (the encoder's own stream). */
+int kpw_encoder_encode(kpw_encoder *e, const uint8_t *d_data, const uint64_t *d_offsets, uint64_t n,
+                       int final, int64_t next_row_group_size, void *hip_stream, kpw_batch_info *info);
+
+/* Copy page bodies [off, off+len) of the last batch to host memory. */
+int kpw_encoder_copy_pages(kpw_encoder *e, uint64_t off, uint64_t len, void *host_dst);
+
+/* Timing of the last encode: per-stage device milliseconds measured with HIP events on the
+ * encoder's stream (index order: decode, plan, dictionary, rle, plain+stats, assemble,
+ * compress, total). Returns number of entries written (<= cap). */
+int kpw_encoder_stage_times(const kpw_encoder *e, float *ms, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KPW_GPU_H */

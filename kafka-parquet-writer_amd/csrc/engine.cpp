@@ -1,0 +1,593 @@
+// engine.cpp — host orchestration: one handle = one device + one HIP stream.
+//
+// encode(): device-resident record batch -> row groups exactly where parquet-mr would cut
+// them -> per column chunk: dictionary page (if any) + one data page, compressed.
+// Host syncs per batch: decode error index, row-group plan, page layout, (snappy sizes),
+// chunk metadata — all small; every byte of record/page data stays in HBM.
+#include "engine.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "kpw_chunk.h"
+#include "kpw_scan.h"
+
+namespace kpw {
+
+void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, uint64_t *tmp, hipStream_t s);
+void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, uint64_t *tmp, hipStream_t s);
+void launch_snappy_finish(const SnappyArgs &a, const uint32_t *page_frag0, hipStream_t s);
+void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, const uint8_t *data, uint64_t *meta,
+                         uint8_t *blob, hipStream_t s);
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) return fail(KPW_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int DevBuf::ensure(size_t bytes)
+{
+    if (bytes <= cap && p) return 0;
+    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    size_t c = bytes < 256 ? 256 : bytes + bytes / 8;
+    if (hipMalloc(&p, c) != hipSuccess) { p = nullptr; return -1; }
+    cap = c;
+    return 0;
+}
+DevBuf::~DevBuf()
+{
+    if (p) (void)hipFree(p);
+}
+
+Engine::~Engine()
+{
+    for (auto &e : ev_) if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+int Engine::fail(int code, const std::string &msg)
+{
+    err_ = msg;
+    return code;
+}
+
+static int proto_phys(int pt, int &wt, int &utf8, int &vsize)
+{
+    utf8 = 0;
+    vsize = 0;
+    switch (pt) {
+    case KPW_PT_DOUBLE: wt = 1; vsize = 8; return KPW_DOUBLE;
+    case KPW_PT_FLOAT: wt = 5; vsize = 4; return KPW_FLOAT;
+    case KPW_PT_INT64: case KPW_PT_UINT64: case KPW_PT_SINT64: wt = 0; vsize = 8; return KPW_INT64;
+    case KPW_PT_FIXED64: case KPW_PT_SFIXED64: wt = 1; vsize = 8; return KPW_INT64;
+    case KPW_PT_INT32: case KPW_PT_UINT32: case KPW_PT_SINT32: wt = 0; vsize = 4; return KPW_INT32;
+    case KPW_PT_FIXED32: case KPW_PT_SFIXED32: wt = 5; vsize = 4; return KPW_INT32;
+    case KPW_PT_BOOL: wt = 0; return KPW_BOOLEAN;
+    case KPW_PT_STRING: wt = 2; utf8 = 1; return KPW_BYTE_ARRAY;
+    case KPW_PT_BYTES: wt = 2; return KPW_BYTE_ARRAY;
+    default: return -1;
+    }
+}
+
+int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
+{
+    if (!schema || !pr || !schema->columns || schema->num_columns <= 0 || !schema->message_name)
+        return fail(KPW_ERR_INVALID_ARG, "null schema/props");
+    if (schema->num_columns > MAX_COLS) return fail(KPW_ERR_UNSUPPORTED, "more than 256 columns");
+    if (pr->writer_version != 1) return fail(KPW_ERR_UNSUPPORTED, "only PARQUET_1_0 is reachable from the reference");
+    if (pr->codec != KPW_UNCOMPRESSED && pr->codec != KPW_SNAPPY) return fail(KPW_ERR_UNSUPPORTED, "codec");
+    if (pr->block_size <= 0 || pr->page_size <= 0 || pr->dictionary_page_size <= 0) return fail(KPW_ERR_INVALID_ARG, "sizes");
+    if (pr->dfs_block_size > 0) return fail(KPW_ERR_UNSUPPORTED, "HDFS padding alignment (next round)");
+    props = *pr;
+    message_name = schema->message_name;
+    proto_class = schema->proto_class ? schema->proto_class : schema->message_name;
+    for (int c = 0; c < schema->num_columns; c++) {
+        const kpw_column_desc &d = schema->columns[c];
+        ColInfo ci;
+        int wt, utf8, vsize;
+        int phys = proto_phys(d.proto_type, wt, utf8, vsize);
+        if (phys < 0 || !d.name || d.field_number <= 0 || (d.label != KPW_LABEL_OPTIONAL && d.label != KPW_LABEL_REQUIRED))
+            return fail(KPW_ERR_UNSUPPORTED, std::string("column ") + (d.name ? d.name : "?") + ": unsupported proto field");
+        ci.name = d.name;
+        ci.field_number = d.field_number;
+        ci.proto_type = d.proto_type;
+        ci.label = d.label;
+        ci.phys = phys;
+        ci.wire_type = wt;
+        ci.optional = d.label == KPW_LABEL_OPTIONAL;
+        ci.utf8 = utf8;
+        ci.vsize = vsize;
+        ci.dict = props.enable_dictionary && phys != KPW_BOOLEAN;
+        cols.push_back(ci);
+        if (ci.optional) opt_idx_.push_back((uint32_t)c);
+        if (phys == KPW_BOOLEAN) bool_idx_.push_back((uint32_t)c);
+    }
+    device = dev;
+    CK(hipSetDevice(dev));
+    CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    for (auto &e : ev_) CK(hipEventCreate(&e));
+    const size_t nc = cols.size();
+    col_vals.resize(nc); col_soff.resize(nc); col_slen.resize(nc); col_pres.resize(nc); col_vbits.resize(nc); col_pcnt.resize(nc);
+    std::vector<int16_t> fmap(FMAP_SIZE, -1);
+    for (size_t c = 0; c < nc; c++)
+        if (cols[c].field_number < FMAP_SIZE) fmap[cols[c].field_number] = (int16_t)c;
+    if (d_fmap.ensure(FMAP_SIZE * sizeof(int16_t))) return fail(KPW_ERR_NOMEM, "fmap");
+    CK(hipMemcpy(d_fmap.p, fmap.data(), FMAP_SIZE * sizeof(int16_t), hipMemcpyHostToDevice));
+    if (d_opt.ensure(std::max<size_t>(1, opt_idx_.size()) * 4) || d_bool.ensure(std::max<size_t>(1, bool_idx_.size()) * 4))
+        return fail(KPW_ERR_NOMEM, "idx");
+    if (!opt_idx_.empty()) CK(hipMemcpy(d_opt.p, opt_idx_.data(), opt_idx_.size() * 4, hipMemcpyHostToDevice));
+    if (!bool_idx_.empty()) CK(hipMemcpy(d_bool.p, bool_idx_.data(), bool_idx_.size() * 4, hipMemcpyHostToDevice));
+    return KPW_OK;
+}
+
+#define ENS(buf, bytes) do { if ((buf).ensure(bytes)) return fail(KPW_ERR_NOMEM, "device allocation failed: " #buf); } while (0)
+
+// Lays out tiles for the given jobs, uploads them and runs the structure pass.
+int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, RleScratch &sc)
+{
+    hipStream_t s = stream;
+    npt = net = 0;
+    uint64_t e0 = 0;
+    static thread_local std::vector<uint32_t> ptj, etj;
+    ptj.clear();
+    etj.clear();
+    for (size_t j = 0; j < jobs.size(); j++) {
+        RleJob &J = jobs[j];
+        const uint64_t len = J.len;
+        J.tile0 = npt;
+        J.ntiles = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
+        npt += J.ntiles;
+        const uint64_t cap = len / 8 + 2;
+        J.etile0 = net;
+        J.netiles = (uint32_t)((cap + 255) / 256);
+        net += J.netiles;
+        J.e0 = e0;
+        e0 += (uint64_t)J.netiles * 256;
+        J.n_long = J.n_rle = 0;
+        J.total_bytes = J.total_groups = J.final_gap_off = J.final_gap_groups = J.final_gap_start = 0;
+        ptj.insert(ptj.end(), J.ntiles, (uint32_t)j);
+        etj.insert(etj.end(), J.netiles, (uint32_t)j);
+    }
+    const size_t nj = jobs.size();
+    ENS(r_ptile_job, npt * 4); ENS(r_last, npt * 8); ENS(r_prev, npt * 8); ENS(r_lrcnt, npt * 4); ENS(r_lroff, npt * 4);
+    ENS(r_etile_job, net * 4); ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_emap, net * 4); ENS(r_emappre, net * 4);
+    ENS(r_rcnt, net * 4); ENS(r_roff, net * 4); ENS(r_rg, e0 * 4); ENS(r_rb, e0 * 4); ENS(r_rbytes, e0 * 8);
+    ENS(r_rgroups, e0 * 8); ENS(r_etbytes, net * 8); ENS(r_etgroups, net * 8); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8);
+    ENS(r_jnlong, nj * 4); ENS(r_jnrle, nj * 4); ENS(r_jbtot, nj * 8); ENS(r_jgtot, nj * 8); ENS(d_jobs, nj * sizeof(RleJob));
+    CK(hipMemcpyAsync(r_ptile_job.p, ptj.data(), npt * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(r_etile_job.p, etj.data(), net * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(d_jobs.p, jobs.data(), nj * sizeof(RleJob), hipMemcpyHostToDevice, s));
+    sc.ptile_job = r_ptile_job.as<uint32_t>();
+    sc.first_brk = nullptr;
+    sc.last_brk = r_last.as<int64_t>();
+    sc.prev_brk = r_prev.as<int64_t>();
+    sc.lr_cnt = r_lrcnt.as<uint32_t>();
+    sc.lr_off = r_lroff.as<uint32_t>();
+    sc.etile_job = r_etile_job.as<uint32_t>();
+    sc.lr_a = r_lra.as<uint32_t>();
+    sc.lr_b = r_lrb.as<uint32_t>();
+    sc.emap = r_emap.as<uint32_t>();
+    sc.emap_pre = r_emappre.as<uint32_t>();
+    sc.r_cnt = r_rcnt.as<uint32_t>();
+    sc.r_off = r_roff.as<uint32_t>();
+    sc.r_g = r_rg.as<uint32_t>();
+    sc.r_b = r_rb.as<uint32_t>();
+    sc.r_bytes = r_rbytes.as<uint64_t>();
+    sc.r_groups = r_rgroups.as<uint64_t>();
+    sc.et_bytes = r_etbytes.as<uint64_t>();
+    sc.et_groups = r_etgroups.as<uint64_t>();
+    sc.r_boff = r_rboff.as<uint64_t>();
+    sc.r_goff = r_rgoff.as<uint64_t>();
+    sc.job_nlong = r_jnlong.as<uint32_t>();
+    sc.job_nrle = r_jnrle.as<uint32_t>();
+    sc.job_btot = r_jbtot.as<uint64_t>();
+    sc.job_gtot = r_jgtot.as<uint64_t>();
+    return KPW_OK;
+}
+
+static inline uint64_t next_pow2(uint64_t x)
+{
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
+                   hipStream_t user_stream, BatchOut &out)
+{
+    out = BatchOut();
+    CK(hipSetDevice(device));
+    if (user_stream) {  // order our stream after the caller's work
+        CK(hipEventRecord(ev_[8], user_stream));
+        CK(hipStreamWaitEvent(stream, ev_[8], 0));
+    }
+    hipStream_t s = stream;
+    const int nc = (int)cols.size();
+    const uint32_t nopt = (uint32_t)opt_idx_.size();
+    CK(hipEventRecord(ev_[0], s));
+    if (n == 0) {
+        for (int i = 0; i < 8; i++) stage_ms[i] = 0;
+        return KPW_OK;
+    }
+    if (n >= 0xFFFFFFF0ull) return fail(KPW_ERR_LIMIT, "batch too large (>= 2^32 records)");
+    const uint64_t nwords = n / 64 + 2;
+
+    // ---------------------------------------------------------------- K1 decode
+    std::vector<DevCol> hc(nc);
+    for (int c = 0; c < nc; c++) {
+        const ColInfo &ci = cols[c];
+        DevCol &d = hc[c];
+        memset(&d, 0, sizeof(d));
+        d.phys = ci.phys; d.proto_type = ci.proto_type; d.wire_type = ci.wire_type; d.optional = ci.optional;
+        d.field_number = ci.field_number; d.vsize = ci.vsize; d.dict = ci.dict;
+        if (ci.vsize) { ENS(col_vals[c], n * ci.vsize); d.vals = col_vals[c].p; }
+        if (ci.phys == KPW_BYTE_ARRAY) {
+            ENS(col_soff[c], n * 8); ENS(col_slen[c], n * 4);
+            d.soff = col_soff[c].as<uint64_t>(); d.slen = col_slen[c].as<uint32_t>();
+        }
+        if (ci.optional) {
+            ENS(col_pres[c], nwords * 8); ENS(col_pcnt[c], (nwords + 1) * 4);
+            CK(hipMemsetAsync(col_pres[c].p, 0, nwords * 8, s));
+            d.pres = col_pres[c].as<uint64_t>(); d.pcnt = col_pcnt[c].as<uint32_t>();
+        }
+        if (ci.phys == KPW_BOOLEAN) {
+            ENS(col_vbits[c], nwords * 8);
+            CK(hipMemsetAsync(col_vbits[c].p, 0, nwords * 8, s));
+            d.vbits = col_vbits[c].as<uint64_t>();
+        }
+    }
+    ENS(d_cols, nc * sizeof(DevCol));
+    CK(hipMemcpyAsync(d_cols.p, hc.data(), nc * sizeof(DevCol), hipMemcpyHostToDevice, s));
+    ENS(d_raw, n * 4); ENS(d_err, 64);
+    CK(hipMemsetAsync(d_err.p, 0xFF, 8, s));
+    DecodeArgs da;
+    da.data = d_data; da.off = d_off; da.n = n; da.cols = d_cols.as<DevCol>(); da.ncols = nc; da.pad = 0;
+    da.fmap = d_fmap.as<int16_t>(); da.raw = d_raw.as<uint32_t>(); da.err_min = d_err.as<unsigned long long>();
+    launch_decode(da, s);
+    CK(hipGetLastError());
+    CK(hipEventRecord(ev_[1], s));
+    uint64_t err_idx = ~0ull;
+    CK(hipMemcpyAsync(&err_idx, d_err.p, 8, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    const uint64_t ne = std::min<uint64_t>(n, err_idx);
+    out.invalid_record = err_idx < n ? (int64_t)err_idx : -1;
+
+    // ---------------------------------------------------------------- planning inputs
+    ENS(d_scan_tmp, mj_scan_tmp_words(std::max<uint64_t>(ne + 1, nwords + 1), std::max<uint32_t>(1, nopt)) * 8 + 64);
+    ENS(d_P, (ne + 1) * 8);
+    if (nopt) launch_pcnt_scan(d_cols.as<DevCol>(), d_opt.as<uint32_t>(), nopt, nwords, d_scan_tmp.as<uint64_t>(), s);
+    launch_prefix_raw(d_raw.as<uint32_t>(), ne, d_P.as<uint64_t>(), d_scan_tmp.as<uint64_t>(), s);
+    if (ne == 0) {
+        out.records_consumed = 0;
+        out.open_records = 0;
+        CK(hipStreamSynchronize(s));
+        return KPW_OK;
+    }
+    RleScratch sc{};
+    uint32_t npt = 0, net = 0;
+    std::vector<RleJob> pj;
+    if (nopt) {
+        pj.resize(nopt);
+        for (uint32_t k = 0; k < nopt; k++) {
+            RleJob &J = pj[k];
+            memset(&J, 0, sizeof(J));
+            J.src.kind = 0;
+            J.src.ptr = hc[opt_idx_[k]].pres;
+            J.src.base = 0;
+            J.len = (uint32_t)ne;
+            J.bw = 1;
+            J.out_off = (uint64_t)k * (ne + 1);
+        }
+        int st = run_rle(pj, npt, net, sc);
+        if (st) return st;
+        ENS(d_ev, (uint64_t)nopt * (ne + 1));
+        ENS(d_E, (uint64_t)nopt * (ne + 1) * 4);
+        ENS(d_gend, (uint64_t)nopt * nwords * 8);
+        CK(hipMemsetAsync(d_ev.p, 0, (uint64_t)nopt * (ne + 1), s));
+        CK(hipMemsetAsync(d_gend.p, 0, (uint64_t)nopt * nwords * 8, s));
+        launch_rle_structure(d_jobs.as<RleJob>(), (int)nopt, npt, net, sc, s);
+        launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), d_gend.as<uint64_t>(), nwords, s);
+        launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ne, nopt, d_scan_tmp.as<uint64_t>(), s);
+    }
+    // ---------------------------------------------------------------- A9 plan
+    const int32_t max_rgs = (int32_t)(ne / 100 + 4);
+    ENS(d_rg_start, max_rgs * 8); ENS(d_rg_end, max_rgs * 8); ENS(d_plan_out, 64);
+    PlanArgs pa{};
+    pa.n = ne; pa.final_flush = final_flush ? 1 : 0; pa.ncols = nc; pa.next_rg_size = next_rg_size;
+    pa.P = d_P.as<uint64_t>(); pa.cols = d_cols.as<DevCol>(); pa.opt_cols = d_opt.as<uint32_t>(); pa.nopt = (int32_t)nopt;
+    pa.nbool = (int32_t)bool_idx_.size(); pa.bool_cols = d_bool.as<uint32_t>();
+    pa.E = nopt ? d_E.as<uint32_t>() : nullptr; pa.gend = nopt ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
+    pa.rg_start = d_rg_start.as<int64_t>(); pa.rg_end = d_rg_end.as<int64_t>(); pa.max_rgs = max_rgs;
+    pa.out = d_plan_out.as<int64_t>();
+    launch_plan(pa, s);
+    CK(hipGetLastError());
+    int64_t po[4];
+    CK(hipMemcpyAsync(po, d_plan_out.p, 32, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    CK(hipEventRecord(ev_[2], s));
+    const int nrg = (int)po[0];
+    if (po[3]) return fail(KPW_ERR_DEVICE, "planner row-group table overflow");
+    std::vector<int64_t> rs(nrg), re(nrg);
+    if (nrg) {
+        CK(hipMemcpyAsync(rs.data(), d_rg_start.p, nrg * 8, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(re.data(), d_rg_end.p, nrg * 8, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+    }
+    out.records_consumed = po[1];
+    out.open_records = (int64_t)ne - po[1];
+    out.open_buffered = po[2];
+    for (int r = 0; r < nrg; r++) out.rgs.push_back(RowGroupOut{rs[r], re[r] - rs[r], r * nc});
+    if (nrg == 0) {
+        for (int i = 3; i < 8; i++) CK(hipEventRecord(ev_[i], s));
+        CK(hipStreamSynchronize(s));
+        return KPW_OK;
+    }
+
+    // ---------------------------------------------------------------- chunk descriptors
+    const int nch = nrg * nc;
+    std::vector<ChunkDesc> ch(nch);
+    std::vector<uint32_t> ctj, cfirst(nch), ccount(nch);
+    std::vector<RleJob> ej;
+    uint64_t ht_off = 0, ids_off = 0;
+    for (int r = 0; r < nrg; r++) {
+        for (int c = 0; c < nc; c++) {
+            const int ci = r * nc + c;
+            ChunkDesc &C = ch[ci];
+            memset(&C, 0, sizeof(C));
+            C.s = rs[r]; C.e = re[r]; C.col = c; C.rg = r;
+            C.is_dict = cols[c].dict ? 1 : 0;
+            C.smin = ~0ull; C.smax = 0;
+            const uint64_t len = (uint64_t)(C.e - C.s);
+            C.ids_off = ids_off;
+            C.ent_off = ids_off;
+            ids_off += len;
+            if (C.is_dict) {
+                C.ht_cap = (uint32_t)std::min<uint64_t>(next_pow2(std::max<uint64_t>(16, 2 * len)), 1u << 19);
+                C.ht_off = ht_off;
+                ht_off += C.ht_cap + 1;
+            }
+            C.dl_job = C.id_job = -1;
+            if (cols[c].optional) {
+                RleJob J;
+                memset(&J, 0, sizeof(J));
+                J.src.kind = 0; J.src.ptr = hc[c].pres; J.src.base = (uint64_t)C.s;
+                J.len = (uint32_t)len; J.bw = 1;
+                C.dl_job = (int32_t)ej.size();
+                ej.push_back(J);
+            }
+            if (C.is_dict) {
+                RleJob J;
+                memset(&J, 0, sizeof(J));
+                J.src.kind = 1; J.src.ptr = nullptr; J.src.base = C.ids_off;   // ptr patched below
+                J.len = (uint32_t)len; J.bw = 0;
+                C.id_job = (int32_t)ej.size();
+                ej.push_back(J);
+            }
+            const uint32_t nt = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
+            cfirst[ci] = (uint32_t)ctj.size();
+            ccount[ci] = nt;
+            ctj.insert(ctj.end(), nt, (uint32_t)ci);
+        }
+    }
+    const uint32_t nct = (uint32_t)ctj.size();
+    ENS(d_chunks, nch * sizeof(ChunkDesc)); ENS(d_ctile_chunk, nct * 4); ENS(d_ctile_first, nch * 4); ENS(d_ctile_count, nch * 4);
+    ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
+    ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8);
+    ENS(d_ht_key, std::max<uint64_t>(1, ht_off) * 8); ENS(d_ht_min, std::max<uint64_t>(1, ht_off) * 4);
+    ENS(d_ht_id, std::max<uint64_t>(1, ht_off) * 4);
+    ENS(d_ids, std::max<uint64_t>(1, ids_off) * 4); ENS(d_ent_rec, std::max<uint64_t>(1, ids_off) * 8);
+    ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
+    ENS(d_page_off, 2 * nch * 8); ENS(d_page_len, 2 * nch * 8); ENS(d_tot, 64);
+    for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
+    CK(hipMemcpyAsync(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(d_ctile_chunk.p, ctj.data(), nct * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(d_ctile_first.p, cfirst.data(), nch * 4, hipMemcpyHostToDevice, s));
+    CK(hipMemcpyAsync(d_ctile_count.p, ccount.data(), nch * 4, hipMemcpyHostToDevice, s));
+    if (ht_off) {
+        CK(hipMemsetAsync(d_ht_key.p, 0xFF, ht_off * 8, s));
+        CK(hipMemsetAsync(d_ht_min.p, 0xFF, ht_off * 4, s));
+    }
+    ChunkArgs a{};
+    a.ch = d_chunks.as<ChunkDesc>(); a.nchunks = nch; a.nctiles = nct; a.cols = d_cols.as<DevCol>(); a.data = d_data;
+    a.ctile_chunk = d_ctile_chunk.as<uint32_t>(); a.ctile_first = d_ctile_first.as<uint32_t>();
+    a.ctile_count = d_ctile_count.as<uint32_t>(); a.tile_raw = d_tile_raw.as<uint64_t>();
+    a.tile_raw_off = d_tile_raw_off.as<uint64_t>(); a.tile_smin = d_tile_smin.as<uint64_t>();
+    a.tile_smax = d_tile_smax.as<uint64_t>(); a.tile_cnt = d_tile_cnt.as<uint32_t>(); a.tile_sz = d_tile_sz.as<uint64_t>();
+    a.ht_key = d_ht_key.as<uint64_t>(); a.ht_min = d_ht_min.as<uint32_t>(); a.ht_id = d_ht_id.as<uint32_t>();
+    a.ids = d_ids.as<uint32_t>(); a.ent_rec = d_ent_rec.as<uint64_t>(); a.ent_boff = d_ent_boff.as<uint64_t>();
+    a.max_dict_bytes = (uint32_t)props.dictionary_page_size;
+
+    // ---------------------------------------------------------------- K6 + K2
+    launch_chunk_stats(a, s);
+    CK(hipGetLastError());
+    uint32_t enpt = 0, enet = 0;
+    RleScratch esc{};
+    if (!ej.empty()) {
+        int st = run_rle(ej, enpt, enet, esc);
+        if (st) return st;
+    }
+    launch_dict(a, d_jobs.as<RleJob>(), s);
+    CK(hipGetLastError());
+    CK(hipEventRecord(ev_[3], s));
+    // ---------------------------------------------------------------- K3 (dl + ids)
+    if (!ej.empty()) launch_rle_structure(d_jobs.as<RleJob>(), (int)ej.size(), enpt, enet, esc, s);
+    CK(hipGetLastError());
+    CK(hipEventRecord(ev_[4], s));
+    // ---------------------------------------------------------------- layout + K4 + page bodies
+    launch_layout(a, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), s);
+    uint64_t body_tot = 0;
+    CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    ENS(d_body, body_tot + 16);
+    CK(hipMemsetAsync(d_body.p, 0, body_tot + 16, s));
+    launch_chunk_write(a, d_body.as<uint8_t>(), s);
+    if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), s);
+    CK(hipGetLastError());
+    CK(hipEventRecord(ev_[5], s));
+    std::vector<uint64_t> poff(2 * nch), plen(2 * nch), pcoff, pclen;
+    CK(hipMemcpyAsync(poff.data(), d_page_off.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(plen.data(), d_page_len.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    // ---------------------------------------------------------------- K7
+    if (props.codec == KPW_SNAPPY) {
+        std::vector<uint32_t> fpage, fidx, pfrag0(2 * nch);
+        for (int p = 0; p < 2 * nch; p++) {
+            pfrag0[p] = (uint32_t)fpage.size();
+            const uint64_t nf = (plen[p] + SNAPPY_FRAG - 1) / SNAPPY_FRAG;
+            for (uint64_t k = 0; k < nf; k++) { fpage.push_back((uint32_t)p); fidx.push_back((uint32_t)k); }
+        }
+        const uint32_t nf = (uint32_t)fpage.size();
+        ENS(d_frag_page, std::max<uint32_t>(1, nf) * 4); ENS(d_frag_idx, std::max<uint32_t>(1, nf) * 4);
+        ENS(d_frag_out, (uint64_t)std::max<uint32_t>(1, nf) * SNAPPY_FRAG_CAP); ENS(d_frag_len, std::max<uint32_t>(1, nf) * 4);
+        ENS(d_frag_coff, std::max<uint32_t>(1, nf) * 8); ENS(d_page_coff, 2 * nch * 8); ENS(d_page_clen, 2 * nch * 8);
+        ENS(d_page_frag0, 2 * nch * 4);
+        ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * nch * 8 + 64);
+        if (nf) {
+            CK(hipMemcpyAsync(d_frag_page.p, fpage.data(), nf * 4, hipMemcpyHostToDevice, s));
+            CK(hipMemcpyAsync(d_frag_idx.p, fidx.data(), nf * 4, hipMemcpyHostToDevice, s));
+        }
+        CK(hipMemcpyAsync(d_page_frag0.p, pfrag0.data(), 2 * nch * 4, hipMemcpyHostToDevice, s));
+        SnappyArgs sa{};
+        sa.in = d_body.as<uint8_t>(); sa.page_off = d_page_off.as<uint64_t>(); sa.page_len = d_page_len.as<uint64_t>();
+        sa.npages = 2 * nch; sa.nfrags = nf; sa.frag_page = d_frag_page.as<uint32_t>(); sa.frag_idx = d_frag_idx.as<uint32_t>();
+        sa.frag_out = d_frag_out.as<uint8_t>(); sa.frag_len = d_frag_len.as<uint32_t>();
+        sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
+        sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
+        launch_snappy(sa, s);
+        launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), s);
+        CK(hipGetLastError());
+        pcoff.resize(2 * nch);
+        pclen.resize(2 * nch);
+        uint64_t ctot = 0;
+        CK(hipMemcpyAsync(pcoff.data(), d_page_coff.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(pclen.data(), d_page_clen.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(&ctot, d_tot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        pages_dev_ = d_comp.as<uint8_t>();
+        pages_len_ = ctot;
+    } else {
+        pcoff = poff;
+        pclen = plen;
+        pages_dev_ = d_body.as<uint8_t>();
+        pages_len_ = body_tot;
+    }
+    CK(hipEventRecord(ev_[6], s));
+    // ---------------------------------------------------------------- metadata
+    CK(hipMemcpyAsync(ch.data(), d_chunks.p, nch * sizeof(ChunkDesc), hipMemcpyDeviceToHost, s));
+    // binary min/max bytes: gather (offset, len) pairs, then the bytes into one blob
+    std::vector<uint64_t> smeta(4 * nch, 0);
+    ENS(d_smeta, 4 * nch * 8);
+    launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(), nullptr, s);
+    CK(hipMemcpyAsync(smeta.data(), d_smeta.p, 4 * nch * 8, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    std::vector<std::string> bmin(nch), bmax(nch);
+    {
+        uint64_t blob_len = 0;
+        std::vector<uint64_t> boff(nch);
+        for (int ci = 0; ci < nch; ci++) {
+            boff[ci] = blob_len;
+            if (cols[ch[ci].col].phys == KPW_BYTE_ARRAY && ch[ci].has_minmax) blob_len += smeta[4 * ci + 1] + smeta[4 * ci + 3];
+        }
+        if (blob_len) {
+            std::vector<uint8_t> blob(blob_len);
+            ENS(d_sblob, blob_len);
+            launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(),
+                                d_sblob.as<uint8_t>(), s);
+            CK(hipMemcpyAsync(blob.data(), d_sblob.p, blob_len, hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            for (int ci = 0; ci < nch; ci++) {
+                if (cols[ch[ci].col].phys != KPW_BYTE_ARRAY || !ch[ci].has_minmax) continue;
+                const uint64_t l1 = smeta[4 * ci + 1], l2 = smeta[4 * ci + 3];
+                bmin[ci].assign((const char *)blob.data() + boff[ci], l1);
+                bmax[ci].assign((const char *)blob.data() + boff[ci] + l1, l2);
+            }
+        }
+    }
+    CK(hipEventRecord(ev_[7], s));
+    CK(hipEventSynchronize(ev_[7]));
+    for (int i = 0; i < 7; i++) CK(hipEventElapsedTime(&stage_ms[i], ev_[i], ev_[i + 1]));
+    CK(hipEventElapsedTime(&stage_ms[7], ev_[0], ev_[7]));
+
+    // ---------------------------------------------------------------- results
+    for (int ci = 0; ci < nch; ci++) {
+        const ChunkDesc &C = ch[ci];
+        const ColInfo &col = cols[C.col];
+        ChunkOut co;
+        co.column = C.col;
+        co.first_page = (int32_t)out.pages.size();
+        co.num_values = C.e - C.s;
+        co.has_dictionary = C.dictpage_len > 0;
+        if (C.dictpage_len) {
+            PageOut p;
+            p.page_type = KPW_DICTIONARY_PAGE;
+            p.num_values = (int32_t)C.dict_n;
+            p.encoding = KPW_ENC_PLAIN_DICTIONARY;
+            p.dl_encoding = p.rl_encoding = 0;
+            p.has_stats = 0;
+            p.uncompressed_size = (int64_t)plen[2 * ci];
+            p.compressed_size = (int64_t)pclen[2 * ci];
+            p.offset = pcoff[2 * ci];
+            p.null_count = 0;
+            p.has_min_max = 0;
+            out.pages.push_back(p);
+        }
+        PageOut p;
+        p.page_type = KPW_DATA_PAGE;
+        p.num_values = (int32_t)(C.e - C.s);
+        p.encoding = (C.is_dict && !C.fallback) ? KPW_ENC_PLAIN_DICTIONARY : KPW_ENC_PLAIN;
+        p.dl_encoding = col.optional ? KPW_ENC_RLE : KPW_ENC_BIT_PACKED;
+        p.rl_encoding = KPW_ENC_BIT_PACKED;
+        p.has_stats = 1;
+        p.uncompressed_size = (int64_t)plen[2 * ci + 1];
+        p.compressed_size = (int64_t)pclen[2 * ci + 1];
+        p.offset = pcoff[2 * ci + 1];
+        p.null_count = (int64_t)C.null_count;
+        p.has_min_max = C.has_minmax ? 1 : 0;
+        if (C.has_minmax) {
+            if (col.phys == KPW_BYTE_ARRAY) {
+                p.min = bmin[ci];
+                p.max = bmax[ci];
+            } else {
+                auto unkey = [&](uint64_t k) -> uint64_t {
+                    switch (col.phys) {
+                    case KPW_INT32: return (uint32_t)k ^ 0x80000000u;
+                    case KPW_INT64: return k ^ 0x8000000000000000ull;
+                    case KPW_FLOAT: { uint32_t b = (uint32_t)k; return (b >> 31) ? (b & 0x7fffffffu) : (uint32_t)~b; }
+                    case KPW_DOUBLE: return (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+                    default: return k;
+                    }
+                };
+                auto le = [&](uint64_t v) {
+                    std::string s2;
+                    const int nb = col.phys == KPW_BOOLEAN ? 1 : col.vsize;
+                    for (int i = 0; i < nb; i++) s2.push_back((char)(uint8_t)(v >> (8 * i)));
+                    return s2;
+                };
+                p.min = le(unkey(C.smin));
+                p.max = le(unkey(C.smax));
+            }
+        }
+        out.pages.push_back(p);
+        co.num_pages = (int32_t)out.pages.size() - co.first_page;
+        out.chunks.push_back(co);
+        // single-page regime guard: ColumnWriterV1.accountForValueWritten never cut a page iff
+        // the column's buffered size stayed <= pageSize up to the row-group flush.
+        const uint64_t colmem = (col.phys == KPW_BOOLEAN ? (C.nn + 7) / 8 : C.raw_bytes) + C.dl_len;
+        if (colmem > (uint64_t)props.page_size)
+            return fail(KPW_ERR_UNSUPPORTED, "column '" + col.name + "' would be split into several pages "
+                                             "(pageSize smaller than a column chunk): multi-page chunks are the next round");
+    }
+    out.d_pages = pages_dev_;
+    out.pages_len = pages_len_;
+    return KPW_OK;
+}
+
+int Engine::copy_pages(uint64_t off, uint64_t len, void *host)
+{
+    if (!pages_dev_ || off + len > pages_len_) return fail(KPW_ERR_INVALID_ARG, "copy_pages range");
+    CK(hipMemcpy(host, pages_dev_ + off, len, hipMemcpyDeviceToHost));
+    return KPW_OK;
+}
+
+}  // namespace kpw

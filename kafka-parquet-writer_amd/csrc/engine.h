@@ -1,0 +1,99 @@
+// engine.h — host orchestration of one encoder handle (one device, one stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/kpw_types.h"
+#include "kpw_kernels.h"
+
+namespace kpw {
+
+struct ColInfo {
+    std::string name;
+    int32_t field_number, proto_type, label;
+    int32_t phys, wire_type, optional, utf8, vsize, dict;
+};
+
+struct PageOut {
+    int32_t page_type, num_values, encoding, dl_encoding, rl_encoding, has_stats;
+    int64_t uncompressed_size, compressed_size;
+    uint64_t offset;            // into the device page buffer
+    int64_t null_count;
+    int32_t has_min_max;
+    std::string min, max;       // Statistics.getMinBytes / getMaxBytes
+};
+
+struct ChunkOut {
+    int32_t column;
+    int32_t first_page, num_pages, has_dictionary;
+    int64_t num_values;
+};
+
+struct RowGroupOut {
+    int64_t first_record, num_records;
+    int32_t first_chunk;
+};
+
+struct BatchOut {
+    std::vector<RowGroupOut> rgs;
+    std::vector<ChunkOut> chunks;
+    std::vector<PageOut> pages;
+    const uint8_t *d_pages = nullptr;   // device
+    uint64_t pages_len = 0;
+    int64_t records_consumed = 0, open_records = 0, open_buffered = 0, invalid_record = -1;
+};
+
+class DevBuf {
+public:
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes);
+    ~DevBuf();
+    template <typename T> T *as() const { return (T *)p; }
+};
+
+class Engine {
+public:
+    Engine() = default;
+    ~Engine();
+    int init(int device, const kpw_schema *schema, const kpw_props *props);
+    int encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
+               hipStream_t user_stream, BatchOut &out);
+    int copy_pages(uint64_t off, uint64_t len, void *host);
+    const std::string &error() const { return err_; }
+    std::vector<ColInfo> cols;
+    kpw_props props{};
+    std::string message_name, proto_class;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    float stage_ms[8] = {0};
+
+private:
+    int fail(int code, const std::string &msg);
+    std::string err_;
+    // decode buffers
+    std::vector<DevBuf> col_vals, col_soff, col_slen, col_pres, col_vbits, col_pcnt;
+    DevBuf d_cols, d_fmap, d_raw, d_P, d_err, d_scan_tmp, d_opt, d_bool;
+    // planning
+    DevBuf d_ev, d_E, d_gend, d_rg_start, d_rg_end, d_plan_out;
+    // rle scratch (shared by planning and encoding)
+    DevBuf r_ptile_job, r_last, r_prev, r_lrcnt, r_lroff, r_etile_job, r_lra, r_lrb, r_emap, r_emappre, r_rcnt, r_roff,
+        r_rg, r_rb, r_rbytes, r_rgroups, r_etbytes, r_etgroups, r_rboff, r_rgoff, r_jnlong, r_jnrle, r_jbtot, r_jgtot,
+        d_jobs;
+    // chunks
+    DevBuf d_chunks, d_ctile_chunk, d_ctile_first, d_ctile_count, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
+        d_tile_cnt, d_tile_sz, d_ht_key, d_ht_min, d_ht_id, d_ids, d_ent_rec, d_ent_boff, d_page_off, d_page_len, d_tot,
+        d_body;
+    // snappy
+    DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
+    DevBuf d_smeta, d_sblob;
+    hipEvent_t ev_[9] = {};
+    std::vector<uint32_t> opt_idx_, bool_idx_;
+    int run_rle(std::vector<RleJob> &jobs, uint32_t &nptiles, uint32_t &netiles, RleScratch &sc);
+    uint8_t *pages_dev_ = nullptr;
+    uint64_t pages_len_ = 0;
+};
+
+}  // namespace kpw

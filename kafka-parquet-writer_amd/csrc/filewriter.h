@@ -1,0 +1,63 @@
+// filewriter.h — host-side Parquet file assembly (what north_star keeps on the host):
+// Thrift-compact page headers, column-chunk/row-group metadata and the footer, restating
+// parquet-mr 1.10.1 ParquetFileWriter + ParquetMetadataConverter as driven by
+// ColumnChunkPageWriteStore.flushToFileWriter (dictionary page first, then data pages).
+#pragma once
+#include <stdint.h>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+namespace kpw {
+
+struct StatsOut {
+    int phys = 0;
+    bool has = false;       // hasNonNullValue
+    int64_t nulls = 0;
+    std::string min, max;
+};
+
+struct ChunkMeta {
+    int phys, codec;
+    std::vector<int> encodings;                   // insertion order, de-duplicated
+    std::vector<std::pair<int, int>> dict_stats;  // (encoding, pages)
+    std::vector<std::pair<int, int>> data_stats;
+    int64_t num_values, total_uncomp, total_comp, data_page_offset;
+    StatsOut stats;
+};
+
+struct RowGroupMeta {
+    int64_t rows, total_bytes;
+    std::vector<ChunkMeta> chunks;
+};
+
+class FileWriter {
+public:
+    FileWriter(const std::vector<ColInfo> &cols, const std::string &message_name, const std::string &proto_class,
+               const kpw_props &props);
+    ~FileWriter();
+    int open(const char *path);       // nullptr = memory
+    // Appends one encoded row group; `pages` is host memory holding the batch's page bodies
+    // (indexed by PageOut.offset relative to pages_base).
+    int write_row_group(const BatchOut &b, int rg, const uint8_t *pages, uint64_t pages_base);
+    int close();                      // footer + magic
+    int64_t pos() const { return pos_; }
+    const std::vector<uint8_t> &memory() const { return mem_; }
+    const std::string &error() const { return err_; }
+
+private:
+    int put(const void *p, size_t n);
+    std::vector<ColInfo> cols_;
+    std::string message_name_, proto_class_;
+    kpw_props props_;
+    FILE *fp_ = nullptr;
+    std::vector<uint8_t> mem_;
+    int64_t pos_ = 0;
+    std::vector<RowGroupMeta> rgs_;
+    std::string err_;
+    bool closed_ = false;
+};
+
+}  // namespace kpw

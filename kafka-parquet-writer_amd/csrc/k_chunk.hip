@@ -1,0 +1,613 @@
+// k_chunk.hip — per column-chunk kernels (one chunk = one column of one row group = one
+// data page in the single-page regime):
+//   K6 statistics   (Int/Long/Float/Double/Boolean/BinaryStatistics, parquet-mr 1.10.1
+//                    PrimitiveComparator order; null_count)
+//   K2 dictionary   (Plain*DictionaryValuesWriter: ids in first-occurrence order over the
+//                    chunk, dictionaryByteSize += 4/8/4+len per new entry, fallback when it
+//                    exceeds dictPageSize; FallbackValuesWriter.isCompressionSatisfying on the
+//                    (first and only) page)
+//   K4 PLAIN        (PlainValuesWriter little-endian values / 4-byte-length binaries,
+//                    BooleanPlainValuesWriter LSB-first bits)
+//   page layout     (ColumnWriterV1.writePage: rl(empty) | dl(4-byte length + RLE) | values;
+//                    dictionary page first in the chunk, ColumnChunkPageWriter order)
+//
+// Chunks are processed through "chunk tiles" (2048 records of one chunk per 256-thread
+// block, 8 consecutive records per thread) so ranks of non-null values follow record
+// order: rank = popcount prefix of the presence bits (pcnt + in-word popcount).
+#include "kpw_device.h"
+#include "kpw_kernels.h"
+#include "kpw_chunk.h"
+
+namespace kpw {
+
+__device__ __forceinline__ bool present_at(const DevCol &c, uint64_t r)
+{
+    return !c.optional || ((c.pres[r >> 6] >> (r & 63)) & 1ull);
+}
+__device__ __forceinline__ uint64_t rank_base(const DevCol &c, uint64_t s, uint64_t x)
+{
+    if (!c.optional) return x - s;
+    auto pc = [&](uint64_t y) -> uint64_t {
+        const uint64_t wi = y >> 6;
+        const uint64_t m = (y & 63) ? (c.pres[wi] & ((1ull << (y & 63)) - 1)) : 0ull;
+        return (uint64_t)c.pcnt[wi] + (uint64_t)__popcll(m);
+    };
+    return pc(x) - pc(s);
+}
+
+__device__ __forceinline__ uint64_t fixed_val(const DevCol &c, uint64_t r)
+{
+    return c.vsize == 4 ? (uint64_t)((const uint32_t *)c.vals)[r] : ((const uint64_t *)c.vals)[r];
+}
+
+// order-preserving key for the Java comparators
+__device__ __forceinline__ uint64_t order_key(int phys, uint64_t v)
+{
+    switch (phys) {
+    case 1: return (uint64_t)((uint32_t)v ^ 0x80000000u);
+    case 2: return v ^ 0x8000000000000000ull;
+    case 4: { uint32_t b = (uint32_t)v; return (uint64_t)((b >> 31) ? ~b : (b | 0x80000000u)); }
+    case 5: return (v >> 63) ? ~v : (v | 0x8000000000000000ull);
+    default: return v;  // boolean 0/1
+    }
+}
+
+__device__ __forceinline__ int bin_cmp(const uint8_t *data, uint64_t oa, uint32_t la, uint64_t ob, uint32_t lb)
+{
+    const uint32_t m = la < lb ? la : lb;
+    for (uint32_t i = 0; i < m; i++) {
+        const uint8_t x = data[oa + i], y = data[ob + i];
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return la == lb ? 0 : (la < lb ? -1 : 1);
+}
+
+// ------------------------------------------------------------------ K6 stats + sizes
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
+                                                           const uint32_t *ctile_chunk, const uint32_t *ctile_first,
+                                                           uint64_t *tile_raw, uint64_t *tile_smin, uint64_t *tile_smax)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    __shared__ uint64_t li[KPW_BLOCK], la[KPW_BLOCK];
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    ChunkDesc &C = ch[ci];
+    const DevCol &col = cols[C.col];
+    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    uint64_t nn = 0, raw = 0;
+    uint64_t kmin = ~0ull, kmax = 0;
+    uint64_t imin = ~0ull, imax = ~0ull;   // binary: record index of min / max candidate
+    for (int k = 0; k < 8; k++) {
+        const uint64_t r = p0 + k;
+        if (r >= (uint64_t)C.e) break;
+        if (!present_at(col, r)) continue;
+        nn++;
+        if (col.phys == 6) {
+            const uint32_t l = col.slen[r];
+            raw += 4 + l;
+            if (imin == ~0ull || bin_cmp(data, col.soff[r], l, col.soff[imin], col.slen[imin]) < 0) imin = r;
+            if (imax == ~0ull || bin_cmp(data, col.soff[r], l, col.soff[imax], col.slen[imax]) > 0) imax = r;
+        } else if (col.phys == 0) {
+            const uint64_t v = (col.vbits[r >> 6] >> (r & 63)) & 1ull;
+            kmin = v < kmin ? v : kmin;
+            kmax = v > kmax ? v : kmax;
+        } else {
+            raw += (uint64_t)col.vsize;
+            const uint64_t key = order_key(col.phys, fixed_val(col, r));
+            kmin = key < kmin ? key : kmin;
+            kmax = key > kmax ? key : kmax;
+        }
+    }
+    const uint64_t snn = block_reduce<uint64_t, OpSum64>(nn, lds);
+    const uint64_t sraw = block_reduce<uint64_t, OpSum64>(raw, lds);
+    if (col.phys == 6) {
+        // block reduce of (min index, max index) with the unsigned lexicographic comparator
+        li[threadIdx.x] = imin;
+        la[threadIdx.x] = imax;
+        __syncthreads();
+        for (int d = KPW_BLOCK / 2; d > 0; d >>= 1) {
+            if ((int)threadIdx.x < d) {
+                const uint64_t a = li[threadIdx.x], b = li[threadIdx.x + d];
+                // keep the earlier record on ties (same bytes -> same output anyway)
+                if (b != ~0ull && (a == ~0ull || bin_cmp(data, col.soff[b], col.slen[b], col.soff[a], col.slen[a]) < 0)) li[threadIdx.x] = b;
+                const uint64_t x = la[threadIdx.x], y = la[threadIdx.x + d];
+                if (y != ~0ull && (x == ~0ull || bin_cmp(data, col.soff[y], col.slen[y], col.soff[x], col.slen[x]) > 0)) la[threadIdx.x] = y;
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) { tile_smin[t] = li[0]; tile_smax[t] = la[0]; tile_raw[t] = sraw; }
+    } else {
+        if (snn) {
+            // wave-level min/max then one atomic per wave
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint64_t a = __shfl_xor(kmin, o, 64), b = __shfl_xor(kmax, o, 64);
+                kmin = a < kmin ? a : kmin;
+                kmax = b > kmax ? b : kmax;
+            }
+            if ((threadIdx.x & 63) == 0) {
+                if (kmin != ~0ull) atomicMin((unsigned long long *)&C.smin, (unsigned long long)kmin);
+                atomicMax((unsigned long long *)&C.smax, (unsigned long long)kmax);
+            }
+        }
+        if (threadIdx.x == 0) tile_raw[t] = sraw;
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(&C.nn, (uint32_t)snn);
+        atomicAdd((unsigned long long *)&C.raw_bytes, (unsigned long long)sraw);
+    }
+}
+
+// per chunk: combine tile candidates of binary min/max; null count; has_minmax
+__global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats_final(ChunkDesc *ch, int nchunks, const DevCol *cols, const uint8_t *data,
+                                                                 const uint32_t *ctile_first, const uint32_t *ctile_count,
+                                                                 const uint64_t *tile_smin, const uint64_t *tile_smax)
+{
+    const int ci = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ci >= nchunks) return;
+    ChunkDesc &C = ch[ci];
+    const DevCol &col = cols[C.col];
+    C.null_count = (uint64_t)(C.e - C.s) - C.nn;
+    C.has_minmax = C.nn > 0;
+    if (col.phys == 6 && C.nn) {
+        uint64_t a = ~0ull, b = ~0ull;
+        for (uint32_t k = 0; k < ctile_count[ci]; k++) {
+            const uint64_t x = tile_smin[ctile_first[ci] + k], y = tile_smax[ctile_first[ci] + k];
+            if (x != ~0ull && (a == ~0ull || bin_cmp(data, col.soff[x], col.slen[x], col.soff[a], col.slen[a]) < 0)) a = x;
+            if (y != ~0ull && (b == ~0ull || bin_cmp(data, col.soff[y], col.slen[y], col.soff[b], col.slen[b]) > 0)) b = y;
+        }
+        C.smin = a;
+        C.smax = b;
+    }
+}
+
+// ------------------------------------------------------------------ K2 dictionary
+
+constexpr uint64_t HT_EMPTY = ~0ull;
+
+__device__ __forceinline__ uint64_t str_hash(const uint8_t *p, uint32_t n)
+{
+    uint64_t h = 1469598103934665603ull ^ n;
+    for (uint32_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; }
+    return mix64(h);
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
+                                                           const uint32_t *ctile_chunk, const uint32_t *ctile_first,
+                                                           uint64_t *ht_key, uint32_t *ht_min, uint32_t *slotof, uint32_t max_dict_bytes)
+{
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    ChunkDesc &C = ch[ci];
+    if (!C.is_dict) return;
+    if (__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    const DevCol &col = cols[C.col];
+    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    if (p0 >= (uint64_t)C.e) return;
+    uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+    const uint32_t cap = C.ht_cap;
+    uint64_t *keys = ht_key + C.ht_off;
+    uint32_t *mins = ht_min + C.ht_off;
+    const bool is_bin = col.phys == 6;
+    for (int k = 0; k < 8; k++) {
+        const uint64_t r = p0 + k;
+        if (r >= (uint64_t)C.e) break;
+        if (!present_at(col, r)) continue;
+        uint64_t key, h;
+        uint32_t esize;
+        if (is_bin) {
+            key = r;
+            const uint32_t l = col.slen[r];
+            h = str_hash(data + col.soff[r], l);
+            esize = 4 + l;
+        } else {
+            key = fixed_val(col, r);
+            h = mix64(key);
+            esize = (uint32_t)col.vsize;
+        }
+        uint32_t slot;
+        bool ok = false;
+        if (!is_bin && key == HT_EMPTY) {
+            slot = cap;  // reserved slot for the sentinel value
+            const unsigned long long old = atomicCAS((unsigned long long *)&keys[slot], (unsigned long long)HT_EMPTY, 0ull);
+            if (old == HT_EMPTY) {
+                const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
+                atomicAdd(&C.dict_n, 1u);
+                if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            atomicMin(&mins[slot], (uint32_t)rank);
+            ok = true;
+        } else {
+            uint32_t i = (uint32_t)(h & (cap - 1));
+            for (uint32_t probe = 0; probe < cap; probe++) {
+                uint64_t cur = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cur == HT_EMPTY) {
+                    const unsigned long long old = atomicCAS((unsigned long long *)&keys[i], (unsigned long long)HT_EMPTY,
+                                                             (unsigned long long)key);
+                    if (old == HT_EMPTY) {
+                        const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
+                        atomicAdd(&C.dict_n, 1u);
+                        if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        atomicMin(&mins[i], (uint32_t)rank);
+                        slot = i;
+                        ok = true;
+                        break;
+                    }
+                    cur = old;
+                }
+                bool eq;
+                if (is_bin) eq = bin_cmp(data, col.soff[cur], col.slen[cur], col.soff[r], col.slen[r]) == 0;
+                else eq = cur == key;
+                if (eq) {
+                    atomicMin(&mins[i], (uint32_t)rank);
+                    slot = i;
+                    ok = true;
+                    break;
+                }
+                i = (i + 1) & (cap - 1);
+            }
+        }
+        if (!ok) {
+            atomicOr(&C.overflow, 1u);
+            __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        slotof[C.ids_off + rank] = slot;
+        rank++;
+    }
+}
+
+// count (write=0) / assign (write=1) first occurrences in record order
+__global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
+                                                           const uint32_t *ctile_first, const uint32_t *ht_min, uint32_t *ht_id,
+                                                           const uint32_t *slotof, uint32_t *tile_cnt, uint64_t *tile_sz,
+                                                           const uint32_t *tile_cnt_off, const uint64_t *tile_sz_off,
+                                                           uint64_t *ent_rec, uint64_t *ent_boff, int write)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    __shared__ uint32_t ldu[KPW_BLOCK];
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    const ChunkDesc &C = ch[ci];
+    const bool active = C.is_dict && !C.fallback;
+    const DevCol &col = cols[C.col];
+    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    uint32_t cnt = 0;
+    uint64_t sz = 0;
+    uint32_t firsts = 0;  // bitmask over the 8 records
+    if (active && p0 < (uint64_t)C.e) {
+        uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+        for (int k = 0; k < 8; k++) {
+            const uint64_t r = p0 + k;
+            if (r >= (uint64_t)C.e) break;
+            if (!present_at(col, r)) continue;
+            const uint32_t slot = slotof[C.ids_off + rank];
+            if (ht_min[C.ht_off + slot] == (uint32_t)rank) {
+                firsts |= 1u << k;
+                cnt++;
+                sz += col.phys == 6 ? 4 + col.slen[r] : (uint64_t)col.vsize;
+            }
+            rank++;
+        }
+    }
+    if (!write) {
+        const uint32_t sc = block_reduce<uint32_t, OpSum32>(cnt, ldu);
+        const uint64_t ss = block_reduce<uint64_t, OpSum64>(sz, lds);
+        if (threadIdx.x == 0) { tile_cnt[t] = sc; tile_sz[t] = ss; }
+        return;
+    }
+    uint32_t tc;
+    uint64_t ts;
+    uint32_t eid = block_scan_excl<uint32_t, OpSum32>(cnt, ldu, &tc) + tile_cnt_off[t];
+    uint64_t boff = block_scan_excl<uint64_t, OpSum64>(sz, lds, &ts) + tile_sz_off[t];
+    if (!firsts) return;
+    uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+    for (int k = 0; k < 8; k++) {
+        const uint64_t r = p0 + k;
+        if (r >= (uint64_t)C.e) break;
+        if (!present_at(col, r)) continue;
+        if ((firsts >> k) & 1) {
+            const uint32_t slot = slotof[C.ids_off + rank];
+            ht_id[C.ht_off + slot] = eid;
+            ent_rec[C.ent_off + eid] = r;
+            ent_boff[C.ent_off + eid] = boff;
+            boff += col.phys == 6 ? 4 + col.slen[r] : (uint64_t)col.vsize;
+            eid++;
+        }
+        rank++;
+    }
+}
+
+// slot -> id for every value (overwrites slotof in place); sets id-job width/length
+__global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
+                                                        const uint32_t *ctile_first, const uint32_t *ht_id, uint32_t *ids)
+{
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    const ChunkDesc &C = ch[ci];
+    if (!C.is_dict || C.fallback) return;
+    const DevCol &col = cols[C.col];
+    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    if (p0 >= (uint64_t)C.e) return;
+    uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+    for (int k = 0; k < 8; k++) {
+        const uint64_t r = p0 + k;
+        if (r >= (uint64_t)C.e) break;
+        if (!present_at(col, r)) continue;
+        const uint64_t o = C.ids_off + rank;
+        ids[o] = ht_id[C.ht_off + ids[o]];
+        rank++;
+    }
+}
+
+__global__ void k_dict_jobs(ChunkDesc *ch, int nchunks, RleJob *jobs, uint32_t max_dict_bytes)
+{
+    const int ci = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ci >= nchunks) return;
+    ChunkDesc &C = ch[ci];
+    if (!C.is_dict) return;
+    if (C.dict_bytes > max_dict_bytes || C.overflow) C.fallback = 1;
+    RleJob &J = jobs[C.id_job];
+    if (C.fallback) { J.len = 0; J.bw = 0; return; }
+    // DictionaryValuesWriter.getBytes: bitWidth = getWidthFromMaxInt(dictSize - 1)
+    const uint32_t m = C.dict_n - 1;
+    C.bw = m ? 32 - __clz(m) : (C.dict_n ? 0 : 32);
+    J.len = C.nn;
+    J.bw = C.bw;
+}
+
+// ------------------------------------------------------------------ layout (one block, all chunks)
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks, const DevCol *cols, RleJob *jobs, uint64_t *page_off,
+                                                      uint64_t *page_len, uint64_t *tot)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    uint64_t carry = 0;
+    for (int b = 0; b < nchunks; b += KPW_BLOCK) {
+        const int ci = b + threadIdx.x;
+        uint64_t body = 0;
+        if (ci < nchunks) {
+            ChunkDesc &C = ch[ci];
+            const DevCol &col = cols[C.col];
+            C.dl_len = col.optional ? jobs[C.dl_job].total_bytes : 0;
+            uint64_t val = 0, dictp = 0;
+            if (C.is_dict && !C.fallback) {
+                val = 1 + jobs[C.id_job].total_bytes;
+                // FallbackValuesWriter.getBytes on the first page: isCompressionSatisfying
+                if (!(val + C.dict_bytes < C.raw_bytes)) C.fallback = 1;
+                else dictp = C.dict_bytes;
+            }
+            if (!C.is_dict || C.fallback) {
+                val = col.phys == 0 ? (uint64_t)(C.nn + 7) / 8 : C.raw_bytes;
+                dictp = 0;
+                if (C.is_dict) {  // do not write ids
+                    RleJob &J = jobs[C.id_job];
+                    J.n_rle = 0; J.total_groups = 0; J.final_gap_groups = 0; J.total_bytes = 0;
+                }
+            }
+            C.val_len = val;
+            C.dictpage_len = dictp;
+            body = dictp + (col.optional ? 4 + C.dl_len : 0) + val;
+        }
+        uint64_t t2;
+        const uint64_t ex = block_scan_excl<uint64_t, OpSum64>(body, lds, &t2) + carry;
+        if (ci < nchunks) {
+            ChunkDesc &C = ch[ci];
+            const DevCol &col = cols[C.col];
+            C.body_off = ex;
+            const uint64_t dpage = ex + C.dictpage_len;
+            if (col.optional) jobs[C.dl_job].out_off = dpage + 4;
+            if (C.is_dict) jobs[C.id_job].out_off = dpage + (col.optional ? 4 + C.dl_len : 0) + 1;
+            page_off[2 * ci] = ex;
+            page_len[2 * ci] = C.dictpage_len;
+            page_off[2 * ci + 1] = dpage;
+            page_len[2 * ci + 1] = body - C.dictpage_len;
+        }
+        carry += t2;
+    }
+    if (threadIdx.x == 0) tot[0] = carry;
+}
+
+// ------------------------------------------------------------------ writers
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_chunk_headers(const ChunkDesc *ch, int nchunks, const DevCol *cols, uint8_t *out)
+{
+    const int ci = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ci >= nchunks) return;
+    const ChunkDesc &C = ch[ci];
+    const DevCol &col = cols[C.col];
+    uint8_t *p = out + C.body_off + C.dictpage_len;
+    if (col.optional) {
+        const uint32_t l = (uint32_t)C.dl_len;
+        p[0] = (uint8_t)l; p[1] = (uint8_t)(l >> 8); p[2] = (uint8_t)(l >> 16); p[3] = (uint8_t)(l >> 24);
+        p += 4 + C.dl_len;
+    }
+    if (C.is_dict && !C.fallback) p[0] = (uint8_t)C.bw;
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_dict_page(const ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
+                                                         const uint32_t *ctile_chunk, const uint32_t *ctile_first,
+                                                         const uint64_t *ent_rec, const uint64_t *ent_boff, uint8_t *out)
+{
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    const ChunkDesc &C = ch[ci];
+    if (!C.is_dict || C.fallback) return;
+    const DevCol &col = cols[C.col];
+    const uint64_t e0 = (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    uint8_t *page = out + C.body_off;
+    for (int k = 0; k < 8; k++) {
+        const uint64_t e = e0 + k;
+        if (e >= C.dict_n) break;
+        const uint64_t r = ent_rec[C.ent_off + e];
+        uint8_t *o = page + ent_boff[C.ent_off + e];
+        if (col.phys == 6) {
+            const uint32_t l = col.slen[r];
+            o[0] = (uint8_t)l; o[1] = (uint8_t)(l >> 8); o[2] = (uint8_t)(l >> 16); o[3] = (uint8_t)(l >> 24);
+            const uint8_t *src = data + col.soff[r];
+            for (uint32_t i = 0; i < l; i++) o[4 + i] = src[i];
+        } else {
+            const uint64_t v = fixed_val(col, r);
+            for (int i = 0; i < col.vsize; i++) o[i] = (uint8_t)(v >> (8 * i));
+        }
+    }
+}
+
+// PLAIN values (fixed / binary) for chunks without dictionary encoding
+__global__ void __launch_bounds__(KPW_BLOCK) k_plain(const ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
+                                                     const uint32_t *ctile_chunk, const uint32_t *ctile_first,
+                                                     const uint64_t *tile_raw_off, uint8_t *out)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    const ChunkDesc &C = ch[ci];
+    const DevCol &col = cols[C.col];
+    if ((C.is_dict && !C.fallback) || col.phys == 0) return;
+    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    uint8_t *vout = out + C.body_off + (col.optional ? 4 + C.dl_len : 0);
+    if (col.phys == 6) {
+        uint64_t sz = 0;
+        for (int k = 0; k < 8; k++) {
+            const uint64_t r = p0 + k;
+            if (r >= (uint64_t)C.e) break;
+            if (present_at(col, r)) sz += 4 + col.slen[r];
+        }
+        uint64_t tot;
+        uint64_t o = block_scan_excl<uint64_t, OpSum64>(sz, lds, &tot) + tile_raw_off[t];
+        for (int k = 0; k < 8; k++) {
+            const uint64_t r = p0 + k;
+            if (r >= (uint64_t)C.e) break;
+            if (!present_at(col, r)) continue;
+            const uint32_t l = col.slen[r];
+            uint8_t *d = vout + o;
+            d[0] = (uint8_t)l; d[1] = (uint8_t)(l >> 8); d[2] = (uint8_t)(l >> 16); d[3] = (uint8_t)(l >> 24);
+            const uint8_t *src = data + col.soff[r];
+            for (uint32_t i = 0; i < l; i++) d[4 + i] = src[i];
+            o += 4 + l;
+        }
+    } else {
+        if (p0 >= (uint64_t)C.e) return;
+        uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+        for (int k = 0; k < 8; k++) {
+            const uint64_t r = p0 + k;
+            if (r >= (uint64_t)C.e) break;
+            if (!present_at(col, r)) continue;
+            const uint64_t v = fixed_val(col, r);
+            uint8_t *d = vout + rank * col.vsize;
+            for (int i = 0; i < col.vsize; i++) d[i] = (uint8_t)(v >> (8 * i));
+            rank++;
+        }
+    }
+}
+
+// BooleanPlainValuesWriter: compacted value bits, LSB first (output pre-zeroed)
+__global__ void __launch_bounds__(KPW_BLOCK) k_plain_bool(const ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
+                                                          const uint32_t *ctile_first, uint8_t *out)
+{
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    const ChunkDesc &C = ch[ci];
+    const DevCol &col = cols[C.col];
+    if (col.phys != 0) return;
+    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    if (p0 >= (uint64_t)C.e) return;
+    uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+    const uint64_t base_bit = (C.body_off + (col.optional ? 4 + C.dl_len : 0)) * 8;
+    for (int k = 0; k < 8; k++) {
+        const uint64_t r = p0 + k;
+        if (r >= (uint64_t)C.e) break;
+        if (!present_at(col, r)) continue;
+        if ((col.vbits[r >> 6] >> (r & 63)) & 1ull) {
+            const uint64_t bit = base_bit + rank;
+            atomicOr((uint32_t *)(out + ((bit >> 3) & ~3ull)), 1u << (((bit >> 3) & 3) * 8 + (bit & 7)));
+        }
+        rank++;
+    }
+}
+
+// Binary statistics: meta[4c..4c+3] = (min offset, min len, max offset, max len) of chunk c
+// (pass 1, blob == nullptr); pass 2 copies the bytes into blob at the running offset.
+__global__ void __launch_bounds__(KPW_BLOCK) k_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols,
+                                                            const uint8_t *data, uint64_t *meta, uint8_t *blob)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    uint64_t carry = 0;
+    for (int b = 0; b < nchunks; b += KPW_BLOCK) {
+        const int ci = b + threadIdx.x;
+        uint64_t len = 0;
+        bool bin = false;
+        if (ci < nchunks) {
+            const ChunkDesc &C = ch[ci];
+            const DevCol &col = cols[C.col];
+            bin = col.phys == 6 && C.has_minmax;
+            if (!blob) {
+                if (bin) {
+                    meta[4 * ci] = col.soff[C.smin]; meta[4 * ci + 1] = col.slen[C.smin];
+                    meta[4 * ci + 2] = col.soff[C.smax]; meta[4 * ci + 3] = col.slen[C.smax];
+                } else {
+                    meta[4 * ci] = meta[4 * ci + 1] = meta[4 * ci + 2] = meta[4 * ci + 3] = 0;
+                }
+            } else if (bin) {
+                len = meta[4 * ci + 1] + meta[4 * ci + 3];
+            }
+        }
+        if (!blob) continue;
+        uint64_t tot;
+        const uint64_t o = block_scan_excl<uint64_t, OpSum64>(len, lds, &tot) + carry;
+        if (ci < nchunks && bin) {
+            const uint64_t l1 = meta[4 * ci + 1], l2 = meta[4 * ci + 3];
+            for (uint64_t i = 0; i < l1; i++) blob[o + i] = data[meta[4 * ci] + i];
+            for (uint64_t i = 0; i < l2; i++) blob[o + l1 + i] = data[meta[4 * ci + 2] + i];
+        }
+        carry += tot;
+    }
+}
+
+void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, const uint8_t *data, uint64_t *meta,
+                         uint8_t *blob, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_stats_gather, dim3(1), dim3(KPW_BLOCK), 0, s, ch, nchunks, cols, data, meta, blob);
+}
+
+// ------------------------------------------------------------------ host launchers
+
+void launch_chunk_stats(const ChunkArgs &a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_chunk_stats, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
+                       a.tile_raw, a.tile_smin, a.tile_smax);
+    hipLaunchKernelGGL(k_chunk_stats_final, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, a.cols, a.data,
+                       a.ctile_first, a.ctile_count, a.tile_smin, a.tile_smax);
+}
+
+void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_dict_insert, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
+                       a.ht_key, a.ht_min, a.ids, a.max_dict_bytes);
+    hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes);
+    hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
+                       a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0);
+    seg_tile_scan_u32(a.tile_cnt, a.tile_cnt, a.ctile_chunk, a.nctiles, s);
+    seg_tile_scan_u64(a.tile_sz, a.tile_sz, a.ctile_chunk, a.nctiles, s);
+    hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
+                       a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1);
+    hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht_id, a.ids);
+}
+
+void launch_layout(const ChunkArgs &a, RleJob *jobs, uint64_t *page_off, uint64_t *page_len, uint64_t *tot, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_layout, dim3(1), dim3(KPW_BLOCK), 0, s, a.ch, a.nchunks, a.cols, jobs, page_off, page_len, tot);
+}
+
+void launch_chunk_write(const ChunkArgs &a, uint8_t *out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_chunk_headers, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, a.cols, out);
+    hipLaunchKernelGGL(k_dict_page, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
+                       a.ent_rec, a.ent_boff, out);
+    seg_tile_scan_u64(a.tile_raw, a.tile_raw_off, a.ctile_chunk, a.nctiles, s);
+    hipLaunchKernelGGL(k_plain, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
+                       a.tile_raw_off, out);
+    hipLaunchKernelGGL(k_plain_bool, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, out);
+}
+
+}  // namespace kpw

@@ -1,0 +1,220 @@
+// k_decode.hip — K1: proto2 wire bytes -> per-column (columnar) buffers.
+//
+// Restates, per record, what the reference does on the worker thread before any Parquet
+// encoding happens (KafkaProtoParquetWriter.java:268-277):
+//   parser.parseFrom(record.value())  — protobuf-java CodedInputStream + the generated
+//       proto2 parse loop (src/test/java/ir/sahab/kafka/test/proto/TestMessage.java:85-139):
+//       switch on the full tag, last occurrence wins, unknown fields (including a known
+//       number with a foreign wire type) skipped, groups skipped recursively, varints of at
+//       most 10 bytes, missing required field -> InvalidProtocolBufferException
+//       (isInitialized, TestMessage.java:263-278);
+//   ProtoWriteSupport.write -> RecordConsumer.add* (parquet-protobuf 1.10.1): one value or
+//       one null per column per record, doubles/floats observed through
+//       doubleToLongBits/floatToIntBits (NaN canonicalised).
+//
+// Layout: one lane per record, 256-record blocks; each wave covers 64 consecutive records
+// so presence / boolean bits are produced with one __ballot per column per wave
+// (word w of a bitmask = records [64w, 64w+64)).  Fixed-width values are stored record-
+// indexed (SoA, coalesced per wave), strings as (absolute offset, length) into the batch
+// bytes — the bytes are never copied here; the PLAIN/dictionary kernels gather them.
+#include "kpw_device.h"
+#include "kpw_kernels.h"
+
+namespace kpw {
+
+__device__ __forceinline__ bool rd_varint64(const uint8_t *d, uint64_t &pos, uint64_t end, uint64_t &out)
+{
+    uint64_t r = 0;
+#pragma unroll 1
+    for (int i = 0; i < 10; i++) {
+        if (pos >= end) return false;
+        uint8_t b = d[pos++];
+        r |= (uint64_t)(b & 0x7f) << (7 * i);
+        if (!(b & 0x80)) { out = r; return true; }
+    }
+    return false;
+}
+
+// Skip one unknown field whose tag has already been read. Groups are skipped
+// iteratively with a bounded stack (protobuf-java recursion limit 100).
+__device__ bool skip_field(const uint8_t *d, uint64_t &pos, uint64_t end, uint32_t tag)
+{
+    uint32_t wt = tag & 7;
+    uint64_t v;
+    switch (wt) {
+    case 0: return rd_varint64(d, pos, end, v);
+    case 1: if (end - pos < 8) return false; pos += 8; return true;
+    case 2:
+        if (!rd_varint64(d, pos, end, v)) return false;
+        if ((int32_t)(uint32_t)v < 0) return false;
+        if (end - pos < (uint32_t)v) return false;
+        pos += (uint32_t)v;
+        return true;
+    case 5: if (end - pos < 4) return false; pos += 4; return true;
+    case 3: {
+        uint32_t stack[100];
+        int depth = 0;
+        stack[depth++] = tag >> 3;
+#pragma unroll 1
+        while (depth > 0) {
+            uint64_t t64;
+            if (!rd_varint64(d, pos, end, t64)) return false;
+            uint32_t t = (uint32_t)t64;
+            if ((t >> 3) == 0) return false;
+            uint32_t w = t & 7;
+            if (w == 4) {
+                if ((t >> 3) != stack[depth - 1]) return false;
+                depth--;
+            } else if (w == 3) {
+                if (depth >= 100) return false;
+                stack[depth++] = t >> 3;
+            } else if (w == 0) {
+                if (!rd_varint64(d, pos, end, v)) return false;
+            } else if (w == 1) {
+                if (end - pos < 8) return false; pos += 8;
+            } else if (w == 5) {
+                if (end - pos < 4) return false; pos += 4;
+            } else if (w == 2) {
+                if (!rd_varint64(d, pos, end, v)) return false;
+                if ((int32_t)(uint32_t)v < 0) return false;
+                if (end - pos < (uint32_t)v) return false;
+                pos += (uint32_t)v;
+            } else {
+                return false;
+            }
+        }
+        return true;
+    }
+    default: return false;  // END_GROUP at top level (checkLastTagWas fails) or wire type 6/7
+    }
+}
+
+__device__ __forceinline__ uint64_t canon_double(uint64_t b)
+{
+    if ((b & 0x7ff0000000000000ull) == 0x7ff0000000000000ull && (b & 0x000fffffffffffffull)) return 0x7ff8000000000000ull;
+    return b;
+}
+__device__ __forceinline__ uint32_t canon_float(uint32_t b)
+{
+    if ((b & 0x7f800000u) == 0x7f800000u && (b & 0x007fffffu)) return 0x7fc00000u;
+    return b;
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
+{
+    __shared__ int16_t fmap[FMAP_SIZE];
+    __shared__ DevCol cols[64];   // first 64 columns cached; rest read from global
+    for (int i = threadIdx.x; i < FMAP_SIZE; i += blockDim.x) fmap[i] = a.fmap[i];
+    const int ncached = a.ncols < 64 ? a.ncols : 64;
+    for (int i = threadIdx.x; i < ncached; i += blockDim.x) cols[i] = a.cols[i];
+    __syncthreads();
+
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = r < a.n;
+    uint64_t seen[4] = {0, 0, 0, 0};
+    uint64_t bval[4] = {0, 0, 0, 0};   // boolean values (by column)
+    bool bad = false;
+    uint32_t raw = 0;
+
+    if (valid) {
+        const uint8_t *d = a.data;
+        uint64_t pos = a.off[r], end = a.off[r + 1];
+#pragma unroll 1
+        while (pos < end) {
+            uint64_t t64;
+            if (!rd_varint64(d, pos, end, t64)) { bad = true; break; }
+            const uint32_t tag = (uint32_t)t64;
+            const uint32_t fno = tag >> 3, wt = tag & 7;
+            if (fno == 0) { bad = true; break; }
+            int c = -1;
+            if (fno < FMAP_SIZE) c = fmap[fno];
+            else {
+                for (int k = 0; k < a.ncols; k++) if ((uint32_t)a.cols[k].field_number == fno) { c = k; break; }
+            }
+            const DevCol *col = nullptr;
+            if (c >= 0) col = c < 64 ? &cols[c] : &a.cols[c];
+            if (c < 0 || (uint32_t)col->wire_type != wt) {
+                if (!skip_field(d, pos, end, tag)) { bad = true; break; }
+                continue;
+            }
+            uint64_t v = 0;
+            if (wt == 0) {
+                if (!rd_varint64(d, pos, end, v)) { bad = true; break; }
+                switch (col->proto_type) {
+                case 5: case 13: v = (uint32_t)v; break;                                            // int32/uint32
+                case 17: { uint32_t u = (uint32_t)v; v = (uint32_t)((u >> 1) ^ (0u - (u & 1))); break; }  // sint32
+                case 18: v = (v >> 1) ^ (0ull - (v & 1)); break;                                   // sint64
+                case 8: v = v != 0; break;                                                          // bool
+                default: break;
+                }
+            } else if (wt == 1) {
+                if (end - pos < 8) { bad = true; break; }
+                v = 0;
+                for (int i = 0; i < 8; i++) v |= (uint64_t)d[pos + i] << (8 * i);
+                pos += 8;
+                if (col->phys == 5) v = canon_double(v);
+            } else if (wt == 5) {
+                if (end - pos < 4) { bad = true; break; }
+                v = 0;
+                for (int i = 0; i < 4; i++) v |= (uint64_t)d[pos + i] << (8 * i);
+                pos += 4;
+                if (col->phys == 4) v = canon_float((uint32_t)v);
+            } else {  // wt == 2
+                uint64_t l;
+                if (!rd_varint64(d, pos, end, l)) { bad = true; break; }
+                if ((int32_t)(uint32_t)l < 0 || end - pos < (uint32_t)l) { bad = true; break; }
+                col->soff[r] = pos;
+                col->slen[r] = (uint32_t)l;
+                pos += (uint32_t)l;
+            }
+            if (col->phys == 0) {
+                if (v) bval[c >> 6] |= 1ull << (c & 63); else bval[c >> 6] &= ~(1ull << (c & 63));
+            } else if (col->vsize == 4) {
+                ((uint32_t *)col->vals)[r] = (uint32_t)v;
+            } else if (col->vsize == 8) {
+                ((uint64_t *)col->vals)[r] = v;
+            }
+            seen[c >> 6] |= 1ull << (c & 63);
+        }
+        if (!bad) {
+            for (int c = 0; c < a.ncols; c++) {
+                const DevCol *col = c < 64 ? &cols[c] : &a.cols[c];
+                const bool pr = (seen[c >> 6] >> (c & 63)) & 1;
+                if (!pr) {
+                    if (!col->optional) { bad = true; break; }
+                    continue;
+                }
+                if (col->phys == 6) raw += 4 + col->slen[r];
+                else if (col->phys != 0) raw += (uint32_t)col->vsize;
+            }
+        }
+        if (bad) atomicMin(a.err_min, (unsigned long long)r);
+        a.raw[r] = bad ? 0 : raw;
+    }
+
+    // presence / boolean bitmasks: one ballot per column per wave (all lanes take part)
+    const uint64_t word = r >> 6;
+    // lane 0 of a wave lying wholly past n must not write (bitmasks hold n/64+2 words)
+    const bool lane0 = (threadIdx.x & 63) == 0 && r < a.n;
+    for (int c = 0; c < a.ncols; c++) {
+        const DevCol *col = c < 64 ? &cols[c] : &a.cols[c];
+        const bool pr = valid && !bad && ((seen[c >> 6] >> (c & 63)) & 1);
+        if (col->optional) {
+            uint64_t m = __ballot(pr);
+            if (lane0) col->pres[word] = m;
+        }
+        if (col->phys == 0) {
+            uint64_t m = __ballot(pr && ((bval[c >> 6] >> (c & 63)) & 1));
+            if (lane0) col->vbits[word] = m;
+        }
+    }
+}
+
+void launch_decode(const DecodeArgs &a, hipStream_t s)
+{
+    if (a.n == 0) return;
+    const uint64_t blocks = (a.n + KPW_BLOCK - 1) / KPW_BLOCK;
+    hipLaunchKernelGGL(k_decode, dim3((unsigned)blocks), dim3(KPW_BLOCK), 0, s, a);
+}
+
+}  // namespace kpw

@@ -1,0 +1,202 @@
+// k_plan.hip — A9: row-group boundary planner.
+//
+// Restates parquet-mr 1.10.1 InternalParquetRecordWriter.checkBlockSizeReached exactly:
+// check when recordCount >= recordCountForNextMemCheck (100 at a row-group start, also
+// after a flush because flushRowGroupToStore zeroes recordCount first); memSize =
+// columnStore.getBufferedSize(); recordSize = memSize / recordCount; flush iff
+// memSize > nextRowGroupSize - 2*recordSize; otherwise next check at
+// min(max(100, (recordCount + (long)(nextRowGroupSize / (float)recordSize)) / 2),
+//     recordCount + 10000) (Java float division, saturating float->long cast, wrapping add).
+//
+// memSize for the single-page-per-chunk regime (every column's page check stays below
+// pageSize; verified on the host from the encoded chunk sizes) is
+//   sum over columns of  rl(0) + dl.getBufferedSize() + data.getBufferedSize()
+// = [P[r]-P[s]]                         FallbackValuesWriter.rawDataByteSize / PlainValuesWriter
+// + sum_bool ceil(count/8)              BooleanPlainValuesWriter (ByteBasedBitPackingEncoder)
+// + sum_optional E_s(r)                 RunLengthBitPackingHybridEncoder baos.size() for the
+//                                       definition levels written since the row-group start s.
+// E_s(r) comes from the global RLE parse (E_g, started at record 0) once the local parse
+// started at s re-synchronises with it (both end an RLE run at the same position; from
+// there on the encoders are in identical states), and from a short local walk before.
+//
+// One wave walks the row groups sequentially; lanes split the optional/boolean columns.
+#include "kpw_device.h"
+#include "kpw_kernels.h"
+
+namespace kpw {
+
+struct Walker {
+    int64_t p;          // next group start
+    int64_t conv_pos;   // position of the RLE event where the parse re-synchronised
+    int64_t delta;      // E_s - E_g after conv_pos
+    uint64_t eacc;      // bytes emitted by events consumed so far
+    int64_t pend_pos;   // pending element event position (-1 none)
+    int64_t pend_next;
+    uint32_t pend_bytes, pend_rle;
+    uint32_t grp;       // groups in the current bit-packed run
+    uint32_t state;     // 0 walking, 1 converged, 2 no more events in the batch
+};
+
+__device__ __forceinline__ int32_t java_f2i(float f)
+{
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return 2147483647;
+    if (f <= -2147483648.0f) return (-2147483647 - 1);
+    return (int32_t)f;
+}
+__device__ __forceinline__ int64_t java_f2l(float f)
+{
+    if (f != f) return 0;
+    if (f >= 9223372036854775808.0f) return 9223372036854775807ll;
+    if (f <= -9223372036854775808.0f) return (-9223372036854775807ll - 1);
+    return (int64_t)f;
+}
+__device__ __forceinline__ int64_t jadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// E_s(r) for one optional column (dl width 1).
+__device__ uint64_t walker_query(Walker &w, int64_t r, const uint64_t *pres, uint64_t n, const uint32_t *Eg,
+                                 const uint64_t *gend)
+{
+    while (w.state == 0) {
+        if (w.pend_pos < 0) {
+            const int64_t p = w.p;
+            if (p + 8 > (int64_t)n) { w.state = 2; break; }
+            const uint32_t x8 = (uint32_t)(bits_window(pres, (uint64_t)p) & 0xffu);
+            if (x8 == 0 || x8 == 0xffu) {
+                const uint64_t fill = x8 ? ~0ull : 0ull;
+                int64_t pos = p + 8, b = (int64_t)n;
+                while (pos < (int64_t)n) {
+                    uint64_t d = bits_window(pres, (uint64_t)pos) ^ fill;
+                    if (d) { b = pos + __ffsll((long long)d) - 1; break; }
+                    pos += 64;
+                }
+                if (b > (int64_t)n) b = (int64_t)n;
+                if (b >= (int64_t)n) { w.state = 2; break; }
+                w.pend_pos = b;
+                w.pend_next = b;
+                w.pend_bytes = varint_len32((uint32_t)(b - p) << 1) + 1;
+                w.pend_rle = 1;
+            } else {
+                w.pend_pos = p + 7;
+                w.pend_next = p + 8;
+                w.pend_bytes = 1 + ((w.grp % 63) == 0 ? 1 : 0);
+                w.pend_rle = 0;
+            }
+        }
+        if (w.pend_pos >= r) break;
+        w.eacc += w.pend_bytes;
+        w.p = w.pend_next;
+        if (w.pend_rle) {
+            w.grp = 0;
+            const uint64_t b = (uint64_t)w.pend_pos;
+            if ((gend[b >> 6] >> (b & 63)) & 1) {
+                w.state = 1;
+                w.conv_pos = (int64_t)b;
+                w.delta = (int64_t)w.eacc - (int64_t)Eg[b + 1];
+            }
+        } else {
+            w.grp++;
+        }
+        w.pend_pos = -1;
+    }
+    if (w.state == 1 && r > w.conv_pos) return (uint64_t)((int64_t)Eg[r] + w.delta);
+    return w.eacc;
+}
+
+__device__ __forceinline__ uint64_t pc_at(const DevCol &c, uint64_t x)
+{
+    const uint64_t wi = x >> 6;
+    const uint64_t m = (x & 63) ? (c.pres[wi] & ((1ull << (x & 63)) - 1)) : 0ull;
+    return (uint64_t)c.pcnt[wi] + (uint64_t)__popcll(m);
+}
+
+__device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
+{
+    const int lane = threadIdx.x;
+    uint64_t part = 0;
+    for (int k = lane; k < a.nopt; k += 64) {
+        const DevCol &c = a.cols[a.opt_cols[k]];
+        part += walker_query(W[k], r, c.pres, a.n, a.E + (uint64_t)k * (a.n + 1), a.gend + (uint64_t)k * a.gend_stride);
+    }
+    for (int k = lane; k < a.nbool; k += 64) {
+        const DevCol &c = a.cols[a.bool_cols[k]];
+        const uint64_t cnt = c.optional ? pc_at(c, (uint64_t)r) - pc_at(c, (uint64_t)s) : (uint64_t)(r - s);
+        part += (cnt + 7) / 8;
+    }
+    return wave_sum(part) + (a.P[r] - a.P[s]);
+}
+
+__global__ void __launch_bounds__(64) k_plan(PlanArgs a)
+{
+    __shared__ Walker W[MAX_COLS];
+    const int lane = threadIdx.x;
+    const int64_t n = (int64_t)a.n;
+    const int64_t T = a.next_rg_size;
+    int64_t s = 0;
+    int32_t nrg = 0;
+    int64_t overflow = 0;
+    for (;;) {
+        for (int k = lane; k < a.nopt; k += 64) {
+            Walker w;
+            w.p = s; w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
+            w.pend_bytes = 0; w.pend_rle = 0; w.grp = 0; w.state = 0;
+            W[k] = w;
+        }
+        __syncthreads();
+        int64_t rc = 100;
+        bool cut = false;
+        int64_t r = 0;
+        while (s + rc <= n) {
+            r = s + rc;
+            const int64_t M = (int64_t)eval_mem(a, W, s, r);
+            const int64_t rs = M / rc;
+            if (M > T - 2 * rs) { cut = true; break; }
+            const float q = __fdiv_rn((float)T, (float)rs);
+            const int64_t est = jadd(rc, java_f2l(q)) / 2;
+            const int64_t lo = est > 100 ? est : 100;
+            const int64_t hi = jadd(rc, 10000);
+            int64_t nc = lo < hi ? lo : hi;
+            if (nc < rc + 1) nc = rc + 1;
+            rc = nc;
+        }
+        if (cut) {
+            if (nrg < a.max_rgs) { if (lane == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = r; } }
+            else overflow = 1;
+            nrg++;
+            s = r;
+            __syncthreads();
+            continue;
+        }
+        // the open row group [s, n)
+        int64_t open_buf = 0;
+        if (s < n) open_buf = (int64_t)eval_mem(a, W, s, n);
+        if (a.final_flush && s < n) {
+            if (nrg < a.max_rgs) { if (lane == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = n; } }
+            else overflow = 1;
+            nrg++;
+            s = n;
+            open_buf = 0;
+        }
+        if (lane == 0) {
+            a.out[0] = nrg;
+            a.out[1] = s;
+            a.out[2] = open_buf;
+            a.out[3] = overflow;
+        }
+        break;
+    }
+}
+
+void launch_plan(const PlanArgs &a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, a);
+}
+
+}  // namespace kpw

@@ -1,0 +1,417 @@
+// k_rle.hip — K3: RLE / bit-packing hybrid, byte-identical to parquet-mr 1.10.1
+// RunLengthBitPackingHybridEncoder (writeInt / writeOrAppendBitPackedRun / writeRleRun /
+// endPreviousBitPackedRun / toBytes), reformulated for a data-parallel GPU.
+//
+// The sequential encoder's behaviour is fully determined by where its 8-value groups
+// start.  Group starts form an arithmetic progression (phase = start mod 8) that only
+// changes after an RLE run; an RLE run starts at a group start g iff v[g..g+7] are equal,
+// and then extends to the end b of that maximal run of equal values (the next group
+// starts at b).  Hence only "long runs" (maximal runs of >= 8 equal values) matter: for a
+// long run [a, b) entered with phase phi, the first group start inside it is
+// g = a + ((phi - a) mod 8); it becomes an RLE run iff g + 8 <= b, and the phase after it
+// is b mod 8 (else phi is unchanged).  Each long run is therefore an 8-state transfer map;
+// an exclusive composition scan over long runs yields every decision in parallel.
+// Bit-packed groups fill the gaps between RLE runs; a gap of G groups costs G*bw bytes
+// plus ceil(G/63) run headers ((groups<<1)|1, at most 63 groups per run); the final
+// partial group is zero padded (toBytes).  An RLE run costs varint(len<<1) +
+// ceil(bw/8) value bytes.
+//
+// Pipeline per batch of jobs (all launched back to back, no host sync):
+//   bounds -> [seg max-scan] -> longruns(count) -> [scan] -> longruns(write)
+//   -> phase_reduce -> [seg compose-scan] -> phase_apply(count) -> [scan] -> phase_apply(write)
+//   -> r_sizes -> [seg scans] -> r_finalize -> (write_runs + write_groups) | events
+#include "kpw_device.h"
+#include "kpw_kernels.h"
+#include "kpw_scan.h"
+
+namespace kpw {
+
+__device__ __forceinline__ ValSrc job_src(const RleJob &J)
+{
+    ValSrc s;
+    s.kind = J.src.kind;
+    s.pad = 0;
+    s.ptr = J.src.ptr;
+    s.base = J.src.base;
+    return s;
+}
+
+__device__ __forceinline__ uint32_t run_map(uint32_t a, uint32_t b)
+{
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t phi = 0; phi < 8; phi++) {
+        uint32_t g = a + ((phi - a) & 7u);
+        uint32_t o = (g + 8 <= b) ? (b & 7u) : phi;
+        m |= o << (3 * phi);
+    }
+    return m;
+}
+
+// ------------------------------------------------------------------ long runs
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_bounds(const RleJob *jobs, const uint32_t *ptile_job, int64_t *last_brk)
+{
+    __shared__ int64_t lds[KPW_BLOCK];
+    const uint32_t t = blockIdx.x;
+    const RleJob &J = jobs[ptile_job[t]];
+    const ValSrc src = job_src(J);
+    const int64_t len = J.len;
+    const int64_t p0 = (int64_t)(t - J.tile0) * KPW_TILE_P + threadIdx.x * 8;
+    int64_t last = -1;
+    if (p0 < len) {
+        uint32_t prev = p0 > 0 ? src_get(src, p0 - 1) : 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int64_t i = p0 + k;
+            if (i >= len) break;
+            const uint32_t v = src_get(src, i);
+            if (i == 0 || v != prev) last = i;
+            prev = v;
+        }
+    }
+    last = block_reduce<int64_t, OpMaxI64>(last, lds);
+    if (threadIdx.x == 0) last_brk[t] = last;
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(const RleJob *jobs, const uint32_t *ptile_job, const int64_t *prev_brk,
+                                                            uint32_t *cnt, const uint32_t *off, uint32_t *lr_a, uint32_t *lr_b,
+                                                            int write)
+{
+    __shared__ int64_t ldsi[KPW_BLOCK];
+    __shared__ uint32_t ldsu[KPW_BLOCK];
+    const uint32_t t = blockIdx.x;
+    const RleJob &J = jobs[ptile_job[t]];
+    const ValSrc src = job_src(J);
+    const int64_t len = J.len;
+    const int64_t p0 = (int64_t)(t - J.tile0) * KPW_TILE_P + threadIdx.x * 8;
+    uint32_t brk = 0;
+    int64_t local_last = -1;
+    if (p0 < len) {
+        uint32_t prev = p0 > 0 ? src_get(src, p0 - 1) : 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int64_t i = p0 + k;
+            if (i >= len) break;
+            const uint32_t v = src_get(src, i);
+            if (i == 0 || v != prev) { brk |= 1u << k; local_last = i; }
+            prev = v;
+        }
+    }
+    int64_t tot_i;
+    int64_t incoming = block_scan_excl<int64_t, OpMaxI64>(local_last, ldsi, &tot_i);
+    const int64_t pb = (t == J.tile0) ? -1 : prev_brk[t];
+    if (pb > incoming) incoming = pb;
+
+    // pass: count (and optionally write) long runs ending in this thread's positions
+    uint32_t c = 0;
+    for (int pass = 0; pass < (write ? 2 : 1); pass++) {
+        uint64_t base = 0;
+        if (pass == 1) {
+            uint32_t tot;
+            uint32_t ex = block_scan_excl<uint32_t, OpSum32>(c, ldsu, &tot);
+            base = J.e0 + off[t] + ex;
+        }
+        int64_t prev = incoming;
+        uint32_t k2 = 0;
+        for (int k = 0; k < 8; k++) {
+            const int64_t i = p0 + k;
+            if (i >= len) break;
+            if ((brk >> k) & 1) {
+                if (i > 0 && i - prev >= 8) {
+                    if (pass == 1) { lr_a[base + k2] = (uint32_t)prev; lr_b[base + k2] = (uint32_t)i; }
+                    k2++;
+                }
+                prev = i;
+            }
+            if (i == len - 1 && len - prev >= 8) {  // final run of the stream
+                if (pass == 1) { lr_a[base + k2] = (uint32_t)prev; lr_b[base + k2] = (uint32_t)len; }
+                k2++;
+            }
+        }
+        c = k2;
+    }
+    if (!write) {
+        uint32_t s = block_reduce<uint32_t, OpSum32>(c, ldsu);
+        if (threadIdx.x == 0) cnt[t] = s;
+    }
+}
+
+// ------------------------------------------------------------------ phase scan over long runs
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_phase_reduce(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *lr_a,
+                                                            const uint32_t *lr_b, uint32_t *emap)
+{
+    __shared__ uint32_t lds[KPW_BLOCK];
+    const uint32_t u = blockIdx.x;
+    const RleJob &J = jobs[etile_job[u]];
+    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
+    uint32_t m = OpMapCompose::id();
+    if (k < J.n_long) m = run_map(lr_a[J.e0 + k], lr_b[J.e0 + k]);
+    m = block_reduce<uint32_t, OpMapCompose>(m, lds);
+    if (threadIdx.x == 0) emap[u] = m;
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_phase_apply(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *lr_a,
+                                                           const uint32_t *lr_b, const uint32_t *emap_pre, uint32_t *r_cnt,
+                                                           const uint32_t *r_off, uint32_t *r_g, uint32_t *r_b, int write)
+{
+    __shared__ uint32_t lds[KPW_BLOCK];
+    const uint32_t u = blockIdx.x;
+    const RleJob &J = jobs[etile_job[u]];
+    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
+    const bool valid = k < J.n_long;
+    uint32_t a = 0, b = 0, m = OpMapCompose::id();
+    if (valid) { a = lr_a[J.e0 + k]; b = lr_b[J.e0 + k]; m = run_map(a, b); }
+    uint32_t tot;
+    const uint32_t ex = block_scan_excl<uint32_t, OpMapCompose>(m, lds, &tot);
+    const uint32_t phi = pm_get(ex, pm_get(emap_pre[u], 0));
+    const uint32_t g = a + ((phi - a) & 7u);
+    const uint32_t rle = (valid && g + 8 <= b) ? 1u : 0u;
+    if (!write) {
+        uint32_t s = block_reduce<uint32_t, OpSum32>(rle, lds);
+        if (threadIdx.x == 0) r_cnt[u] = s;
+    } else {
+        uint32_t t2;
+        uint32_t idx = block_scan_excl<uint32_t, OpSum32>(rle, lds, &t2);
+        if (rle) {
+            const uint64_t o = J.e0 + r_off[u] + idx;
+            r_g[o] = g;
+            r_b[o] = b;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ sizes / offsets
+
+__device__ __forceinline__ uint64_t gap_bytes(uint64_t G, uint32_t bw) { return G * bw + (G + 62) / 63; }
+__device__ __forceinline__ uint32_t rle_bytes(uint32_t L, uint32_t bw) { return varint_len32(L << 1) + (bw + 7) / 8; }
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_r_sizes(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
+                                                       const uint32_t *r_b, uint64_t *r_bytes, uint64_t *r_groups,
+                                                       uint64_t *et_bytes, uint64_t *et_groups)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    const uint32_t u = blockIdx.x;
+    const RleJob &J = jobs[etile_job[u]];
+    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
+    uint64_t by = 0, gr = 0;
+    if (k < J.n_rle) {
+        const uint32_t g = r_g[J.e0 + k], b = r_b[J.e0 + k];
+        const uint32_t pe = k ? r_b[J.e0 + k - 1] : 0;
+        gr = (g - pe) >> 3;
+        by = gap_bytes(gr, J.bw) + rle_bytes(b - g, J.bw);
+        r_bytes[J.e0 + k] = by;
+        r_groups[J.e0 + k] = gr;
+    }
+    uint64_t sb = block_reduce<uint64_t, OpSum64>(by, lds);
+    uint64_t sg = block_reduce<uint64_t, OpSum64>(gr, lds);
+    if (threadIdx.x == 0) { et_bytes[u] = sb; et_groups[u] = sg; }
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_r_finalize(RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_b,
+                                                          const uint64_t *r_bytes, const uint64_t *r_groups,
+                                                          const uint64_t *et_boff, const uint64_t *et_goff,
+                                                          const uint64_t *job_btot, const uint64_t *job_gtot,
+                                                          uint64_t *r_boff, uint64_t *r_goff)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    const uint32_t u = blockIdx.x;
+    const uint32_t j = etile_job[u];
+    RleJob &J = jobs[j];
+    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
+    const bool valid = k < J.n_rle;
+    const uint64_t by = valid ? r_bytes[J.e0 + k] : 0;
+    const uint64_t gr = valid ? r_groups[J.e0 + k] : 0;
+    uint64_t t1, t2;
+    const uint64_t eb = block_scan_excl<uint64_t, OpSum64>(by, lds, &t1);
+    const uint64_t eg = block_scan_excl<uint64_t, OpSum64>(gr, lds, &t2);
+    if (valid) {
+        r_boff[J.e0 + k] = et_boff[u] + eb;
+        r_goff[J.e0 + k] = et_goff[u] + eg;
+    }
+    const bool owner = (J.n_rle == 0) ? (u == J.etile0 && threadIdx.x == 0) : (k == (uint64_t)J.n_rle - 1);
+    if (owner) {
+        const uint64_t last_end = J.n_rle ? r_b[J.e0 + J.n_rle - 1] : 0;
+        const uint64_t fg = (J.len > last_end) ? ((uint64_t)J.len - last_end + 7) / 8 : 0;
+        const uint64_t rb = J.n_rle ? job_btot[j] : 0;
+        const uint64_t rg = J.n_rle ? job_gtot[j] : 0;
+        J.final_gap_start = last_end;
+        J.final_gap_off = rb;
+        J.final_gap_groups = fg;
+        J.total_bytes = rb + gap_bytes(fg, J.bw);
+        J.total_groups = rg + fg;
+    }
+}
+
+// ------------------------------------------------------------------ writers
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_write_runs(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
+                                                              const uint32_t *r_b, const uint64_t *r_boff, uint8_t *out)
+{
+    const uint32_t u = blockIdx.x;
+    const RleJob &J = jobs[etile_job[u]];
+    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
+    if (k >= J.n_rle) return;
+    const uint32_t g = r_g[J.e0 + k], b = r_b[J.e0 + k];
+    const uint32_t pe = k ? r_b[J.e0 + k - 1] : 0;
+    const uint64_t G = (g - pe) >> 3;
+    uint8_t *o = out + J.out_off + r_boff[J.e0 + k] + gap_bytes(G, J.bw);
+    uint32_t v = (b - g) << 1;
+    while (v >= 0x80u) { *o++ = (uint8_t)(v | 0x80u); v >>= 7; }
+    *o++ = (uint8_t)v;
+    const uint32_t val = src_get(job_src(J), g);
+    for (uint32_t i = 0; i < (J.bw + 7) / 8; i++) o[i] = (uint8_t)(val >> (8 * i));
+}
+
+struct GroupLoc { uint64_t gs, within, G, gap_off; };
+
+__device__ __forceinline__ GroupLoc locate_group(const RleJob &J, uint64_t q, const uint32_t *r_g, const uint32_t *r_b,
+                                                 const uint64_t *r_boff, const uint64_t *r_goff)
+{
+    GroupLoc L;
+    const uint64_t fstart = J.total_groups - J.final_gap_groups;
+    if (q >= fstart) {
+        L.gs = J.final_gap_start; L.within = q - fstart; L.G = J.final_gap_groups; L.gap_off = J.final_gap_off;
+        return L;
+    }
+    // largest k with r_goff[k] <= q
+    uint64_t lo = 0, hi = J.n_rle;  // invariant: answer in [lo, hi)
+    while (hi - lo > 1) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (r_goff[J.e0 + mid] <= q) lo = mid; else hi = mid;
+    }
+    const uint64_t k = lo;
+    L.gs = k ? r_b[J.e0 + k - 1] : 0;
+    L.within = q - r_goff[J.e0 + k];
+    L.G = (r_g[J.e0 + k] - L.gs) >> 3;
+    L.gap_off = r_boff[J.e0 + k];
+    return L;
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_write_groups(const RleJob *jobs, const uint32_t *ptile_job, const uint32_t *r_g,
+                                                                const uint32_t *r_b, const uint64_t *r_boff, const uint64_t *r_goff,
+                                                                uint8_t *out)
+{
+    const uint32_t t = blockIdx.x;
+    const RleJob &J = jobs[ptile_job[t]];
+    const uint64_t q = (uint64_t)(t - J.tile0) * KPW_BLOCK + threadIdx.x;
+    if (q >= J.total_groups) return;
+    const GroupLoc L = locate_group(J, q, r_g, r_b, r_boff, r_goff);
+    const uint32_t bw = J.bw;
+    const uint64_t m = L.within / 63, wi = L.within % 63;
+    uint8_t *base = out + J.out_off + L.gap_off + m * (63ull * bw + 1);
+    if (wi == 0) {
+        const uint64_t ng = (L.G - 63 * m) < 63 ? (L.G - 63 * m) : 63;
+        base[0] = (uint8_t)((ng << 1) | 1);
+    }
+    const ValSrc src = job_src(J);
+    uint64_t w[4] = {0, 0, 0, 0};
+    const uint64_t p = L.gs + L.within * 8;
+    const uint64_t mask = bw >= 32 ? 0xffffffffull : ((1ull << bw) - 1);
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+        const uint64_t pos = p + v;
+        const uint64_t x = (pos < J.len) ? (src_get(src, pos) & mask) : 0;
+        const uint32_t bp = v * bw;
+        if (bw) {
+            w[bp >> 6] |= x << (bp & 63);
+            if ((bp & 63) + bw > 64) w[(bp >> 6) + 1] |= x >> (64 - (bp & 63));
+        }
+    }
+    uint8_t *o = base + 1 + wi * bw;
+    for (uint32_t i = 0; i < bw; i++) o[i] = (uint8_t)(w[i >> 3] >> (8 * (i & 7)));
+}
+
+// Planning mode: per-position emitted-byte events (event at the position whose write
+// emits the bytes) and a bitmask of RLE-run end positions.
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_ev_runs(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
+                                                           const uint32_t *r_b, uint8_t *ev, uint64_t *gend, uint64_t gend_stride)
+{
+    const uint32_t u = blockIdx.x;
+    const uint32_t j = etile_job[u];
+    const RleJob &J = jobs[j];
+    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
+    if (k >= J.n_rle) return;
+    const uint32_t g = r_g[J.e0 + k], b = r_b[J.e0 + k];
+    if (b >= J.len) return;  // emitted only by toBytes()
+    ev[J.out_off + b] = (uint8_t)rle_bytes(b - g, J.bw);
+    atomicOr((unsigned long long *)&gend[j * gend_stride + (b >> 6)], 1ull << (b & 63));
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_ev_groups(const RleJob *jobs, const uint32_t *ptile_job, const uint32_t *r_g,
+                                                             const uint32_t *r_b, const uint64_t *r_boff, const uint64_t *r_goff,
+                                                             uint8_t *ev)
+{
+    const uint32_t t = blockIdx.x;
+    const RleJob &J = jobs[ptile_job[t]];
+    const uint64_t q = (uint64_t)(t - J.tile0) * KPW_BLOCK + threadIdx.x;
+    if (q >= J.total_groups) return;
+    const GroupLoc L = locate_group(J, q, r_g, r_b, r_boff, r_goff);
+    const uint64_t last = L.gs + L.within * 8 + 7;
+    if (last >= J.len) return;  // partial group: emitted only by toBytes()
+    ev[J.out_off + last] = (uint8_t)(J.bw + ((L.within % 63) == 0 ? 1 : 0));
+}
+
+// ------------------------------------------------------------------ host launchers
+
+// copy per-job totals from a u32 array into RleJob.n_long / n_rle
+__global__ void k_store_counts(RleJob *jobs, int njobs, const uint32_t *tot, int which)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= njobs) return;
+    if (which == 0) jobs[j].n_long = tot[j]; else jobs[j].n_rle = tot[j];
+}
+void launch_rle_store_counts(RleJob *jobs_d, int njobs, const uint32_t *tot, int which, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_store_counts, dim3((njobs + 255) / 256), dim3(256), 0, s, jobs_d, njobs, tot, which);
+}
+
+
+void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc,
+                          hipStream_t s)
+{
+    if (!njobs || !n_ptiles) return;
+    hipLaunchKernelGGL(k_rle_bounds, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.last_brk);
+    seg_tile_scan<int64_t, OpMaxI64>(sc.last_brk, sc.prev_brk, sc.ptile_job, n_ptiles, nullptr, s);
+    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.prev_brk,
+                       sc.lr_cnt, sc.lr_off, sc.lr_a, sc.lr_b, 0);
+    // n_long per job lands in jobs[j].n_long via the job-total pointer trick below
+    seg_tile_scan<uint32_t, OpSum32>(sc.lr_cnt, sc.lr_off, sc.ptile_job, n_ptiles, sc.job_nlong, s);
+    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.prev_brk,
+                       sc.lr_cnt, sc.lr_off, sc.lr_a, sc.lr_b, 1);
+    launch_rle_store_counts(jobs_d, njobs, sc.job_nlong, 0, s);
+    hipLaunchKernelGGL(k_phase_reduce, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b, sc.emap);
+    seg_tile_scan<uint32_t, OpMapCompose>(sc.emap, sc.emap_pre, sc.etile_job, n_etiles, nullptr, s);
+    hipLaunchKernelGGL(k_phase_apply, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b,
+                       sc.emap_pre, sc.r_cnt, sc.r_off, sc.r_g, sc.r_b, 0);
+    seg_tile_scan<uint32_t, OpSum32>(sc.r_cnt, sc.r_off, sc.etile_job, n_etiles, sc.job_nrle, s);
+    hipLaunchKernelGGL(k_phase_apply, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b,
+                       sc.emap_pre, sc.r_cnt, sc.r_off, sc.r_g, sc.r_b, 1);
+    launch_rle_store_counts(jobs_d, njobs, sc.job_nrle, 1, s);
+    hipLaunchKernelGGL(k_r_sizes, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b,
+                       sc.r_bytes, sc.r_groups, sc.et_bytes, sc.et_groups);
+    seg_tile_scan<uint64_t, OpSum64>(sc.et_bytes, sc.et_bytes, sc.etile_job, n_etiles, sc.job_btot, s);
+    seg_tile_scan<uint64_t, OpSum64>(sc.et_groups, sc.et_groups, sc.etile_job, n_etiles, sc.job_gtot, s);
+    hipLaunchKernelGGL(k_r_finalize, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_b, sc.r_bytes,
+                       sc.r_groups, sc.et_bytes, sc.et_groups, sc.job_btot, sc.job_gtot, sc.r_boff, sc.r_goff);
+}
+
+void launch_rle_write(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc, uint8_t *out, hipStream_t s)
+{
+    if (!n_ptiles) return;
+    hipLaunchKernelGGL(k_rle_write_runs, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b, sc.r_boff, out);
+    hipLaunchKernelGGL(k_rle_write_groups, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.r_g, sc.r_b,
+                       sc.r_boff, sc.r_goff, out);
+}
+
+void launch_rle_events(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc, uint8_t *ev,
+                       uint64_t *gend, uint64_t gend_stride, hipStream_t s)
+{
+    if (!n_ptiles) return;
+    hipLaunchKernelGGL(k_rle_ev_runs, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b, ev, gend, gend_stride);
+    hipLaunchKernelGGL(k_rle_ev_groups, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.r_g, sc.r_b,
+                       sc.r_boff, sc.r_goff, ev);
+}
+
+}  // namespace kpw

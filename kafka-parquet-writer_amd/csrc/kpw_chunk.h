@@ -1,0 +1,64 @@
+// kpw_chunk.h — chunk-kernel arguments and launchers (k_chunk.hip, k_snappy.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kpw_kernels.h"
+#include "kpw_scan.h"
+
+namespace kpw {
+
+struct ChunkArgs {
+    ChunkDesc *ch;
+    int32_t nchunks;
+    uint32_t nctiles;
+    const DevCol *cols;
+    const uint8_t *data;
+    const uint32_t *ctile_chunk;   // chunk of each chunk tile
+    const uint32_t *ctile_first;   // per chunk: first tile
+    const uint32_t *ctile_count;   // per chunk: number of tiles
+    uint64_t *tile_raw, *tile_raw_off, *tile_smin, *tile_smax;
+    uint32_t *tile_cnt;
+    uint64_t *tile_sz;
+    uint64_t *ht_key;
+    uint32_t *ht_min, *ht_id;
+    uint32_t *ids;
+    uint64_t *ent_rec, *ent_boff;
+    uint32_t max_dict_bytes;
+};
+
+inline void seg_tile_scan_u32(const uint32_t *in, uint32_t *out, const uint32_t *seg, uint32_t n, hipStream_t s)
+{
+    seg_tile_scan<uint32_t, OpSum32>(in, out, seg, n, nullptr, s);
+}
+inline void seg_tile_scan_u64(const uint64_t *in, uint64_t *out, const uint32_t *seg, uint32_t n, hipStream_t s)
+{
+    seg_tile_scan<uint64_t, OpSum64>(in, out, seg, n, nullptr, s);
+}
+
+void launch_chunk_stats(const ChunkArgs &a, hipStream_t s);
+void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s);
+void launch_layout(const ChunkArgs &a, RleJob *jobs, uint64_t *page_off, uint64_t *page_len, uint64_t *tot, hipStream_t s);
+void launch_chunk_write(const ChunkArgs &a, uint8_t *out, hipStream_t s);
+
+// Snappy (K7)
+struct SnappyArgs {
+    const uint8_t *in;           // uncompressed page bodies
+    const uint64_t *page_off;    // [npages]
+    const uint64_t *page_len;
+    uint32_t npages;
+    uint32_t nfrags;             // total fragments (host computed)
+    const uint32_t *frag_page;   // [nfrags]
+    const uint32_t *frag_idx;    // fragment index within its page
+    uint8_t *frag_out;           // nfrags * SNAPPY_FRAG_CAP
+    uint32_t *frag_len;
+    uint64_t *page_coff;         // exclusive compressed offsets [npages]
+    uint64_t *page_clen;         // compressed lengths
+    uint64_t *frag_coff;         // per fragment output offset
+    uint8_t *out;                // compressed pages
+    uint64_t *tot;               // [0] total compressed bytes
+};
+constexpr uint32_t SNAPPY_FRAG = 65536;
+constexpr uint32_t SNAPPY_FRAG_CAP = 32 + SNAPPY_FRAG + SNAPPY_FRAG / 6 + 16;
+void launch_snappy(const SnappyArgs &a, hipStream_t s);
+
+}  // namespace kpw

@@ -1,0 +1,107 @@
+// kpw_device.h — device helpers shared by the CDNA4 kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define KPW_BLOCK 256           // threads per block for the streaming kernels (4 waves)
+#define KPW_TILE_P 2048         // positions per position-tile (256 threads x 8)
+#define KPW_TILE_E 256          // elements per element-tile (1 per thread)
+
+namespace kpw {
+
+struct OpSum64 { __device__ static uint64_t id() { return 0; } __device__ static uint64_t op(uint64_t a, uint64_t b) { return a + b; } };
+struct OpSum32 { __device__ static uint32_t id() { return 0; } __device__ static uint32_t op(uint32_t a, uint32_t b) { return a + b; } };
+struct OpMaxI64 { __device__ static int64_t id() { return -1; } __device__ static int64_t op(int64_t a, int64_t b) { return a > b ? a : b; } };
+
+// 8-state phase map: out[phi] in 3 bits each (24 bits).  compose(f, g) = "f then g".
+__device__ __forceinline__ uint32_t pm_get(uint32_t m, uint32_t phi) { return (m >> (3 * phi)) & 7u; }
+struct OpMapCompose {
+    __device__ static uint32_t id() { return 0xFAC688u; }  // identity: phi -> phi (0,1,..,7 packed)
+    __device__ static uint32_t op(uint32_t f, uint32_t g) {
+        uint32_t h = 0;
+#pragma unroll
+        for (uint32_t p = 0; p < 8; p++) h |= pm_get(g, pm_get(f, p)) << (3 * p);
+        return h;
+    }
+};
+
+// Inclusive block scan over KPW_BLOCK threads (order preserving, any associative Op).
+template <typename T, typename Op>
+__device__ __forceinline__ T block_scan_incl(T v, T *lds)
+{
+    const int t = threadIdx.x;
+    lds[t] = v;
+    __syncthreads();
+    for (int d = 1; d < KPW_BLOCK; d <<= 1) {
+        T x = (t >= d) ? lds[t - d] : Op::id();
+        __syncthreads();
+        if (t >= d) lds[t] = Op::op(x, lds[t]);
+        __syncthreads();
+    }
+    T r = lds[t];
+    __syncthreads();
+    return r;
+}
+
+// Exclusive scan; *total receives the block aggregate.
+template <typename T, typename Op>
+__device__ __forceinline__ T block_scan_excl(T v, T *lds, T *total)
+{
+    T inc = block_scan_incl<T, Op>(v, lds);
+    lds[threadIdx.x] = inc;
+    __syncthreads();
+    T ex = threadIdx.x ? lds[threadIdx.x - 1] : Op::id();
+    *total = lds[KPW_BLOCK - 1];
+    __syncthreads();
+    return ex;
+}
+
+template <typename T, typename Op>
+__device__ __forceinline__ T block_reduce(T v, T *lds)
+{
+    T tot;
+    (void)block_scan_excl<T, Op>(v, lds, &tot);
+    return tot;
+}
+
+// Value source for the RLE/bit-packing hybrid: either a bitmask (definition levels,
+// bit i of the stream = bit (base+i)) or a u32 array (dictionary ids).
+struct ValSrc {
+    uint32_t kind;   // 0 = bits, 1 = u32
+    uint32_t pad;
+    const void *ptr;
+    uint64_t base;
+};
+__device__ __forceinline__ uint32_t src_get(const ValSrc &s, uint64_t i)
+{
+    if (s.kind == 0) {
+        uint64_t b = s.base + i;
+        return (uint32_t)((((const uint64_t *)s.ptr)[b >> 6] >> (b & 63)) & 1ull);
+    }
+    return ((const uint32_t *)s.ptr)[s.base + i];
+}
+
+__device__ __forceinline__ uint32_t varint_len32(uint32_t v)
+{
+    uint32_t n = 1;
+    while (v >= 0x80u) { v >>= 7; n++; }
+    return n;
+}
+
+// 64-bit hash (splitmix finaliser) for dictionary keys.
+__device__ __forceinline__ uint64_t mix64(uint64_t x)
+{
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return x;
+}
+
+__device__ __forceinline__ uint64_t bits_window(const uint64_t *w, uint64_t bit)
+{
+    // 64 bits starting at absolute bit index `bit` (words are padded by one extra word)
+    uint64_t lo = w[bit >> 6];
+    uint32_t sh = (uint32_t)(bit & 63);
+    if (!sh) return lo;
+    return (lo >> sh) | (w[(bit >> 6) + 1] << (64 - sh));
+}
+
+}  // namespace kpw

@@ -1,0 +1,153 @@
+// kpw_kernels.h — structs shared by host orchestration (engine.cpp) and the HIP kernels,
+// plus the host-side launch wrappers.  Internal to libkpw_gpu.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kpw {
+
+constexpr int MAX_COLS = 256;
+constexpr int FMAP_SIZE = 1024;
+constexpr uint64_t KPW_TILE_P_H = 2048;   // host copy of KPW_TILE_P
+
+// One schema column as the device sees it (decode outputs live in these buffers).
+struct DevCol {
+    int32_t phys;          // kpw_physical_type
+    int32_t proto_type;    // kpw_proto_type
+    int32_t wire_type;     // expected proto wire type
+    int32_t optional;
+    int32_t field_number;
+    int32_t vsize;         // 4 / 8 fixed width, 0 for BYTE_ARRAY and BOOLEAN
+    int32_t dict;          // dictionary-capable (non-boolean and dictionary enabled)
+    int32_t pad;
+    void *vals;            // u32 / u64 [n] (fixed width)
+    uint64_t *soff;        // BYTE_ARRAY: absolute byte offset of the value in the batch data
+    uint32_t *slen;        // BYTE_ARRAY: length
+    uint64_t *pres;        // optional: presence bits [nwords]
+    uint64_t *vbits;       // BOOLEAN: value bits [nwords]
+    uint32_t *pcnt;        // optional: exclusive prefix popcount of pres per word [nwords+1]
+};
+
+struct DecodeArgs {
+    const uint8_t *data;
+    const uint64_t *off;
+    uint64_t n;
+    const DevCol *cols;
+    int32_t ncols;
+    int32_t pad;
+    const int16_t *fmap;   // field number -> column (-1), size FMAP_SIZE
+    uint32_t *raw;         // per record: raw (plain-equivalent) bytes of non-boolean present values
+    unsigned long long *err_min;
+};
+
+// Generic RLE/bit-packing hybrid job (one encoded stream).
+struct ValSrcH {
+    uint32_t kind, pad;
+    const void *ptr;
+    uint64_t base;
+};
+struct RleJob {
+    ValSrcH src;
+    uint32_t len;          // number of values (device may lower it; upper bound used for tiling)
+    uint32_t bw;           // bit width (device may set it)
+    uint32_t tile0, ntiles;        // position tiles [tile0, tile0+ntiles)
+    uint32_t etile0, netiles;      // element tiles (long runs / RLE runs)
+    uint64_t e0;                   // base index into element arrays (capacity netiles*KPW_TILE_E)
+    uint64_t out_off;              // encode: output byte offset; plan: event array base (positions)
+    // results (device written)
+    uint32_t n_long, n_rle;
+    uint64_t total_bytes;
+    uint64_t total_groups;
+    uint64_t final_gap_off;        // byte offset of the final gap
+    uint64_t final_gap_groups;
+    uint64_t final_gap_start;      // position where the final gap starts
+};
+
+struct RleScratch {
+    // position tiles
+    uint32_t *ptile_job;
+    int64_t *first_brk, *last_brk, *prev_brk;
+    uint32_t *lr_cnt, *lr_off;     // long runs per position tile / exclusive offsets
+    // element tiles
+    uint32_t *etile_job;
+    uint32_t *lr_a, *lr_b;         // long runs (a, b)
+    uint32_t *emap, *emap_pre;     // element-tile phase map aggregate / exclusive prefix
+    uint32_t *r_cnt, *r_off;       // RLE runs per element tile / offsets
+    uint32_t *r_g, *r_b;           // RLE runs (g, b)
+    uint64_t *r_bytes, *r_groups;  // per RLE run: gap+run bytes, gap groups (then exclusive offsets)
+    uint64_t *et_bytes, *et_groups;        // element-tile sums -> offsets
+    uint64_t *r_boff, *r_goff;     // per RLE run: byte offset of its gap, groups before its gap
+    // per job
+    uint32_t *job_nlong, *job_nrle;
+    uint64_t *job_btot, *job_gtot;
+};
+
+// Plan / chunk descriptors -------------------------------------------------------------
+
+struct PlanArgs {
+    uint64_t n;                    // records in the batch
+    int32_t final_flush;           // close(): flush the trailing row group
+    int32_t ncols;
+    int64_t next_rg_size;          // nextRowGroupSize
+    const uint64_t *P;             // exclusive prefix of raw bytes [n+1]
+    const DevCol *cols;
+    const uint32_t *opt_cols;      // indices of optional columns
+    int32_t nopt;
+    int32_t nbool;
+    const uint32_t *bool_cols;     // indices of boolean columns
+    const uint32_t *E;             // per optional column k: E[k*(n+1) + r] global emitted dl bytes
+    const uint64_t *gend;          // per optional column k: bitmask of global RLE ends [(n/64+2)]
+    uint64_t gend_stride;          // words per column
+    // outputs
+    int64_t *rg_start;             // [max_rgs]
+    int64_t *rg_end;
+    int32_t max_rgs;
+    int32_t pad;
+    int64_t *out;                  // [0]=n_rgs [1]=open_start [2]=open_buffered [3]=overflow
+};
+
+struct ChunkDesc {
+    int64_t s, e;                  // record range in the batch
+    int32_t col, rg;
+    uint32_t nn;                   // non-null values (device)
+    uint32_t is_dict;              // dictionary attempted (device may clear on fallback)
+    uint64_t raw_bytes;            // plain-equivalent bytes (rawDataByteSize / plain size)
+    uint64_t dict_bytes;           // dictionaryByteSize
+    uint32_t dict_n;               // dictionary entries
+    uint32_t fallback;             // 1 = PLAIN (fallback or not satisfying)
+    uint32_t overflow;             // hash table overflow -> fallback
+    uint32_t bw;                   // id bit width
+    // hash table
+    uint64_t ht_off;               // slot offset
+    uint32_t ht_cap;               // power of two
+    uint32_t pad2;
+    uint64_t ids_off;              // ids array offset (nn entries)
+    uint64_t ent_off;              // dictionary entries array offset (first-occurrence value index)
+    // stats
+    uint64_t smin, smax;           // fixed: canonical bits; binary: value index of min/max
+    uint32_t has_minmax, pad3;
+    uint64_t null_count;
+    // layout
+    uint64_t dl_len;               // RLE def-level bytes (without the 4-byte prefix)
+    uint64_t val_len;              // values part of the data page
+    uint64_t dictpage_len;         // dictionary page bytes (0 if none)
+    uint64_t body_off;             // byte offset of this chunk's uncompressed bodies (dict page, then data page)
+    uint64_t dl_scratch, id_scratch;   // offsets of RLE outputs in the rle output scratch
+    int32_t dl_job, id_job;
+};
+
+// ---------------------------------------------------------------- launch wrappers
+void launch_decode(const DecodeArgs &a, hipStream_t s);
+void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, uint64_t *tile_tmp, hipStream_t s);
+
+void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t n_etiles,
+                          const RleScratch &sc, hipStream_t s);
+void launch_rle_store_counts(RleJob *jobs_d, int njobs, const uint32_t *tot, int which, hipStream_t s);
+void launch_rle_write(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc,
+                      uint8_t *out, hipStream_t s);
+void launch_rle_events(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc,
+                       uint8_t *ev, uint64_t *gend, uint64_t gend_stride, hipStream_t s);
+
+void launch_plan(const PlanArgs &a, hipStream_t s);
+
+}  // namespace kpw

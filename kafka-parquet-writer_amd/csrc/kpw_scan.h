@@ -1,0 +1,21 @@
+// kpw_scan.h — scan launchers (k_scan.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kpw_kernels.h"
+
+namespace kpw {
+
+struct OpSum64;
+struct OpSum32;
+struct OpMaxI64;
+struct OpMapCompose;
+
+uint64_t mj_scan_tmp_words(uint64_t len, uint32_t njobs);
+void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, uint64_t *tmp, hipStream_t s);
+void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, uint64_t *tmp, hipStream_t s);
+
+template <typename T, typename Op>
+void seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, hipStream_t s);
+
+}  // namespace kpw

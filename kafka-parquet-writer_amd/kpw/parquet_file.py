@@ -1,0 +1,145 @@
+"""ParquetFile / ParquetProperties — host-side mirror of the reference seam.
+
+Reference: src/main/java/ir/sahab/kafka/reader/ParquetFile.java
+  ParquetFile(Path filePath, Class<T> protoClass, ParquetProperties properties)   :36-54
+  write(T record) throws IOException                                            :59-62
+  close() throws IOException                                                    :65-68
+  getCreationDate()                                                             :70-72
+  getDataSize()                                                                 :77-79
+  getNumWrittenRecords()                                                        :81-83
+  ParquetProperties(hadoopConf, blockSize, compressionCodecName, pageSize,
+                    enableDictionary)                                           :105-122
+
+Differences forced by the GPU boundary: write() takes the serialized record value
+(record.value(), KafkaProtoParquetWriter.java:270) instead of a parsed T — parsing is
+kernel K1 — and write_batch() accepts many values at once.  An invalid value raises
+InvalidProtoError, the reference's IllegalStateException path (KPW:271-276); records
+before it stay written.  Instances are not thread-safe (ParquetFile.java:19-20).
+"""
+import ctypes
+import datetime
+
+import numpy as np
+
+from ._lib import (KpwError, InvalidProtoError, load_library, make_schema, _PropsC, UNCOMPRESSED, SNAPPY,
+                   KPW_ERR_INVALID_PROTO)
+
+MiB = 1024 * 1024
+
+
+class ParquetProperties:
+    """ParquetFile.ParquetProperties (ParquetFile.java:105-122).  hadoop_conf is accepted
+    for signature parity and ignored (the output stream is a local path or memory)."""
+
+    def __init__(self, hadoop_conf=None, block_size=128 * MiB, compression_codec_name=UNCOMPRESSED,
+                 page_size=128 * MiB, enable_dictionary=True):
+        self.hadoop_conf = hadoop_conf
+        self.block_size = int(block_size)
+        self.compression_codec_name = int(compression_codec_name)
+        self.page_size = int(page_size)
+        self.enable_dictionary = bool(enable_dictionary)
+
+    def to_c(self):
+        # ParquetFile.java:48-50 only ever calls enableDictionaryEncoding(); parquet-mr 1.10.1's
+        # builder defaults dictionary encoding to ON, so the reference writes dictionaries
+        # even when enableDictionary is false.  Reproduced here on purpose.
+        effective_dictionary = 1
+        return _PropsC(self.block_size, self.page_size, MiB, effective_dictionary, self.compression_codec_name, 1, 0,
+                       0, 8 * MiB)
+
+
+def _as_batch(values):
+    if isinstance(values, tuple) and len(values) == 2:
+        data, offsets = values
+        return np.ascontiguousarray(data, dtype=np.uint8), np.ascontiguousarray(offsets, dtype=np.uint64)
+    values = list(values)
+    offsets = np.zeros(len(values) + 1, dtype=np.uint64)
+    if values:
+        np.cumsum([len(v) for v in values], out=offsets[1:])
+    data = np.frombuffer(b"".join(values), dtype=np.uint8) if values else np.zeros(1, np.uint8)
+    return np.ascontiguousarray(data), offsets
+
+
+class ParquetFile:
+    """A Parquet file of proto messages, encoded on an MI355X (HIP C-ABI)."""
+
+    def __init__(self, file_path, proto_schema, properties=None, device=0):
+        self._L = load_library()
+        self.file_path = file_path
+        self.proto_schema = proto_schema
+        self._props = properties or ParquetProperties()
+        self._schema_c, self._keep = make_schema(proto_schema)
+        pc = self._props.to_c()
+        st = ctypes.c_int(0)
+        path = file_path.encode() if isinstance(file_path, str) else file_path
+        self._h = self._L.kpw_writer_open(device, ctypes.byref(self._schema_c), ctypes.byref(pc), path, ctypes.byref(st))
+        if not self._h:
+            raise KpwError(st.value, "ParquetFile open")
+        self._creation = datetime.datetime.now()
+
+    def _check(self, st, what):
+        if st == 0:
+            return
+        msg = (self._L.kpw_writer_last_error(self._h) or b"").decode(errors="replace")
+        if st == KPW_ERR_INVALID_PROTO:
+            raise InvalidProtoError(st, msg, self._L.kpw_writer_failed_record(self._h))
+        raise KpwError(st, "%s: %s" % (what, msg))
+
+    def write(self, record_value: bytes):
+        """ParquetFile.write(T) for one serialized record value."""
+        self.write_batch([record_value])
+
+    def write_batch(self, values):
+        """values: list of bytes, or (data uint8[], offsets uint64[n+1])."""
+        data, offsets = _as_batch(values)
+        n = len(offsets) - 1
+        self._check(self._L.kpw_writer_write(self._h, data.ctypes.data, offsets.ctypes.data, n), "write")
+
+    def write_until_full(self, values, max_file_size):
+        data, offsets = _as_batch(values)
+        n = len(offsets) - 1
+        na = ctypes.c_uint64(0)
+        full = ctypes.c_int(0)
+        self._check(self._L.kpw_writer_write_until_full(self._h, data.ctypes.data, offsets.ctypes.data, n,
+                                                        max_file_size, ctypes.byref(na), ctypes.byref(full)),
+                    "write_until_full")
+        return na.value, bool(full.value)
+
+    def get_data_size(self):
+        v = self._L.kpw_writer_data_size(self._h)
+        if v < 0:
+            self._check(-5, "getDataSize")
+        return v
+
+    def get_num_written_records(self):
+        return self._L.kpw_writer_num_records(self._h)
+
+    def get_creation_date(self):
+        return self._creation
+
+    def close(self):
+        self._check(self._L.kpw_writer_close(self._h), "close")
+
+    def file_bytes(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        self._check(self._L.kpw_writer_file_bytes(self._h, ctypes.byref(p), ctypes.byref(n)), "file_bytes")
+        return ctypes.string_at(p.value, n.value)
+
+    # AutoCloseable
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.kpw_writer_free(h)
+            self._h = None
+
+    # reference-style camelCase aliases
+    getDataSize = get_data_size
+    getNumWrittenRecords = get_num_written_records
+    getCreationDate = get_creation_date

@@ -1,0 +1,123 @@
+"""Helpers for the GPU parity tests: run the HIP encoder on device-resident batches and
+compare, page by page, with the CPU oracle's file for the same records and properties."""
+import io
+
+import numpy as np
+
+import oracle
+import pqwalk
+
+MiB = 1024 * 1024
+
+
+def to_device(data, offsets):
+    import torch
+    d = torch.from_numpy(np.ascontiguousarray(data) if len(data) else np.zeros(1, np.uint8)).to("cuda")
+    o = torch.from_numpy(offsets.astype(np.int64)).to("cuda")
+    return d, o
+
+
+def gpu_encoder_pages(schema, data, offsets, codec=0, block_size=128 * MiB, page_size=128 * MiB, dictionary=True):
+    """Returns (row_groups, [(rg, col, [page dicts with 'body'])]) from the HIP encoder."""
+    import kpw
+    import torch
+    enc = kpw.Encoder(kpw.Schema(schema.message_name, schema.columns, schema.proto_class), codec=codec,
+                      block_size=block_size, page_size=page_size, enable_dictionary=dictionary)
+    d, o = to_device(data, offsets)
+    torch.cuda.synchronize()
+    info = enc.encode(d.data_ptr(), o.data_ptr(), len(offsets) - 1, final=True)
+    blob = enc.pages_bytes()
+    pages = enc.pages()
+    chunks = enc.chunks()
+    rgs = enc.row_groups()
+    out = []
+    ncols = len(schema.columns)
+    for ci, ch in enumerate(chunks):
+        pl = []
+        for p in pages[ch["first_page"]:ch["first_page"] + ch["num_pages"]]:
+            q = dict(p)
+            q["body"] = blob[p["offset"]:p["offset"] + p["compressed_size"]]
+            pl.append(q)
+        out.append((ci // ncols, ch["column"], pl))
+    return rgs, out, info, enc
+
+
+def oracle_pages(fb):
+    """Group oracle file pages by (rg, col)."""
+    res = {}
+    for pg in pqwalk.pages(fb):
+        res.setdefault((pg["rg"], pg["col"]), []).append(pg)
+    return res
+
+
+def oracle_row_groups(fb):
+    fm = pqwalk.footer(fb)
+    out, start = [], 0
+    for rg in fm[4]:
+        out.append((start, rg[3]))
+        start += rg[3]
+    return out
+
+
+def compare_pages(schema, data, offsets, **kw):
+    """Returns a list of human-readable mismatches (empty = byte-identical pages)."""
+    codec = kw.get("codec", 0)
+    props = oracle.make_props(block_size=kw.get("block_size", 128 * MiB), page_size=kw.get("page_size", 128 * MiB),
+                              codec=codec, enable_dictionary=kw.get("dictionary", True))
+    fb = oracle.encode_file(schema, data, offsets, props)
+    rgs, gpages, info, enc = gpu_encoder_pages(schema, data, offsets, **kw)
+    errs = []
+    orgs = oracle_row_groups(fb)
+    if [tuple(r) for r in rgs] != [tuple(r) for r in orgs]:
+        errs.append("row groups differ: gpu %r oracle %r" % (rgs[:8], orgs[:8]))
+        return errs
+    op = oracle_pages(fb)
+    for rg, col, pl in gpages:
+        ol = op.get((rg, col), [])
+        name = schema.columns[col][0]
+        if len(ol) != len(pl):
+            errs.append("rg %d col %s: page count gpu %d oracle %d" % (rg, name, len(pl), len(ol)))
+            continue
+        for k, (g, o) in enumerate(zip(pl, ol)):
+            h = o["header"]
+            ptype = h[1]
+            if g["page_type"] != ptype:
+                errs.append("rg %d col %s page %d: type gpu %d oracle %d" % (rg, name, k, g["page_type"], ptype))
+                continue
+            if g["uncompressed_size"] != h[2] or g["compressed_size"] != h[3]:
+                errs.append("rg %d col %s page %d: sizes gpu (%d,%d) oracle (%d,%d)" % (
+                    rg, name, k, g["uncompressed_size"], g["compressed_size"], h[2], h[3]))
+            if ptype == 0:
+                dh = h[5]
+                if (g["num_values"], g["encoding"], g["dl_encoding"]) != (dh[1], dh[2], dh[3]):
+                    errs.append("rg %d col %s page %d: header gpu %r oracle %r" % (
+                        rg, name, k, (g["num_values"], g["encoding"], g["dl_encoding"]), (dh[1], dh[2], dh[3])))
+                st = dh.get(5, {})
+                if st.get(3, None) is not None and st.get(3) != g["null_count"]:
+                    errs.append("rg %d col %s: null_count gpu %d oracle %d" % (rg, name, g["null_count"], st.get(3)))
+                if 6 in st and (st[6] != g["min"] or st[5] != g["max"]):
+                    errs.append("rg %d col %s: min/max gpu %r/%r oracle %r/%r" % (rg, name, g["min"][:20], g["max"][:20],
+                                                                                st[6][:20], st[5][:20]))
+            else:
+                if g["num_values"] != h[7][1]:
+                    errs.append("rg %d col %s dict entries gpu %d oracle %d" % (rg, name, g["num_values"], h[7][1]))
+            if g["body"] != o["body"]:
+                a, b = g["body"], o["body"]
+                i = next((j for j in range(min(len(a), len(b))) if a[j] != b[j]), min(len(a), len(b)))
+                errs.append("rg %d col %s page %d type %d: body differs at byte %d (len gpu %d oracle %d): gpu %s oracle %s" % (
+                    rg, name, k, ptype, i, len(a), len(b), a[max(0, i - 8):i + 16].hex(), b[max(0, i - 8):i + 16].hex()))
+    return errs
+
+
+def gpu_file(schema, data, offsets, props=None, batches=1):
+    """Full file through the ParquetFile drop-in (kpw_writer_*), in memory."""
+    import kpw
+    pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class), props)
+    n = len(offsets) - 1
+    step = max(1, (n + batches - 1) // batches)
+    for i in range(0, n, step):
+        j = min(n, i + step)
+        sub = offsets[i:j + 1] - offsets[i]
+        pf.write_batch((data[int(offsets[i]):int(offsets[j])], sub))
+    pf.close()
+    return pf.file_bytes()
