@@ -1,0 +1,190 @@
+#!/usr/bin/env python
+"""bench.py — Parquet encode throughput on MI355X (BASELINE.json metric, config C2).
+
+Workload: Rec8 records (proto2, ~62 B), 100 M per GPU, dictionary on,
+SNAPPY, 128 MiB row groups, 128 MiB pages (reference default).  One "step" = one pass of
+the flush path over the whole device-resident batch: K1 decode -> row-group planner ->
+K2 dictionary / K3 RLE / K4 PLAIN / K6 stats -> K7 Snappy, every page of every row group
+produced in HBM (kpw_encoder_encode, final=1).  Record bytes are resident in HBM before
+timing starts; page bytes stay in HBM (the PCIe-inclusive rate is reported separately).
+
+value = sum over ranks of serialized record-value bytes / max-over-ranks wall time (GB/s,
+the reference's `written.bytes` definition, KafkaProtoParquetWriter.java:115,280).
+Multi-GPU: one process per GPU, each encoding its own partition (weak scaling, no
+data-path collective).  The barrier/max use torch.distributed (RCCL).
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in ("kafka-parquet-writer_amd", "synth"):
+    sys.path.insert(0, os.path.join(ROOT, p))
+
+import numpy as np  # noqa: E402
+
+MiB = 1024 * 1024
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+
+
+def log(msg):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(kind, seed, sample_records, threads):
+    """The CPU oracle (a C restatement of parquet-mr 1.10.1's write path, kind "port") on a
+    bounded sample of the same workload: `threads` independent files (one per thread, like
+    the reference's threadCount writers), each encoding sample_records/threads records."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import synth
+    per = max(1, sample_records // threads)
+    chunks = [synth.generate(kind, seed, per, start=i * per) for i in range(threads)]
+    props = oracle.make_props(codec=oracle.SNAPPY)
+    total_bytes = sum(int(o[-1]) for _, o in chunks)
+    errs = []
+
+    def work(i):
+        try:
+            d, o = chunks[i]
+            oracle.encode_file(synth.REC8, d, o, props)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    return dict(value=round(total_bytes / dt / 1e9, 4), unit="GB/s", cores=threads, kind="port",
+                sample="%d Rec8 records (%d per thread, %.1f MB), SNAPPY, 128 MiB row groups, %d threads, %.2f s"
+                       % (per * threads, per, total_bytes / 1e6, threads, dt),
+                records_per_s=round(per * threads / dt, 1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--records", type=int, default=100_000_000, help="records per GPU (C2: 100 M)")
+    ap.add_argument("--codec", type=int, default=1, help="0 UNCOMPRESSED, 1 SNAPPY (C2)")
+    ap.add_argument("--cpu-sample", type=int, default=8_000_000, help="records for the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+
+    import kpw
+    import synth
+    seed = 0xC0FFEE02 if world == 1 else 0xC0FFEE05 + rank
+    t0 = time.perf_counter()
+    data, offs = synth.generate(synth.KIND_REC8, seed, args.records)
+    log("generated %d records (%.2f GB) in %.1fs" % (args.records, len(data) / 1e9, time.perf_counter() - t0))
+    d_data = torch.from_numpy(data).to("cuda")
+    d_off = torch.from_numpy(offs.view(np.int64)).to("cuda")
+    nbytes = int(offs[-1])
+    n = args.records
+    del data
+    enc = kpw.Encoder(kpw.Schema(synth.REC8.message_name, synth.REC8.columns, synth.REC8.proto_class),
+                      device=local_rank, codec=args.codec, block_size=128 * MiB, page_size=128 * MiB)
+    torch.cuda.synchronize()
+
+    def step():
+        return enc.encode(d_data.data_ptr(), d_off.data_ptr(), n, final=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stage_acc = None
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        info = step()
+        st = np.array(enc.stage_times(), dtype=np.float64)
+        stage_acc = st if stage_acc is None else stage_acc + st
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # per-step page statistics (for algorithmic bytes of the compression kernel)
+    pages = enc.pages()
+    unc = sum(p["uncompressed_size"] for p in pages)
+    comp = sum(p["compressed_size"] for p in pages)
+    stages = (stage_acc / args.steps).tolist()
+    nrg = info.num_row_groups
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * nbytes * args.steps / elapsed / 1e9
+    rec_s = world * n * args.steps / elapsed
+    # K1 decode: algorithmic bytes = record bytes + offsets in; columnar values out
+    # (ts 8, user_id 4, status 4, price 8, score 8, key16 8+4, region 8+4 per record,
+    #  presence/boolean bits n/8 per optional column + flag bits, raw sizes 4 per record)
+    k1_bytes = nbytes + 8 * (n + 1) + n * (8 + 4 + 4 + 8 + 8 + 12 + 12 + 4) + (5 * n) // 8
+    names = ["decode", "plan", "stats+dict", "rle", "layout+plain+write", "compress", "metadata", "total",
+             "k_decode", "k_snappy_frag"]
+    stage = dict(zip(names, [round(x, 3) for x in stages]))
+    k_dec_ms = stages[8] if len(stages) > 8 else stages[0]
+    k_sn_ms = stages[9] if len(stages) > 9 else stages[5]
+    kern = {"k_decode": (k1_bytes, k_dec_ms), "k_snappy_frag": (unc + comp, k_sn_ms)}
+    dom = max(kern, key=lambda k: kern[k][1])
+    ab, ams = kern[dom]
+    achieved = ab / (ams * 1e-3) / 1e9 if ams > 0 else 0.0
+    roof = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBPS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBPS, 5), traffic=None, algorithmic_bytes_per_launch=int(ab),
+                avg_launch_ms=round(ams, 4))
+    cpu = None
+    if not args.no_cpu_baseline and world >= 1:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 8)
+        cpu = cpu_baseline(synth.KIND_REC8, seed, args.cpu_sample, threads)
+    out = {
+        "metric": "Parquet encode GB/s + records/sec (whole node) at 1/2/4/8 MI355X vs CPU writer",
+        "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic (counter-based proto2 Rec8 generator; no broker, in-memory record source)",
+        "config": {"workload": "C2: Rec8 (8 cols), %d records/GPU, PLAIN_DICTIONARY + SNAPPY, 128 MiB row groups, "
+                               "128 MiB pages, parquet-mr 1.10.1 v1 semantics" % n,
+                   "records_per_gpu": n, "bytes_per_gpu": nbytes, "row_groups_per_gpu": nrg,
+                   "codec": "SNAPPY" if args.codec else "UNCOMPRESSED", "parallelism": "partition-sharded x%d" % world},
+        "records_per_s": round(rec_s, 1),
+        "stage_ms": stage,
+        "pages": {"uncompressed_bytes": int(unc), "compressed_bytes": int(comp), "count": len(pages)},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -113,7 +113,7 @@ extern "C" int kpw_encoder_copy_pages(kpw_encoder *e, uint64_t off, uint64_t len
 extern "C" int kpw_encoder_stage_times(const kpw_encoder *e, float *ms, int cap)
 {
     if (!e || !ms) return 0;
-    int n = cap < 8 ? cap : 8;
+    int n = cap < 10 ? cap : 10;
     for (int i = 0; i < n; i++) ms[i] = e->eng.stage_ms[i];
     return n;
 }

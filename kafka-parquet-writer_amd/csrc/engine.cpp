@@ -43,6 +43,7 @@ DevBuf::~DevBuf()
 Engine::~Engine()
 {
     for (auto &e : ev_) if (e) (void)hipEventDestroy(e);
+    for (auto &e : kev_) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -107,6 +108,7 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     CK(hipSetDevice(dev));
     CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto &e : ev_) CK(hipEventCreate(&e));
+    for (auto &e : kev_) CK(hipEventCreate(&e));
     const size_t nc = cols.size();
     col_vals.resize(nc); col_soff.resize(nc); col_slen.resize(nc); col_pres.resize(nc); col_vbits.resize(nc); col_pcnt.resize(nc);
     std::vector<int16_t> fmap(FMAP_SIZE, -1);
@@ -207,7 +209,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     const uint32_t nopt = (uint32_t)opt_idx_.size();
     CK(hipEventRecord(ev_[0], s));
     if (n == 0) {
-        for (int i = 0; i < 8; i++) stage_ms[i] = 0;
+        for (int i = 0; i < 10; i++) stage_ms[i] = 0;
         return KPW_OK;
     }
     if (n >= 0xFFFFFFF0ull) return fail(KPW_ERR_LIMIT, "batch too large (>= 2^32 records)");
@@ -244,7 +246,9 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     DecodeArgs da;
     da.data = d_data; da.off = d_off; da.n = n; da.cols = d_cols.as<DevCol>(); da.ncols = nc; da.pad = 0;
     da.fmap = d_fmap.as<int16_t>(); da.raw = d_raw.as<uint32_t>(); da.err_min = d_err.as<unsigned long long>();
+    CK(hipEventRecord(kev_[0], s));
     launch_decode(da, s);
+    CK(hipEventRecord(kev_[1], s));
     CK(hipGetLastError());
     CK(hipEventRecord(ev_[1], s));
     uint64_t err_idx = ~0ull;
@@ -343,7 +347,9 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             C.ent_off = ids_off;
             ids_off += len;
             if (C.is_dict) {
-                C.ht_cap = (uint32_t)std::min<uint64_t>(next_pow2(std::max<uint64_t>(16, 2 * len)), 1u << 19);
+                // >= 4x the most entries a dictionary can hold before its 1 MiB fallback
+                // (262145 four-byte entries), so probe chains stay short until fallback
+                C.ht_cap = (uint32_t)std::min<uint64_t>(next_pow2(std::max<uint64_t>(16, 2 * len)), 1u << 20);
                 C.ht_off = ht_off;
                 ht_off += C.ht_cap + 1;
             }
@@ -454,7 +460,9 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         sa.frag_out = d_frag_out.as<uint8_t>(); sa.frag_len = d_frag_len.as<uint32_t>();
         sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
         sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
+        CK(hipEventRecord(kev_[2], s));
         launch_snappy(sa, s);
+        CK(hipEventRecord(kev_[3], s));
         launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), s);
         CK(hipGetLastError());
         pcoff.resize(2 * nch);
@@ -508,6 +516,9 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     CK(hipEventSynchronize(ev_[7]));
     for (int i = 0; i < 7; i++) CK(hipEventElapsedTime(&stage_ms[i], ev_[i], ev_[i + 1]));
     CK(hipEventElapsedTime(&stage_ms[7], ev_[0], ev_[7]));
+    CK(hipEventElapsedTime(&stage_ms[8], kev_[0], kev_[1]));
+    stage_ms[9] = 0;
+    if (props.codec == KPW_SNAPPY) CK(hipEventElapsedTime(&stage_ms[9], kev_[2], kev_[3]));
 
     // ---------------------------------------------------------------- results
     for (int ci = 0; ci < nch; ci++) {

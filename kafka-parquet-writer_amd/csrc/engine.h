@@ -68,7 +68,7 @@ public:
     std::string message_name, proto_class;
     int device = 0;
     hipStream_t stream = nullptr;
-    float stage_ms[8] = {0};
+    float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 k_snappy_frag
 
 private:
     int fail(int code, const std::string &msg);
@@ -90,6 +90,7 @@ private:
     DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
     DevBuf d_smeta, d_sblob;
     hipEvent_t ev_[9] = {};
+    hipEvent_t kev_[4] = {};
     std::vector<uint32_t> opt_idx_, bool_idx_;
     int run_rle(std::vector<RleJob> &jobs, uint32_t &nptiles, uint32_t &netiles, RleScratch &sc);
     uint8_t *pages_dev_ = nullptr;

@@ -193,6 +193,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
         const uint64_t r = p0 + k;
         if (r >= (uint64_t)C.e) break;
         if (!present_at(col, r)) continue;
+        // the chunk's fallback is already decided (dictionary bytes > dictPageSize): every
+        // further insert is wasted work on a filling table
+        if (__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
         uint64_t key, h;
         uint32_t esize;
         if (is_bin) {
@@ -239,12 +242,17 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
                 if (is_bin) eq = bin_cmp(data, col.soff[cur], col.slen[cur], col.soff[r], col.slen[r]) == 0;
                 else eq = cur == key;
                 if (eq) {
-                    atomicMin(&mins[i], (uint32_t)rank);
+                    // a (possibly stale) recorded rank can only be >= the true minimum, so
+                    // skipping when it is already <= rank is safe; avoids serialising
+                    // low-cardinality columns on a handful of hot atomics
+                    if (__hip_atomic_load(&mins[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)rank)
+                        atomicMin(&mins[i], (uint32_t)rank);
                     slot = i;
                     ok = true;
                     break;
                 }
                 i = (i + 1) & (cap - 1);
+                if ((probe & 15) == 15 && __hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
             }
         }
         if (!ok) {

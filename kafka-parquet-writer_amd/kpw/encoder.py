@@ -34,8 +34,8 @@ class Encoder:
         return self.info
 
     def stage_times(self):
-        arr = (ctypes.c_float * 8)()
-        n = self._L.kpw_encoder_stage_times(self._h, arr, 8)
+        arr = (ctypes.c_float * 10)()
+        n = self._L.kpw_encoder_stage_times(self._h, arr, 10)
         return list(arr[:n])
 
     def pages_bytes(self):

@@ -108,7 +108,7 @@ class ParquetFile:
     def get_data_size(self):
         v = self._L.kpw_writer_data_size(self._h)
         if v < 0:
-            self._check(-5, "getDataSize")
+            self._check(KPW_ERR_INVALID_PROTO if self._L.kpw_writer_failed_record(self._h) >= 0 else -5, "getDataSize")
         return v
 
     def get_num_written_records(self):
