@@ -110,7 +110,7 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     for (auto &e : ev_) CK(hipEventCreate(&e));
     for (auto &e : kev_) CK(hipEventCreate(&e));
     const size_t nc = cols.size();
-    col_vals.resize(nc); col_soff.resize(nc); col_slen.resize(nc); col_pres.resize(nc); col_vbits.resize(nc); col_pcnt.resize(nc);
+    col_vals.resize(nc); col_shash.resize(nc); col_soff.resize(nc); col_slen.resize(nc); col_pres.resize(nc); col_vbits.resize(nc); col_pcnt.resize(nc);
     std::vector<int16_t> fmap(FMAP_SIZE, -1);
     for (size_t c = 0; c < nc; c++)
         if (cols[c].field_number < FMAP_SIZE) fmap[cols[c].field_number] = (int16_t)c;
@@ -227,6 +227,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         if (ci.phys == KPW_BYTE_ARRAY) {
             ENS(col_soff[c], n * 8); ENS(col_slen[c], n * 4);
             d.soff = col_soff[c].as<uint64_t>(); d.slen = col_slen[c].as<uint32_t>();
+            if (ci.dict) { ENS(col_shash[c], n * 8); d.shash = col_shash[c].as<uint64_t>(); }
         }
         if (ci.optional) {
             ENS(col_pres[c], nwords * 8); ENS(col_pcnt[c], (nwords + 1) * 4);
@@ -386,14 +387,10 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_page_off, 2 * nch * 8); ENS(d_page_len, 2 * nch * 8); ENS(d_tot, 64);
     for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
-    CK(hipMemcpyAsync(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
     CK(hipMemcpyAsync(d_ctile_chunk.p, ctj.data(), nct * 4, hipMemcpyHostToDevice, s));
     CK(hipMemcpyAsync(d_ctile_first.p, cfirst.data(), nch * 4, hipMemcpyHostToDevice, s));
     CK(hipMemcpyAsync(d_ctile_count.p, ccount.data(), nch * 4, hipMemcpyHostToDevice, s));
-    if (ht_off) {
-        CK(hipMemsetAsync(d_ht_key.p, 0xFF, ht_off * 8, s));
-        CK(hipMemsetAsync(d_ht_min.p, 0xFF, ht_off * 4, s));
-    }
+    ENS(d_collision, 64);
     ChunkArgs a{};
     a.ch = d_chunks.as<ChunkDesc>(); a.nchunks = nch; a.nctiles = nct; a.cols = d_cols.as<DevCol>(); a.data = d_data;
     a.ctile_chunk = d_ctile_chunk.as<uint32_t>(); a.ctile_first = d_ctile_first.as<uint32_t>();
@@ -403,28 +400,44 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     a.ht_key = d_ht_key.as<uint64_t>(); a.ht_min = d_ht_min.as<uint32_t>(); a.ht_id = d_ht_id.as<uint32_t>();
     a.ids = d_ids.as<uint32_t>(); a.ent_rec = d_ent_rec.as<uint64_t>(); a.ent_boff = d_ent_boff.as<uint64_t>();
     a.max_dict_bytes = (uint32_t)props.dictionary_page_size;
-
-    // ---------------------------------------------------------------- K6 + K2
-    launch_chunk_stats(a, s);
-    CK(hipGetLastError());
+    a.data_end = d_off + n;
+    a.collision = d_collision.as<uint32_t>();
     uint32_t enpt = 0, enet = 0;
     RleScratch esc{};
-    if (!ej.empty()) {
-        int st = run_rle(ej, enpt, enet, esc);
-        if (st) return st;
-    }
-    launch_dict(a, d_jobs.as<RleJob>(), s);
-    CK(hipGetLastError());
-    CK(hipEventRecord(ev_[3], s));
-    // ---------------------------------------------------------------- K3 (dl + ids)
-    if (!ej.empty()) launch_rle_structure(d_jobs.as<RleJob>(), (int)ej.size(), enpt, enet, esc, s);
-    CK(hipGetLastError());
-    CK(hipEventRecord(ev_[4], s));
-    // ---------------------------------------------------------------- layout + K4 + page bodies
-    launch_layout(a, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), s);
     uint64_t body_tot = 0;
-    CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
+    // BYTE_ARRAY dictionaries are keyed by a 64-bit hash and verified byte-for-byte; a
+    // verified collision re-runs the chunk phase with byte comparisons (exact_strings).
+    for (int attempt = 0; attempt < 2; attempt++) {
+        a.exact_strings = attempt;
+        CK(hipMemcpyAsync(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
+        CK(hipMemsetAsync(d_collision.p, 0, 4, s));
+        if (ht_off) {
+            CK(hipMemsetAsync(d_ht_key.p, 0xFF, ht_off * 8, s));
+            CK(hipMemsetAsync(d_ht_min.p, 0xFF, ht_off * 4, s));
+        }
+        // ------------------------------------------------------------ K6 + K2
+        launch_chunk_stats(a, s);
+        CK(hipGetLastError());
+        if (!ej.empty()) {
+            int st = run_rle(ej, enpt, enet, esc);
+            if (st) return st;
+        }
+        launch_dict(a, d_jobs.as<RleJob>(), s);
+        CK(hipGetLastError());
+        CK(hipEventRecord(ev_[3], s));
+        // ------------------------------------------------------------ K3 (dl + ids)
+        if (!ej.empty()) launch_rle_structure(d_jobs.as<RleJob>(), (int)ej.size(), enpt, enet, esc, s);
+        CK(hipGetLastError());
+        CK(hipEventRecord(ev_[4], s));
+        // ------------------------------------------------------------ layout
+        launch_layout(a, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), s);
+        uint32_t coll = 0;
+        CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(&coll, d_collision.p, 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        if (!coll) break;
+        if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
+    }
     ENS(d_body, body_tot + 16);
     CK(hipMemsetAsync(d_body.p, 0, body_tot + 16, s));
     launch_chunk_write(a, d_body.as<uint8_t>(), s);

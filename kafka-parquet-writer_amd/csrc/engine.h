@@ -74,7 +74,7 @@ private:
     int fail(int code, const std::string &msg);
     std::string err_;
     // decode buffers
-    std::vector<DevBuf> col_vals, col_soff, col_slen, col_pres, col_vbits, col_pcnt;
+    std::vector<DevBuf> col_vals, col_shash, col_soff, col_slen, col_pres, col_vbits, col_pcnt;
     DevBuf d_cols, d_fmap, d_raw, d_P, d_err, d_scan_tmp, d_opt, d_bool;
     // planning
     DevBuf d_ev, d_E, d_gend, d_rg_start, d_rg_end, d_plan_out;
@@ -88,7 +88,7 @@ private:
         d_body;
     // snappy
     DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
-    DevBuf d_smeta, d_sblob;
+    DevBuf d_smeta, d_sblob, d_collision;
     hipEvent_t ev_[9] = {};
     hipEvent_t kev_[4] = {};
     std::vector<uint32_t> opt_idx_, bool_idx_;

@@ -52,22 +52,14 @@ __device__ __forceinline__ uint64_t order_key(int phys, uint64_t v)
     }
 }
 
-__device__ __forceinline__ int bin_cmp(const uint8_t *data, uint64_t oa, uint32_t la, uint64_t ob, uint32_t lb)
-{
-    const uint32_t m = la < lb ? la : lb;
-    for (uint32_t i = 0; i < m; i++) {
-        const uint8_t x = data[oa + i], y = data[ob + i];
-        if (x != y) return x < y ? -1 : 1;
-    }
-    return la == lb ? 0 : (la < lb ? -1 : 1);
-}
-
 // ------------------------------------------------------------------ K6 stats + sizes
 
 __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
                                                            const uint32_t *ctile_chunk, const uint32_t *ctile_first,
-                                                           uint64_t *tile_raw, uint64_t *tile_smin, uint64_t *tile_smax)
+                                                           uint64_t *tile_raw, uint64_t *tile_smin, uint64_t *tile_smax,
+                                                           const uint64_t *data_end_p)
 {
+    const uint64_t data_end = *data_end_p;
     __shared__ uint64_t lds[KPW_BLOCK];
     __shared__ uint64_t li[KPW_BLOCK], la[KPW_BLOCK];
     const uint32_t t = blockIdx.x;
@@ -86,8 +78,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
         if (col.phys == 6) {
             const uint32_t l = col.slen[r];
             raw += 4 + l;
-            if (imin == ~0ull || bin_cmp(data, col.soff[r], l, col.soff[imin], col.slen[imin]) < 0) imin = r;
-            if (imax == ~0ull || bin_cmp(data, col.soff[r], l, col.soff[imax], col.slen[imax]) > 0) imax = r;
+            if (imin == ~0ull || bytes_cmp(data, col.soff[r], l, col.soff[imin], col.slen[imin], data_end) < 0) imin = r;
+            if (imax == ~0ull || bytes_cmp(data, col.soff[r], l, col.soff[imax], col.slen[imax], data_end) > 0) imax = r;
         } else if (col.phys == 0) {
             const uint64_t v = (col.vbits[r >> 6] >> (r & 63)) & 1ull;
             kmin = v < kmin ? v : kmin;
@@ -110,9 +102,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
             if ((int)threadIdx.x < d) {
                 const uint64_t a = li[threadIdx.x], b = li[threadIdx.x + d];
                 // keep the earlier record on ties (same bytes -> same output anyway)
-                if (b != ~0ull && (a == ~0ull || bin_cmp(data, col.soff[b], col.slen[b], col.soff[a], col.slen[a]) < 0)) li[threadIdx.x] = b;
+                if (b != ~0ull && (a == ~0ull || bytes_cmp(data, col.soff[b], col.slen[b], col.soff[a], col.slen[a], data_end) < 0)) li[threadIdx.x] = b;
                 const uint64_t x = la[threadIdx.x], y = la[threadIdx.x + d];
-                if (y != ~0ull && (x == ~0ull || bin_cmp(data, col.soff[y], col.slen[y], col.soff[x], col.slen[x]) > 0)) la[threadIdx.x] = y;
+                if (y != ~0ull && (x == ~0ull || bytes_cmp(data, col.soff[y], col.slen[y], col.soff[x], col.slen[x], data_end) > 0)) la[threadIdx.x] = y;
             }
             __syncthreads();
         }
@@ -138,130 +130,201 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
     }
 }
 
-// per chunk: combine tile candidates of binary min/max; null count; has_minmax
+// per chunk (one block): combine tile candidates of binary min/max; null count; has_minmax
 __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats_final(ChunkDesc *ch, int nchunks, const DevCol *cols, const uint8_t *data,
                                                                  const uint32_t *ctile_first, const uint32_t *ctile_count,
-                                                                 const uint64_t *tile_smin, const uint64_t *tile_smax)
+                                                                 const uint64_t *tile_smin, const uint64_t *tile_smax,
+                                                                 const uint64_t *data_end_p)
 {
-    const int ci = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ci >= nchunks) return;
+    __shared__ uint64_t li[KPW_BLOCK], la[KPW_BLOCK];
+    const uint64_t data_end = *data_end_p;
+    const int ci = blockIdx.x;
     ChunkDesc &C = ch[ci];
     const DevCol &col = cols[C.col];
-    C.null_count = (uint64_t)(C.e - C.s) - C.nn;
-    C.has_minmax = C.nn > 0;
-    if (col.phys == 6 && C.nn) {
-        uint64_t a = ~0ull, b = ~0ull;
-        for (uint32_t k = 0; k < ctile_count[ci]; k++) {
-            const uint64_t x = tile_smin[ctile_first[ci] + k], y = tile_smax[ctile_first[ci] + k];
-            if (x != ~0ull && (a == ~0ull || bin_cmp(data, col.soff[x], col.slen[x], col.soff[a], col.slen[a]) < 0)) a = x;
-            if (y != ~0ull && (b == ~0ull || bin_cmp(data, col.soff[y], col.slen[y], col.soff[b], col.slen[b]) > 0)) b = y;
-        }
-        C.smin = a;
-        C.smax = b;
+    if (threadIdx.x == 0) {
+        C.null_count = (uint64_t)(C.e - C.s) - C.nn;
+        C.has_minmax = C.nn > 0;
     }
+    if (col.phys != 6 || !C.nn) return;
+    uint64_t a = ~0ull, b = ~0ull;
+    for (uint32_t k = threadIdx.x; k < ctile_count[ci]; k += KPW_BLOCK) {
+        const uint64_t x = tile_smin[ctile_first[ci] + k], y = tile_smax[ctile_first[ci] + k];
+        if (x != ~0ull && (a == ~0ull || bytes_cmp(data, col.soff[x], col.slen[x], col.soff[a], col.slen[a], data_end) < 0)) a = x;
+        if (y != ~0ull && (b == ~0ull || bytes_cmp(data, col.soff[y], col.slen[y], col.soff[b], col.slen[b], data_end) > 0)) b = y;
+    }
+    li[threadIdx.x] = a;
+    la[threadIdx.x] = b;
+    __syncthreads();
+    for (int d = KPW_BLOCK / 2; d > 0; d >>= 1) {
+        if ((int)threadIdx.x < d) {
+            const uint64_t x = li[threadIdx.x], y = li[threadIdx.x + d];
+            if (y != ~0ull && (x == ~0ull || bytes_cmp(data, col.soff[y], col.slen[y], col.soff[x], col.slen[x], data_end) < 0)) li[threadIdx.x] = y;
+            const uint64_t u = la[threadIdx.x], v = la[threadIdx.x + d];
+            if (v != ~0ull && (u == ~0ull || bytes_cmp(data, col.soff[v], col.slen[v], col.soff[u], col.slen[u], data_end) > 0)) la[threadIdx.x] = v;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { C.smin = li[0]; C.smax = la[0]; }
 }
 
 // ------------------------------------------------------------------ K2 dictionary
 
 constexpr uint64_t HT_EMPTY = ~0ull;
 
-__device__ __forceinline__ uint64_t str_hash(const uint8_t *p, uint32_t n)
+// Insert one key into the chunk's global open-addressing table; returns the slot or -1 when
+// the table is full / the chunk already fell back.  Plain loads are used where a stale
+// value is harmless: keys only go EMPTY -> key (a stale EMPTY just leads to a CAS that
+// returns the real key), and recorded ranks only decrease.
+__device__ __forceinline__ int64_t global_insert(ChunkDesc &C, uint64_t *keys, uint32_t *mins, uint32_t cap, uint64_t key,
+                                                 uint64_t h, uint32_t rank, uint32_t esize, uint32_t max_dict_bytes,
+                                                 bool is_bin, const DevCol &col, const uint8_t *data, uint64_t r,
+                                                 uint64_t data_end)
 {
-    uint64_t h = 1469598103934665603ull ^ n;
-    for (uint32_t i = 0; i < n; i++) { h ^= p[i]; h *= 1099511628211ull; }
-    return mix64(h);
-}
-
-__global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
-                                                           const uint32_t *ctile_chunk, const uint32_t *ctile_first,
-                                                           uint64_t *ht_key, uint32_t *ht_min, uint32_t *slotof, uint32_t max_dict_bytes)
-{
-    const uint32_t t = blockIdx.x;
-    const uint32_t ci = ctile_chunk[t];
-    ChunkDesc &C = ch[ci];
-    if (!C.is_dict) return;
-    if (__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    const DevCol &col = cols[C.col];
-    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
-    if (p0 >= (uint64_t)C.e) return;
-    uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
-    const uint32_t cap = C.ht_cap;
-    uint64_t *keys = ht_key + C.ht_off;
-    uint32_t *mins = ht_min + C.ht_off;
-    const bool is_bin = col.phys == 6;
-    for (int k = 0; k < 8; k++) {
-        const uint64_t r = p0 + k;
-        if (r >= (uint64_t)C.e) break;
-        if (!present_at(col, r)) continue;
-        // the chunk's fallback is already decided (dictionary bytes > dictPageSize): every
-        // further insert is wasted work on a filling table
-        if (__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-        uint64_t key, h;
-        uint32_t esize;
-        if (is_bin) {
-            key = r;
-            const uint32_t l = col.slen[r];
-            h = str_hash(data + col.soff[r], l);
-            esize = 4 + l;
-        } else {
-            key = fixed_val(col, r);
-            h = mix64(key);
-            esize = (uint32_t)col.vsize;
+    if (!is_bin && key == HT_EMPTY) {
+        const uint32_t slot = cap;  // reserved slot for the sentinel value
+        if (atomicCAS((unsigned long long *)&keys[slot], (unsigned long long)HT_EMPTY, 0ull) == HT_EMPTY) {
+            const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
+            atomicAdd(&C.dict_n, 1u);
+            if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        uint32_t slot;
-        bool ok = false;
-        if (!is_bin && key == HT_EMPTY) {
-            slot = cap;  // reserved slot for the sentinel value
-            const unsigned long long old = atomicCAS((unsigned long long *)&keys[slot], (unsigned long long)HT_EMPTY, 0ull);
+        if (mins[slot] > rank) atomicMin(&mins[slot], rank);
+        return slot;
+    }
+    uint32_t i = (uint32_t)(h & (cap - 1));
+    for (uint32_t probe = 0; probe < cap; probe++) {
+        uint64_t cur = keys[i];
+        if (cur == HT_EMPTY) {
+            const unsigned long long old = atomicCAS((unsigned long long *)&keys[i], (unsigned long long)HT_EMPTY, (unsigned long long)key);
             if (old == HT_EMPTY) {
                 const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
                 atomicAdd(&C.dict_n, 1u);
                 if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicMin(&mins[i], rank);
+                return i;
             }
-            atomicMin(&mins[slot], (uint32_t)rank);
-            ok = true;
-        } else {
-            uint32_t i = (uint32_t)(h & (cap - 1));
-            for (uint32_t probe = 0; probe < cap; probe++) {
-                uint64_t cur = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (cur == HT_EMPTY) {
-                    const unsigned long long old = atomicCAS((unsigned long long *)&keys[i], (unsigned long long)HT_EMPTY,
-                                                             (unsigned long long)key);
-                    if (old == HT_EMPTY) {
-                        const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
-                        atomicAdd(&C.dict_n, 1u);
-                        if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        atomicMin(&mins[i], (uint32_t)rank);
-                        slot = i;
-                        ok = true;
-                        break;
-                    }
-                    cur = old;
-                }
-                bool eq;
-                if (is_bin) eq = bin_cmp(data, col.soff[cur], col.slen[cur], col.soff[r], col.slen[r]) == 0;
-                else eq = cur == key;
-                if (eq) {
-                    // a (possibly stale) recorded rank can only be >= the true minimum, so
-                    // skipping when it is already <= rank is safe; avoids serialising
-                    // low-cardinality columns on a handful of hot atomics
-                    if (__hip_atomic_load(&mins[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)rank)
-                        atomicMin(&mins[i], (uint32_t)rank);
-                    slot = i;
-                    ok = true;
-                    break;
-                }
-                i = (i + 1) & (cap - 1);
-                if ((probe & 15) == 15 && __hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-            }
+            cur = old;
         }
-        if (!ok) {
+        const bool eq = is_bin ? bytes_cmp(data, col.soff[cur], col.slen[cur], col.soff[r], col.slen[r], data_end) == 0 : cur == key;
+        if (eq) {
+            if (mins[i] > rank) atomicMin(&mins[i], rank);
+            return i;
+        }
+        i = (i + 1) & (cap - 1);
+        if ((probe & 15) == 15 && __hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return -1;
+    }
+    return -1;
+}
+
+// One block per chunk tile (2048 records).  Keys are first deduplicated in an LDS table
+// (first rank per key within the tile); each distinct key then goes to the chunk's global
+// table once, so low-cardinality columns do not serialise on a few hot global slots.
+constexpr uint32_t LDS_T = 2048;
+constexpr uint32_t LDS_PROBES = 32;
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
+                                                           const uint32_t *ctile_chunk, const uint32_t *ctile_first,
+                                                           uint64_t *ht_key, uint32_t *ht_min, uint32_t *slotof, uint32_t max_dict_bytes,
+                                                           int exact, const uint64_t *data_end_p)
+{
+    __shared__ uint64_t lkey[LDS_T];
+    __shared__ uint32_t lmin[LDS_T];
+    __shared__ uint32_t lslot[LDS_T];
+    __shared__ uint64_t lrec[LDS_T];
+    const uint64_t data_end = *data_end_p;
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    ChunkDesc &C = ch[ci];
+    __shared__ uint32_t skip;
+    if (!C.is_dict) return;
+    // block-uniform: another block may set `fallback` while this one reads it
+    if (threadIdx.x == 0) skip = __hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (skip) return;
+    const DevCol &col = cols[C.col];
+    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    const uint32_t cap = C.ht_cap;
+    uint64_t *keys = ht_key + C.ht_off;
+    uint32_t *mins = ht_min + C.ht_off;
+    // BYTE_ARRAY keys: the 64-bit hash computed by K1 (verified byte-for-byte afterwards in
+    // k_dict_ids); `exact` re-runs with byte comparisons after a detected hash collision
+    // (then the LDS stage is skipped: every value goes straight to the global table).
+    const bool is_bin = col.phys == 6 && exact;
+    for (uint32_t i = threadIdx.x; i < LDS_T; i += KPW_BLOCK) { lkey[i] = HT_EMPTY; lmin[i] = 0xffffffffu; }
+    __syncthreads();
+    uint64_t rank0 = p0 < (uint64_t)C.e ? rank_base(col, (uint64_t)C.s, p0) : 0;
+    int32_t li[8];
+    uint64_t keyv[8];
+    uint32_t rk[8];
+    uint32_t npres = 0;
+    // phase 1: LDS dedup
+    for (int k = 0; k < 8; k++) {
+        li[k] = -2;  // not present
+        const uint64_t r = p0 + k;
+        if (r >= (uint64_t)C.e) continue;
+        if (!present_at(col, r)) continue;
+        uint64_t key;
+        if (is_bin) key = r;
+        else if (col.phys == 6) key = col.shash[r];
+        else key = fixed_val(col, r);
+        keyv[k] = key;
+        rk[k] = (uint32_t)(rank0 + npres);
+        npres++;
+        li[k] = -1;  // global path
+        if (is_bin || key == HT_EMPTY) continue;
+        uint32_t i = (uint32_t)(mix64(key) >> 40) & (LDS_T - 1);
+        for (uint32_t probe = 0; probe < LDS_PROBES; probe++) {
+            uint64_t cur = lkey[i];
+            if (cur == HT_EMPTY) {
+                const unsigned long long old = atomicCAS((unsigned long long *)&lkey[i], (unsigned long long)HT_EMPTY,
+                                                         (unsigned long long)key);
+                cur = old == HT_EMPTY ? key : old;
+                if (old == HT_EMPTY) lrec[i] = r;
+            }
+            if (cur == key) {
+                atomicMin(&lmin[i], rk[k]);
+                li[k] = (int32_t)i;
+                break;
+            }
+            i = (i + 1) & (LDS_T - 1);
+        }
+    }
+    __syncthreads();
+    // phase 2: one global insert per distinct key of the tile
+    for (uint32_t i = threadIdx.x; i < LDS_T; i += KPW_BLOCK) {
+        const uint64_t key = lkey[i];
+        if (key == HT_EMPTY) continue;
+        const uint64_t r = lrec[i];
+        const uint32_t esize = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize;
+        const int64_t g = global_insert(C, keys, mins, cap, key, mix64(key), lmin[i], esize, max_dict_bytes, false, col, data, r,
+                                        data_end);
+        lslot[i] = g < 0 ? 0xffffffffu : (uint32_t)g;
+        if (g < 0 && !__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
             atomicOr(&C.overflow, 1u);
             __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
         }
-        slotof[C.ids_off + rank] = slot;
-        rank++;
+    }
+    __syncthreads();
+    // phase 3: slots for every value (LDS hit or direct global insert)
+    for (int k = 0; k < 8; k++) {
+        if (li[k] == -2) continue;
+        const uint64_t r = p0 + k;
+        int64_t g;
+        if (li[k] >= 0) {
+            g = lslot[li[k]] == 0xffffffffu ? -1 : (int64_t)lslot[li[k]];
+        } else {
+            if (__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+            uint64_t h;
+            uint32_t esize;
+            if (is_bin) { h = bytes_hash(data, col.soff[r], col.slen[r], data_end); esize = 4 + col.slen[r]; }
+            else { h = mix64(keyv[k]); esize = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize; }
+            g = global_insert(C, keys, mins, cap, keyv[k], h, rk[k], esize, max_dict_bytes, is_bin, col, data, r, data_end);
+            if (g < 0 && !__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                atomicOr(&C.overflow, 1u);
+                __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (g < 0) return;
+        slotof[C.ids_off + rk[k]] = (uint32_t)g;
     }
 }
 
@@ -328,8 +391,11 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
 
 // slot -> id for every value (overwrites slotof in place); sets id-job width/length
 __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
-                                                        const uint32_t *ctile_first, const uint32_t *ht_id, uint32_t *ids)
+                                                        const uint32_t *ctile_first, const uint32_t *ht_id, uint32_t *ids,
+                                                        const uint8_t *data, const uint64_t *ent_rec, const uint64_t *data_end_p,
+                                                        uint32_t *collision)
 {
+    const uint64_t data_end = *data_end_p;
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
@@ -343,7 +409,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, con
         if (r >= (uint64_t)C.e) break;
         if (!present_at(col, r)) continue;
         const uint64_t o = C.ids_off + rank;
-        ids[o] = ht_id[C.ht_off + ids[o]];
+        const uint32_t id = ht_id[C.ht_off + ids[o]];
+        ids[o] = id;
+        if (col.phys == 6) {  // verify the hash-keyed dictionary byte-for-byte
+            const uint64_t e = ent_rec[C.ent_off + id];
+            if (col.slen[e] != col.slen[r] || bytes_cmp(data, col.soff[e], col.slen[e], col.soff[r], col.slen[r], data_end) != 0)
+                atomicOr(collision, 1u);
+        }
         rank++;
     }
 }
@@ -583,15 +655,15 @@ void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, c
 void launch_chunk_stats(const ChunkArgs &a, hipStream_t s)
 {
     hipLaunchKernelGGL(k_chunk_stats, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
-                       a.tile_raw, a.tile_smin, a.tile_smax);
-    hipLaunchKernelGGL(k_chunk_stats_final, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, a.cols, a.data,
-                       a.ctile_first, a.ctile_count, a.tile_smin, a.tile_smax);
+                       a.tile_raw, a.tile_smin, a.tile_smax, a.data_end);
+    hipLaunchKernelGGL(k_chunk_stats_final, dim3(a.nchunks), dim3(KPW_BLOCK), 0, s, a.ch, a.nchunks, a.cols, a.data,
+                       a.ctile_first, a.ctile_count, a.tile_smin, a.tile_smax, a.data_end);
 }
 
 void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
 {
     hipLaunchKernelGGL(k_dict_insert, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
-                       a.ht_key, a.ht_min, a.ids, a.max_dict_bytes);
+                       a.ht_key, a.ht_min, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
     hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
                        a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0);
@@ -599,7 +671,8 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
     seg_tile_scan_u64(a.tile_sz, a.tile_sz, a.ctile_chunk, a.nctiles, s);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
                        a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1);
-    hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht_id, a.ids);
+    hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht_id, a.ids,
+                       a.data, a.ent_rec, a.data_end, a.collision);
 }
 
 void launch_layout(const ChunkArgs &a, RleJob *jobs, uint64_t *page_off, uint64_t *page_len, uint64_t *tot, hipStream_t s)

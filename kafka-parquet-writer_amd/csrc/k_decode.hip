@@ -111,6 +111,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
 
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = r < a.n;
+    const uint64_t data_end = a.off[a.n];
     uint64_t seen[4] = {0, 0, 0, 0};
     uint64_t bval[4] = {0, 0, 0, 0};   // boolean values (by column)
     bool bad = false;
@@ -165,6 +166,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
                 if ((int32_t)(uint32_t)l < 0 || end - pos < (uint32_t)l) { bad = true; break; }
                 col->soff[r] = pos;
                 col->slen[r] = (uint32_t)l;
+                if (col->dict) col->shash[r] = bytes_hash(d, pos, (uint32_t)l, data_end);
                 pos += (uint32_t)l;
             }
             if (col->phys == 0) {

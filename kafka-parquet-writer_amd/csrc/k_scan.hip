@@ -116,34 +116,41 @@ void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njo
 // ------------------------------------------------------------------ single-block segmented tile scans
 // Exclusive, segmented by job id (seg[t]); job totals written to tot[job] when tot != nullptr.
 
-template <typename T, typename Op>
-struct SegPair { T v; uint32_t head; };
-
-template <typename T, typename Op>
-__device__ __forceinline__ SegPair<T, Op> seg_combine(SegPair<T, Op> a, SegPair<T, Op> b)
-{
-    SegPair<T, Op> r;
-    r.head = a.head | b.head;
-    r.v = b.head ? b.v : Op::op(a.v, b.v);
-    return r;
-}
+// Each thread owns SEG_PER consecutive elements: a sequential segmented scan in registers,
+// then one Hillis-Steele segmented scan over the 256 thread aggregates per chunk of
+// 256*SEG_PER elements, carrying (value, segment) between chunks.
+constexpr int SEG_PER = 8;
 
 template <typename T, typename Op>
 __global__ void __launch_bounds__(KPW_BLOCK) k_seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot)
 {
     __shared__ T lv[KPW_BLOCK];
     __shared__ uint32_t lh[KPW_BLOCK];
-    T carry = Op::id();
-    uint32_t carry_seg = 0xffffffffu;
-    for (uint32_t b = 0; b < n; b += KPW_BLOCK) {
-        const uint32_t k = b + threadIdx.x;
-        const bool valid = k < n;
-        const uint32_t sg = valid ? seg[k] : 0xfffffffeu;
-        const uint32_t prev_sg = k == 0 ? 0xffffffffu : (k - 1 < n ? seg[k - 1] : 0xfffffffeu);
-        T v = valid ? in[k] : Op::id();
-        uint32_t head = (k == b) ? (sg != carry_seg) : (sg != prev_sg);
-        // inclusive segmented scan (Hillis-Steele on pairs)
-        lv[threadIdx.x] = v;
+    __shared__ T lcarry;
+    __shared__ uint32_t lcarry_seg;
+    if (threadIdx.x == 0) { lcarry = Op::id(); lcarry_seg = 0xffffffffu; }
+    __syncthreads();
+    const uint32_t CH = KPW_BLOCK * SEG_PER;
+    for (uint32_t b = 0; b < n; b += CH) {
+        const uint32_t k0 = b + threadIdx.x * SEG_PER;
+        T v[SEG_PER];
+        uint32_t sg[SEG_PER];
+        // local inclusive segmented scan; `head` = a segment starts inside my range
+        T acc = Op::id();
+        uint32_t head = 0;
+        uint32_t prev = (k0 == 0) ? 0xffffffffu : (k0 - 1 < n ? seg[k0 - 1] : 0xfffffffeu);
+        if (k0 == b && b != 0) prev = lcarry_seg;
+        const uint32_t first_seg = k0 < n ? seg[k0] : 0xfffffffeu;
+#pragma unroll
+        for (int i = 0; i < SEG_PER; i++) {
+            const uint32_t k = k0 + i;
+            sg[i] = k < n ? seg[k] : 0xfffffffeu;
+            v[i] = k < n ? in[k] : Op::id();
+            const uint32_t p = i ? sg[i - 1] : prev;
+            if (sg[i] != p) { head = 1; acc = v[i]; } else acc = Op::op(acc, v[i]);
+        }
+        // block scan over (acc, head) of the threads; thread t's aggregate covers its range
+        lv[threadIdx.x] = acc;
         lh[threadIdx.x] = head;
         __syncthreads();
         for (int d = 1; d < KPW_BLOCK; d <<= 1) {
@@ -159,25 +166,31 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_seg_tile_scan(const T *in, T *out
             }
             __syncthreads();
         }
-        T incl = lv[threadIdx.x];
-        uint32_t inclh = lh[threadIdx.x];
-        // fold the carry from the previous chunk into elements before the first head
-        if (!inclh) incl = Op::op(carry, incl);
-        __syncthreads();
-        lv[threadIdx.x] = incl;
-        __syncthreads();
-        if (valid) {
-            T ex;
-            if (head) ex = Op::id();
-            else ex = (threadIdx.x == 0) ? carry : lv[threadIdx.x - 1];
-            out[k] = ex;
-            const bool last_of_seg = (k + 1 >= n) || (seg[k + 1] != sg);
-            if (last_of_seg && tot) tot[sg] = incl;
+        // exclusive prefix entering my range (value continuing my first segment)
+        T in_pre;
+        if (threadIdx.x == 0) in_pre = lcarry;
+        else in_pre = lv[threadIdx.x - 1];
+        const uint32_t pre_head = threadIdx.x == 0 ? 0u : lh[threadIdx.x - 1];
+        // fold the carry into everything before the chunk's first head
+        if (threadIdx.x != 0 && !pre_head) in_pre = Op::op(lcarry, in_pre);
+        // does my first element continue the incoming segment?
+        const bool cont = (k0 < n) && (first_seg == prev);
+        T run = cont ? in_pre : Op::id();
+#pragma unroll
+        for (int i = 0; i < SEG_PER; i++) {
+            const uint32_t k = k0 + i;
+            if (k >= n) break;
+            const uint32_t p = i ? sg[i - 1] : prev;
+            if (sg[i] != p) run = Op::id();
+            out[k] = run;
+            run = Op::op(run, v[i]);
+            const bool last_of_seg = (k + 1 >= n) || (seg[k + 1] != sg[i]);
+            if (last_of_seg && tot) tot[sg[i]] = run;
         }
         __syncthreads();
-        const uint32_t lastk = (b + KPW_BLOCK <= n) ? KPW_BLOCK - 1 : (n - 1 - b);
-        carry = lv[lastk];
-        carry_seg = seg[b + lastk];
+        // carry = inclusive value at the last valid element of this chunk
+        const uint32_t last = (b + CH <= n) ? (b + CH - 1) : (n - 1);
+        if (k0 <= last && last < k0 + SEG_PER) { lcarry = run; lcarry_seg = seg[last]; }
         __syncthreads();
     }
 }

@@ -3,7 +3,7 @@
 // CompressFragment).  parquet-mr 1.10.1 SnappyCompressor makes one Snappy.compress call per
 // page (data pages and the dictionary page); snappy compresses independent 64 KiB
 // fragments with a fresh hash table each, so fragments are the unit of parallelism: one
-// wave per fragment, the fragment (<= 64 KiB) and its uint16 hash table (<= 32 KiB) in LDS.
+// wave per fragment; the fragment's uint16 hash table (<= 32 KiB) in LDS, input from L1/L2.
 // The wave runs the sequential match loop in lock-step (every lane holds the same scalar
 // state); literal copies and match-length extension use all 64 lanes.
 #include "kpw_device.h"
@@ -13,27 +13,26 @@ namespace kpw {
 
 constexpr int SNAPPY_MAX_TABLE = 1 << 14;
 
-struct SnLds {
-    uint32_t in[SNAPPY_FRAG / 4 + 4];
-    uint16_t table[SNAPPY_MAX_TABLE];
+// Input bytes are read straight from the page buffer in global memory (L1/L2 resident while
+// the wave scans its fragment); only the uint16 hash table (<= 32 KiB) lives in LDS, so five
+// fragments run per CU.  `src` is the fragment start; reads never go semantically beyond
+// the fragment (positions <= ip_limit+7 or < ip_end), and the page buffer is padded.
+struct Src {
+    const uint8_t *p;
+    __device__ __forceinline__ uint32_t ld32(uint32_t i) const
+    {
+        const uintptr_t a = (uintptr_t)(p + i);
+        const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3) * 8;
+        const uint32_t lo = w[0];
+        return sh ? ((lo >> sh) | (w[1] << (32 - sh))) : lo;
+    }
+    __device__ __forceinline__ uint8_t ld8(uint32_t i) const { return p[i]; }
 };
 
-__device__ __forceinline__ uint32_t lds_ld32(const uint32_t *w, uint32_t p)
-{
-    const uint32_t a = w[p >> 2], b = w[(p >> 2) + 1];
-    const uint32_t sh = (p & 3) * 8;
-    return sh ? ((a >> sh) | (b << (32 - sh))) : a;
-}
-__device__ __forceinline__ uint8_t lds_ld8(const uint32_t *w, uint32_t p) { return (uint8_t)(w[p >> 2] >> ((p & 3) * 8)); }
 __device__ __forceinline__ uint32_t sn_hash(uint32_t bytes, int shift) { return (bytes * 0x1e35a7bdu) >> shift; }
 
-// lane-parallel literal copy: LDS [src, src+len) -> global op
-__device__ __forceinline__ void copy_lit(uint8_t *op, const uint32_t *w, uint32_t src, uint32_t len, int lane)
-{
-    for (uint32_t i = lane; i < len; i += 64) op[i] = lds_ld8(w, src + i);
-}
-
-__device__ __forceinline__ uint32_t emit_literal(uint8_t *out, uint32_t op, const uint32_t *w, uint32_t lit, uint32_t len, int lane)
+__device__ __forceinline__ uint32_t emit_literal(uint8_t *out, uint32_t op, const Src &in, uint32_t lit, uint32_t len, int lane)
 {
     uint32_t n = len - 1;
     if (n < 60) {
@@ -46,7 +45,7 @@ __device__ __forceinline__ uint32_t emit_literal(uint8_t *out, uint32_t op, cons
         while (nn > 0) { if (lane == 0) out[op] = (uint8_t)(nn & 0xff); op++; nn >>= 8; count++; }
         if (lane == 0) out[base] = (uint8_t)((59 + count) << 2);
     }
-    copy_lit(out + op, w, lit, len, lane);
+    for (uint32_t i = lane; i < len; i += 64) out[op + i] = in.ld8(lit + i);
     return op + len;
 }
 
@@ -74,13 +73,18 @@ __device__ __forceinline__ uint32_t emit_copy(uint8_t *out, uint32_t op, uint32_
     return emit_copy_lt64(out, op, offset, len, lane);
 }
 
-// number of matching bytes of [s1..) vs [s2..s2_limit) — lane-parallel, 64 bytes per step
-__device__ __forceinline__ uint32_t find_match_length(const uint32_t *w, uint32_t s1, uint32_t s2, uint32_t s2_limit, int lane)
+// matching bytes of [s1..) vs [s2..s2_limit): a scalar 4-byte check first (most matches
+// are short), then 64 lanes compare 64 bytes per step
+__device__ __forceinline__ uint32_t find_match_length(const Src &in, uint32_t s1, uint32_t s2, uint32_t s2_limit, int lane)
 {
+    if (s2 + 4 <= s2_limit) {
+        const uint32_t x = in.ld32(s1) ^ in.ld32(s2);
+        if (x) return (uint32_t)(__ffs((int)x) - 1) >> 3;
+    }
     uint32_t m = 0;
     for (;;) {
         const uint32_t p2 = s2 + m + lane;
-        const bool ok = p2 < s2_limit && lds_ld8(w, s1 + m + lane) == lds_ld8(w, p2);
+        const bool ok = p2 < s2_limit && in.ld8(s1 + m + lane) == in.ld8(p2);
         const uint64_t bad = __ballot(!ok);
         if (bad) return m + (uint32_t)(__ffsll((long long)bad) - 1);
         m += 64;
@@ -89,7 +93,7 @@ __device__ __forceinline__ uint32_t find_match_length(const uint32_t *w, uint32_
 
 __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
 {
-    __shared__ SnLds L;
+    __shared__ uint16_t table[SNAPPY_MAX_TABLE];
     const int lane = threadIdx.x;
     const uint32_t f = blockIdx.x;
     const uint32_t pg = a.frag_page[f];
@@ -97,23 +101,12 @@ __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
     const uint64_t plen = a.page_len[pg];
     const uint64_t fstart = (uint64_t)fi * SNAPPY_FRAG;
     const uint32_t n = (uint32_t)((plen - fstart) < SNAPPY_FRAG ? (plen - fstart) : SNAPPY_FRAG);
-    const uint8_t *src = a.in + a.page_off[pg] + fstart;
-    // stage the fragment into LDS (byte loads, coalesced across lanes) and zero the table
+    const Src in{a.in + a.page_off[pg] + fstart};
     uint32_t tsize = 256;
     while (tsize < SNAPPY_MAX_TABLE && tsize < n) tsize <<= 1;
-    for (uint32_t i = lane; i < (n + 3) / 4 + 2; i += 64) {
-        uint32_t v = 0;
-        for (int k = 0; k < 4; k++) {
-            const uint32_t p = i * 4 + k;
-            if (p < n) v |= (uint32_t)src[p] << (8 * k);
-        }
-        L.in[i] = v;
-    }
-    for (uint32_t i = lane; i < tsize; i += 64) L.table[i] = 0;
+    for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
     __syncthreads();
 
-    const uint32_t *w = L.in;
-    uint16_t *table = L.table;
     uint8_t *out = a.frag_out + (uint64_t)f * SNAPPY_FRAG_CAP;
     uint32_t op = 0;
     int shift = 32;
@@ -124,7 +117,7 @@ __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
     if (n >= 15) {
         const uint32_t ip_limit = n - 15;
         ip = 1;
-        uint32_t next_hash = sn_hash(lds_ld32(w, ip), shift);
+        uint32_t next_hash = sn_hash(in.ld32(ip), shift);
         for (;;) {
             uint32_t skip = 32;
             uint32_t next_ip = ip;
@@ -135,36 +128,28 @@ __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
                 const uint32_t step = skip++ >> 5;
                 next_ip = ip + step;
                 if (next_ip > ip_limit) goto emit_remainder;
-                next_hash = sn_hash(lds_ld32(w, next_ip), shift);
+                next_hash = sn_hash(in.ld32(next_ip), shift);
                 candidate = table[hash];
-                __syncthreads();  // every lane read the old entry before lane 0 overwrites it
                 if (lane == 0) table[hash] = (uint16_t)ip;
-                __syncthreads();
-                if (lds_ld32(w, ip) == lds_ld32(w, candidate)) break;
+                if (in.ld32(ip) == in.ld32(candidate)) break;
             }
-            op = emit_literal(out, op, w, next_emit, ip - next_emit, lane);
+            op = emit_literal(out, op, in, next_emit, ip - next_emit, lane);
             uint32_t input_lo, input_hi;
             for (;;) {
                 const uint32_t base = ip;
-                const uint32_t matched = 4 + find_match_length(w, candidate + 4, ip + 4, ip_end, lane);
+                const uint32_t matched = 4 + find_match_length(in, candidate + 4, ip + 4, ip_end, lane);
                 ip += matched;
                 op = emit_copy(out, op, base - candidate, matched, lane);
                 next_emit = ip;
                 if (ip >= ip_limit) goto emit_remainder;
-                const uint32_t insert_tail = ip - 1;
-                input_lo = lds_ld32(w, insert_tail);           // bytes [ip-1, ip+3)
-                input_hi = lds_ld32(w, insert_tail + 4);       // bytes [ip+3, ip+7)
-                const uint32_t b1 = (input_lo >> 8) | (input_hi << 24);  // GetUint32AtOffset(.., 1)
-                const uint32_t prev_hash = sn_hash(input_lo, shift);
-                __syncthreads();
-                if (lane == 0) table[prev_hash] = (uint16_t)(ip - 1);
-                __syncthreads();
+                input_lo = in.ld32(ip - 1);         // bytes [ip-1, ip+3)
+                input_hi = in.ld32(ip + 3);         // bytes [ip+3, ip+7)
+                const uint32_t b1 = (input_lo >> 8) | (input_hi << 24);
+                if (lane == 0) table[sn_hash(input_lo, shift)] = (uint16_t)(ip - 1);
                 const uint32_t cur_hash = sn_hash(b1, shift);
                 candidate = table[cur_hash];
-                const uint32_t candidate_bytes = lds_ld32(w, candidate);
-                __syncthreads();
+                const uint32_t candidate_bytes = in.ld32(candidate);
                 if (lane == 0) table[cur_hash] = (uint16_t)ip;
-                __syncthreads();
                 if (b1 != candidate_bytes) break;
             }
             next_hash = sn_hash((input_lo >> 16) | (input_hi << 16), shift);
@@ -172,7 +157,7 @@ __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
         }
     }
 emit_remainder:
-    if (next_emit < ip_end) op = emit_literal(out, op, w, next_emit, ip_end - next_emit, lane);
+    if (next_emit < ip_end) op = emit_literal(out, op, in, next_emit, ip_end - next_emit, lane);
     if (lane == 0) a.frag_len[f] = op;
 }
 

@@ -24,6 +24,9 @@ struct ChunkArgs {
     uint32_t *ids;
     uint64_t *ent_rec, *ent_boff;
     uint32_t max_dict_bytes;
+    int32_t exact_strings;         // 1: BYTE_ARRAY dictionary keys compared byte-for-byte (collision retry)
+    const uint64_t *data_end;      // device pointer to offsets[n] (end of the record bytes)
+    uint32_t *collision;           // device flag: a hash-keyed string dictionary failed verification
 };
 
 inline void seg_tile_scan_u32(const uint32_t *in, uint32_t *out, const uint32_t *seg, uint32_t n, hipStream_t s)

@@ -95,6 +95,50 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x)
     return x;
 }
 
+// 8 bytes at base[off..off+8) (base 8-byte aligned), zero beyond `end`; two aligned loads
+// + funnel shift instead of 8 byte loads.
+__device__ __forceinline__ uint64_t ldu64(const uint8_t *base, uint64_t off, uint64_t end)
+{
+    if (off + 16 <= end) {
+        const uint64_t a = off & ~7ull;
+        const uint64_t lo = *(const uint64_t *)(base + a), hi = *(const uint64_t *)(base + a + 8);
+        const uint32_t sh = (uint32_t)(off & 7) * 8;
+        return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+    }
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++)
+        if (off + i < end) v |= (uint64_t)base[off + i] << (8 * i);
+    return v;
+}
+__device__ __forceinline__ uint64_t tail_mask(uint64_t rem) { return rem >= 8 ? ~0ull : ((1ull << (8 * rem)) - 1); }
+
+// 64-bit hash of a byte string (dictionary keys of BYTE_ARRAY columns).
+__device__ __forceinline__ uint64_t bytes_hash(const uint8_t *base, uint64_t off, uint32_t len, uint64_t end)
+{
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ len;
+    for (uint32_t k = 0; k < len; k += 8) {
+        const uint64_t w = ldu64(base, off + k, end) & tail_mask(len - k);
+        h = (h ^ w) * 0xff51afd7ed558ccdull;
+        h ^= h >> 29;
+    }
+    return mix64(h);
+}
+
+// unsigned lexicographic compare (BinaryStatistics / UNSIGNED_LEXICOGRAPHICAL comparator)
+__device__ __forceinline__ int bytes_cmp(const uint8_t *base, uint64_t oa, uint32_t la, uint64_t ob, uint32_t lb, uint64_t end)
+{
+    const uint32_t m = la < lb ? la : lb;
+    for (uint32_t k = 0; k < m; k += 8) {
+        const uint64_t msk = tail_mask(m - k);
+        const uint64_t x = ldu64(base, oa + k, end) & msk, y = ldu64(base, ob + k, end) & msk;
+        if (x != y) {
+            const uint64_t bx = __builtin_bswap64(x), by = __builtin_bswap64(y);
+            return bx < by ? -1 : 1;
+        }
+    }
+    return la == lb ? 0 : (la < lb ? -1 : 1);
+}
+
 __device__ __forceinline__ uint64_t bits_window(const uint64_t *w, uint64_t bit)
 {
     // 64 bits starting at absolute bit index `bit` (words are padded by one extra word)
