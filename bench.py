@@ -70,6 +70,50 @@ def cpu_baseline(kind, seed, sample_records, threads):
                 records_per_s=round(per * threads / dt, 1))
 
 
+def dist_init(world, local_rank, backend="nccl"):
+    """One process per GPU (torchrun env). backend "nccl" is RCCL on ROCm; tests use gloo."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    if backend == "nccl":
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        dist.init_process_group(backend=backend)
+    return dist
+
+
+def timed_steps(step, steps, warmup, dist=None, sync=lambda: None):
+    """W untimed warmup steps, then exactly K timed steps bracketed by barrier + device sync
+    on both sides; returns (max-over-ranks elapsed seconds, per-step results)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    out = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out.append(step())
+    sync()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    return reduce_scalar(elapsed, dist, "max"), out
+
+
+def reduce_scalar(x, dist=None, op="sum"):
+    """Scalar all-reduce across ranks (bookkeeping only; the data path has no collective)."""
+    if not dist:
+        return x
+    import torch
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,7 +121,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--records", type=int, default=100_000_000, help="records per GPU (C2: 100 M)")
     ap.add_argument("--codec", type=int, default=1, help="0 UNCOMPRESSED, 1 SNAPPY (C2)")
-    ap.add_argument("--cpu-sample", type=int, default=8_000_000, help="records for the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=24_000_000,
+                    help="records for the CPU baseline sample (~1.5 GB, ~16 s of single-core oracle work)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -87,10 +132,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     torch.cuda.set_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+    dist = dist_init(world, local_rank)
 
     import kpw
     import synth
@@ -110,26 +152,20 @@ def main():
     def step():
         return enc.encode(d_data.data_ptr(), d_off.data_ptr(), n, final=True)
 
+    stage_acc = np.zeros(10)
+
+    def timed():
+        info = step()
+        stage_acc[:] += np.array(enc.stage_times(), dtype=np.float64)[:10]
+        return info
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stage_acc = None
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        info = step()
-        st = np.array(enc.stage_times(), dtype=np.float64)
-        stage_acc = st if stage_acc is None else stage_acc + st
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, infos = timed_steps(timed, args.steps, 0, dist, torch.cuda.synchronize)
+    info = infos[-1]
+    # whole-job units: every rank's own partition
+    total_bytes = reduce_scalar(nbytes * args.steps, dist)
+    total_records = reduce_scalar(n * args.steps, dist)
 
     # per-step page statistics (for algorithmic bytes of the compression kernel)
     pages = enc.pages()
@@ -144,8 +180,8 @@ def main():
         return
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * nbytes * args.steps / elapsed / 1e9
-    rec_s = world * n * args.steps / elapsed
+    value = total_bytes / elapsed / 1e9
+    rec_s = total_records / elapsed
     # K1 decode: algorithmic bytes = record bytes + offsets in; columnar values out
     # (ts 8, user_id 4, status 4, price 8, score 8, key16 8+4, region 8+4 per record,
     #  presence/boolean bits n/8 per optional column + flag bits, raw sizes 4 per record)
@@ -163,7 +199,7 @@ def main():
                 frac=round(achieved / HBM_PEAK_GBPS, 5), traffic=None, algorithmic_bytes_per_launch=int(ab),
                 avg_launch_ms=round(ams, 4))
     cpu = None
-    if not args.no_cpu_baseline and world >= 1:
+    if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         threads = args.cpu_threads or min(16, os.cpu_count() or 8)
         cpu = cpu_baseline(synth.KIND_REC8, seed, args.cpu_sample, threads)
     out = {

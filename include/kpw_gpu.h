@@ -134,9 +134,10 @@ int kpw_encoder_encode(kpw_encoder *e, const uint8_t *d_data, const uint64_t *d_
 /* Copy page bodies [off, off+len) of the last batch to host memory. */
 int kpw_encoder_copy_pages(kpw_encoder *e, uint64_t off, uint64_t len, void *host_dst);
 
-/* Timing of the last encode: per-stage device milliseconds measured with HIP events on the
- * encoder's stream (index order: decode, plan, dictionary, rle, plain+stats, assemble,
- * compress, total). Returns number of entries written (<= cap). */
+/* Timing of the last encode: device milliseconds measured with HIP events on the encoder's
+ * stream.  Index order: [0] decode, [1] plan, [2] stats+dictionary, [3] rle,
+ * [4] layout+plain+write, [5] compress, [6] metadata, [7] total, [8] k_decode kernel alone,
+ * [9] k_snappy_frag kernel alone (0 when uncompressed).  Returns entries written (<= cap). */
 int kpw_encoder_stage_times(const kpw_encoder *e, float *ms, int cap);
 
 #ifdef __cplusplus

@@ -1,0 +1,57 @@
+"""N>1 bench bookkeeping on CPU (gloo, world_size 2): barrier-bracketed timing, max over
+ranks, whole-job unit sums.  The data path itself has no collective: each
+rank encodes its own partition, so only these scalars cross ranks."""
+import os
+import socket
+import sys
+import time
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import bench
+    dist = bench.dist_init(world, rank, backend="gloo")
+    calls = []
+
+    def step():
+        calls.append(1)
+        time.sleep(0.05 * (rank + 1))   # rank 1 is the slow one
+        return rank
+
+    elapsed, outs = bench.timed_steps(step, steps=3, warmup=2, dist=dist)
+    units = bench.reduce_scalar(100 * (rank + 1), dist)
+    q.put((rank, elapsed, len(calls), outs, units))
+    dist.destroy_process_group()
+
+
+def test_two_rank_timing_and_units():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, e0, c0, o0, u0), (r1, e1, c1, o1, u1) = res
+    assert c0 == c1 == 5                       # warmup 2 + exactly 3 timed steps
+    assert o0 == [0, 0, 0] and o1 == [1, 1, 1]
+    assert e0 == pytest.approx(e1)             # every rank reports the max over ranks
+    assert e0 >= 3 * 0.1 * 0.95                # ... which is the slow rank's time
+    assert u0 == u1 == 300                     # whole-job units = sum over ranks
