@@ -378,6 +378,19 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         }
     }
     const uint32_t nct = (uint32_t)ctj.size();
+    // Dictionary insertion order: tile k of every dictionary chunk before tile k+1 of any, so
+    // each chunk is scanned roughly in record order and a chunk that crosses the 1 MiB
+    // fallback threshold stops after a few tiles instead of inserting all of its values.
+    std::vector<uint32_t> dorder;
+    {
+        uint32_t maxnt = 0;
+        for (int ci = 0; ci < nch; ci++) if (ch[ci].is_dict) maxnt = std::max(maxnt, ccount[ci]);
+        for (uint32_t k = 0; k < maxnt; k++)
+            for (int ci = 0; ci < nch; ci++)
+                if (ch[ci].is_dict && k < ccount[ci]) dorder.push_back(cfirst[ci] + k);
+    }
+    ENS(d_dict_order, std::max<size_t>(1, dorder.size()) * 4);
+    if (!dorder.empty()) CK(hipMemcpyAsync(d_dict_order.p, dorder.data(), dorder.size() * 4, hipMemcpyHostToDevice, s));
     ENS(d_chunks, nch * sizeof(ChunkDesc)); ENS(d_ctile_chunk, nct * 4); ENS(d_ctile_first, nch * 4); ENS(d_ctile_count, nch * 4);
     ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
     ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8);
@@ -402,6 +415,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     a.max_dict_bytes = (uint32_t)props.dictionary_page_size;
     a.data_end = d_off + n;
     a.collision = d_collision.as<uint32_t>();
+    a.dict_order = d_dict_order.as<uint32_t>(); a.ndict_tiles = (uint32_t)dorder.size();
     uint32_t enpt = 0, enet = 0;
     RleScratch esc{};
     uint64_t body_tot = 0;
@@ -438,8 +452,9 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         if (!coll) break;
         if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
     }
-    ENS(d_body, body_tot + 16);
-    CK(hipMemsetAsync(d_body.p, 0, body_tot + 16, s));
+    // +512: K7 reads its input through 256-byte register windows that may run past the last page
+    ENS(d_body, body_tot + 512);
+    CK(hipMemsetAsync(d_body.p, 0, body_tot + 512, s));
     launch_chunk_write(a, d_body.as<uint8_t>(), s);
     if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), s);
     CK(hipGetLastError());

@@ -88,7 +88,7 @@ private:
         d_body;
     // snappy
     DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
-    DevBuf d_smeta, d_sblob, d_collision;
+    DevBuf d_smeta, d_sblob, d_collision, d_dict_order;
     hipEvent_t ev_[9] = {};
     hipEvent_t kev_[4] = {};
     std::vector<uint32_t> opt_idx_, bool_idx_;

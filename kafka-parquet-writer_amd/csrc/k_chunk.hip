@@ -222,7 +222,7 @@ constexpr uint32_t LDS_T = 2048;
 constexpr uint32_t LDS_PROBES = 32;
 
 __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
-                                                           const uint32_t *ctile_chunk, const uint32_t *ctile_first,
+                                                           const uint32_t *order, const uint32_t *ctile_chunk, const uint32_t *ctile_first,
                                                            uint64_t *ht_key, uint32_t *ht_min, uint32_t *slotof, uint32_t max_dict_bytes,
                                                            int exact, const uint64_t *data_end_p)
 {
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     __shared__ uint32_t lslot[LDS_T];
     __shared__ uint64_t lrec[LDS_T];
     const uint64_t data_end = *data_end_p;
-    const uint32_t t = blockIdx.x;
+    const uint32_t t = order[blockIdx.x];
     const uint32_t ci = ctile_chunk[t];
     ChunkDesc &C = ch[ci];
     __shared__ uint32_t skip;
@@ -662,8 +662,9 @@ void launch_chunk_stats(const ChunkArgs &a, hipStream_t s)
 
 void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_dict_insert, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
-                       a.ht_key, a.ht_min, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
+    if (a.ndict_tiles)
+        hipLaunchKernelGGL(k_dict_insert, dim3(a.ndict_tiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order,
+                           a.ctile_chunk, a.ctile_first, a.ht_key, a.ht_min, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
     hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
                        a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0);

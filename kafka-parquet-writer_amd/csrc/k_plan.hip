@@ -133,6 +133,31 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
     return wave_sum(part) + (a.P[r] - a.P[s]);
 }
 
+// memSize at record r for one lane, valid only when every walker is past its convergence
+// point (or has no further events): E_s(r) is then O(1) per column.
+__device__ uint64_t eval_mem_lane(const PlanArgs &a, const Walker *W, int64_t s, int64_t r)
+{
+    uint64_t m = a.P[r] - a.P[s];
+    for (int k = 0; k < a.nopt; k++) {
+        const Walker &w = W[k];
+        m += w.state == 1 ? (uint64_t)((int64_t)a.E[(uint64_t)k * (a.n + 1) + r] + w.delta) : w.eacc;
+    }
+    for (int k = 0; k < a.nbool; k++) {
+        const DevCol &c = a.cols[a.bool_cols[k]];
+        const uint64_t cnt = c.optional ? pc_at(c, (uint64_t)r) - pc_at(c, (uint64_t)s) : (uint64_t)(r - s);
+        m += (cnt + 7) / 8;
+    }
+    return m;
+}
+
+__device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walker *W, int64_t r)
+{
+    bool ok = true;
+    for (int k = threadIdx.x; k < a.nopt; k += 64)
+        ok = ok && (W[k].state == 2 || (W[k].state == 1 && W[k].conv_pos < r));
+    return __ballot(!ok) == 0;
+}
+
 __global__ void __launch_bounds__(64) k_plan(PlanArgs a)
 {
     __shared__ Walker W[MAX_COLS];
@@ -154,6 +179,34 @@ __global__ void __launch_bounds__(64) k_plan(PlanArgs a)
         bool cut = false;
         int64_t r = 0;
         while (s + rc <= n) {
+            // Far from the cut every next check is recordCount + 10000 (the clamp): once the
+            // walkers are converged, lanes evaluate memSize at the next 64 clamp-step check
+            // points and the scalar replay below takes parquet-mr's decisions over them,
+            // stopping where a decision leaves the clamp path (or cuts).
+            if (walkers_converged(a, W, s + rc)) {
+                const int64_t rcj = rc + 10000 * (int64_t)lane;
+                const uint64_t Mj = (s + rcj <= n) ? eval_mem_lane(a, W, s, s + rcj) : 0;
+                bool left = false;
+                for (int j = 0; j < 64; j++) {
+                    const int64_t rcv = rc + 10000 * (int64_t)j;
+                    if (s + rcv > n) { rc = rcv; left = true; break; }
+                    const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)Mj, j);
+                    const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(Mj >> 32), j);
+                    const int64_t M = (int64_t)(((uint64_t)mhi << 32) | mlo);
+                    const int64_t rs = M / rcv;
+                    if (M > T - 2 * rs) { cut = true; r = s + rcv; left = true; break; }
+                    const float q = __fdiv_rn((float)T, (float)rs);
+                    const int64_t est = jadd(rcv, java_f2l(q)) / 2;
+                    const int64_t lo = est > 100 ? est : 100;
+                    const int64_t hi = jadd(rcv, 10000);
+                    int64_t nc = lo < hi ? lo : hi;
+                    if (nc < rcv + 1) nc = rcv + 1;
+                    if (nc != rcv + 10000) { rc = nc; left = true; break; }
+                }
+                if (cut) break;
+                if (!left) rc += 10000 * 64;
+                continue;
+            }
             r = s + rc;
             const int64_t M = (int64_t)eval_mem(a, W, s, r);
             const int64_t rs = M / rc;

@@ -5,24 +5,34 @@
 // fragments with a fresh hash table each, so fragments are the unit of parallelism: one
 // wave per fragment; the fragment's uint16 hash table (<= 32 KiB) in LDS, input from L1/L2.
 // The wave runs the sequential match loop in lock-step (every lane holds the same scalar
-// state); literal copies and match-length extension use all 64 lanes.
+// state); literal copies and match-length extension use all 64 lanes.  The literal search
+// is batched: the positions it probes before the next match do not depend on the data
+// (ip += skip++ >> 5), so lane k probes the k-th next position; candidates come from the
+// table as it was before the batch, or from the nearest earlier probe with the same hash
+// (detected by a write/read-back on the table), and only probes up to the first hit are
+// committed to the table — the same table states and output as the sequential loop.
 #include "kpw_device.h"
 #include "kpw_chunk.h"
 
 namespace kpw {
 
 constexpr int SNAPPY_MAX_TABLE = 1 << 14;
+#ifndef SNAPPY_SEQ_PROBES
+#define SNAPPY_SEQ_PROBES 2     // sequential probes after each match before batching (tests/microbench/snappy_bench.hip)
+#endif
 
 // Input bytes are read straight from the page buffer in global memory (L1/L2 resident while
 // the wave scans its fragment); only the uint16 hash table (<= 32 KiB) lives in LDS, so five
 // fragments run per CU.  `src` is the fragment start; reads never go semantically beyond
 // the fragment (positions <= ip_limit+7 or < ip_end), and the page buffer is padded.
+typedef const __attribute__((address_space(1))) uint8_t g_u8;
+typedef const __attribute__((address_space(1))) uint32_t g_u32;
 struct Src {
-    const uint8_t *p;
+    g_u8 *p;
     __device__ __forceinline__ uint32_t ld32(uint32_t i) const
     {
         const uintptr_t a = (uintptr_t)(p + i);
-        const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+        g_u32 *w = (g_u32 *)(a & ~(uintptr_t)3);
         const uint32_t sh = (uint32_t)(a & 3) * 8;
         const uint32_t lo = w[0];
         return sh ? ((lo >> sh) | (w[1] << (32 - sh))) : lo;
@@ -31,6 +41,16 @@ struct Src {
 };
 
 __device__ __forceinline__ uint32_t sn_hash(uint32_t bytes, int shift) { return (bytes * 0x1e35a7bdu) >> shift; }
+
+__device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
+
+// sum_{x < v} floor(x / 32): the search loop's position after probes with skip values
+// s, s+1, ..., s+k-1 is ip + skip_sum(s+k) - skip_sum(s) (snappy: ip += skip++ >> 5)
+__device__ __forceinline__ uint32_t skip_sum(uint32_t v)
+{
+    const uint32_t q = v >> 5, r = v & 31;
+    return 16u * q * (q - 1u) + r * q;   // 32 * q(q-1)/2 for the whole blocks of 32, r * q for the rest
+}
 
 __device__ __forceinline__ uint32_t emit_literal(uint8_t *out, uint32_t op, const Src &in, uint32_t lit, uint32_t len, int lane)
 {
@@ -45,7 +65,12 @@ __device__ __forceinline__ uint32_t emit_literal(uint8_t *out, uint32_t op, cons
         while (nn > 0) { if (lane == 0) out[op] = (uint8_t)(nn & 0xff); op++; nn >>= 8; count++; }
         if (lane == 0) out[base] = (uint8_t)((59 + count) << 2);
     }
-    for (uint32_t i = lane; i < len; i += 64) out[op + i] = in.ld8(lit + i);
+    uint32_t i = lane;
+    for (; i + 192 < len; i += 256) {
+        const uint8_t b0 = in.ld8(lit + i), b1 = in.ld8(lit + i + 64), b2 = in.ld8(lit + i + 128), b3 = in.ld8(lit + i + 192);
+        out[op + i] = b0; out[op + i + 64] = b1; out[op + i + 128] = b2; out[op + i + 192] = b3;
+    }
+    for (; i < len; i += 64) out[op + i] = in.ld8(lit + i);
     return op + len;
 }
 
@@ -91,6 +116,7 @@ __device__ __forceinline__ uint32_t find_match_length(const Src &in, uint32_t s1
     }
 }
 
+template <int SEQ>
 __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
 {
     __shared__ uint16_t table[SNAPPY_MAX_TABLE];
@@ -101,7 +127,7 @@ __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
     const uint64_t plen = a.page_len[pg];
     const uint64_t fstart = (uint64_t)fi * SNAPPY_FRAG;
     const uint32_t n = (uint32_t)((plen - fstart) < SNAPPY_FRAG ? (plen - fstart) : SNAPPY_FRAG);
-    const Src in{a.in + a.page_off[pg] + fstart};
+    const Src in{(g_u8 *)(a.in + a.page_off[pg] + fstart)};
     uint32_t tsize = 256;
     while (tsize < SNAPPY_MAX_TABLE && tsize < n) tsize <<= 1;
     for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
@@ -117,21 +143,83 @@ __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
     if (n >= 15) {
         const uint32_t ip_limit = n - 15;
         ip = 1;
-        uint32_t next_hash = sn_hash(in.ld32(ip), shift);
         for (;;) {
+            // ---- literal search: the first SEQ probes one at a time (short literals between
+            // nearby matches are the common case on compressible pages), then 64 probe
+            // positions per step (see header comment)
             uint32_t skip = 32;
-            uint32_t next_ip = ip;
             uint32_t candidate;
+            int nseq = 0;
+            uint32_t cur_s = SEQ > 0 ? in.ld32(ip) : 0u;
             for (;;) {
-                ip = next_ip;
-                const uint32_t hash = next_hash;
-                const uint32_t step = skip++ >> 5;
-                next_ip = ip + step;
-                if (next_ip > ip_limit) goto emit_remainder;
-                next_hash = sn_hash(in.ld32(next_ip), shift);
-                candidate = table[hash];
-                if (lane == 0) table[hash] = (uint16_t)ip;
-                if (in.ld32(ip) == in.ld32(candidate)) break;
+                if (nseq < SEQ) {
+                    nseq++;
+                    const uint32_t h = sn_hash(cur_s, shift);
+                    const uint32_t next_ip = ip + (skip++ >> 5);
+                    if (next_ip > ip_limit) goto emit_remainder;
+                    const uint32_t nxt = in.ld32(next_ip);   // issued before the dependent table/candidate loads
+                    candidate = table[h];
+                    table[h] = (uint16_t)ip;
+                    if (cur_s == in.ld32(candidate)) break;
+                    ip = next_ip;
+                    cur_s = nxt;
+                    continue;
+                }
+                const uint32_t base_f = skip_sum(skip);
+                const uint32_t ipk = ip + skip_sum(skip + lane) - base_f;         // lane k's probe position
+                const uint32_t ipk1 = ip + skip_sum(skip + lane + 1) - base_f;    // its next_ip
+                const bool valid = ipk1 <= ip_limit;
+                const uint64_t vmask = __ballot(valid);
+                const uint32_t cur = valid ? in.ld32(ipk) : 0u;
+                const uint32_t h = sn_hash(cur, shift);
+                // compiler barriers (cbar): the read-back must really be issued after every
+                // lane's store (no store-to-load forwarding), and the lane-ordered store loops
+                // below must not be merged into one store whose same-address winner would be
+                // unspecified.  LDS operations of one wave execute in program order.
+                uint32_t old = 0;
+                if (valid) old = table[h];
+                if (valid) table[h] = (uint16_t)ipk;
+                cbar();
+                uint32_t chk = ipk;
+                if (valid) chk = table[h];
+                const uint64_t losers = __ballot(valid && (uint16_t)chk != (uint16_t)ipk);
+                uint32_t cand = old;
+                uint64_t grp = 0;   // lanes sharing my hash (only when some hash repeats)
+                if (losers) {
+                    // several probes share a hash: group them (one ballot per repeated hash);
+                    // a probe's candidate is then the nearest earlier probe of its group
+                    uint64_t L = losers;
+                    while (L) {
+                        const int leader = __ffsll((long long)L) - 1;
+                        const uint32_t hv = __builtin_amdgcn_readlane(h, leader);
+                        const uint64_t g = __ballot(valid && h == hv);
+                        if ((g >> lane) & 1) grp = g;
+                        L &= ~g;
+                    }
+                    const uint64_t below = grp & ((1ull << lane) - 1);
+                    const int pred = below ? 63 - __clzll((long long)below) : lane;
+                    const uint32_t ipp = __shfl(ipk, pred, 64);
+                    if (below) cand = ipp;
+                }
+                const uint64_t hit = __ballot(valid && in.ld32(cand) == cur);
+                if (hit) {
+                    const int m = __ffsll((long long)hit) - 1;
+                    // probes after the hit never ran: put their slots back; among the probes
+                    // up to the hit, the last of each hash group holds the slot
+                    if (valid && lane > m) table[h] = (uint16_t)old;
+                    if (losers) {
+                        cbar();
+                        const uint64_t upto = m == 63 ? ~0ull : ((2ull << m) - 1);
+                        if (lane <= m && ((grp & upto) >> lane) <= 1) table[h] = (uint16_t)ipk;
+                    }
+                    ip = __shfl(ipk, m, 64);
+                    candidate = __shfl(cand, m, 64);
+                    break;
+                }
+                if (vmask != ~0ull) goto emit_remainder;   // the first invalid probe ends the fragment
+                if (losers && (grp >> lane) <= 1) table[h] = (uint16_t)ipk;   // last of each group wins
+                ip = ip + skip_sum(skip + 64) - base_f;
+                skip += 64;
             }
             op = emit_literal(out, op, in, next_emit, ip - next_emit, lane);
             uint32_t input_lo, input_hi;
@@ -152,12 +240,529 @@ __global__ void __launch_bounds__(64) k_snappy_frag(SnappyArgs a)
                 if (lane == 0) table[cur_hash] = (uint16_t)ip;
                 if (b1 != candidate_bytes) break;
             }
-            next_hash = sn_hash((input_lo >> 16) | (input_hi << 16), shift);
             ++ip;
         }
     }
 emit_remainder:
     if (next_emit < ip_end) op = emit_literal(out, op, in, next_emit, ip_end - next_emit, lane);
+    if (lane == 0) a.frag_len[f] = op;
+}
+
+// ------------------------------------------------------------------ register-window variant
+// The match loop above pays a global-memory round trip (plus the wait for earlier byte
+// stores, which share vmcnt) for nearly every step.  Here the 64 lanes hold a 256-byte
+// window of the fragment input, one dword each: reads near ip (and the usual nearby match
+// candidate) are two v_readlane; the window is refilled with one coalesced load when ip
+// moves past it.  Output bytes accumulate in a second 256-byte register window flushed with
+// one coalesced dword store.  The algorithm (and so every output byte) is unchanged.
+typedef __attribute__((address_space(1))) uint32_t g_u32w;
+
+__device__ __forceinline__ uint32_t funnel(uint32_t x, uint32_t y, uint32_t sh) { return sh ? (x >> sh) | (y << (32 - sh)) : x; }
+
+struct InWin {
+    uintptr_t base;   // absolute address of fragment byte 0
+    uintptr_t lo;     // lowest address read (base & ~3: inside the page buffer)
+    uintptr_t A;      // 4-aligned absolute address of the window start
+    uint32_t w;       // bytes [A + 4 lane, A + 4 lane + 4)
+    int lane;
+    // called with all 64 lanes active (wave-uniform control flow only)
+    __device__ __forceinline__ void refill(uintptr_t abs)
+    {
+        A = abs >= lo + 64 ? ((abs - 64) & ~(uintptr_t)3) : lo;
+        w = *(g_u32 *)(A + 4 * (uintptr_t)lane);
+    }
+    __device__ __forceinline__ uint32_t gld32(uintptr_t abs) const
+    {
+        const uintptr_t a = abs & ~(uintptr_t)3;
+        const uint32_t x = a >= lo ? *(g_u32 *)a : 0u;
+        const uint32_t y = *(g_u32 *)(a + 4);
+        return funnel(x, y, (uint32_t)(abs & 3) * 8);
+    }
+    // 4 bytes at fragment position p (wave-uniform p)
+    __device__ __forceinline__ uint32_t ld32(uint32_t p)
+    {
+        const uintptr_t abs = base + p;
+        uintptr_t d = abs - A;
+        if (d > 248) {
+            if (abs < A) return gld32(abs);   // behind the window: one global read
+            refill(abs);
+            d = abs - A;
+        }
+        const uint32_t l0 = (uint32_t)d >> 2;
+        const uint32_t x = __builtin_amdgcn_readlane(w, l0);
+        const uint32_t y = __builtin_amdgcn_readlane(w, l0 + 1);
+        return funnel(x, y, ((uint32_t)d & 3) * 8);
+    }
+};
+
+struct OutWin {
+    g_u32w *out;
+    uint32_t ob;      // output position of the window start (multiple of 256)
+    uint32_t w;
+    int lane;
+    __device__ __forceinline__ void flush() { out[(ob >> 2) + lane] = w; w = 0; ob += 256; }
+    __device__ __forceinline__ void put8(uint32_t op, uint32_t b)
+    {
+        if (op - ob >= 256) flush();
+        const uint32_t d = op - ob;
+        if ((uint32_t)lane == (d >> 2)) w |= (b & 0xffu) << ((d & 3) * 8);
+    }
+};
+
+// output [op, op+len) = input [lit, lit+len)
+__device__ __forceinline__ void copy_lit(OutWin &ow, InWin &in, uint32_t op, uint32_t lit, uint32_t len)
+{
+    const int lane = ow.lane;
+    uint32_t done = 0;
+    while (done < len) {
+        const uint32_t opc = op + done;
+        if (opc - ow.ob >= 256) ow.flush();
+        const uint32_t room = ow.ob + 256 - opc;
+        const uint32_t c = (len - done) < room ? (len - done) : room;
+        const int32_t q0 = (int32_t)(ow.ob + 4 * lane);
+        const bool touch = q0 + 4 > (int32_t)opc && q0 < (int32_t)(opc + c);
+        const intptr_t src = (intptr_t)lit + (intptr_t)done + (intptr_t)q0 - (intptr_t)opc;   // >= -3
+        const uintptr_t sabs = in.base + src;
+        const uintptr_t d = sabs - in.A;
+        const uint64_t need = __ballot(touch);
+        const uint64_t ok = __ballot(touch && d <= 248);
+        uint32_t v = 0;
+        if (ok == need) {
+            const uint32_t l0 = touch ? (uint32_t)d >> 2 : 0u;
+            const uint32_t x = __shfl(in.w, (int)l0, 64);
+            const uint32_t y = __shfl(in.w, (int)l0 + 1 < 64 ? (int)l0 + 1 : 63, 64);
+            v = funnel(x, y, ((uint32_t)d & 3) * 8);
+        } else if (touch) {
+            v = in.gld32(sabs);
+        }
+        if (touch) {
+            const int lo_k = (int32_t)opc > q0 ? (int32_t)opc - q0 : 0;
+            const int hi_k = (int32_t)(opc + c) - q0 < 4 ? (int32_t)(opc + c) - q0 : 4;
+            const uint32_t mhi = hi_k >= 4 ? 0xffffffffu : ((1u << (8 * hi_k)) - 1);
+            const uint32_t mlo = (0xffffffffu << (8 * lo_k));
+            ow.w |= v & mhi & mlo;
+        }
+        done += c;
+    }
+}
+
+__device__ __forceinline__ uint32_t emit_literal_w(OutWin &ow, InWin &in, uint32_t op, uint32_t lit, uint32_t len)
+{
+    const uint32_t n = len - 1;
+    if (n < 60) {
+        ow.put8(op++, n << 2);
+    } else {
+        int count = 0;
+        for (uint32_t nn = n; nn > 0; nn >>= 8) count++;
+        ow.put8(op++, (uint32_t)(59 + count) << 2);
+        for (uint32_t nn = n; nn > 0; nn >>= 8) ow.put8(op++, nn & 0xff);
+    }
+    copy_lit(ow, in, op, lit, len);
+    return op + len;
+}
+
+__device__ __forceinline__ uint32_t emit_copy_lt64_w(OutWin &ow, uint32_t op, uint32_t offset, uint32_t len)
+{
+    if (len < 12 && offset < 2048) {
+        ow.put8(op, 1 + ((len - 4) << 2) + ((offset >> 8) << 5));
+        ow.put8(op + 1, offset & 0xff);
+        return op + 2;
+    }
+    ow.put8(op, 2 + ((len - 1) << 2));
+    ow.put8(op + 1, offset & 0xff);
+    ow.put8(op + 2, offset >> 8);
+    return op + 3;
+}
+
+__device__ __forceinline__ uint32_t emit_copy_w(OutWin &ow, uint32_t op, uint32_t offset, uint32_t len)
+{
+    while (len >= 68) { op = emit_copy_lt64_w(ow, op, offset, 64); len -= 64; }
+    if (len > 64) { op = emit_copy_lt64_w(ow, op, offset, 60); len -= 60; }
+    return emit_copy_lt64_w(ow, op, offset, len);
+}
+
+// matching bytes of [s1..) vs [s2..s2_limit): up to 16 bytes through the window, then 64
+// lanes compare 64 bytes per step from global memory (long matches only)
+__device__ __forceinline__ uint32_t find_match_length_w(InWin &in, const Src &g, uint32_t s1, uint32_t s2, uint32_t s2_limit, int lane)
+{
+    uint32_t m = 0;
+#pragma unroll 1
+    for (int k = 0; k < 4 && s2 + m + 4 <= s2_limit; k++) {
+        const uint32_t a = in.ld32(s1 + m);
+        const uint32_t b = in.ld32(s2 + m);
+        const uint32_t x = a ^ b;
+        if (x) return m + ((uint32_t)(__ffs((int)x) - 1) >> 3);
+        m += 4;
+    }
+    for (;;) {
+        const uint32_t p2 = s2 + m + lane;
+        const bool ok = p2 < s2_limit && g.ld8(s1 + m + lane) == g.ld8(p2);
+        const uint64_t bad = __ballot(!ok);
+        if (bad) return m + (uint32_t)(__ffsll((long long)bad) - 1);
+        m += 64;
+    }
+}
+
+template <int SEQ>
+__global__ void __launch_bounds__(64) k_snappy_win(SnappyArgs a)
+{
+    __shared__ uint16_t table[SNAPPY_MAX_TABLE];
+    const int lane = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    const uint32_t pg = a.frag_page[f];
+    const uint32_t fi = a.frag_idx[f];
+    const uint64_t plen = a.page_len[pg];
+    const uint64_t fstart = (uint64_t)fi * SNAPPY_FRAG;
+    const uint32_t n = (uint32_t)((plen - fstart) < SNAPPY_FRAG ? (plen - fstart) : SNAPPY_FRAG);
+    const uint8_t *fbase = a.in + a.page_off[pg] + fstart;
+    const Src g{(g_u8 *)fbase};
+    InWin in;
+    in.base = (uintptr_t)fbase;
+    in.lo = in.base & ~(uintptr_t)3;
+    in.lane = lane;
+    in.refill(in.base);
+    OutWin ow;
+    ow.out = (g_u32w *)(a.frag_out + (uint64_t)f * SNAPPY_FRAG_CAP);
+    ow.ob = 0;
+    ow.w = 0;
+    ow.lane = lane;
+    uint32_t tsize = 256;
+    while (tsize < SNAPPY_MAX_TABLE && tsize < n) tsize <<= 1;
+    for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
+    __syncthreads();
+
+    uint32_t op = 0;
+    int shift = 32;
+    for (uint32_t t = tsize; t > 1; t >>= 1) shift--;
+    const uint32_t ip_end = n;
+    uint32_t next_emit = 0;
+    uint32_t ip = 0;
+    if (n >= 15) {
+        const uint32_t ip_limit = n - 15;
+        ip = 1;
+        for (;;) {
+            uint32_t skip = 32;
+            uint32_t candidate;
+            int nseq = 0;
+            uint32_t cur_s = SEQ > 0 ? in.ld32(ip) : 0u;
+            for (;;) {
+                if (nseq < SEQ) {
+                    nseq++;
+                    const uint32_t h = sn_hash(cur_s, shift);
+                    const uint32_t next_ip = ip + (skip++ >> 5);
+                    if (next_ip > ip_limit) goto emit_remainder;
+                    candidate = table[h];
+                    table[h] = (uint16_t)ip;
+                    const uint32_t cb = in.ld32(candidate);
+                    if (cur_s == cb) break;
+                    ip = next_ip;
+                    cur_s = in.ld32(ip);
+                    continue;
+                }
+                const uint32_t base_f = skip_sum(skip);
+                const uint32_t ipk = ip + skip_sum(skip + lane) - base_f;
+                const uint32_t ipk1 = ip + skip_sum(skip + lane + 1) - base_f;
+                const bool valid = ipk1 <= ip_limit;
+                const uint64_t vmask = __ballot(valid);
+                const uint32_t cur = valid ? g.ld32(ipk) : 0u;
+                const uint32_t h = sn_hash(cur, shift);
+                uint32_t old = 0;
+                if (valid) old = table[h];
+                if (valid) table[h] = (uint16_t)ipk;
+                cbar();
+                uint32_t chk = ipk;
+                if (valid) chk = table[h];
+                const uint64_t losers = __ballot(valid && (uint16_t)chk != (uint16_t)ipk);
+                uint32_t cand = old;
+                uint64_t grp = 0;
+                if (losers) {
+                    uint64_t L = losers;
+                    while (L) {
+                        const int leader = __ffsll((long long)L) - 1;
+                        const uint32_t hv = __builtin_amdgcn_readlane(h, leader);
+                        const uint64_t gm = __ballot(valid && h == hv);
+                        if ((gm >> lane) & 1) grp = gm;
+                        L &= ~gm;
+                    }
+                    const uint64_t below = grp & ((1ull << lane) - 1);
+                    const int pred = below ? 63 - __clzll((long long)below) : lane;
+                    const uint32_t ipp = __shfl(ipk, pred, 64);
+                    if (below) cand = ipp;
+                }
+                const uint64_t hit = __ballot(valid && g.ld32(cand) == cur);
+                if (hit) {
+                    const int m = __ffsll((long long)hit) - 1;
+                    if (valid && lane > m) table[h] = (uint16_t)old;
+                    if (losers) {
+                        cbar();
+                        const uint64_t upto = m == 63 ? ~0ull : ((2ull << m) - 1);
+                        if (lane <= m && ((grp & upto) >> lane) <= 1) table[h] = (uint16_t)ipk;
+                    }
+                    ip = __shfl(ipk, m, 64);
+                    candidate = __shfl(cand, m, 64);
+                    break;
+                }
+                if (vmask != ~0ull) goto emit_remainder;
+                if (losers && (grp >> lane) <= 1) table[h] = (uint16_t)ipk;
+                ip = ip + skip_sum(skip + 64) - base_f;
+                skip += 64;
+            }
+            ip = __builtin_amdgcn_readfirstlane(ip);
+            candidate = __builtin_amdgcn_readfirstlane(candidate);
+            op = emit_literal_w(ow, in, op, next_emit, ip - next_emit);
+            uint32_t input_lo, input_hi;
+            for (;;) {
+                const uint32_t base = ip;
+                const uint32_t matched = 4 + find_match_length_w(in, g, candidate + 4, ip + 4, ip_end, lane);
+                ip += matched;
+                op = emit_copy_w(ow, op, base - candidate, matched);
+                next_emit = ip;
+                if (ip >= ip_limit) goto emit_remainder;
+                input_lo = in.ld32(ip - 1);
+                input_hi = in.ld32(ip + 3);
+                const uint32_t b1 = (input_lo >> 8) | (input_hi << 24);
+                table[sn_hash(input_lo, shift)] = (uint16_t)(ip - 1);
+                const uint32_t cur_hash = sn_hash(b1, shift);
+                candidate = __builtin_amdgcn_readfirstlane((uint32_t)table[cur_hash]);
+                table[cur_hash] = (uint16_t)ip;
+                const uint32_t candidate_bytes = in.ld32(candidate);
+                if (b1 != candidate_bytes) break;
+            }
+            ++ip;
+        }
+    }
+emit_remainder:
+    if (next_emit < ip_end) op = emit_literal_w(ow, in, op, next_emit, ip_end - next_emit);
+    if (op > ow.ob) ow.out[(ow.ob >> 2) + lane] = ow.w;
+    if (lane == 0) a.frag_len[f] = op;
+}
+
+// ------------------------------------------------------------------ scalar variant
+// All match-loop state is wave-uniform, so it lives in SGPRs: input bytes come through the
+// scalar cache (s_load, lgkmcnt) and output bytes leave as lane-parallel byte stores of a
+// uniform 64-bit word.  The hot path never waits on vmcnt, so output stores never sit on
+// its critical path.  Long matches, long literals and the batched search keep vector code.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16 bytes at 4-aligned wave-uniform addresses a0 and a1 (SMEM; inputs are never written by
+// this kernel, and the page buffer is padded past its last page)
+__device__ __forceinline__ void sload2(uint64_t a0, uint64_t a1, u32x4 &x, u32x4 &y)
+{
+    asm volatile("s_load_dwordx4 %0, %2, 0x0\n\t"
+                 "s_load_dwordx4 %1, %3, 0x0\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(x), "=&s"(y)
+                 : "s"(a0), "s"(a1));
+}
+__device__ __forceinline__ void sload1(uint64_t a0, u32x4 &x)
+{
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(x)
+                 : "s"(a0));
+}
+// 8 bytes starting (addr & 3) bytes into the 16 loaded at addr & ~3
+__device__ __forceinline__ uint64_t pick64(const u32x4 &v, uint32_t sh8)
+{
+    const uint64_t lo = ((uint64_t)v.y << 32) | v.x;
+    const uint64_t hi = ((uint64_t)v.w << 32) | v.z;
+    return sh8 ? (lo >> sh8) | (hi << (64 - sh8)) : lo;
+}
+
+struct SIn {
+    uint64_t base;   // absolute address of fragment byte 0
+    __device__ __forceinline__ uint64_t ld64(uint32_t p) const
+    {
+        const uint64_t a = base + p;
+        u32x4 v;
+        sload1(a & ~3ull, v);
+        return pick64(v, (uint32_t)(a & 3) * 8);
+    }
+    __device__ __forceinline__ void ld64x2(uint32_t p, uint32_t q, uint64_t &vp, uint64_t &vq) const
+    {
+        const uint64_t a = base + p, b = base + q;
+        u32x4 x, y;
+        sload2(a & ~3ull, b & ~3ull, x, y);
+        vp = pick64(x, (uint32_t)(a & 3) * 8);
+        vq = pick64(y, (uint32_t)(b & 3) * 8);
+    }
+    __device__ __forceinline__ uint32_t ld32(uint32_t p) const { return (uint32_t)ld64(p); }
+};
+
+__device__ __forceinline__ uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// out[op .. op+c) = bytes of the uniform word w (c <= 8), one lane per byte
+__device__ __forceinline__ void st_word(uint8_t *out, uint32_t op, uint64_t w, uint32_t c, int lane)
+{
+    if ((uint32_t)lane < c) out[op + lane] = (uint8_t)(w >> (8 * lane));
+}
+
+__device__ __forceinline__ uint32_t emit_copy_lt64_s(uint8_t *out, uint32_t op, uint32_t offset, uint32_t len, int lane)
+{
+    if (len < 12 && offset < 2048) {
+        st_word(out, op, (1 + ((len - 4) << 2) + ((offset >> 8) << 5)) | ((offset & 0xff) << 8), 2, lane);
+        return op + 2;
+    }
+    st_word(out, op, (2 + ((len - 1) << 2)) | ((offset & 0xff) << 8) | ((offset >> 8) << 16), 3, lane);
+    return op + 3;
+}
+
+__device__ __forceinline__ uint32_t emit_copy_s(uint8_t *out, uint32_t op, uint32_t offset, uint32_t len, int lane)
+{
+    while (len >= 68) { op = emit_copy_lt64_s(out, op, offset, 64, lane); len -= 64; }
+    if (len > 64) { op = emit_copy_lt64_s(out, op, offset, 60, lane); len -= 60; }
+    return emit_copy_lt64_s(out, op, offset, len, lane);
+}
+
+__device__ __forceinline__ uint32_t emit_literal_s(uint8_t *out, uint32_t op, const SIn &si, const Src &g, uint32_t lit,
+                                                   uint32_t len, int lane)
+{
+    if (len <= 7) {   // tag + bytes in one word
+        const uint64_t b = si.ld64(lit) & ((1ull << (8 * len)) - 1);
+        st_word(out, op, ((uint64_t)((len - 1) << 2)) | (b << 8), 1 + len, lane);
+        return op + 1 + len;
+    }
+    return emit_literal(out, op, g, lit, len, lane);
+}
+
+// matching bytes of [s1..) vs [s2..s2_limit): 8 bytes per scalar step for up to 64 bytes,
+// then 64 lanes compare 64 bytes per step (long matches and the fragment tail)
+__device__ __forceinline__ uint32_t find_match_length_s(const SIn &si, const Src &g, uint32_t s1, uint32_t s2,
+                                                        uint32_t s2_limit, int lane)
+{
+    uint32_t m = 0;
+    while (m < 64 && s2 + m + 8 <= s2_limit) {
+        uint64_t a, b;
+        si.ld64x2(s1 + m, s2 + m, a, b);
+        const uint64_t x = a ^ b;
+        if (x) return m + ((uint32_t)__builtin_ctzll(x) >> 3);
+        m += 8;
+    }
+    for (;;) {
+        const uint32_t p2 = s2 + m + lane;
+        const bool ok = p2 < s2_limit && g.ld8(s1 + m + lane) == g.ld8(p2);
+        const uint64_t bad = __ballot(!ok);
+        if (bad) return m + (uint32_t)(__ffsll((long long)bad) - 1);
+        m += 64;
+    }
+}
+
+template <int SEQ>
+__global__ void __launch_bounds__(64) k_snappy_s(SnappyArgs a)
+{
+    __shared__ uint16_t table[SNAPPY_MAX_TABLE];
+    const int lane = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    const uint32_t pg = a.frag_page[f];
+    const uint32_t fi = a.frag_idx[f];
+    const uint64_t plen = a.page_len[pg];
+    const uint64_t fstart = (uint64_t)fi * SNAPPY_FRAG;
+    const uint32_t n = (uint32_t)((plen - fstart) < SNAPPY_FRAG ? (plen - fstart) : SNAPPY_FRAG);
+    const uint8_t *fbase = a.in + a.page_off[pg] + fstart;
+    const Src g{(g_u8 *)fbase};
+    const SIn si{(uint64_t)(uintptr_t)fbase};
+    uint32_t tsize = 256;
+    while (tsize < SNAPPY_MAX_TABLE && tsize < n) tsize <<= 1;
+    for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
+    __syncthreads();
+
+    uint8_t *out = a.frag_out + (uint64_t)f * SNAPPY_FRAG_CAP;
+    uint32_t op = 0;
+    int shift = 32;
+    for (uint32_t t = tsize; t > 1; t >>= 1) shift--;
+    const uint32_t ip_end = n;
+    uint32_t next_emit = 0;
+    uint32_t ip = 0;
+    if (n >= 15) {
+        const uint32_t ip_limit = n - 15;
+        ip = 1;
+        for (;;) {
+            uint32_t skip = 32;
+            uint32_t candidate;
+            int nseq = 0;
+            for (;;) {
+                if (nseq < SEQ) {
+                    nseq++;
+                    const uint32_t next_ip = ip + (skip++ >> 5);
+                    if (next_ip > ip_limit) goto emit_remainder;
+                    const uint32_t cur_s = si.ld32(ip);
+                    const uint32_t h = sn_hash(cur_s, shift);
+                    candidate = ufl(table[h]);
+                    table[h] = (uint16_t)ip;
+                    if (cur_s == si.ld32(candidate)) break;
+                    ip = next_ip;
+                    continue;
+                }
+                const uint32_t base_f = skip_sum(skip);
+                const uint32_t ipk = ip + skip_sum(skip + lane) - base_f;
+                const uint32_t ipk1 = ip + skip_sum(skip + lane + 1) - base_f;
+                const bool valid = ipk1 <= ip_limit;
+                const uint64_t vmask = __ballot(valid);
+                const uint32_t cur = valid ? g.ld32(ipk) : 0u;
+                const uint32_t h = sn_hash(cur, shift);
+                uint32_t old = 0;
+                if (valid) old = table[h];
+                if (valid) table[h] = (uint16_t)ipk;
+                cbar();
+                uint32_t chk = ipk;
+                if (valid) chk = table[h];
+                const uint64_t losers = __ballot(valid && (uint16_t)chk != (uint16_t)ipk);
+                uint32_t cand = old;
+                uint64_t grp = 0;
+                if (losers) {
+                    uint64_t L = losers;
+                    while (L) {
+                        const int leader = __ffsll((long long)L) - 1;
+                        const uint32_t hv = __builtin_amdgcn_readlane(h, leader);
+                        const uint64_t gm = __ballot(valid && h == hv);
+                        if ((gm >> lane) & 1) grp = gm;
+                        L &= ~gm;
+                    }
+                    const uint64_t below = grp & ((1ull << lane) - 1);
+                    const int pred = below ? 63 - __clzll((long long)below) : lane;
+                    const uint32_t ipp = __shfl(ipk, pred, 64);
+                    if (below) cand = ipp;
+                }
+                const uint64_t hit = __ballot(valid && g.ld32(cand) == cur);
+                if (hit) {
+                    const int m = __ffsll((long long)hit) - 1;
+                    if (valid && lane > m) table[h] = (uint16_t)old;
+                    if (losers) {
+                        cbar();
+                        const uint64_t upto = m == 63 ? ~0ull : ((2ull << m) - 1);
+                        if (lane <= m && ((grp & upto) >> lane) <= 1) table[h] = (uint16_t)ipk;
+                    }
+                    ip = __builtin_amdgcn_readlane(ipk, m);
+                    candidate = __builtin_amdgcn_readlane(cand, m);
+                    break;
+                }
+                if (vmask != ~0ull) goto emit_remainder;
+                if (losers && (grp >> lane) <= 1) table[h] = (uint16_t)ipk;
+                ip = ip + skip_sum(skip + 64) - base_f;
+                skip += 64;
+            }
+            op = emit_literal_s(out, op, si, g, next_emit, ip - next_emit, lane);
+            for (;;) {
+                const uint32_t base = ip;
+                const uint32_t matched = 4 + find_match_length_s(si, g, candidate + 4, ip + 4, ip_end, lane);
+                ip += matched;
+                op = emit_copy_s(out, op, base - candidate, matched, lane);
+                next_emit = ip;
+                if (ip >= ip_limit) goto emit_remainder;
+                const uint64_t in8 = si.ld64(ip - 1);   // bytes [ip-1, ip+7)
+                const uint32_t input_lo = (uint32_t)in8;
+                const uint32_t b1 = (uint32_t)(in8 >> 8);
+                table[sn_hash(input_lo, shift)] = (uint16_t)(ip - 1);
+                const uint32_t cur_hash = sn_hash(b1, shift);
+                candidate = ufl(table[cur_hash]);
+                table[cur_hash] = (uint16_t)ip;
+                if (b1 != si.ld32(candidate)) break;
+            }
+            ++ip;
+        }
+    }
+emit_remainder:
+    if (next_emit < ip_end) op = emit_literal(out, op, g, next_emit, ip_end - next_emit, lane);
     if (lane == 0) a.frag_len[f] = op;
 }
 
@@ -212,7 +817,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_copy(SnappyArgs a)
 void launch_snappy(const SnappyArgs &a, hipStream_t s)
 {
     if (!a.nfrags) return;
-    hipLaunchKernelGGL(k_snappy_frag, dim3(a.nfrags), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_snappy_s<SNAPPY_SEQ_PROBES>, dim3(a.nfrags), dim3(64), 0, s, a);
 }
 
 void launch_snappy_finish(const SnappyArgs &a, const uint32_t *page_frag0, hipStream_t s)

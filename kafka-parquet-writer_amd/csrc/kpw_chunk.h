@@ -27,6 +27,8 @@ struct ChunkArgs {
     int32_t exact_strings;         // 1: BYTE_ARRAY dictionary keys compared byte-for-byte (collision retry)
     const uint64_t *data_end;      // device pointer to offsets[n] (end of the record bytes)
     uint32_t *collision;           // device flag: a hash-keyed string dictionary failed verification
+    const uint32_t *dict_order;    // dictionary chunk tiles, interleaved across chunks
+    uint32_t ndict_tiles;
 };
 
 inline void seg_tile_scan_u32(const uint32_t *in, uint32_t *out, const uint32_t *seg, uint32_t n, hipStream_t s)
@@ -61,7 +63,9 @@ struct SnappyArgs {
     uint64_t *tot;               // [0] total compressed bytes
 };
 constexpr uint32_t SNAPPY_FRAG = 65536;
-constexpr uint32_t SNAPPY_FRAG_CAP = 32 + SNAPPY_FRAG + SNAPPY_FRAG / 6 + 16;
+// per-fragment output slot: max compressed length (32 + n + n/6) rounded up to the 256-byte
+// output window, plus one window of slack for the final partial flush
+constexpr uint32_t SNAPPY_FRAG_CAP = ((32 + SNAPPY_FRAG + SNAPPY_FRAG / 6 + 255) / 256) * 256 + 256;
 void launch_snappy(const SnappyArgs &a, hipStream_t s);
 
 }  // namespace kpw

@@ -51,6 +51,19 @@ def test_fallback_highcard_large():
     assert not errs, "\n".join(errs[:12])
 
 
+@pytest.mark.parametrize("kind,n,block_size", [(synth.KIND_REC8, 400_000, 2 * MiB),
+                                               (synth.KIND_REC8, 700_000, 12 * MiB),
+                                               (synth.KIND_SAMPLE, 300_000, 3 * MiB)],
+                         ids=["rec8_2MiB", "rec8_12MiB", "sample_3MiB"])
+def test_planner_clamp_regime(kind, n, block_size):
+    # row groups of ~10^5 records: most checks take the recordCount + 10000 clamp, which the
+    # planner evaluates 64 check points at a time once the def-level walkers converge
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, 0xC0FFEE07, n, param=20)
+    errs = gh.compare_pages(schema, data, offs, codec=1, block_size=block_size)
+    assert not errs, "\n".join(errs[:12])
+
+
 def test_edge_cases():
     cls = protoutil.message_class(synth.SAMPLE)
     recs = []
@@ -66,6 +79,62 @@ def test_edge_cases():
     for codec in (0, 1):
         errs = gh.compare_pages(synth.SAMPLE, data, offs, codec=codec)
         assert not errs, "\n".join(errs[:12])
+
+
+def _varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _snappy_strings(pattern, rng):
+    """Query strings whose PLAIN page stresses one Snappy regime (multi-fragment pages)."""
+    out = []
+    if pattern == "random":          # incompressible: long literal searches, skip growth
+        for _ in range(1500):
+            out.append(rng.integers(0, 256, int(rng.integers(0, 400)), dtype=np.uint8).tobytes())
+    elif pattern == "periodic":      # short periods: back-to-back matches, table churn
+        for i in range(2500):
+            p = 1 + i % 37
+            unit = rng.integers(0, 256, p, dtype=np.uint8).tobytes()
+            out.append((unit * (200 // p + 1))[: int(rng.integers(1, 200))])
+    elif pattern == "zeros":         # long runs: copies split at 64/68 bytes
+        for i in range(600):
+            out.append(bytes(int(rng.integers(0, 2000))))
+    elif pattern == "nearrep":       # copies of earlier strings with point mutations
+        base = [rng.integers(0, 256, 60, dtype=np.uint8).tobytes() for _ in range(40)]
+        for i in range(4000):
+            b = bytearray(base[int(rng.integers(0, 40))])
+            for _ in range(int(rng.integers(0, 4))):
+                b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+            out.append(bytes(b[: int(rng.integers(4, 61))]))
+    elif pattern == "mixed":         # alternating regimes inside one fragment
+        for i in range(3000):
+            k = i % 4
+            if k == 0:
+                out.append(rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes())
+            elif k == 1:
+                out.append(b"abcd" * int(rng.integers(0, 30)))
+            elif k == 2:
+                out.append(bytes([int(rng.integers(0, 4))]) * int(rng.integers(0, 50)))
+            else:
+                out.append(("%08d" % int(rng.integers(0, 10 ** 8))).encode() * 3)
+    elif pattern == "tiny":          # pages shorter than snappy's 15-byte input margin
+        out = [b"", b"x"]
+    return out
+
+
+@pytest.mark.parametrize("pattern", ["random", "periodic", "zeros", "nearrep", "mixed", "tiny"])
+def test_snappy_patterns(pattern):
+    # dictionary off so the query page is the raw PLAIN strings (the K7 input as written)
+    rng = np.random.default_rng(sum(pattern.encode()))
+    recs = [b"\x0a" + _varint(len(q)) + q + b"\x10" + _varint(i) for i, q in enumerate(_snappy_strings(pattern, rng))]
+    data, offs = synth.pack(recs)
+    errs = gh.compare_pages(synth.SAMPLE, data, offs, codec=1, dictionary=False)
+    assert not errs, "\n".join(errs[:12])
 
 
 @pytest.mark.parametrize("n", [1, 7, 8, 9, 63, 64, 65, 100, 101, 255])
