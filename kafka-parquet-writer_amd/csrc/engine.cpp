@@ -449,6 +449,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, s));
         CK(hipMemcpyAsync(&coll, d_collision.p, 4, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
+        if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
         if (!coll) break;
         if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
     }
@@ -509,6 +510,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         pages_len_ = body_tot;
     }
     CK(hipEventRecord(ev_[6], s));
+    if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
     // ---------------------------------------------------------------- metadata
     CK(hipMemcpyAsync(ch.data(), d_chunks.p, nch * sizeof(ChunkDesc), hipMemcpyDeviceToHost, s));
     // binary min/max bytes: gather (offset, len) pairs, then the bytes into one blob

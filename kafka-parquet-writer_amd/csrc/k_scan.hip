@@ -2,8 +2,8 @@
 //
 //  * multi-job equal-length exclusive scans (reduce -> scan tile sums -> apply), 2048
 //    elements per 256-thread tile, 16-byte-friendly sequential per-thread ranges;
-//  * single-block segmented scans over tile aggregates (tile arrays are small: one entry
-//    per 2048 positions / 256 elements), generic over the combine operator.
+//  * multi-block segmented scans over tile aggregates (one entry per 2048 positions / 256
+//    elements), generic over the combine operator.
 #include "kpw_device.h"
 #include "kpw_kernels.h"
 #include "kpw_scan.h"
@@ -116,90 +116,155 @@ void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njo
 // ------------------------------------------------------------------ single-block segmented tile scans
 // Exclusive, segmented by job id (seg[t]); job totals written to tot[job] when tot != nullptr.
 
-// Each thread owns SEG_PER consecutive elements: a sequential segmented scan in registers,
-// then one Hillis-Steele segmented scan over the 256 thread aggregates per chunk of
-// 256*SEG_PER elements, carrying (value, segment) between chunks.
+// Multi-block, three phases over chunks of CH = 256 * SEG_PER elements (one block each):
+//   1. per chunk, the segmented-scan pair (any head in the chunk, reduction since its last
+//      head) — head = first element of a segment (seg[i] != seg[i-1]);
+//   2. one thread scans the chunk pairs into each chunk's carry-in (running value of the
+//      segment that continues into it);
+//   3. per chunk, a sequential scan of SEG_PER elements per thread plus a Hillis-Steele scan
+//      of the 256 thread aggregates, seeded with the carry-in; segment totals written at
+//      each segment's last element.
 constexpr int SEG_PER = 8;
+constexpr uint32_t SEG_CH = KPW_BLOCK * SEG_PER;
+
+// block-wide inclusive segmented scan of per-thread (value, head) pairs in LDS; returns
+// nothing, leaves lv/lh holding the inclusive scan
+template <typename T, typename Op>
+__device__ __forceinline__ void seg_block_scan(T *lv, uint32_t *lh)
+{
+    for (int d = 1; d < KPW_BLOCK; d <<= 1) {
+        T xv = Op::id();
+        uint32_t xh = 0;
+        const bool take = (int)threadIdx.x >= d;
+        if (take) { xv = lv[threadIdx.x - d]; xh = lh[threadIdx.x - d]; }
+        __syncthreads();
+        if (take) {
+            const uint32_t myh = lh[threadIdx.x];
+            if (!myh) lv[threadIdx.x] = Op::op(xv, lv[threadIdx.x]);
+            lh[threadIdx.x] = myh | xh;
+        }
+        __syncthreads();
+    }
+}
 
 template <typename T, typename Op>
-__global__ void __launch_bounds__(KPW_BLOCK) k_seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot)
+__global__ void __launch_bounds__(KPW_BLOCK) k_seg_reduce(const T *in, const uint32_t *seg, uint32_t n, T *bv, uint32_t *bh)
 {
     __shared__ T lv[KPW_BLOCK];
     __shared__ uint32_t lh[KPW_BLOCK];
-    __shared__ T lcarry;
-    __shared__ uint32_t lcarry_seg;
-    if (threadIdx.x == 0) { lcarry = Op::id(); lcarry_seg = 0xffffffffu; }
-    __syncthreads();
-    const uint32_t CH = KPW_BLOCK * SEG_PER;
-    for (uint32_t b = 0; b < n; b += CH) {
-        const uint32_t k0 = b + threadIdx.x * SEG_PER;
-        T v[SEG_PER];
-        uint32_t sg[SEG_PER];
-        // local inclusive segmented scan; `head` = a segment starts inside my range
-        T acc = Op::id();
-        uint32_t head = 0;
-        uint32_t prev = (k0 == 0) ? 0xffffffffu : (k0 - 1 < n ? seg[k0 - 1] : 0xfffffffeu);
-        if (k0 == b && b != 0) prev = lcarry_seg;
-        const uint32_t first_seg = k0 < n ? seg[k0] : 0xfffffffeu;
+    const uint32_t k0 = blockIdx.x * SEG_CH + threadIdx.x * SEG_PER;
+    T acc = Op::id();
+    uint32_t head = 0;
+    uint32_t prev = k0 == 0 ? 0xffffffffu : (k0 - 1 < n ? seg[k0 - 1] : 0xfffffffeu);
 #pragma unroll
-        for (int i = 0; i < SEG_PER; i++) {
-            const uint32_t k = k0 + i;
-            sg[i] = k < n ? seg[k] : 0xfffffffeu;
-            v[i] = k < n ? in[k] : Op::id();
-            const uint32_t p = i ? sg[i - 1] : prev;
-            if (sg[i] != p) { head = 1; acc = v[i]; } else acc = Op::op(acc, v[i]);
-        }
-        // block scan over (acc, head) of the threads; thread t's aggregate covers its range
-        lv[threadIdx.x] = acc;
-        lh[threadIdx.x] = head;
-        __syncthreads();
-        for (int d = 1; d < KPW_BLOCK; d <<= 1) {
-            T xv = Op::id();
-            uint32_t xh = 0;
-            const bool take = (int)threadIdx.x >= d;
-            if (take) { xv = lv[threadIdx.x - d]; xh = lh[threadIdx.x - d]; }
-            __syncthreads();
-            if (take) {
-                const uint32_t myh = lh[threadIdx.x];
-                if (!myh) lv[threadIdx.x] = Op::op(xv, lv[threadIdx.x]);
-                lh[threadIdx.x] = myh | xh;
-            }
-            __syncthreads();
-        }
-        // exclusive prefix entering my range (value continuing my first segment)
-        T in_pre;
-        if (threadIdx.x == 0) in_pre = lcarry;
-        else in_pre = lv[threadIdx.x - 1];
-        const uint32_t pre_head = threadIdx.x == 0 ? 0u : lh[threadIdx.x - 1];
-        // fold the carry into everything before the chunk's first head
-        if (threadIdx.x != 0 && !pre_head) in_pre = Op::op(lcarry, in_pre);
-        // does my first element continue the incoming segment?
-        const bool cont = (k0 < n) && (first_seg == prev);
-        T run = cont ? in_pre : Op::id();
-#pragma unroll
-        for (int i = 0; i < SEG_PER; i++) {
-            const uint32_t k = k0 + i;
-            if (k >= n) break;
-            const uint32_t p = i ? sg[i - 1] : prev;
-            if (sg[i] != p) run = Op::id();
-            out[k] = run;
-            run = Op::op(run, v[i]);
-            const bool last_of_seg = (k + 1 >= n) || (seg[k + 1] != sg[i]);
-            if (last_of_seg && tot) tot[sg[i]] = run;
-        }
-        __syncthreads();
-        // carry = inclusive value at the last valid element of this chunk
-        const uint32_t last = (b + CH <= n) ? (b + CH - 1) : (n - 1);
-        if (k0 <= last && last < k0 + SEG_PER) { lcarry = run; lcarry_seg = seg[last]; }
-        __syncthreads();
+    for (int i = 0; i < SEG_PER; i++) {
+        const uint32_t k = k0 + i;
+        const uint32_t sg = k < n ? seg[k] : 0xfffffffeu;
+        const T v = k < n ? in[k] : Op::id();
+        if (sg != prev) { head = 1; acc = v; } else acc = Op::op(acc, v);
+        prev = sg;
     }
+    lv[threadIdx.x] = acc;
+    lh[threadIdx.x] = head;
+    __syncthreads();
+    seg_block_scan<T, Op>(lv, lh);
+    if (threadIdx.x == KPW_BLOCK - 1) { bv[blockIdx.x] = lv[threadIdx.x]; bh[blockIdx.x] = lh[threadIdx.x]; }
+}
+
+template <typename T, typename Op>
+__global__ void k_seg_carry(T *bv, const uint32_t *bh, uint32_t nb)
+{
+    if (threadIdx.x != 0) return;
+    T acc = Op::id();
+    for (uint32_t b = 0; b < nb; b++) {
+        const T v = bv[b];
+        const uint32_t h = bh[b];
+        bv[b] = acc;
+        acc = h ? v : Op::op(acc, v);
+    }
+}
+
+template <typename T, typename Op>
+__global__ void __launch_bounds__(KPW_BLOCK) k_seg_apply(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, const T *bv)
+{
+    __shared__ T lv[KPW_BLOCK];
+    __shared__ uint32_t lh[KPW_BLOCK];
+    const uint32_t b = blockIdx.x * SEG_CH;
+    const T lcarry = bv[blockIdx.x];
+    const uint32_t lcarry_seg = b == 0 ? 0xffffffffu : seg[b - 1];
+    const uint32_t k0 = b + threadIdx.x * SEG_PER;
+    T v[SEG_PER];
+    uint32_t sg[SEG_PER];
+    T acc = Op::id();
+    uint32_t head = 0;
+    const uint32_t prev = (k0 == 0) ? 0xffffffffu : (k0 - 1 < n ? seg[k0 - 1] : 0xfffffffeu);
+    const uint32_t first_seg = k0 < n ? seg[k0] : 0xfffffffeu;
+#pragma unroll
+    for (int i = 0; i < SEG_PER; i++) {
+        const uint32_t k = k0 + i;
+        sg[i] = k < n ? seg[k] : 0xfffffffeu;
+        v[i] = k < n ? in[k] : Op::id();
+        const uint32_t p = i ? sg[i - 1] : prev;
+        if (sg[i] != p) { head = 1; acc = v[i]; } else acc = Op::op(acc, v[i]);
+    }
+    lv[threadIdx.x] = acc;
+    lh[threadIdx.x] = head;
+    __syncthreads();
+    seg_block_scan<T, Op>(lv, lh);
+    // exclusive prefix entering my range, continuing my first segment
+    T in_pre = threadIdx.x == 0 ? lcarry : lv[threadIdx.x - 1];
+    const uint32_t pre_head = threadIdx.x == 0 ? 0u : lh[threadIdx.x - 1];
+    if (threadIdx.x != 0 && !pre_head) in_pre = Op::op(lcarry, in_pre);
+    (void)lcarry_seg;
+    const bool cont = (k0 < n) && (first_seg == prev);
+    T run = cont ? in_pre : Op::id();
+#pragma unroll
+    for (int i = 0; i < SEG_PER; i++) {
+        const uint32_t k = k0 + i;
+        if (k >= n) break;
+        const uint32_t p = i ? sg[i - 1] : prev;
+        if (sg[i] != p) run = Op::id();
+        out[k] = run;
+        run = Op::op(run, v[i]);
+        const bool last_of_seg = (k + 1 >= n) || (seg[k + 1] != sg[i]);
+        if (last_of_seg && tot) tot[sg[i]] = run;
+    }
+}
+
+// scratch for the multi-block scans (per-chunk pairs), grown on demand.  Thread-local and
+// per device: writer handles are used by one thread at a time, each encode is blocking, so
+// a thread's scans never overlap.
+struct SegScratch { void *p = nullptr; size_t bytes = 0; };
+static thread_local SegScratch g_seg_scratch[16];
+static thread_local bool g_seg_failed = false;
+
+bool seg_scan_failed_reset()
+{
+    const bool f = g_seg_failed;
+    g_seg_failed = false;
+    return f;
 }
 
 template <typename T, typename Op>
 void seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, hipStream_t s)
 {
     if (!n) return;
-    hipLaunchKernelGGL((k_seg_tile_scan<T, Op>), dim3(1), dim3(KPW_BLOCK), 0, s, in, out, seg, n, tot);
+    const uint32_t nb = (n + SEG_CH - 1) / SEG_CH;
+    const size_t need = (size_t)nb * (sizeof(T) + sizeof(uint32_t)) + 64;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    SegScratch &sc = g_seg_scratch[dev & 15];
+    if (need > sc.bytes) {
+        if (sc.p) { (void)hipStreamSynchronize(s); (void)hipFree(sc.p); }
+        sc.bytes = need * 2;
+        if (hipMalloc(&sc.p, sc.bytes) != hipSuccess) { sc.p = nullptr; sc.bytes = 0; g_seg_failed = true; return; }
+    }
+    void *g_seg_scratch = sc.p;
+    T *bv = (T *)g_seg_scratch;
+    uint32_t *bh = (uint32_t *)((char *)g_seg_scratch + (((size_t)nb * sizeof(T) + 15) & ~(size_t)15));
+    hipLaunchKernelGGL((k_seg_reduce<T, Op>), dim3(nb), dim3(KPW_BLOCK), 0, s, in, seg, n, bv, bh);
+    hipLaunchKernelGGL((k_seg_carry<T, Op>), dim3(1), dim3(64), 0, s, bv, (const uint32_t *)bh, nb);
+    hipLaunchKernelGGL((k_seg_apply<T, Op>), dim3(nb), dim3(KPW_BLOCK), 0, s, in, out, seg, n, tot, (const T *)bv);
 }
 
 template void seg_tile_scan<uint32_t, OpSum32>(const uint32_t *, uint32_t *, const uint32_t *, uint32_t, uint32_t *, hipStream_t);
