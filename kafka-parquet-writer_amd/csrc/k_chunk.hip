@@ -54,6 +54,26 @@ __device__ __forceinline__ uint64_t order_key(int phys, uint64_t v)
 
 // ------------------------------------------------------------------ K6 stats + sizes
 
+// BYTE_ARRAY compare / equality of records a and b through the 16-byte prefix arrays; the
+// batch bytes are read only when both values are longer than 16 bytes with equal prefixes.
+// Unsigned lexicographic order, shorter first on a common prefix (BinaryStatistics).
+__device__ __forceinline__ int str_cmp(const DevCol &col, const uint8_t *data, uint64_t a, uint64_t b, uint64_t data_end)
+{
+    const uint64_t a0 = col.spfx[2 * a], b0 = col.spfx[2 * b];
+    if (a0 != b0) return __builtin_bswap64(a0) < __builtin_bswap64(b0) ? -1 : 1;
+    const uint64_t a1 = col.spfx[2 * a + 1], b1 = col.spfx[2 * b + 1];
+    if (a1 != b1) return __builtin_bswap64(a1) < __builtin_bswap64(b1) ? -1 : 1;
+    const uint32_t la = col.slen[a], lb = col.slen[b];
+    if (la <= 16 || lb <= 16) return la == lb ? 0 : (la < lb ? -1 : 1);
+    return bytes_cmp(data, col.soff[a] + 16, la - 16, col.soff[b] + 16, lb - 16, data_end);
+}
+__device__ __forceinline__ bool str_eq(const DevCol &col, const uint8_t *data, uint64_t a, uint64_t b, uint64_t data_end)
+{
+    const uint32_t la = col.slen[a];
+    if (la != col.slen[b] || col.spfx[2 * a] != col.spfx[2 * b] || col.spfx[2 * a + 1] != col.spfx[2 * b + 1]) return false;
+    return la <= 16 || bytes_cmp(data, col.soff[a] + 16, la - 16, col.soff[b] + 16, la - 16, data_end) == 0;
+}
+
 __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
                                                            const uint32_t *ctile_chunk, const uint32_t *ctile_first,
                                                            uint64_t *tile_raw, uint64_t *tile_smin, uint64_t *tile_smax,
@@ -61,7 +81,6 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
 {
     const uint64_t data_end = *data_end_p;
     __shared__ uint64_t lds[KPW_BLOCK];
-    __shared__ uint64_t li[KPW_BLOCK], la[KPW_BLOCK];
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
     ChunkDesc &C = ch[ci];
@@ -69,17 +88,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
     const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
     uint64_t nn = 0, raw = 0;
     uint64_t kmin = ~0ull, kmax = 0;
-    uint64_t imin = ~0ull, imax = ~0ull;   // binary: record index of min / max candidate
     for (int k = 0; k < 8; k++) {
         const uint64_t r = p0 + k;
         if (r >= (uint64_t)C.e) break;
         if (!present_at(col, r)) continue;
         nn++;
         if (col.phys == 6) {
-            const uint32_t l = col.slen[r];
-            raw += 4 + l;
-            if (imin == ~0ull || bytes_cmp(data, col.soff[r], l, col.soff[imin], col.slen[imin], data_end) < 0) imin = r;
-            if (imax == ~0ull || bytes_cmp(data, col.soff[r], l, col.soff[imax], col.slen[imax], data_end) > 0) imax = r;
+            raw += 4 + col.slen[r];   // min/max: k_str_minmax, after the dictionary phase
         } else if (col.phys == 0) {
             const uint64_t v = (col.vbits[r >> 6] >> (r & 63)) & 1ull;
             kmin = v < kmin ? v : kmin;
@@ -94,21 +109,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
     const uint64_t snn = block_reduce<uint64_t, OpSum64>(nn, lds);
     const uint64_t sraw = block_reduce<uint64_t, OpSum64>(raw, lds);
     if (col.phys == 6) {
-        // block reduce of (min index, max index) with the unsigned lexicographic comparator
-        li[threadIdx.x] = imin;
-        la[threadIdx.x] = imax;
-        __syncthreads();
-        for (int d = KPW_BLOCK / 2; d > 0; d >>= 1) {
-            if ((int)threadIdx.x < d) {
-                const uint64_t a = li[threadIdx.x], b = li[threadIdx.x + d];
-                // keep the earlier record on ties (same bytes -> same output anyway)
-                if (b != ~0ull && (a == ~0ull || bytes_cmp(data, col.soff[b], col.slen[b], col.soff[a], col.slen[a], data_end) < 0)) li[threadIdx.x] = b;
-                const uint64_t x = la[threadIdx.x], y = la[threadIdx.x + d];
-                if (y != ~0ull && (x == ~0ull || bytes_cmp(data, col.soff[y], col.slen[y], col.soff[x], col.slen[x], data_end) > 0)) la[threadIdx.x] = y;
-            }
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) { tile_smin[t] = li[0]; tile_smax[t] = la[0]; tile_raw[t] = sraw; }
+        if (threadIdx.x == 0) tile_raw[t] = sraw;
     } else {
         if (snn) {
             // wave-level min/max then one atomic per wave
@@ -130,27 +131,47 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
     }
 }
 
-// per chunk (one block): combine tile candidates of binary min/max; null count; has_minmax
-__global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats_final(ChunkDesc *ch, int nchunks, const DevCol *cols, const uint8_t *data,
-                                                                 const uint32_t *ctile_first, const uint32_t *ctile_count,
-                                                                 const uint64_t *tile_smin, const uint64_t *tile_smax,
-                                                                 const uint64_t *data_end_p)
+// per chunk: null count, has_minmax (BYTE_ARRAY min/max: k_str_final)
+__global__ void k_chunk_stats_final(ChunkDesc *ch, int nchunks)
+{
+    const int ci = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ci >= nchunks) return;
+    ChunkDesc &C = ch[ci];
+    C.null_count = (uint64_t)(C.e - C.s) - C.nn;
+    C.has_minmax = C.nn > 0;
+}
+
+// BYTE_ARRAY min/max, after the dictionary phase: a complete dictionary holds every
+// distinct value of its chunk, so its entries stand in for the values (one entry per
+// distinct string instead of one compare per value); other chunks reduce their values.
+// One block per chunk tile: tile k covers entries [2048k, 2048k+2048) or its records.
+__global__ void __launch_bounds__(KPW_BLOCK) k_str_minmax(const ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
+                                                          const uint32_t *ctile_chunk, const uint32_t *ctile_first,
+                                                          const uint64_t *ent_rec, uint64_t *tile_smin, uint64_t *tile_smax,
+                                                          const uint64_t *data_end_p)
 {
     __shared__ uint64_t li[KPW_BLOCK], la[KPW_BLOCK];
-    const uint64_t data_end = *data_end_p;
-    const int ci = blockIdx.x;
-    ChunkDesc &C = ch[ci];
+    const uint32_t t = blockIdx.x;
+    const uint32_t ci = ctile_chunk[t];
+    const ChunkDesc &C = ch[ci];
     const DevCol &col = cols[C.col];
-    if (threadIdx.x == 0) {
-        C.null_count = (uint64_t)(C.e - C.s) - C.nn;
-        C.has_minmax = C.nn > 0;
-    }
-    if (col.phys != 6 || !C.nn) return;
+    if (col.phys != 6) return;
+    const uint64_t data_end = *data_end_p;
+    const bool ents = C.is_dict && !C.fallback;
+    const uint64_t q0 = (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
     uint64_t a = ~0ull, b = ~0ull;
-    for (uint32_t k = threadIdx.x; k < ctile_count[ci]; k += KPW_BLOCK) {
-        const uint64_t x = tile_smin[ctile_first[ci] + k], y = tile_smax[ctile_first[ci] + k];
-        if (x != ~0ull && (a == ~0ull || bytes_cmp(data, col.soff[x], col.slen[x], col.soff[a], col.slen[a], data_end) < 0)) a = x;
-        if (y != ~0ull && (b == ~0ull || bytes_cmp(data, col.soff[y], col.slen[y], col.soff[b], col.slen[b], data_end) > 0)) b = y;
+    for (int k = 0; k < 8; k++) {
+        uint64_t r;
+        if (ents) {
+            if (q0 + k >= C.dict_n) break;
+            r = ent_rec[C.ent_off + q0 + k];
+        } else {
+            r = (uint64_t)C.s + q0 + k;
+            if (r >= (uint64_t)C.e) break;
+            if (!present_at(col, r)) continue;
+        }
+        if (a == ~0ull || str_cmp(col, data, r, a, data_end) < 0) a = r;
+        if (b == ~0ull || str_cmp(col, data, r, b, data_end) > 0) b = r;
     }
     li[threadIdx.x] = a;
     la[threadIdx.x] = b;
@@ -158,9 +179,42 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats_final(ChunkDesc *ch, 
     for (int d = KPW_BLOCK / 2; d > 0; d >>= 1) {
         if ((int)threadIdx.x < d) {
             const uint64_t x = li[threadIdx.x], y = li[threadIdx.x + d];
-            if (y != ~0ull && (x == ~0ull || bytes_cmp(data, col.soff[y], col.slen[y], col.soff[x], col.slen[x], data_end) < 0)) li[threadIdx.x] = y;
+            if (y != ~0ull && (x == ~0ull || str_cmp(col, data, y, x, data_end) < 0)) li[threadIdx.x] = y;
             const uint64_t u = la[threadIdx.x], v = la[threadIdx.x + d];
-            if (v != ~0ull && (u == ~0ull || bytes_cmp(data, col.soff[v], col.slen[v], col.soff[u], col.slen[u], data_end) > 0)) la[threadIdx.x] = v;
+            if (v != ~0ull && (u == ~0ull || str_cmp(col, data, v, u, data_end) > 0)) la[threadIdx.x] = v;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { tile_smin[t] = li[0]; tile_smax[t] = la[0]; }
+}
+
+// per BYTE_ARRAY chunk: reduce its tiles' candidates
+__global__ void __launch_bounds__(KPW_BLOCK) k_str_final(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
+                                                         const uint32_t *ctile_first, const uint32_t *ctile_count,
+                                                         const uint64_t *tile_smin, const uint64_t *tile_smax,
+                                                         const uint64_t *data_end_p)
+{
+    __shared__ uint64_t li[KPW_BLOCK], la[KPW_BLOCK];
+    const int ci = blockIdx.x;
+    ChunkDesc &C = ch[ci];
+    const DevCol &col = cols[C.col];
+    if (col.phys != 6 || !C.nn) return;
+    const uint64_t data_end = *data_end_p;
+    uint64_t a = ~0ull, b = ~0ull;
+    for (uint32_t k = threadIdx.x; k < ctile_count[ci]; k += KPW_BLOCK) {
+        const uint64_t x = tile_smin[ctile_first[ci] + k], y = tile_smax[ctile_first[ci] + k];
+        if (x != ~0ull && (a == ~0ull || str_cmp(col, data, x, a, data_end) < 0)) a = x;
+        if (y != ~0ull && (b == ~0ull || str_cmp(col, data, y, b, data_end) > 0)) b = y;
+    }
+    li[threadIdx.x] = a;
+    la[threadIdx.x] = b;
+    __syncthreads();
+    for (int d = KPW_BLOCK / 2; d > 0; d >>= 1) {
+        if ((int)threadIdx.x < d) {
+            const uint64_t x = li[threadIdx.x], y = li[threadIdx.x + d];
+            if (y != ~0ull && (x == ~0ull || str_cmp(col, data, y, x, data_end) < 0)) li[threadIdx.x] = y;
+            const uint64_t u = la[threadIdx.x], v = la[threadIdx.x + d];
+            if (v != ~0ull && (u == ~0ull || str_cmp(col, data, v, u, data_end) > 0)) la[threadIdx.x] = v;
         }
         __syncthreads();
     }
@@ -204,7 +258,7 @@ __device__ __forceinline__ int64_t global_insert(ChunkDesc &C, uint64_t *keys, u
             }
             cur = old;
         }
-        const bool eq = is_bin ? bytes_cmp(data, col.soff[cur], col.slen[cur], col.soff[r], col.slen[r], data_end) == 0 : cur == key;
+        const bool eq = is_bin ? str_eq(col, data, cur, r, data_end) : cur == key;
         if (eq) {
             if (mins[i] > rank) atomicMin(&mins[i], rank);
             return i;
@@ -413,8 +467,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, con
         ids[o] = id;
         if (col.phys == 6) {  // verify the hash-keyed dictionary byte-for-byte
             const uint64_t e = ent_rec[C.ent_off + id];
-            if (col.slen[e] != col.slen[r] || bytes_cmp(data, col.soff[e], col.slen[e], col.soff[r], col.slen[r], data_end) != 0)
-                atomicOr(collision, 1u);
+            if (!str_eq(col, data, e, r, data_end)) atomicOr(collision, 1u);
         }
         rank++;
     }
@@ -656,8 +709,7 @@ void launch_chunk_stats(const ChunkArgs &a, hipStream_t s)
 {
     hipLaunchKernelGGL(k_chunk_stats, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
                        a.tile_raw, a.tile_smin, a.tile_smax, a.data_end);
-    hipLaunchKernelGGL(k_chunk_stats_final, dim3(a.nchunks), dim3(KPW_BLOCK), 0, s, a.ch, a.nchunks, a.cols, a.data,
-                       a.ctile_first, a.ctile_count, a.tile_smin, a.tile_smax, a.data_end);
+    hipLaunchKernelGGL(k_chunk_stats_final, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks);
 }
 
 void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
@@ -674,6 +726,11 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
                        a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1);
     hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht_id, a.ids,
                        a.data, a.ent_rec, a.data_end, a.collision);
+    // BYTE_ARRAY statistics need the dictionary outcome (entries stand in for the values)
+    hipLaunchKernelGGL(k_str_minmax, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
+                       a.ent_rec, a.tile_smin, a.tile_smax, a.data_end);
+    hipLaunchKernelGGL(k_str_final, dim3(a.nchunks), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_first, a.ctile_count,
+                       a.tile_smin, a.tile_smax, a.data_end);
 }
 
 void launch_layout(const ChunkArgs &a, RleJob *jobs, uint64_t *page_off, uint64_t *page_len, uint64_t *tot, hipStream_t s)

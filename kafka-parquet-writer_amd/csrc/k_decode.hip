@@ -166,6 +166,10 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
                 if ((int32_t)(uint32_t)l < 0 || end - pos < (uint32_t)l) { bad = true; break; }
                 col->soff[r] = pos;
                 col->slen[r] = (uint32_t)l;
+                // first 16 bytes, zero padded: exact compares for short strings (stats,
+                // dictionary verification) without touching the batch bytes again
+                col->spfx[2 * r] = l ? ldu64(d, pos, data_end) & tail_mask(l) : 0ull;
+                col->spfx[2 * r + 1] = l > 8 ? ldu64(d, pos + 8, data_end) & tail_mask(l - 8) : 0ull;
                 if (col->dict) col->shash[r] = bytes_hash(d, pos, (uint32_t)l, data_end);
                 pos += (uint32_t)l;
             }

@@ -137,6 +137,28 @@ def test_snappy_patterns(pattern):
     assert not errs, "\n".join(errs[:12])
 
 
+_TRICKY = [b"", b"\x00", b"a", b"a\x00", b"a\x00\x00", b"ab" * 8, b"ab" * 8 + b"\x00", b"ab" * 8 + b"\x01",
+           b"ab" * 8 + b"\x00\x00", b"ab" * 10, b"ab" * 10 + b"c", b"ab" * 9 + b"a", b"\xff" * 16, b"\xff" * 17,
+           b"\xff" * 15 + b"\xfe", b"\x7f" * 20, b"\x80" + b"\x00" * 30, b"\x80" + b"\x00" * 31, b"zz", b"z" * 40]
+
+
+@pytest.mark.parametrize("dictionary", [True, False], ids=["entries", "values"])
+@pytest.mark.parametrize("subset", ["all", "no_extremes"])
+def test_string_stats_tricky(dictionary, subset):
+    # BYTE_ARRAY min/max (unsigned lexicographic, shorter first) through the 16-byte prefix
+    # arrays: ties on the prefix, embedded zeros, lengths 0/16/17, high bytes
+    pool = _TRICKY if subset == "all" else [q for q in _TRICKY if q not in (b"", b"\xff" * 17, b"z" * 40)]
+    rng = np.random.default_rng(7 if dictionary else 8)
+    recs = []
+    for i in range(5000):
+        q = pool[int(rng.integers(0, len(pool)))]
+        recs.append(b"\x0a" + _varint(len(q)) + q + b"\x10" + _varint(i))
+    data, offs = synth.pack(recs)
+    for codec in (0, 1):
+        errs = gh.compare_pages(synth.SAMPLE, data, offs, codec=codec, dictionary=dictionary)
+        assert not errs, "\n".join(errs[:12])
+
+
 @pytest.mark.parametrize("n", [1, 7, 8, 9, 63, 64, 65, 100, 101, 255])
 def test_tiny_batches(n):
     data, offs = synth.generate(synth.KIND_REC8, 99, n)
