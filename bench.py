@@ -70,6 +70,24 @@ def cpu_baseline(kind, seed, sample_records, threads):
                 records_per_s=round(per * threads / dt, 1))
 
 
+SNAPPY_KERNEL = "kpw::k_snappy_s<2>"   # K7 as launched by launch_snappy (k_snappy.hip)
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest profiles/<tag>_pmc_traffic.json
+    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 FETCH correction;
+    profiles/summarize.py).  Returns (bytes, source file) or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return int(k["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
+
+
 def dist_init(world, local_rank, backend="nccl"):
     """One process per GPU (torchrun env). backend "nccl" is RCCL on ROCm; tests use gloo."""
     if world <= 1:
@@ -187,16 +205,21 @@ def main():
     #  presence/boolean bits n/8 per optional column + flag bits, raw sizes 4 per record)
     k1_bytes = nbytes + 8 * (n + 1) + n * (8 + 4 + 4 + 8 + 8 + 12 + 12 + 4) + (5 * n) // 8
     names = ["decode", "plan", "stats+dict", "rle", "layout+plain+write", "compress", "metadata", "total",
-             "k_decode", "k_snappy_frag"]
+             "k_decode", "k_snappy"]
     stage = dict(zip(names, [round(x, 3) for x in stages]))
     k_dec_ms = stages[8] if len(stages) > 8 else stages[0]
     k_sn_ms = stages[9] if len(stages) > 9 else stages[5]
-    kern = {"k_decode": (k1_bytes, k_dec_ms), "k_snappy_frag": (unc + comp, k_sn_ms)}
+    # the two kernels timed live with HIP events on the encoder's stream (kpw_encoder_stage_times
+    # [8], [9]); K7 = one launch of the Snappy fragment kernel over all pages of the batch
+    kern = {"kpw::k_decode": (k1_bytes, k_dec_ms), SNAPPY_KERNEL: (unc + comp, k_sn_ms)}
     dom = max(kern, key=lambda k: kern[k][1])
     ab, ams = kern[dom]
     achieved = ab / (ams * 1e-3) / 1e9 if ams > 0 else 0.0
+    traffic, tsrc = pmc_traffic(dom)
     roof = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBPS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBPS, 5), traffic=None, algorithmic_bytes_per_launch=int(ab),
+                frac=round(achieved / HBM_PEAK_GBPS, 5),
+                traffic=(round(traffic / (ams * 1e-3) / 1e9, 2) if traffic else None),
+                traffic_bytes_per_launch=traffic, traffic_source=tsrc, algorithmic_bytes_per_launch=int(ab),
                 avg_launch_ms=round(ams, 4))
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
