@@ -766,6 +766,201 @@ emit_remainder:
     if (lane == 0) a.frag_len[f] = op;
 }
 
+// ------------------------------------------------------------------ scalar + SGPR window
+// k_snappy_s plus a 64-byte window of the input around ip held in SGPRs (one
+// s_load_dwordx16): on typical pages the match candidate is a few bytes behind ip (the
+// previous record), so the match-length compare, the post-match reads, the candidate check
+// and the literal bytes all come from the window; it is reloaded when ip moves past it, and
+// reads outside it (far candidates) take one direct scalar load.
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+struct SWin {
+    uint64_t base;    // absolute address of fragment byte 0
+    uint64_t lo;      // lowest address read (base & ~3)
+    uint64_t A;       // 4-aligned absolute address of the window start
+    u32x16 w;
+    __device__ __forceinline__ void load(uint32_t p)
+    {
+        const uint64_t a = base + p;
+        A = a >= lo + 16 ? ((a - 16) & ~3ull) : lo;
+        asm volatile("s_load_dwordx16 %0, %1, 0x0\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&s"(w)
+                     : "s"(A));
+    }
+    // 8 bytes at fragment position p when they lie inside the window (o <= 52)
+    __device__ __forceinline__ bool has(uint32_t p) const { return base + p - A <= 52; }
+    __device__ __forceinline__ uint64_t rd(uint32_t p) const
+    {
+        const uint32_t o = (uint32_t)(base + p - A);
+        const uint32_t d = o >> 2, sh = (o & 3) * 8;
+        const uint64_t x = ((uint64_t)w[d + 1] << 32) | w[d];
+        const uint64_t y = w[d + 2];
+        return sh ? (x >> sh) | (y << (64 - sh)) : x;
+    }
+    // 8 bytes at p: window, else reload when ahead, else one scalar load
+    __device__ __forceinline__ uint64_t ld64(uint32_t p, const SIn &si)
+    {
+        if (has(p)) return rd(p);
+        if (base + p >= A) { load(p); return rd(p); }
+        return si.ld64(p);
+    }
+    // 8 bytes at p without moving the window (candidates behind ip)
+    __device__ __forceinline__ uint64_t peek64(uint32_t p, const SIn &si) const { return has(p) ? rd(p) : si.ld64(p); }
+};
+
+__device__ __forceinline__ uint32_t find_match_length_w(SWin &W, const SIn &si, const Src &g, uint32_t s1, uint32_t s2,
+                                                        uint32_t s2_limit, int lane)
+{
+    uint32_t m = 0;
+    while (m < 64 && s2 + m + 8 <= s2_limit) {
+        const uint64_t a = W.peek64(s1 + m, si);
+        const uint64_t b = W.ld64(s2 + m, si);
+        const uint64_t x = a ^ b;
+        if (x) return m + ((uint32_t)__builtin_ctzll(x) >> 3);
+        m += 8;
+    }
+    for (;;) {
+        const uint32_t p2 = s2 + m + lane;
+        const bool ok = p2 < s2_limit && g.ld8(s1 + m + lane) == g.ld8(p2);
+        const uint64_t bad = __ballot(!ok);
+        if (bad) return m + (uint32_t)(__ffsll((long long)bad) - 1);
+        m += 64;
+    }
+}
+
+template <int SEQ>
+__global__ void __launch_bounds__(64) k_snappy_w(SnappyArgs a)
+{
+    __shared__ uint16_t table[SNAPPY_MAX_TABLE];
+    const int lane = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    const uint32_t pg = a.frag_page[f];
+    const uint32_t fi = a.frag_idx[f];
+    const uint64_t plen = a.page_len[pg];
+    const uint64_t fstart = (uint64_t)fi * SNAPPY_FRAG;
+    const uint32_t n = (uint32_t)((plen - fstart) < SNAPPY_FRAG ? (plen - fstart) : SNAPPY_FRAG);
+    const uint8_t *fbase = a.in + a.page_off[pg] + fstart;
+    const Src g{(g_u8 *)fbase};
+    const SIn si{(uint64_t)(uintptr_t)fbase};
+    SWin W;
+    W.base = (uint64_t)(uintptr_t)fbase;
+    W.lo = W.base & ~3ull;
+    W.load(0);
+    uint32_t tsize = 256;
+    while (tsize < SNAPPY_MAX_TABLE && tsize < n) tsize <<= 1;
+    for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
+    __syncthreads();
+
+    uint8_t *out = a.frag_out + (uint64_t)f * SNAPPY_FRAG_CAP;
+    uint32_t op = 0;
+    int shift = 32;
+    for (uint32_t t = tsize; t > 1; t >>= 1) shift--;
+    const uint32_t ip_end = n;
+    uint32_t next_emit = 0;
+    uint32_t ip = 0;
+    if (n >= 15) {
+        const uint32_t ip_limit = n - 15;
+        ip = 1;
+        for (;;) {
+            uint32_t skip = 32;
+            uint32_t candidate;
+            int nseq = 0;
+            for (;;) {
+                if (nseq < SEQ) {
+                    nseq++;
+                    const uint32_t next_ip = ip + (skip++ >> 5);
+                    if (next_ip > ip_limit) goto emit_remainder;
+                    const uint32_t cur_s = (uint32_t)W.ld64(ip, si);
+                    const uint32_t h = sn_hash(cur_s, shift);
+                    candidate = ufl(table[h]);
+                    table[h] = (uint16_t)ip;
+                    if (cur_s == (uint32_t)W.peek64(candidate, si)) break;
+                    ip = next_ip;
+                    continue;
+                }
+                const uint32_t base_f = skip_sum(skip);
+                const uint32_t ipk = ip + skip_sum(skip + lane) - base_f;
+                const uint32_t ipk1 = ip + skip_sum(skip + lane + 1) - base_f;
+                const bool valid = ipk1 <= ip_limit;
+                const uint64_t vmask = __ballot(valid);
+                const uint32_t cur = valid ? g.ld32(ipk) : 0u;
+                const uint32_t h = sn_hash(cur, shift);
+                uint32_t old = 0;
+                if (valid) old = table[h];
+                if (valid) table[h] = (uint16_t)ipk;
+                cbar();
+                uint32_t chk = ipk;
+                if (valid) chk = table[h];
+                const uint64_t losers = __ballot(valid && (uint16_t)chk != (uint16_t)ipk);
+                uint32_t cand = old;
+                uint64_t grp = 0;
+                if (losers) {
+                    uint64_t L = losers;
+                    while (L) {
+                        const int leader = __ffsll((long long)L) - 1;
+                        const uint32_t hv = __builtin_amdgcn_readlane(h, leader);
+                        const uint64_t gm = __ballot(valid && h == hv);
+                        if ((gm >> lane) & 1) grp = gm;
+                        L &= ~gm;
+                    }
+                    const uint64_t below = grp & ((1ull << lane) - 1);
+                    const int pred = below ? 63 - __clzll((long long)below) : lane;
+                    const uint32_t ipp = __shfl(ipk, pred, 64);
+                    if (below) cand = ipp;
+                }
+                const uint64_t hit = __ballot(valid && g.ld32(cand) == cur);
+                if (hit) {
+                    const int m = __ffsll((long long)hit) - 1;
+                    if (valid && lane > m) table[h] = (uint16_t)old;
+                    if (losers) {
+                        cbar();
+                        const uint64_t upto = m == 63 ? ~0ull : ((2ull << m) - 1);
+                        if (lane <= m && ((grp & upto) >> lane) <= 1) table[h] = (uint16_t)ipk;
+                    }
+                    ip = __builtin_amdgcn_readlane(ipk, m);
+                    candidate = __builtin_amdgcn_readlane(cand, m);
+                    break;
+                }
+                if (vmask != ~0ull) goto emit_remainder;
+                if (losers && (grp >> lane) <= 1) table[h] = (uint16_t)ipk;
+                ip = ip + skip_sum(skip + 64) - base_f;
+                skip += 64;
+            }
+            {
+                const uint32_t len = ip - next_emit;
+                if (len <= 7) {
+                    const uint64_t b = W.peek64(next_emit, si) & ((1ull << (8 * len)) - 1);
+                    st_word(out, op, ((uint64_t)((len - 1) << 2)) | (b << 8), 1 + len, lane);
+                    op += 1 + len;
+                } else {
+                    op = emit_literal(out, op, g, next_emit, len, lane);
+                }
+            }
+            for (;;) {
+                const uint32_t base = ip;
+                const uint32_t matched = 4 + find_match_length_w(W, si, g, candidate + 4, ip + 4, ip_end, lane);
+                ip += matched;
+                op = emit_copy_s(out, op, base - candidate, matched, lane);
+                next_emit = ip;
+                if (ip >= ip_limit) goto emit_remainder;
+                const uint64_t in8 = W.ld64(ip - 1, si);   // bytes [ip-1, ip+7)
+                const uint32_t input_lo = (uint32_t)in8;
+                const uint32_t b1 = (uint32_t)(in8 >> 8);
+                table[sn_hash(input_lo, shift)] = (uint16_t)(ip - 1);
+                const uint32_t cur_hash = sn_hash(b1, shift);
+                candidate = ufl(table[cur_hash]);
+                table[cur_hash] = (uint16_t)ip;
+                if (b1 != (uint32_t)W.peek64(candidate, si)) break;
+            }
+            ++ip;
+        }
+    }
+emit_remainder:
+    if (next_emit < ip_end) op = emit_literal(out, op, g, next_emit, ip_end - next_emit, lane);
+    if (lane == 0) a.frag_len[f] = op;
+}
+
 // per page: compressed size = varint(len) + sum of its fragments
 __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_page_sizes(SnappyArgs a, const uint32_t *page_frag0)
 {

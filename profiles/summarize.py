@@ -57,7 +57,7 @@ def main(tag):
         fo.write("# Profile %s — C2 bench (100 M Rec8, SNAPPY, 128 MiB row groups), rocprofv3\n\n" % tag)
         fo.write("Commands: `profiles/profile_round.sh %s` (trace pass: bench --steps 3 = 4 encodes incl. warmup;"
                  " PMC passes: bench --steps 2).\n\n" % tag)
-        fo.write("| kernel | calls | total ms | avg ms | ms / encode | %% | FETCH x2 GB/launch | WRITE GB/launch |\n")
+        fo.write("| kernel | calls | total ms | avg ms | ms / encode | % | FETCH x2 GB/launch | WRITE GB/launch |\n")
         fo.write("|---|---|---|---|---|---|---|---|\n")
         for r in rows[:30]:
             k = short(r["Name"])

@@ -60,6 +60,7 @@ static float run(const SnappyArgs &a, int reps)
     auto launch = [&]() {
         if (KIND == 1) hipLaunchKernelGGL(k_snappy_win<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
         else if (KIND == 2) hipLaunchKernelGGL(k_snappy_s<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
+        else if (KIND == 3) hipLaunchKernelGGL(k_snappy_w<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
         else hipLaunchKernelGGL(k_snappy_frag<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
     };
     launch();
@@ -132,9 +133,8 @@ int main(int argc, char **argv)
         };
         const double gb = (double)(npages * psz) / 1e9;
         struct V { const char *name; float (*fn)(const SnappyArgs &, int); };
-        V vs[] = {{"seq", run<1 << 30, 0>}, {"seq2", run<2, 0>}, {"win2", run<2, 1>},
-                  {"s_seq", run<1 << 30, 2>}, {"s0", run<0, 2>}, {"s1", run<1, 2>}, {"s2", run<2, 2>}, {"s4", run<4, 2>},
-                  {"s8", run<8, 2>}};
+        V vs[] = {{"seq", run<1 << 30, 0>}, {"s2", run<2, 2>}, {"s4", run<4, 2>},
+                  {"w1", run<1, 3>}, {"w2", run<2, 3>}, {"w4", run<4, 3>}, {"w8", run<8, 3>}};
         for (auto &v : vs) {
             CK(hipMemset(d_fout, 0, (size_t)nf * SNAPPY_FRAG_CAP));
             float ms = v.fn(a, 3);
