@@ -45,11 +45,12 @@ enum kpw_codec { KPW_UNCOMPRESSED = 0, KPW_SNAPPY = 1 };
 /* parquet-format Encoding. */
 enum kpw_encoding {
     KPW_ENC_PLAIN = 0, KPW_ENC_PLAIN_DICTIONARY = 2, KPW_ENC_RLE = 3, KPW_ENC_BIT_PACKED = 4,
-    KPW_ENC_DELTA_BINARY_PACKED = 5, KPW_ENC_RLE_DICTIONARY = 8
+    KPW_ENC_DELTA_BINARY_PACKED = 5, KPW_ENC_DELTA_LENGTH_BYTE_ARRAY = 6, KPW_ENC_DELTA_BYTE_ARRAY = 7,
+    KPW_ENC_RLE_DICTIONARY = 8
 };
 
 /* parquet-format PageType. */
-enum kpw_page_type { KPW_DATA_PAGE = 0, KPW_DICTIONARY_PAGE = 2 };
+enum kpw_page_type { KPW_DATA_PAGE = 0, KPW_DICTIONARY_PAGE = 2, KPW_DATA_PAGE_V2 = 3 };
 
 /* One top-level proto2 field = one Parquet leaf column, in descriptor (declaration)
  * order, exactly as ProtoSchemaConverter lays them out.  Only scalar, non-repeated
@@ -88,7 +89,9 @@ typedef struct kpw_props {
     int32_t dictionary_page_size;  /* max dictionary byte size before PLAIN fallback */
     int32_t enable_dictionary;     /* 0/1 (effective) */
     int32_t codec;                 /* enum kpw_codec */
-    int32_t writer_version;        /* 1 = PARQUET_1_0 (the only version the reference reaches) */
+    int32_t writer_version;        /* 1 = PARQUET_1_0 (the only version the reference reaches);
+                                      2 = PARQUET_2_0 (DataPageV2, RLE_DICTIONARY, DELTA_BINARY_PACKED /
+                                      DELTA_BYTE_ARRAY fallback) behind this explicit flag */
     int32_t reserved0;
     int64_t dfs_block_size;        /* 0 = local FS (NoAlignment); >0 = HDFS PaddingAlignment */
     int64_t max_padding_size;      /* parquet-mr MAX_PADDING_SIZE_DEFAULT = 8 MiB */

@@ -61,6 +61,9 @@ void kpwo_free(kpwo_writer *w);
 /* RunLengthBitPackingHybridEncoder over n values of the given width; returns bytes
  * written or -1 if cap is too small. */
 int64_t kpwo_rle_encode(const uint32_t *vals, uint64_t n, int bit_width, uint8_t *out, uint64_t cap);
+/* DeltaBinaryPackingValuesWriterForInteger (is_long 0, low 32 bits of each value) /
+ * ForLong (is_long 1) over n values, getBytes() of a fresh writer; -1 if cap too small. */
+int64_t kpwo_delta_encode(const uint64_t *vals, uint64_t n, int is_long, uint8_t *out, uint64_t cap);
 /* snappy::RawCompress, pinned algorithm (see oracle_snappy.c header). */
 int64_t kpwo_snappy_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap);
 uint64_t kpwo_snappy_max_compressed_length(uint64_t n);

@@ -35,8 +35,8 @@ MiB = 1024 * 1024
 
 
 def make_props(block_size=128 * MiB, page_size=128 * MiB, codec=UNCOMPRESSED, enable_dictionary=True,
-               dictionary_page_size=1 * MiB, dfs_block_size=0, max_padding_size=8 * MiB):
-    return PropsC(block_size, page_size, dictionary_page_size, 1 if enable_dictionary else 0, codec, 1, 0,
+               dictionary_page_size=1 * MiB, dfs_block_size=0, max_padding_size=8 * MiB, writer_version=1):
+    return PropsC(block_size, page_size, dictionary_page_size, 1 if enable_dictionary else 0, codec, writer_version, 0,
                   dfs_block_size, max_padding_size)
 
 
@@ -83,6 +83,9 @@ def lib():
         L.kpwo_rle_encode.restype = ctypes.c_int64
         L.kpwo_rle_encode.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.c_uint64]
+        L.kpwo_delta_encode.restype = ctypes.c_int64
+        L.kpwo_delta_encode.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_uint64]
         L.kpwo_snappy_compress.restype = ctypes.c_int64
         L.kpwo_snappy_compress.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
         L.kpwo_snappy_max_compressed_length.restype = ctypes.c_uint64
@@ -173,6 +176,17 @@ def rle_encode(values, bit_width):
     n = lib().kpwo_rle_encode(v.ctypes.data, len(v), bit_width, out.ctypes.data, cap)
     if n < 0:
         raise OracleError(-1, "rle")
+    return bytes(out[:n])
+
+
+def delta_encode(values, is_long):
+    """DeltaBinaryPackingValuesWriterFor{Integer,Long}.getBytes() of a fresh writer."""
+    v = np.ascontiguousarray(np.asarray(values).astype(np.int64).view(np.uint64))
+    cap = 64 + len(v) * 10
+    out = np.zeros(cap, dtype=np.uint8)
+    n = lib().kpwo_delta_encode(v.ctypes.data, len(v), 1 if is_long else 0, out.ctypes.data, cap)
+    if n < 0:
+        raise OracleError(-1, "delta")
     return bytes(out[:n])
 
 

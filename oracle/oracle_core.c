@@ -296,6 +296,11 @@ static void write_uvarint(buf_t *b, uint32_t v)
     while (v & 0xFFFFFF80u) { buf_u8(b, (uint8_t)((v & 0x7F) | 0x80)); v >>= 7; }
     buf_u8(b, (uint8_t)(v & 0x7F));
 }
+static void write_uvarint64(buf_t *b, uint64_t v)
+{
+    while (v & ~0x7Full) { buf_u8(b, (uint8_t)((v & 0x7F) | 0x80)); v >>= 7; }
+    buf_u8(b, (uint8_t)(v & 0x7F));
+}
 
 static void rle_write_rle_run(rle_t *r)
 {
@@ -346,6 +351,137 @@ int64_t kpwo_rle_encode(const uint32_t *vals, uint64_t n, int bit_width, uint8_t
     if (n_out) memcpy(out, r.out.p, (size_t)n_out);
     buf_free(&r.out);
     return n_out;
+}
+
+/* ------------------------------------------------------------------ DELTA_BINARY_PACKED
+ * DeltaBinaryPackingValuesWriterForInteger / ForLong (parquet-column 1.10.1), config
+ * blockSizeInValues 128, miniBlockNumInABlock 4 (32 values per miniblock).
+ *   writeInteger/Long: the first value is kept aside (firstValue); every later value adds
+ *     delta = v - previousValue (Java int/long wrapping) to deltaBlockBuffer and lowers
+ *     minDeltaInCurrentBlock; a full block of 128 deltas is flushed.
+ *   flushBlockBuffer: deltas -= minDelta (wrapping); zigzag varint(minDelta); bit width of
+ *     each of the ceil(n/32) miniblocks present (32/64 - nlz(OR of its deltas)); ALL four
+ *     width bytes are written from bitWidths[], which is never cleared: the widths of
+ *     miniblocks a partial last block does not have are the previous block's.  Each present
+ *     miniblock is packed as 4 pack8Values calls (LSB first, values masked to the width);
+ *     the last miniblock's padding slots pack whatever deltaBlockBuffer still holds there
+ *     (the previous block's min-reduced deltas, zeros in a fresh writer).
+ *   getBytes: varint(128) varint(4) varint(totalValueCount) zigzag(firstValue) blocks.
+ *   getBufferedSize = flushed block bytes (baos.size()); reset() keeps bitWidths and
+ *     deltaBlockBuffer. */
+typedef struct {
+    int is_long;
+    buf_t out;            /* baos: flushed blocks */
+    int32_t total;        /* totalValueCount */
+    uint64_t first, prev; /* firstValue, previousValue (int version: low 32 bits) */
+    uint64_t dbuf[128];   /* deltaBlockBuffer */
+    int nbuf;             /* deltaValuesToFlush */
+    int64_t min;          /* minDeltaInCurrentBlock (int version: sign-extended int) */
+    int bw[4];            /* bitWidths */
+} deltaw_t;
+
+static void delta_init(deltaw_t *d, int is_long) { memset(d, 0, sizeof(*d)); d->is_long = is_long; d->min = is_long ? INT64_MAX : INT32_MAX; }
+static void delta_reset(deltaw_t *d) { d->total = 0; d->out.n = 0; d->nbuf = 0; d->min = d->is_long ? INT64_MAX : INT32_MAX; }
+static void delta_free(deltaw_t *d) { buf_free(&d->out); }
+static uint32_t zz32(int32_t v) { return ((uint32_t)v << 1) ^ (uint32_t)(v >> 31); }
+static uint64_t zzl(int64_t v) { return ((uint64_t)v << 1) ^ (uint64_t)(v >> 63); }
+
+static void delta_flush_block(deltaw_t *d)
+{
+    const uint64_t wmask = d->is_long ? ~0ull : 0xffffffffull;
+    for (int i = 0; i < d->nbuf; i++) d->dbuf[i] = (d->dbuf[i] - (uint64_t)d->min) & wmask;
+    if (d->is_long) write_uvarint64(&d->out, zzl(d->min)); else write_uvarint(&d->out, zz32((int32_t)d->min));
+    const int nmb = (d->nbuf + 31) / 32;   /* getMiniBlockCountToFlush */
+    for (int m = 0; m < nmb; m++) {
+        uint64_t mask = 0;
+        const int e = (m + 1) * 32 < d->nbuf ? (m + 1) * 32 : d->nbuf;
+        for (int i = m * 32; i < e; i++) mask |= d->dbuf[i];
+        int w = 0;
+        while (mask) { w++; mask >>= 1; }
+        d->bw[m] = w;
+    }
+    for (int m = 0; m < 4; m++) buf_u8(&d->out, (uint8_t)d->bw[m]);
+    for (int m = 0; m < nmb; m++) {
+        const int w = d->bw[m];
+        const uint64_t vm = w >= 64 ? ~0ull : ((1ull << w) - 1);
+        uint8_t pk[256];
+        memset(pk, 0, sizeof pk);
+        for (int i = 0; i < 32; i++) {
+            const uint64_t x = d->dbuf[m * 32 + i] & vm;
+            for (int b = 0; b < w; b++)
+                if ((x >> b) & 1) { const int bit = i * w + b; pk[bit >> 3] |= (uint8_t)(1u << (bit & 7)); }
+        }
+        buf_put(&d->out, pk, (uint64_t)(4 * w));
+    }
+    d->min = d->is_long ? INT64_MAX : INT32_MAX;
+    d->nbuf = 0;
+}
+
+static void delta_write(deltaw_t *d, uint64_t v)
+{
+    if (!d->is_long) v = (uint32_t)v;
+    d->total++;
+    if (d->total == 1) { d->first = d->prev = v; return; }
+    uint64_t delta;
+    int64_t sd;
+    if (d->is_long) { delta = v - d->prev; sd = (int64_t)delta; }
+    else { delta = (uint32_t)((uint32_t)v - (uint32_t)d->prev); sd = (int32_t)(uint32_t)delta; }
+    d->prev = v;
+    d->dbuf[d->nbuf++] = delta;
+    if (sd < d->min) d->min = sd;
+    if (d->nbuf == 128) delta_flush_block(d);
+}
+
+static void delta_get_bytes(deltaw_t *d, buf_t *out)
+{
+    if (d->nbuf != 0) delta_flush_block(d);
+    write_uvarint(out, 128);
+    write_uvarint(out, 4);
+    write_uvarint(out, (uint32_t)d->total);
+    if (d->is_long) write_uvarint64(out, zzl((int64_t)d->first)); else write_uvarint(out, zz32((int32_t)(uint32_t)d->first));
+    buf_put(out, d->out.p, d->out.n);
+}
+
+int64_t kpwo_delta_encode(const uint64_t *vals, uint64_t n, int is_long, uint8_t *out, uint64_t cap)
+{
+    deltaw_t d;
+    delta_init(&d, is_long);
+    for (uint64_t i = 0; i < n; i++) delta_write(&d, vals[i]);
+    buf_t b = {0};
+    delta_get_bytes(&d, &b);
+    int64_t n_out = (int64_t)b.n;
+    if ((uint64_t)n_out > cap) n_out = -1;
+    else if (n_out) memcpy(out, b.p, (size_t)n_out);
+    buf_free(&b);
+    delta_free(&d);
+    return n_out;
+}
+
+/* DeltaByteArrayWriter (prefix lengths: DeltaBinaryPackingValuesWriterForInteger; suffixes:
+ * DeltaLengthByteArrayValuesWriter = lengths DELTA_BINARY_PACKED + concatenated bytes).
+ * writeBytes: prefix = common leading bytes with the previous value; getBytes = prefix
+ * lengths | suffix lengths | suffix bytes; reset() forgets the previous value. */
+typedef struct { deltaw_t pre, len; buf_t sfx; buf_t prev; } dbaw_t;
+
+static void dba_init(dbaw_t *w) { memset(w, 0, sizeof(*w)); delta_init(&w->pre, 0); delta_init(&w->len, 0); }
+static void dba_free(dbaw_t *w) { delta_free(&w->pre); delta_free(&w->len); buf_free(&w->sfx); buf_free(&w->prev); }
+static void dba_reset(dbaw_t *w) { delta_reset(&w->pre); delta_reset(&w->len); w->sfx.n = 0; w->prev.n = 0; }
+static int64_t dba_buffered(const dbaw_t *w) { return (int64_t)(w->pre.out.n + w->len.out.n + w->sfx.n); }
+static void dba_write(dbaw_t *w, const uint8_t *p, uint32_t n)
+{
+    uint32_t m = (uint32_t)w->prev.n < n ? (uint32_t)w->prev.n : n, i = 0;
+    while (i < m && w->prev.p[i] == p[i]) i++;
+    delta_write(&w->pre, i);
+    delta_write(&w->len, n - i);
+    buf_put(&w->sfx, p + i, n - i);
+    w->prev.n = 0;
+    buf_put(&w->prev, p, n);
+}
+static void dba_get_bytes(dbaw_t *w, buf_t *out)
+{
+    delta_get_bytes(&w->pre, out);
+    delta_get_bytes(&w->len, out);
+    buf_put(out, w->sfx.p, w->sfx.n);
 }
 
 /* ------------------------------------------------------------------ statistics
@@ -629,16 +765,6 @@ static void dict_entry_to_plain(const dictw_t *d, int32_t id, plainw_t *pw)
     if (d->phys == KPW_BYTE_ARRAY) plain_bin(pw, d->arena.p + d->eoff[id], d->elen[id]);
     else plain_fixed(pw, d->phys, d->ekeys[id]);
 }
-/* fallBackAllValuesTo */
-static void dict_fall_back_all(dictw_t *d, plainw_t *pw)
-{
-    for (int64_t i = 0; i < d->nenc; i++) dict_entry_to_plain(d, d->enc[i], pw);
-    if (d->last_used_size == 0) {
-        dict_clear_content(d);
-        d->dict_byte_size = 0;
-        d->nenc = 0;
-    }
-}
 
 /* BooleanPlainValuesWriter -> ByteBitPackingValuesWriter(1, LITTLE_ENDIAN) */
 typedef struct { buf_t b; int64_t count; } boolw_t;
@@ -649,57 +775,140 @@ static void bool_write(boolw_t *w, int v)
     w->count++;
 }
 
-/* FallbackValuesWriter state + its wrapped writers */
-enum { DW_PLAIN = 0, DW_FALLBACK = 1, DW_BOOL = 2 };
+/* The non-dictionary writer a column uses directly (dictionary off) or falls back to.
+ *   v1 DefaultV1ValuesWriterFactory: PLAIN for every type (booleans: BooleanPlainValuesWriter).
+ *   v2 DefaultV2ValuesWriterFactory: INT32/INT64 -> DeltaBinaryPackingValuesWriterFor{Integer,Long},
+ *      BINARY -> DeltaByteArrayWriter, FLOAT/DOUBLE -> PlainValuesWriter,
+ *      BOOLEAN -> RunLengthBitPackingHybridValuesWriter(1) (no dictionary). */
+enum { PW_PLAIN = 0, PW_DELTA = 1, PW_DBA = 2 };
 
 typedef struct {
     int kind;
     int phys;
+    plainw_t plain;
+    deltaw_t delta;
+    dbaw_t dba;
+} basew_t;
+
+static void basew_init(basew_t *b, int phys, int v2)
+{
+    memset(b, 0, sizeof(*b));
+    b->phys = phys;
+    b->kind = PW_PLAIN;
+    if (v2 && (phys == KPW_INT32 || phys == KPW_INT64)) { b->kind = PW_DELTA; delta_init(&b->delta, phys == KPW_INT64); }
+    else if (v2 && phys == KPW_BYTE_ARRAY) { b->kind = PW_DBA; dba_init(&b->dba); }
+}
+static void basew_free(basew_t *b) { buf_free(&b->plain.b); delta_free(&b->delta); dba_free(&b->dba); }
+static void basew_write_fixed(basew_t *b, uint64_t key)
+{
+    if (b->kind == PW_DELTA) delta_write(&b->delta, key); else plain_fixed(&b->plain, b->phys, key);
+}
+static void basew_write_bin(basew_t *b, const uint8_t *p, uint32_t n)
+{
+    if (b->kind == PW_DBA) dba_write(&b->dba, p, n); else plain_bin(&b->plain, p, n);
+}
+static int64_t basew_buffered(const basew_t *b)
+{
+    switch (b->kind) {
+    case PW_DELTA: return (int64_t)b->delta.out.n;
+    case PW_DBA: return dba_buffered(&b->dba);
+    default: return (int64_t)b->plain.b.n;
+    }
+}
+static int basew_page(basew_t *b, buf_t *out)
+{
+    switch (b->kind) {
+    case PW_DELTA: delta_get_bytes(&b->delta, out); return KPW_ENC_DELTA_BINARY_PACKED;
+    case PW_DBA: dba_get_bytes(&b->dba, out); return KPW_ENC_DELTA_BYTE_ARRAY;
+    default: buf_put(out, b->plain.b.p, b->plain.b.n); return KPW_ENC_PLAIN;
+    }
+}
+static void basew_reset(basew_t *b)
+{
+    switch (b->kind) {
+    case PW_DELTA: delta_reset(&b->delta); break;
+    case PW_DBA: dba_reset(&b->dba); break;
+    default: b->plain.b.n = 0;
+    }
+}
+
+/* fallBackAllValuesTo */
+static void dict_fall_back_all(dictw_t *d, basew_t *bw)
+{
+    for (int64_t i = 0; i < d->nenc; i++) {
+        const int32_t id = d->enc[i];
+        if (d->phys == KPW_BYTE_ARRAY) basew_write_bin(bw, d->arena.p + d->eoff[id], d->elen[id]);
+        else basew_write_fixed(bw, d->ekeys[id]);
+    }
+    if (d->last_used_size == 0) {
+        dict_clear_content(d);
+        d->dict_byte_size = 0;
+        d->nenc = 0;
+    }
+}
+
+/* FallbackValuesWriter state + its wrapped writers */
+enum { DW_PLAIN = 0, DW_FALLBACK = 1, DW_BOOL = 2, DW_RLEBOOL = 3 };
+
+typedef struct {
+    int kind;
+    int phys;
+    int v2;
     /* fallback */
     dictw_t dict;
-    plainw_t plain;
+    basew_t base;        /* the direct writer (DW_PLAIN) or the fallback writer (DW_FALLBACK) */
     int fell_back, initial_used_and_had_dict, first_page;
     int64_t raw;
     /* bool */
     boolw_t bw;
+    rle_t rb;            /* v2 booleans */
 } dataw_t;
 
 static void dataw_init(dataw_t *w, int phys, const kpw_props *pr)
 {
     memset(w, 0, sizeof(*w));
     w->phys = phys;
-    if (phys == KPW_BOOLEAN) w->kind = DW_BOOL;
-    else if (pr->enable_dictionary) { w->kind = DW_FALLBACK; dict_init(&w->dict, phys, pr->dictionary_page_size); w->first_page = 1; }
+    w->v2 = pr->writer_version == 2;
+    if (phys == KPW_BOOLEAN) {
+        w->kind = w->v2 ? DW_RLEBOOL : DW_BOOL;
+        if (w->v2) rle_init(&w->rb, 1);
+        return;
+    }
+    basew_init(&w->base, phys, w->v2);
+    if (pr->enable_dictionary) { w->kind = DW_FALLBACK; dict_init(&w->dict, phys, pr->dictionary_page_size); w->first_page = 1; }
     else w->kind = DW_PLAIN;
 }
 static void dataw_free(dataw_t *w)
 {
     if (w->kind == DW_FALLBACK) dict_free(&w->dict);
-    buf_free(&w->plain.b);
+    basew_free(&w->base);
     buf_free(&w->bw.b);
+    buf_free(&w->rb.out);
 }
 static int64_t dataw_buffered(const dataw_t *w)
 {
     switch (w->kind) {
     case DW_BOOL: return (w->bw.count + 7) / 8;
-    case DW_FALLBACK: return w->raw;
-    default: return (int64_t)w->plain.b.n;
+    case DW_RLEBOOL: return (int64_t)w->rb.out.n;   /* RunLengthBitPackingHybridEncoder.getBufferedSize */
+    case DW_FALLBACK: return w->raw;                 /* FallbackValuesWriter: rawDataByteSize */
+    default: return basew_buffered(&w->base);
     }
 }
-static void dataw_fall_back(dataw_t *w) { w->fell_back = 1; dict_fall_back_all(&w->dict, &w->plain); }
+static void dataw_fall_back(dataw_t *w) { w->fell_back = 1; dict_fall_back_all(&w->dict, &w->base); }
 
 static void dataw_write(dataw_t *w, const pval_t *v)
 {
     if (w->kind == DW_BOOL) { bool_write(&w->bw, v->bits != 0); return; }
+    if (w->kind == DW_RLEBOOL) { rle_write(&w->rb, v->bits != 0); return; }
     int is_bin = w->phys == KPW_BYTE_ARRAY;
     uint64_t key = is_bin ? 0 : canon_bits(w->phys, v->bits);
     if (w->kind == DW_PLAIN) {
-        if (is_bin) plain_bin(&w->plain, v->ptr, v->len); else plain_fixed(&w->plain, w->phys, key);
+        if (is_bin) basew_write_bin(&w->base, v->ptr, v->len); else basew_write_fixed(&w->base, key);
         return;
     }
     w->raw += is_bin ? (int64_t)v->len + 4 : (w->phys == KPW_INT32 || w->phys == KPW_FLOAT ? 4 : 8);
     if (w->fell_back) {
-        if (is_bin) plain_bin(&w->plain, v->ptr, v->len); else plain_fixed(&w->plain, w->phys, key);
+        if (is_bin) basew_write_bin(&w->base, v->ptr, v->len); else basew_write_fixed(&w->base, key);
     } else {
         dict_write(&w->dict, key, v->ptr, v->len);
         /* checkFallback: shouldFallBack() */
@@ -707,16 +916,21 @@ static void dataw_write(dataw_t *w, const pval_t *v)
     }
 }
 
-/* getBytes() then getEncoding() — ColumnWriterV1.writePage evaluation order. */
+/* getBytes() then getEncoding() — ColumnWriterV1/V2.writePage evaluation order. */
 static int dataw_page(dataw_t *w, buf_t *out)
 {
+    const int dict_enc = w->v2 ? KPW_ENC_RLE_DICTIONARY : KPW_ENC_PLAIN_DICTIONARY;
     switch (w->kind) {
     case DW_BOOL:
         buf_put(out, w->bw.b.p, w->bw.b.n);
         return KPW_ENC_PLAIN;
+    case DW_RLEBOOL:   /* RunLengthBitPackingHybridValuesWriter.getBytes: 4-byte LE length + RLE */
+        rle_finish(&w->rb);
+        buf_le32(out, (uint32_t)w->rb.out.n);
+        buf_put(out, w->rb.out.p, w->rb.out.n);
+        return KPW_ENC_RLE;
     case DW_PLAIN:
-        buf_put(out, w->plain.b.p, w->plain.b.n);
-        return KPW_ENC_PLAIN;
+        return basew_page(&w->base, out);
     }
     int enc;
     if (!w->fell_back && w->first_page) {
@@ -726,27 +940,28 @@ static int dataw_page(dataw_t *w, buf_t *out)
         if ((int64_t)tmp.n + w->dict.dict_byte_size < w->raw) {
             buf_put(out, tmp.p, tmp.n);
             buf_free(&tmp);
-            enc = KPW_ENC_PLAIN_DICTIONARY;
+            enc = dict_enc;
             goto have_enc;
         }
         buf_free(&tmp);
         dataw_fall_back(w);
     }
-    if (w->fell_back) { buf_put(out, w->plain.b.p, w->plain.b.n); enc = KPW_ENC_PLAIN; }
-    else { dict_get_bytes(&w->dict, out); enc = KPW_ENC_PLAIN_DICTIONARY; }
+    if (w->fell_back) enc = basew_page(&w->base, out);
+    else { dict_get_bytes(&w->dict, out); enc = dict_enc; }
 have_enc:
-    if (!w->fell_back && !w->initial_used_and_had_dict) w->initial_used_and_had_dict = (enc == KPW_ENC_PLAIN_DICTIONARY);
+    if (!w->fell_back && !w->initial_used_and_had_dict) w->initial_used_and_had_dict = (enc == dict_enc);
     return enc;
 }
 static void dataw_reset(dataw_t *w)
 {
     switch (w->kind) {
     case DW_BOOL: w->bw.b.n = 0; w->bw.count = 0; break;
-    case DW_PLAIN: w->plain.b.n = 0; break;
+    case DW_RLEBOOL: rle_reset(&w->rb); break;
+    case DW_PLAIN: basew_reset(&w->base); break;
     default:
         w->raw = 0;
         w->first_page = 0;
-        if (w->fell_back) w->plain.b.n = 0; else w->dict.nenc = 0;
+        if (w->fell_back) basew_reset(&w->base); else w->dict.nenc = 0;
     }
 }
 /* toDictPageAndClose: returns 1 + page bytes/num entries if a dictionary page exists */
@@ -784,12 +999,14 @@ typedef struct {
     encset_t rl_encs, dl_encs;
     int *data_encs; int ndata_encs, data_encs_cap;
     int has_dict; buf_t dict_bytes; int32_t dict_uncomp, dict_nent;
+    int64_t rows_written;  /* ColumnWriterV2.rowsWrittenSoFar */
 } colw_t;
 
 /* finished column chunk metadata kept for the footer */
 typedef struct {
     int phys;
     int codec;
+    int v2;                /* EncodingStats.usesV2Pages */
     encset_t encs;
     enccount_t dict_stats, data_stats;
     int64_t num_values, total_uncomp, total_comp, data_page_offset;
@@ -811,6 +1028,9 @@ struct kpwo_writer {
     rgmeta_t *rgs; int nrgs, rgcap;
     int closed;
     uint8_t *ctmp; uint64_t ctmp_cap;
+    /* ColumnWriteStoreV2 (writer_version 2): store-level page size checks per record */
+    int v2;
+    int64_t v2_rows, v2_next_check;
 };
 
 static void page_compress(kpwo_writer *w, const buf_t *in, buf_t *out)
@@ -881,6 +1101,65 @@ static void pagestore_write_page(kpwo_writer *w, colw_t *c, const buf_t *body, i
     buf_free(&comp);
 }
 
+/* ColumnChunkPageWriter.writePageV2: rl and dl stay uncompressed in front of the
+ * compressed values; ParquetMetadataConverter.writeDataPageV2Header (is_compressed is
+ * never set, so it is not serialised). */
+static void pagestore_write_page_v2(kpwo_writer *w, colw_t *c, int32_t rows, int32_t nulls, int32_t nvalues,
+                                    const buf_t *dl, int data_enc, const buf_t *data)
+{
+    buf_t comp = {0};
+    page_compress(w, data, &comp);
+    const int32_t uncomp = (int32_t)(data->n + dl->n), compsz = (int32_t)(comp.n + dl->n);
+    buf_t hdr = {0};
+    tc_t t = {&hdr, {0}, 0};
+    tc_i32(&t, 1, KPW_DATA_PAGE_V2);
+    tc_i32(&t, 2, uncomp);
+    tc_i32(&t, 3, compsz);
+    tc_struct_begin(&t, 8);
+    tc_i32(&t, 1, nvalues);
+    tc_i32(&t, 2, nulls);
+    tc_i32(&t, 3, rows);
+    tc_i32(&t, 4, data_enc);
+    tc_i32(&t, 5, (int32_t)dl->n);
+    tc_i32(&t, 6, 0);
+    if (!stats_empty(&c->pstats)) tc_statistics(&t, 8, &c->pstats);
+    tc_struct_end(&t);
+    buf_u8(&hdr, 0);
+    c->uncomp_len += uncomp;
+    c->comp_len += compsz;
+    c->total_values += nvalues;
+    if (!c->tstats_init) { stats_copy(&c->tstats, &c->pstats); c->tstats_init = 1; }
+    else stats_merge(&c->tstats, &c->pstats);
+    buf_put(&c->pages, hdr.p, hdr.n);
+    buf_put(&c->pages, dl->p, dl->n);
+    buf_put(&c->pages, comp.p, comp.n);
+    if (c->ndata_encs == c->data_encs_cap) { c->data_encs_cap = c->data_encs_cap ? c->data_encs_cap * 2 : 16; c->data_encs = (int *)xrealloc(c->data_encs, (size_t)c->data_encs_cap * sizeof(int)); }
+    c->data_encs[c->ndata_encs++] = data_enc;
+    buf_free(&hdr);
+    buf_free(&comp);
+}
+
+/* ColumnWriterV2.writePage(rowCount): dataColumn.getBytes()/getEncoding() first, then the
+ * levels (max level 0 -> empty); RLE levels carry no length prefix in a v2 page. */
+static void colw_write_page_v2(kpwo_writer *w, colw_t *c, int64_t row_count)
+{
+    const int32_t page_rows = (int32_t)(row_count - c->rows_written);
+    c->rows_written = row_count;
+    buf_t data = {0}, dl = {0};
+    const int enc = dataw_page(&c->data, &data);
+    if (c->ci->optional) {
+        rle_finish(&c->dl);
+        buf_put(&dl, c->dl.out.p, c->dl.out.n);
+    }
+    pagestore_write_page_v2(w, c, page_rows, (int32_t)c->pstats.nulls, c->value_count, &dl, enc, &data);
+    buf_free(&data);
+    buf_free(&dl);
+    if (c->ci->optional) rle_reset(&c->dl);
+    dataw_reset(&c->data);
+    c->value_count = 0;
+    stats_reset(&c->pstats, c->ci->phys);
+}
+
 /* ColumnWriterV1.writePage */
 static void colw_write_page(kpwo_writer *w, colw_t *c)
 {
@@ -935,13 +1214,46 @@ static void colw_write_value(kpwo_writer *w, colw_t *c, const pval_t *v)
         rle_write(&c->dl, 0);
         c->pstats.nulls++;
     }
-    colw_account(w, c);
+    if (w->v2) ++c->value_count;   /* ColumnWriterV2: page checks happen per record, in the store */
+    else colw_account(w, c);
 }
 
-/* ColumnWriterV1.flush */
+/* ColumnWriteStoreV2.sizeCheck (1.10.1), run from endRecord when rowCount reaches
+ * rowCountForNextSizeCheck.  thresholdTolerance = (long)(pageSize * 0.1f); a column whose
+ * page has <= tolerance bytes left is written out; rowsToFillPage keeps parquet-mr's
+ * `(long)((float)rows) / usedMem * remainingMem` (integer division first). */
+static void store_size_check_v2(kpwo_writer *w)
+{
+    const int64_t ps = w->props.page_size;
+    const int64_t tol = (int64_t)((float)ps * 0.1f);
+    int64_t min_wait = INT64_MAX;
+    for (int k = 0; k < w->ncols; k++) {
+        colw_t *c = &w->cw[k];
+        const int64_t used = colw_mem(c);
+        const int64_t rows = w->v2_rows - c->rows_written;
+        int64_t remaining = ps - used;
+        if (remaining <= tol) {
+            colw_write_page_v2(w, c, w->v2_rows);
+            remaining = ps;
+        }
+        const int64_t fill = used == 0 ? 10000 : ((int64_t)(float)rows / used) * remaining;
+        if (fill < min_wait) min_wait = fill;
+    }
+    if (min_wait == INT64_MAX) min_wait = 100;
+    int64_t half = min_wait / 2;
+    if (half < 100) half = 100;
+    if (half > 10000) half = 10000;
+    w->v2_next_check = w->v2_rows + half;
+}
+
+/* ColumnWriterV1.flush / ColumnWriteStoreV2.flush + ColumnWriterV2.finalizeColumnChunk */
 static void colw_flush(kpwo_writer *w, colw_t *c)
 {
-    if (c->value_count > 0) colw_write_page(w, c);
+    if (w->v2) {
+        if (w->v2_rows - c->rows_written > 0) colw_write_page_v2(w, c, w->v2_rows);
+    } else if (c->value_count > 0) {
+        colw_write_page(w, c);
+    }
     buf_t dp = {0};
     int32_t nent = 0;
     if (dataw_dict_page(&c->data, &dp, &nent)) {
@@ -991,6 +1303,8 @@ static int64_t next_row_group_size(const kpwo_writer *w)
 static void store_init(kpwo_writer *w)
 {
     for (int c = 0; c < w->ncols; c++) colw_init(&w->cw[c], &w->cols[c], &w->props);
+    w->v2_rows = 0;
+    w->v2_next_check = 100;   /* props.getMinRowCountForPageSizeCheck() */
 }
 static void store_free(kpwo_writer *w)
 {
@@ -1013,10 +1327,13 @@ static void flush_row_group(kpwo_writer *w)
             memset(m, 0, sizeof(*m));
             m->phys = w->cols[c].phys;
             m->codec = w->props.codec;
+            m->v2 = w->v2;
             m->num_values = cc->total_values;
             m->data_page_offset = (int64_t)w->out.n; /* startColumn: currentChunkFirstDataPage */
             int64_t uncomp = 0, comp = 0;
             if (cc->has_dict) {
+                /* DictionaryValuesWriter: PLAIN_DICTIONARY (v1) / PLAIN (v2) dictionary pages */
+                const int denc = w->v2 ? KPW_ENC_PLAIN : KPW_ENC_PLAIN_DICTIONARY;
                 buf_t hdr = {0};
                 tc_t t = {&hdr, {0}, 0};
                 tc_i32(&t, 1, KPW_DICTIONARY_PAGE);
@@ -1024,7 +1341,7 @@ static void flush_row_group(kpwo_writer *w)
                 tc_i32(&t, 3, (int32_t)cc->dict_bytes.n);
                 tc_struct_begin(&t, 7);
                 tc_i32(&t, 1, cc->dict_nent);
-                tc_i32(&t, 2, KPW_ENC_PLAIN_DICTIONARY);
+                tc_i32(&t, 2, denc);
                 tc_struct_end(&t);
                 buf_u8(&hdr, 0);
                 uncomp += cc->dict_uncomp + (int64_t)hdr.n;
@@ -1032,8 +1349,8 @@ static void flush_row_group(kpwo_writer *w)
                 buf_put(&w->out, hdr.p, hdr.n);
                 buf_put(&w->out, cc->dict_bytes.p, cc->dict_bytes.n);
                 buf_free(&hdr);
-                enccount_add(&m->dict_stats, KPW_ENC_PLAIN_DICTIONARY);
-                encset_add(&m->encs, KPW_ENC_PLAIN_DICTIONARY);
+                enccount_add(&m->dict_stats, denc);
+                encset_add(&m->encs, denc);
             }
             int64_t headers = (int64_t)cc->pages.n - cc->comp_len;
             uncomp += cc->uncomp_len + headers;
@@ -1177,7 +1494,8 @@ static void write_footer(kpwo_writer *w)
             }
             for (int i = 0; i < m->data_stats.n; i++) {
                 tc_elem_struct_begin(&t);
-                tc_i32(&t, 1, KPW_DATA_PAGE); tc_i32(&t, 2, m->data_stats.enc[i]); tc_i32(&t, 3, m->data_stats.cnt[i]);
+                tc_i32(&t, 1, m->v2 ? KPW_DATA_PAGE_V2 : KPW_DATA_PAGE);
+                tc_i32(&t, 2, m->data_stats.enc[i]); tc_i32(&t, 3, m->data_stats.cnt[i]);
                 tc_struct_end(&t);
             }
             tc_struct_end(&t);   /* ColumnMetaData */
@@ -1237,7 +1555,8 @@ kpwo_writer *kpwo_open(const kpw_schema *schema, const kpw_props *props, int *st
 {
     int st = KPW_OK;
     if (!schema || !props || schema->num_columns <= 0 || !schema->columns || !schema->message_name) { st = KPW_ERR_INVALID_ARG; goto fail; }
-    if (props->writer_version != 1 || (props->codec != KPW_UNCOMPRESSED && props->codec != KPW_SNAPPY) ||
+    if ((props->writer_version != 1 && props->writer_version != 2) ||
+        (props->codec != KPW_UNCOMPRESSED && props->codec != KPW_SNAPPY) ||
         props->block_size <= 0 || props->page_size <= 0 || props->dictionary_page_size <= 0) { st = KPW_ERR_UNSUPPORTED; goto fail; }
     kpwo_writer *w = (kpwo_writer *)xmalloc(sizeof(*w));
     memset(w, 0, sizeof(*w));
@@ -1266,6 +1585,7 @@ kpwo_writer *kpwo_open(const kpw_schema *schema, const kpw_props *props, int *st
     w->message_name = strdup(schema->message_name);
     w->proto_class = schema->proto_class ? strdup(schema->proto_class) : NULL;
     w->props = *props;
+    w->v2 = props->writer_version == 2;
     w->cw = (colw_t *)xmalloc((size_t)w->ncols * sizeof(colw_t));
     w->vals = (pval_t *)xmalloc((size_t)w->ncols * sizeof(pval_t));
     buf_put(&w->out, "PAR1", 4);
@@ -1285,6 +1605,10 @@ int kpwo_write(kpwo_writer *w, const uint8_t *rec, uint64_t len)
     if (w->closed) return KPW_ERR_STATE;
     if (proto_decode(w->cols, w->ncols, rec, len, w->vals)) return KPW_ERR_INVALID_PROTO;
     for (int c = 0; c < w->ncols; c++) colw_write_value(w, &w->cw[c], &w->vals[c]);
+    if (w->v2) {   /* ColumnWriteStoreV2.endRecord (MessageColumnIO endMessage), before the block check */
+        ++w->v2_rows;
+        if (w->v2_rows >= w->v2_next_check) store_size_check_v2(w);
+    }
     ++w->record_count;
     check_block_size(w);
     ++w->num_records;

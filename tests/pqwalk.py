@@ -98,8 +98,13 @@ def decompress_pages(buf, codec_name="snappy"):
     out = []
     for pg in pages(buf):
         h = pg["header"]
-        if codec_name == "snappy":
-            raw = pa.decompress(pg["body"], decompressed_size=h[2], codec="snappy", asbytes=True)
+        # DataPageV2 (type 3): rl + dl bytes stay uncompressed in front of the values
+        lv = (h[8][5] + h[8][6]) if h[1] == 3 else 0
+        if codec_name == "snappy" and h[2] == lv:
+            raw = pg["body"]
+        elif codec_name == "snappy":
+            raw = pg["body"][:lv] + pa.decompress(pg["body"][lv:], decompressed_size=h[2] - lv, codec="snappy",
+                                                  asbytes=True)
         else:
             raw = pg["body"]
         assert len(raw) == h[2]

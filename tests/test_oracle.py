@@ -75,6 +75,106 @@ def test_oracle_readback(kind, param, n, codec, page_size, block_size, dictionar
     pqwalk.decompress_pages(fb, "snappy" if codec == oracle.SNAPPY else "none")
 
 
+V2_CASES = [(synth.KIND_SAMPLE, 30, 3000), (synth.KIND_REC8, 0, 4000), (synth.KIND_HIGHCARD, 0, 1500)]
+
+
+@pytest.mark.parametrize("kind,param,n", V2_CASES)
+@pytest.mark.parametrize("codec", [oracle.UNCOMPRESSED, oracle.SNAPPY])
+@pytest.mark.parametrize("page_size,block_size", [(128 * MiB, 128 * MiB), (8192, 64 * 1024)])
+@pytest.mark.parametrize("dictionary", [True, False])
+def test_oracle_v2_readback(kind, param, n, codec, page_size, block_size, dictionary):
+    """PARQUET_2_0 (A10): DataPageV2, RLE_DICTIONARY, DELTA_BINARY_PACKED / DELTA_BYTE_ARRAY
+    fallback, RLE booleans — every file reads back value-exact through pyarrow."""
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, 0xC0FFEE11 + kind, n, param=param)
+    props = oracle.make_props(block_size=block_size, page_size=page_size, codec=codec, enable_dictionary=dictionary,
+                              writer_version=2)
+    fb = oracle.encode_file(schema, data, offs, props)
+    _readback(schema, synth.records(data, offs), fb)
+    pqwalk.decompress_pages(fb, "snappy" if codec == oracle.SNAPPY else "none")
+    assert {p["header"][1] for p in pqwalk.pages(fb)} <= {2, 3}   # dictionary + DataPageV2 only
+
+
+def _arrow_v2_values(arr, encoding):
+    """Values bytes of the single DataPageV2 pyarrow writes for a non-nullable column."""
+    t = pa.table({"x": arr}, schema=pa.schema([pa.field("x", arr.type, nullable=False)]))
+    b = io.BytesIO()
+    pq.write_table(t, b, use_dictionary=False, column_encoding={"x": encoding}, data_page_version="2.0",
+                   compression="NONE", write_statistics=False)
+    pgs = [p for p in pqwalk.pages(b.getvalue()) if p["header"][1] == 3]
+    assert len(pgs) == 1
+    h = pgs[0]["header"][8]
+    return pgs[0]["body"][h[5] + h[6]:]
+
+
+@pytest.mark.parametrize("n", [1, 2, 33, 100, 129, 257, 1 + 128 * 40])
+@pytest.mark.parametrize("kind", ["small", "wide", "neg", "const"])
+def test_delta_int32_matches_pyarrow(n, kind):
+    """DeltaBinaryPackingValuesWriterForInteger vs Arrow's independent DELTA_BINARY_PACKED
+    encoder (same 128-value blocks / 4 miniblocks for int32): byte-identical whenever the
+    page has no partial block after a full one — the only place parquet-mr's never-cleared
+    bitWidths/deltaBlockBuffer show (pinned separately below)."""
+    rng = np.random.default_rng(n * 7 + len(kind))
+    if kind == "small":
+        v = np.cumsum(rng.integers(-5, 50, n))
+    elif kind == "wide":
+        v = rng.integers(-2 ** 31, 2 ** 31, n)
+    elif kind == "neg":
+        v = -np.arange(n) * 7
+    else:
+        v = np.full(n, 42)
+    v = v.astype(np.int32)
+    assert oracle.delta_encode(v.astype(np.int64), False) == _arrow_v2_values(pa.array(v, type=pa.int32()),
+                                                                           "DELTA_BINARY_PACKED")
+
+
+def test_delta_partial_block_stale_state():
+    """parquet-mr quirk restated: a partial last block writes the previous block's widths for
+    its missing miniblocks and packs the previous block's reduced deltas as padding (Arrow
+    writes zeros there).  Everything before the last block's width bytes is identical."""
+    def varint_at(b, p):
+        r = s = 0
+        while True:
+            c = b[p]
+            p += 1
+            r |= (c & 0x7F) << s
+            s += 7
+            if not c & 0x80:
+                return r, p
+
+    v = np.cumsum(np.random.default_rng(5).integers(0, 1000, 200)).astype(np.int32)   # 128 + 71 deltas
+    ours = oracle.delta_encode(v.astype(np.int64), False)
+    arrow = _arrow_v2_values(pa.array(v, type=pa.int32()), "DELTA_BINARY_PACKED")
+    assert len(ours) == len(arrow) and ours != arrow
+    p = 0
+    for _ in range(4):                       # block size, miniblocks, count, first value
+        _, p = varint_at(ours, p)
+    _, p = varint_at(ours, p)                # block 0: min delta
+    w0 = list(ours[p:p + 4])
+    p += 4 + sum(4 * w for w in w0)
+    _, p = varint_at(ours, p)                # block 1: min delta
+    w1 = list(ours[p:p + 4])
+    assert ours[:p + 3] == arrow[:p + 3]     # identical up to the first stale width byte
+    assert w1[3] == w0[3] and arrow[p + 3] == 0   # 3 miniblocks present; the 4th width is block 0's
+    pad0 = p + 4 + 4 * w1[0] + 4 * w1[1] + (7 * w1[2] + 7) // 8   # 7 real values in miniblock 2
+    assert ours[p + 4:pad0 - 1] == arrow[p + 4:pad0 - 1]
+    assert any(ours[pad0:]) and not any(arrow[pad0:])   # stale padding vs zeros
+
+
+@pytest.mark.parametrize("n", [1, 5, 129, 257, 1 + 128 * 9])
+def test_delta_byte_array_matches_pyarrow(n):
+    """DeltaByteArrayWriter (prefix lengths + DeltaLengthByteArray suffixes) vs Arrow's
+    DELTA_BYTE_ARRAY encoder, through a whole v2 file of the oracle (no dictionary)."""
+    rng = np.random.default_rng(n)
+    words = [("key%04d" % int(rng.integers(0, 300))).encode() +
+             bytes(rng.integers(97, 100, int(rng.integers(0, 6))).astype(np.uint8)) for _ in range(n)]
+    recs = [b"\x0a" + _varint(len(w)) + w + b"\x10" + _varint(i) for i, w in enumerate(words)]
+    data, offs = synth.pack(recs)
+    fb = oracle.encode_file(synth.SAMPLE, data, offs, oracle.make_props(writer_version=2, enable_dictionary=False))
+    page = [p for p in pqwalk.pages(fb) if p["col"] == 0][0]
+    assert page["body"] == _arrow_v2_values(pa.array(words, type=pa.binary()), "DELTA_BYTE_ARRAY")
+
+
 def _sample_msg(**kw):
     cls = protoutil.message_class(synth.SAMPLE)
     m = cls()
