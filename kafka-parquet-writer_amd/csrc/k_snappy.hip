@@ -648,7 +648,7 @@ __device__ __forceinline__ uint32_t find_match_length_s(const SIn &si, const Src
 }
 
 template <int SEQ>
-__global__ void __launch_bounds__(64) k_snappy_s(SnappyArgs a)
+__device__ __forceinline__ void k_snappy_s_body(const SnappyArgs &a)
 {
     __shared__ uint16_t table[SNAPPY_MAX_TABLE];
     const int lane = threadIdx.x;
@@ -764,6 +764,12 @@ __global__ void __launch_bounds__(64) k_snappy_s(SnappyArgs a)
 emit_remainder:
     if (next_emit < ip_end) op = emit_literal(out, op, g, next_emit, ip_end - next_emit, lane);
     if (lane == 0) a.frag_len[f] = op;
+}
+
+template <int SEQ>
+__global__ void __launch_bounds__(64) k_snappy_s(SnappyArgs a)
+{
+    k_snappy_s_body<SEQ>(a);
 }
 
 // ------------------------------------------------------------------ scalar + SGPR window
@@ -961,6 +967,241 @@ emit_remainder:
     if (lane == 0) a.frag_len[f] = op;
 }
 
+// ------------------------------------------------------------------ register-table variant
+// The LDS table above caps residency at 5 fragments per CU (32 KiB each) and puts an LDS
+// round trip on every probe.  Here the 16384-entry uint16 table lives in 128 VGPRs of the
+// wave (4 vectors of 32 dwords; entry h -> register h>>7, lane (h>>1)&63, half h&1), read
+// with one indexed v_movrels + v_readlane and written with v_movreld of a lane-selected
+// value; the input comes through a 256-byte VGPR window (InWin).  No LDS: occupancy is
+// bound by registers only.  The literal search is sequential, so a fragment whose literal
+// search runs past VT_ABORT probes (incompressible data) stops and is left to k_snappy_s
+// (frag_len = VT_ABORTED), which has the 64-probe batched search.  Same algorithm, same
+// output bytes.
+constexpr uint32_t VT_ABORTED = 0xffffffffu;
+#ifndef VT_ABORT
+#define VT_ABORT 128
+#endif
+
+// The table is pinned to v128..v255: k_snappy_v is compiled with amdgpu_num_vgpr(128), so
+// the register allocator only uses v0..v127, and one asm statement that clobbers
+// v128..v255 makes the kernel descriptor allocate all 256 (checked: .vgpr_count 256, no
+// scratch; tests/microbench/vtab_probe.hip).  A compiler-visible vector table does not
+// work: ext_vector element stores with a runtime index go to scratch, and vector SSA values
+// are copied whole at every control-flow merge.  Rows are read/written through VGPR index
+// mode (s_set_gpr_idx_on, index = row < 128); volatile asm statements keep program order.
+#define VT_CLOBBERS \
+    "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", \
+    "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", \
+    "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v164", "v165", "v166", "v167", "v168", "v169", \
+    "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178", "v179", "v180", "v181", "v182", "v183", \
+    "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191", "v192", "v193", "v194", "v195", "v196", "v197", \
+    "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", \
+    "v212", "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224", "v225", \
+    "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", \
+    "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", \
+    "v254", "v255"
+
+// (gfx950 has no v_movrels/v_movreld: VGPR index mode is the only runtime register index)
+__device__ __forceinline__ uint32_t vt_row(uint32_t r)
+{
+    uint32_t x;
+    asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_mov_b32 %0, v128\n\ts_set_gpr_idx_off" : "=v"(x) : "s"(r & 127u) : "m0");
+    return x;
+}
+__device__ __forceinline__ void vt_set_row(uint32_t r, uint32_t v)
+{
+    asm volatile("s_set_gpr_idx_on %1, gpr_idx(DST)\n\tv_mov_b32 v128, %0\n\ts_set_gpr_idx_off" : : "v"(v), "s"(r & 127u) : "m0");
+}
+
+// entry h (< 16384) -> row h>>7, lane (h>>1)&63, half h&1
+struct VTab {
+    uint32_t lane;
+    __device__ __forceinline__ void clear() const
+    {
+        asm volatile("; k_snappy_v: v128..v255 hold the hash table" ::: VT_CLOBBERS);
+        for (uint32_t r = 0; r < 128; r++) vt_set_row(r, 0);
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t h) const
+    {
+        const uint32_t x = __builtin_amdgcn_readlane(vt_row(h >> 7), (h >> 1) & 63);
+        return (h & 1) ? (x >> 16) : (x & 0xffffu);
+    }
+    __device__ __forceinline__ void put(uint32_t h, uint32_t v) const
+    {
+        const uint32_t r = h >> 7;
+        const uint32_t old = vt_row(r);
+        const uint32_t sh = (h & 1) * 16;
+        const uint32_t nv = (old & ~(0xffffu << sh)) | ((v & 0xffffu) << sh);
+        vt_set_row(r, lane == ((h >> 1) & 63) ? nv : old);
+    }
+    // candidate = table[h]; table[h] = v  (one row read)
+    __device__ __forceinline__ uint32_t swap(uint32_t h, uint32_t v) const
+    {
+        const uint32_t r = h >> 7, L = (h >> 1) & 63, sh = (h & 1) * 16;
+        const uint32_t old = vt_row(r);
+        const uint32_t x = __builtin_amdgcn_readlane(old, L);
+        const uint32_t nv = (old & ~(0xffffu << sh)) | ((v & 0xffffu) << sh);
+        vt_set_row(r, lane == L ? nv : old);
+        return (x >> sh) & 0xffffu;
+    }
+};
+
+// 256-byte input window in one VGPR (lane i = dword i), all bookkeeping in 32-bit scalars
+// relative to abs0 = (fragment start & ~3); a refill waits for its load right away so no
+// later read of the window waits on vmcnt (which the output byte stores share).
+struct VWin {
+    const uint8_t *abs0;
+    uint32_t off0;    // fragment byte 0 = abs0 + off0
+    uint32_t A;       // window start (multiple of 4, relative to abs0)
+    uint32_t w;
+    int lane;
+    __device__ __forceinline__ void refill(uint32_t q)
+    {
+        A = q >= 64 ? ((q - 64) & ~3u) : 0u;
+        w = ((const __attribute__((address_space(1))) uint32_t *)(abs0 + A))[lane];
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    }
+    // 4 / 8 bytes at fragment position p; `advance` may move the window forward, reads behind
+    // it (old candidates) take one scalar load
+    __device__ __forceinline__ uint32_t ld32(uint32_t p, const SIn &si, bool advance)
+    {
+        const uint32_t q = p + off0;
+        uint32_t d = q - A;
+        if (d > 248) {
+            if (!advance || q < A) return si.ld32(p);
+            refill(q);
+            d = q - A;
+        }
+        const uint32_t l0 = d >> 2, sh = (d & 3) * 8;
+        const uint32_t x = __builtin_amdgcn_readlane(w, l0);
+        const uint32_t y = __builtin_amdgcn_readlane(w, l0 + 1);
+        return sh ? (x >> sh) | (y << (32 - sh)) : x;
+    }
+    __device__ __forceinline__ uint64_t ld64(uint32_t p, const SIn &si, bool advance)
+    {
+        const uint32_t q = p + off0;
+        uint32_t d = q - A;
+        if (d > 244) {
+            if (!advance || q < A) return si.ld64(p);
+            refill(q);
+            d = q - A;
+        }
+        const uint32_t l0 = d >> 2, sh = (d & 3) * 8;
+        const uint32_t x = __builtin_amdgcn_readlane(w, l0);
+        const uint32_t y = __builtin_amdgcn_readlane(w, l0 + 1);
+        const uint32_t z = __builtin_amdgcn_readlane(w, l0 + 2);
+        const uint64_t lo = ((uint64_t)y << 32) | x;
+        return sh ? (lo >> sh) | ((uint64_t)z << (64 - sh)) : lo;
+    }
+};
+
+__device__ __forceinline__ uint32_t find_match_length_v(VWin &in, const SIn &si, const Src &g, uint32_t s1, uint32_t s2,
+                                                        uint32_t s2_limit, int lane)
+{
+    uint32_t m = 0;
+    while (m < 64 && s2 + m + 8 <= s2_limit) {
+        const uint64_t b = in.ld64(s2 + m, si, true);
+        const uint64_t a = in.ld64(s1 + m, si, false);
+        const uint64_t x = a ^ b;
+        if (x) return m + ((uint32_t)__builtin_ctzll(x) >> 3);
+        m += 8;
+    }
+    for (;;) {
+        const uint32_t p2 = s2 + m + lane;
+        const bool ok = p2 < s2_limit && g.ld8(s1 + m + lane) == g.ld8(p2);
+        const uint64_t bad = __ballot(!ok);
+        if (bad) return m + (uint32_t)(__ffsll((long long)bad) - 1);
+        m += 64;
+    }
+}
+
+__global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k_snappy_v(SnappyArgs a)
+{
+    const int lane = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    const uint32_t pg = a.frag_page[f];
+    const uint32_t fi = a.frag_idx[f];
+    const uint64_t plen = a.page_len[pg];
+    const uint64_t fstart = (uint64_t)fi * SNAPPY_FRAG;
+    const uint32_t n = (uint32_t)((plen - fstart) < SNAPPY_FRAG ? (plen - fstart) : SNAPPY_FRAG);
+    const uint8_t *fbase = a.in + a.page_off[pg] + fstart;
+    const Src g{(g_u8 *)fbase};
+    const SIn si{(uint64_t)(uintptr_t)fbase};
+    VWin in;
+    in.abs0 = (const uint8_t *)((uintptr_t)fbase & ~(uintptr_t)3);
+    in.off0 = (uint32_t)((uintptr_t)fbase & 3);
+    in.lane = lane;
+    in.refill(0);
+    VTab T;
+    T.lane = (uint32_t)lane;
+    T.clear();
+    uint32_t tsize = 256;
+    while (tsize < SNAPPY_MAX_TABLE && tsize < n) tsize <<= 1;
+
+    uint8_t *out = a.frag_out + (uint64_t)f * SNAPPY_FRAG_CAP;
+    uint32_t op = 0;
+    int shift = 32;
+    for (uint32_t t = tsize; t > 1; t >>= 1) shift--;
+    const uint32_t ip_end = n;
+    uint32_t next_emit = 0;
+    uint32_t ip = 0;
+    if (n >= 15) {
+        const uint32_t ip_limit = n - 15;
+        ip = 1;
+        for (;;) {
+            uint32_t skip = 32;
+            uint32_t candidate;
+            for (;;) {
+                const uint32_t next_ip = ip + (skip++ >> 5);
+                if (next_ip > ip_limit) goto emit_remainder;
+                if (skip > 32 + VT_ABORT) {
+                    if (lane == 0) a.frag_len[f] = VT_ABORTED;
+                    return;
+                }
+                const uint32_t cur_s = in.ld32(ip, si, true);
+                candidate = T.swap(sn_hash(cur_s, shift), ip);
+                if (cur_s == in.ld32(candidate, si, false)) break;
+                ip = next_ip;
+            }
+            {
+                const uint32_t len = ip - next_emit;
+                if (len <= 7) {
+                    const uint64_t b = in.ld64(next_emit, si, false) & ((1ull << (8 * len)) - 1);
+                    st_word(out, op, ((uint64_t)((len - 1) << 2)) | (b << 8), 1 + len, lane);
+                    op += 1 + len;
+                } else {
+                    op = emit_literal(out, op, g, next_emit, len, lane);
+                }
+            }
+            for (;;) {
+                const uint32_t base = ip;
+                const uint32_t matched = 4 + find_match_length_v(in, si, g, candidate + 4, ip + 4, ip_end, lane);
+                ip += matched;
+                op = emit_copy_s(out, op, base - candidate, matched, lane);
+                next_emit = ip;
+                if (ip >= ip_limit) goto emit_remainder;
+                const uint64_t in8 = in.ld64(ip - 1, si, true);   // bytes [ip-1, ip+7)
+                const uint32_t input_lo = (uint32_t)in8;
+                const uint32_t b1 = (uint32_t)(in8 >> 8);
+                T.put(sn_hash(input_lo, shift), ip - 1);
+                candidate = T.swap(sn_hash(b1, shift), ip);
+                if (b1 != in.ld32(candidate, si, false)) break;
+            }
+            ++ip;
+        }
+    }
+emit_remainder:
+    if (next_emit < ip_end) op = emit_literal(out, op, g, next_emit, ip_end - next_emit, lane);
+    if (lane == 0) a.frag_len[f] = op;
+}
+
+// k_snappy_s restricted to the fragments k_snappy_v gave up on
+__global__ void __launch_bounds__(64) k_snappy_s_rest(SnappyArgs a)
+{
+    if (a.frag_len[blockIdx.x] != VT_ABORTED) return;
+    k_snappy_s_body<SNAPPY_SEQ_PROBES>(a);
+}
+
 // per page: compressed size = varint(len) + sum of its fragments
 __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_page_sizes(SnappyArgs a, const uint32_t *page_frag0)
 {
@@ -1009,10 +1250,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_copy(SnappyArgs a)
     for (uint32_t i = threadIdx.x; i < n; i += KPW_BLOCK) d[i] = s[i];
 }
 
+// K7: the register-table kernel on every fragment (8 waves/CU, no LDS), then the batched
+// LDS kernel on the fragments it gave up on (incompressible data: long literal searches)
 void launch_snappy(const SnappyArgs &a, hipStream_t s)
 {
     if (!a.nfrags) return;
-    hipLaunchKernelGGL(k_snappy_s<SNAPPY_SEQ_PROBES>, dim3(a.nfrags), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, s, a);
 }
 
 void launch_snappy_finish(const SnappyArgs &a, const uint32_t *page_frag0, hipStream_t s)

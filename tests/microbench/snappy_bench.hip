@@ -61,6 +61,10 @@ static float run(const SnappyArgs &a, int reps)
         if (KIND == 1) hipLaunchKernelGGL(k_snappy_win<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
         else if (KIND == 2) hipLaunchKernelGGL(k_snappy_s<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
         else if (KIND == 3) hipLaunchKernelGGL(k_snappy_w<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
+        else if (KIND == 4) {   // register-table kernel, batched LDS kernel for the fragments it gives up on
+            hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, 0, a);
+            hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, 0, a);
+        } else if (KIND == 5) hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, 0, a);
         else hipLaunchKernelGGL(k_snappy_frag<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
     };
     launch();
@@ -133,8 +137,15 @@ int main(int argc, char **argv)
         };
         const double gb = (double)(npages * psz) / 1e9;
         struct V { const char *name; float (*fn)(const SnappyArgs &, int); };
-        V vs[] = {{"seq", run<1 << 30, 0>}, {"s2", run<2, 2>}, {"s4", run<4, 2>},
-                  {"w1", run<1, 3>}, {"w2", run<2, 3>}, {"w4", run<4, 3>}, {"w8", run<8, 3>}};
+        V vs[] = {{"s2", run<2, 2>}, {"v+s2", run<2, 4>}};
+        {   // how many fragments the register-table kernel gives up on
+            (void)run<2, 5>(a, 1);
+            std::vector<uint32_t> fl(nf);
+            CK(hipMemcpy(fl.data(), d_flen, nf * 4, hipMemcpyDeviceToHost));
+            uint32_t ab = 0;
+            for (uint32_t f = 0; f < nf; f++) ab += fl[f] == VT_ABORTED;
+            printf("kind=%-8s v-kernel aborted %u of %u fragments\n", kind, ab, nf);
+        }
         for (auto &v : vs) {
             CK(hipMemset(d_fout, 0, (size_t)nf * SNAPPY_FRAG_CAP));
             float ms = v.fn(a, 3);
