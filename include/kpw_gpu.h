@@ -74,19 +74,22 @@ const char *kpw_encoder_last_error(const kpw_encoder *e);
 
 /* Per-page metadata of one encoded page (data or dictionary). */
 typedef struct kpw_page_info {
-    int32_t page_type;          /* KPW_DATA_PAGE / KPW_DICTIONARY_PAGE */
+    int32_t page_type;          /* KPW_DATA_PAGE / KPW_DATA_PAGE_V2 (writer_version 2) / KPW_DICTIONARY_PAGE */
     int32_t num_values;         /* data: values incl. nulls; dictionary: entries */
     int32_t encoding;           /* values encoding (data) or dictionary encoding */
-    int32_t dl_encoding;        /* KPW_ENC_RLE (optional) / KPW_ENC_BIT_PACKED (required) */
-    int32_t rl_encoding;        /* KPW_ENC_BIT_PACKED (DevNull, no repeated fields) */
+    int32_t dl_encoding;        /* v1: KPW_ENC_RLE (optional) / KPW_ENC_BIT_PACKED (required) */
+    int32_t rl_encoding;        /* v1: KPW_ENC_BIT_PACKED (DevNull, no repeated fields) */
     int32_t has_stats;          /* 0 for dictionary pages */
-    int64_t uncompressed_size;
-    int64_t compressed_size;
+    int64_t uncompressed_size;  /* v2: level bytes + uncompressed values */
+    int64_t compressed_size;    /* v2: level bytes + compressed values */
     uint64_t offset;            /* byte offset of the (compressed) body in the batch output */
     int64_t null_count;
     int32_t has_min_max;
     int32_t min_len, max_len;   /* stats bytes (Statistics.getMinBytes/getMaxBytes) */
+    int32_t dl_byte_length;     /* v2: definition-level bytes at the start of the body (never compressed) */
     uint64_t min_off, max_off;  /* offsets into kpw_batch_info.stats_bytes */
+    int32_t num_rows;           /* v2 DataPageHeaderV2.num_rows (= num_values: no repeated fields) */
+    int32_t reserved;
 } kpw_page_info;
 
 typedef struct kpw_chunk_info {

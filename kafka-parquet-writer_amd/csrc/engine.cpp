@@ -76,11 +76,17 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     if (!schema || !pr || !schema->columns || schema->num_columns <= 0 || !schema->message_name)
         return fail(KPW_ERR_INVALID_ARG, "null schema/props");
     if (schema->num_columns > MAX_COLS) return fail(KPW_ERR_UNSUPPORTED, "more than 256 columns");
-    if (pr->writer_version != 1) return fail(KPW_ERR_UNSUPPORTED, "only PARQUET_1_0 is reachable from the reference");
+    if (pr->writer_version != 1 && pr->writer_version != 2) return fail(KPW_ERR_UNSUPPORTED, "writer_version must be 1 or 2");
+    // PARQUET_2_0 without a dictionary writes DELTA streams directly, and their page-size
+    // accounting (DeltaBinaryPacking getBufferedSize = flushed blocks) is not planned here.
+    // The reference can never turn the dictionary off (ParquetFile.java:48-50).
+    if (pr->writer_version == 2 && !pr->enable_dictionary)
+        return fail(KPW_ERR_UNSUPPORTED, "PARQUET_2_0 requires the dictionary on (the only setting the reference produces)");
     if (pr->codec != KPW_UNCOMPRESSED && pr->codec != KPW_SNAPPY) return fail(KPW_ERR_UNSUPPORTED, "codec");
     if (pr->block_size <= 0 || pr->page_size <= 0 || pr->dictionary_page_size <= 0) return fail(KPW_ERR_INVALID_ARG, "sizes");
     if (pr->dfs_block_size > 0) return fail(KPW_ERR_UNSUPPORTED, "HDFS padding alignment (next round)");
     props = *pr;
+    v2_ = pr->writer_version == 2;
     message_name = schema->message_name;
     proto_class = schema->proto_class ? schema->proto_class : schema->message_name;
     for (int c = 0; c < schema->num_columns; c++) {
@@ -111,6 +117,7 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     for (auto &e : kev_) CK(hipEventCreate(&e));
     const size_t nc = cols.size();
     col_vals.resize(nc); col_shash.resize(nc); col_spfx.resize(nc); col_soff.resize(nc); col_slen.resize(nc); col_pres.resize(nc); col_vbits.resize(nc); col_pcnt.resize(nc);
+    col_cbits.resize(bool_idx_.size());
     std::vector<int16_t> fmap(FMAP_SIZE, -1);
     for (size_t c = 0; c < nc; c++)
         if (cols[c].field_number < FMAP_SIZE) fmap[cols[c].field_number] = (int16_t)c;
@@ -269,40 +276,78 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         CK(hipStreamSynchronize(s));
         return KPW_OK;
     }
+    // RLE streams whose emitted bytes count in checkBlockSizeReached: definition levels of
+    // optional columns; in v2 also the boolean values (RunLengthBitPackingHybridValuesWriter)
+    const uint32_t nbool = (uint32_t)bool_idx_.size();
+    const uint32_t nstreams = nopt + (v2_ ? nbool : 0);
     RleScratch sc{};
     uint32_t npt = 0, net = 0;
     std::vector<RleJob> pj;
-    if (nopt) {
-        pj.resize(nopt);
-        for (uint32_t k = 0; k < nopt; k++) {
+    std::vector<PlanStream> hs(nstreams);
+    std::vector<uint64_t *> cbits(nbool, nullptr);
+    if (v2_) {
+        for (uint32_t i = 0; i < nbool; i++) {
+            const uint32_t c = bool_idx_[i];
+            if (cols[c].optional) {
+                ENS(col_cbits[i], nwords * 8);
+                CK(hipMemsetAsync(col_cbits[i].p, 0, nwords * 8, s));
+                cbits[i] = col_cbits[i].as<uint64_t>();
+            } else {
+                cbits[i] = hc[c].vbits;   // required: the record-indexed value bits are the stream
+            }
+        }
+    }
+    for (uint32_t k = 0; k < nstreams; k++) {
+        PlanStream &S = hs[k];
+        S.pad = 0;
+        S.len = ne;
+        if (k < nopt) { S.bits = hc[opt_idx_[k]].pres; S.rank_col = -1; }
+        else {
+            const uint32_t c = bool_idx_[k - nopt];
+            S.bits = cbits[k - nopt];
+            S.rank_col = cols[c].optional ? (int32_t)c : -1;   // optional: length set on the device
+        }
+    }
+    ENS(d_streams, std::max<size_t>(1, nstreams) * sizeof(PlanStream));
+    if (nstreams) CK(hipMemcpyAsync(d_streams.p, hs.data(), nstreams * sizeof(PlanStream), hipMemcpyHostToDevice, s));
+    if (nstreams) {
+        pj.resize(nstreams);
+        for (uint32_t k = 0; k < nstreams; k++) {
             RleJob &J = pj[k];
             memset(&J, 0, sizeof(J));
             J.src.kind = 0;
-            J.src.ptr = hc[opt_idx_[k]].pres;
+            J.src.ptr = hs[k].bits;
             J.src.base = 0;
-            J.len = (uint32_t)ne;
+            J.len = (uint32_t)ne;    // upper bound; optional boolean streams are shortened on the device
             J.bw = 1;
             J.out_off = (uint64_t)k * (ne + 1);
         }
         int st = run_rle(pj, npt, net, sc);
         if (st) return st;
-        ENS(d_ev, (uint64_t)nopt * (ne + 1));
-        ENS(d_E, (uint64_t)nopt * (ne + 1) * 4);
-        ENS(d_gend, (uint64_t)nopt * nwords * 8);
-        CK(hipMemsetAsync(d_ev.p, 0, (uint64_t)nopt * (ne + 1), s));
-        CK(hipMemsetAsync(d_gend.p, 0, (uint64_t)nopt * nwords * 8, s));
-        launch_rle_structure(d_jobs.as<RleJob>(), (int)nopt, npt, net, sc, s);
+        if (v2_ && nbool) {
+            ENS(d_cbits_ptr, nbool * sizeof(uint64_t *));
+            CK(hipMemcpyAsync(d_cbits_ptr.p, cbits.data(), nbool * sizeof(uint64_t *), hipMemcpyHostToDevice, s));
+            launch_bool_streams(d_cols.as<DevCol>(), d_bool.as<uint32_t>(), nbool, ne, d_cbits_ptr.as<uint64_t *>(),
+                                d_jobs.as<RleJob>(), nopt, d_streams.as<PlanStream>(), nopt, s);
+        }
+        ENS(d_ev, (uint64_t)nstreams * (ne + 1));
+        ENS(d_E, (uint64_t)nstreams * (ne + 1) * 4);
+        ENS(d_gend, (uint64_t)nstreams * nwords * 8);
+        CK(hipMemsetAsync(d_ev.p, 0, (uint64_t)nstreams * (ne + 1), s));
+        CK(hipMemsetAsync(d_gend.p, 0, (uint64_t)nstreams * nwords * 8, s));
+        launch_rle_structure(d_jobs.as<RleJob>(), (int)nstreams, npt, net, sc, s);
         launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), d_gend.as<uint64_t>(), nwords, s);
-        launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ne, nopt, d_scan_tmp.as<uint64_t>(), s);
+        launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ne, nstreams, d_scan_tmp.as<uint64_t>(), s);
     }
     // ---------------------------------------------------------------- A9 plan
     const int32_t max_rgs = (int32_t)(ne / 100 + 4);
     ENS(d_rg_start, max_rgs * 8); ENS(d_rg_end, max_rgs * 8); ENS(d_plan_out, 64);
     PlanArgs pa{};
     pa.n = ne; pa.final_flush = final_flush ? 1 : 0; pa.ncols = nc; pa.next_rg_size = next_rg_size;
-    pa.P = d_P.as<uint64_t>(); pa.cols = d_cols.as<DevCol>(); pa.opt_cols = d_opt.as<uint32_t>(); pa.nopt = (int32_t)nopt;
-    pa.nbool = (int32_t)bool_idx_.size(); pa.bool_cols = d_bool.as<uint32_t>();
-    pa.E = nopt ? d_E.as<uint32_t>() : nullptr; pa.gend = nopt ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
+    pa.P = d_P.as<uint64_t>(); pa.cols = d_cols.as<DevCol>();
+    pa.streams = d_streams.as<PlanStream>(); pa.nstreams = (int32_t)nstreams;
+    pa.nbool = v2_ ? 0 : (int32_t)nbool; pa.bool_cols = d_bool.as<uint32_t>();
+    pa.E = nstreams ? d_E.as<uint32_t>() : nullptr; pa.gend = nstreams ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
     pa.rg_start = d_rg_start.as<int64_t>(); pa.rg_end = d_rg_end.as<int64_t>(); pa.max_rgs = max_rgs;
     pa.out = d_plan_out.as<int64_t>();
     launch_plan(pa, s);
@@ -334,6 +379,10 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     std::vector<ChunkDesc> ch(nch);
     std::vector<uint32_t> ctj, cfirst(nch), ccount(nch);
     std::vector<RleJob> ej;
+    std::vector<DeltaJob> dj;          // v2 DELTA streams (INT32/INT64: 1, BYTE_ARRAY: prefix + suffix lengths)
+    std::vector<uint32_t> dblk_job;    // job of each DELTA block tile
+    std::vector<int> bool_pos(nc, -1);
+    for (uint32_t i = 0; i < nbool; i++) bool_pos[bool_idx_[i]] = (int)i;
     uint64_t ht_off = 0, ids_off = 0;
     for (int r = 0; r < nrg; r++) {
         for (int c = 0; c < nc; c++) {
@@ -370,6 +419,33 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
                 J.len = (uint32_t)len; J.bw = 0;
                 C.id_job = (int32_t)ej.size();
                 ej.push_back(J);
+            }
+            C.bool_job = -1;
+            C.dj0 = -1;
+            if (v2_ && cols[c].phys == KPW_BOOLEAN) {   // RunLengthBitPackingHybridValuesWriter(1)
+                RleJob J;
+                memset(&J, 0, sizeof(J));
+                J.src.kind = 0; J.src.ptr = cbits[bool_pos[c]];
+                J.src.base = cols[c].optional ? 0 : (uint64_t)C.s;   // optional: rank of C.s, set on the device
+                J.len = (uint32_t)len; J.bw = 1;
+                C.bool_job = (int32_t)ej.size();
+                ej.push_back(J);
+            }
+            if (v2_ && C.is_dict && (cols[c].phys == KPW_INT32 || cols[c].phys == KPW_INT64 || cols[c].phys == KPW_BYTE_ARRAY)) {
+                C.dj0 = (int32_t)dj.size();
+                const bool ba = cols[c].phys == KPW_BYTE_ARRAY;
+                const uint32_t nblk = (uint32_t)std::max<uint64_t>(1, len > 1 ? (len - 1 + 127) / 128 : 1);
+                for (int k = 0; k < (ba ? 2 : 1); k++) {
+                    DeltaJob D;
+                    memset(&D, 0, sizeof(D));
+                    D.vals = nullptr;   // patched below: dense values (u64) or prefix/suffix lengths (u32)
+                    D.base = C.ids_off;
+                    D.flags = DJ_INACTIVE | (cols[c].phys == KPW_INT64 ? DJ_LONG : 0u) | (ba ? DJ_U32_SRC : 0u);
+                    D.blk0 = (uint32_t)dblk_job.size();
+                    D.nblk = nblk;
+                    dblk_job.insert(dblk_job.end(), nblk, (uint32_t)dj.size());
+                    dj.push_back(D);
+                }
             }
             const uint32_t nt = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
             cfirst[ci] = (uint32_t)ctj.size();
@@ -416,6 +492,31 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     a.data_end = d_off + n;
     a.collision = d_collision.as<uint32_t>();
     a.dict_order = d_dict_order.as<uint32_t>(); a.ndict_tiles = (uint32_t)dorder.size();
+    a.v2 = v2_ ? 1 : 0;
+    // v2 DELTA streams: dense inputs share the chunks' rank-indexed id space (ids_off)
+    DeltaArgs dla{};
+    ENS(d_page_pre, 2 * nch * 8);
+    a.page_pre = d_page_pre.as<uint64_t>();
+    if (v2_) {
+        ENS(d_dense, std::max<uint64_t>(1, ids_off) * 8); ENS(d_pre, std::max<uint64_t>(1, ids_off) * 4);
+        ENS(d_sfx, std::max<uint64_t>(1, ids_off) * 4);
+        ENS(d_tile_sfx, nct * 8); ENS(d_tile_sfx_off, nct * 8); ENS(d_chunk_sfx, nch * 8);
+        CK(hipMemsetAsync(d_chunk_sfx.p, 0, nch * 8, s));
+        for (int ci = 0; ci < nch; ci++) {
+            const ChunkDesc &C = ch[ci];
+            if (C.dj0 < 0) continue;
+            if (cols[C.col].phys == KPW_BYTE_ARRAY) { dj[C.dj0].vals = d_pre.p; dj[C.dj0 + 1].vals = d_sfx.p; }
+            else dj[C.dj0].vals = d_dense.p;
+        }
+        const size_t nb = std::max<size_t>(1, dblk_job.size());
+        ENS(d_djobs, std::max<size_t>(1, dj.size()) * sizeof(DeltaJob)); ENS(d_blk_job, nb * 4); ENS(d_blk_min, nb * 8);
+        ENS(d_blk_w, nb * 4); ENS(d_blk_sz, nb * 8); ENS(d_blk_off, nb * 8); ENS(d_btot, std::max<size_t>(1, dj.size()) * 8);
+        if (!dblk_job.empty()) CK(hipMemcpyAsync(d_blk_job.p, dblk_job.data(), dblk_job.size() * 4, hipMemcpyHostToDevice, s));
+        dla.jobs = d_djobs.as<DeltaJob>(); dla.njobs = (uint32_t)dj.size(); dla.nblk = (uint32_t)dblk_job.size();
+        dla.blk_job = d_blk_job.as<uint32_t>(); dla.blk_min = d_blk_min.as<uint64_t>(); dla.blk_w = d_blk_w.as<uint32_t>();
+        dla.blk_sz = d_blk_sz.as<uint64_t>(); dla.blk_off = d_blk_off.as<uint64_t>(); dla.btot = d_btot.as<uint64_t>();
+        a.djobs = dla.jobs; a.djobs_w = dla.jobs; a.chunk_sfx = d_chunk_sfx.as<uint64_t>();
+    }
     uint32_t enpt = 0, enet = 0;
     RleScratch esc{};
     uint64_t body_tot = 0;
@@ -429,19 +530,29 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             CK(hipMemsetAsync(d_ht_key.p, 0xFF, ht_off * 8, s));
             CK(hipMemsetAsync(d_ht_min.p, 0xFF, ht_off * 4, s));
         }
+        if (v2_ && !dj.empty()) CK(hipMemcpyAsync(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), hipMemcpyHostToDevice, s));
         // ------------------------------------------------------------ K6 + K2
         launch_chunk_stats(a, s);
         CK(hipGetLastError());
         if (!ej.empty()) {
             int st = run_rle(ej, enpt, enet, esc);
             if (st) return st;
+            if (v2_) launch_v2_bool_jobs(a, d_jobs.as<RleJob>(), s);
         }
         launch_dict(a, d_jobs.as<RleJob>(), s);
         CK(hipGetLastError());
         CK(hipEventRecord(ev_[3], s));
-        // ------------------------------------------------------------ K3 (dl + ids)
+        // ------------------------------------------------------------ K3 (dl + ids + v2 booleans)
         if (!ej.empty()) launch_rle_structure(d_jobs.as<RleJob>(), (int)ej.size(), enpt, enet, esc, s);
         CK(hipGetLastError());
+        // ------------------------------------------------------------ A10 (v2 fallback: DELTA streams)
+        if (v2_) {
+            launch_v2_decide(a, d_jobs.as<RleJob>(), dla.jobs, s);
+            launch_v2_dense(a, d_dense.as<uint64_t>(), d_pre.as<uint32_t>(), d_sfx.as<uint32_t>(), d_tile_sfx.as<uint64_t>(),
+                            d_tile_sfx_off.as<uint64_t>(), d_chunk_sfx.as<uint64_t>(), s);
+            launch_delta_structure(dla, s);
+            CK(hipGetLastError());
+        }
         CK(hipEventRecord(ev_[4], s));
         // ------------------------------------------------------------ layout
         launch_layout(a, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), s);
@@ -456,13 +567,18 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     // +512: K7 reads its input through 256-byte register windows that may run past the last page
     ENS(d_body, body_tot + 512);
     CK(hipMemsetAsync(d_body.p, 0, body_tot + 512, s));
-    launch_chunk_write(a, d_body.as<uint8_t>(), s);
+    launch_chunk_write(a, d_jobs.as<RleJob>(), d_body.as<uint8_t>(), s);
     if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), s);
+    if (v2_) {
+        launch_delta_write(dla, d_body.as<uint8_t>(), s);
+        launch_dba_suffixes(a, d_pre.as<uint32_t>(), dla.jobs, d_tile_sfx_off.as<uint64_t>(), d_body.as<uint8_t>(), s);
+    }
     CK(hipGetLastError());
     CK(hipEventRecord(ev_[5], s));
-    std::vector<uint64_t> poff(2 * nch), plen(2 * nch), pcoff, pclen;
+    std::vector<uint64_t> poff(2 * nch), plen(2 * nch), ppre(2 * nch, 0), pcoff, pclen;
     CK(hipMemcpyAsync(poff.data(), d_page_off.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
     CK(hipMemcpyAsync(plen.data(), d_page_len.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
+    if (v2_) CK(hipMemcpyAsync(ppre.data(), d_page_pre.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
     // ---------------------------------------------------------------- K7
     if (props.codec == KPW_SNAPPY) {
@@ -489,6 +605,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         sa.frag_out = d_frag_out.as<uint8_t>(); sa.frag_len = d_frag_len.as<uint32_t>();
         sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
         sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
+        sa.page_pre = v2_ ? d_page_pre.as<uint64_t>() : nullptr;
         CK(hipEventRecord(kev_[2], s));
         launch_snappy(sa, s);
         CK(hipEventRecord(kev_[3], s));
@@ -503,9 +620,10 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         CK(hipStreamSynchronize(s));
         pages_dev_ = d_comp.as<uint8_t>();
         pages_len_ = ctot;
-    } else {
-        pcoff = poff;
-        pclen = plen;
+    } else {   // uncompressed: a (v2) page body starts at its level prefix
+        pcoff.resize(2 * nch);
+        pclen.resize(2 * nch);
+        for (int p = 0; p < 2 * nch; p++) { pcoff[p] = poff[p] - ppre[p]; pclen[p] = plen[p] + ppre[p]; }
         pages_dev_ = d_body.as<uint8_t>();
         pages_len_ = body_tot;
     }
@@ -563,7 +681,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             PageOut p;
             p.page_type = KPW_DICTIONARY_PAGE;
             p.num_values = (int32_t)C.dict_n;
-            p.encoding = KPW_ENC_PLAIN_DICTIONARY;
+            p.encoding = v2_ ? KPW_ENC_PLAIN : KPW_ENC_PLAIN_DICTIONARY;   // DictionaryValuesWriter v1 / v2 page encoding
             p.dl_encoding = p.rl_encoding = 0;
             p.has_stats = 0;
             p.uncompressed_size = (int64_t)plen[2 * ci];
@@ -574,15 +692,26 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             out.pages.push_back(p);
         }
         PageOut p;
-        p.page_type = KPW_DATA_PAGE;
+        p.page_type = v2_ ? KPW_DATA_PAGE_V2 : KPW_DATA_PAGE;
         p.num_values = (int32_t)(C.e - C.s);
-        p.encoding = (C.is_dict && !C.fallback) ? KPW_ENC_PLAIN_DICTIONARY : KPW_ENC_PLAIN;
+        if (!v2_) {
+            p.encoding = (C.is_dict && !C.fallback) ? KPW_ENC_PLAIN_DICTIONARY : KPW_ENC_PLAIN;
+        } else if (col.phys == KPW_BOOLEAN) {
+            p.encoding = KPW_ENC_RLE;
+        } else if (C.is_dict && !C.fallback) {
+            p.encoding = KPW_ENC_RLE_DICTIONARY;
+        } else {   // DefaultV2ValuesWriterFactory fallback writers
+            p.encoding = col.phys == KPW_BYTE_ARRAY ? KPW_ENC_DELTA_BYTE_ARRAY
+                       : (col.phys == KPW_INT32 || col.phys == KPW_INT64) ? KPW_ENC_DELTA_BINARY_PACKED : KPW_ENC_PLAIN;
+        }
         p.dl_encoding = col.optional ? KPW_ENC_RLE : KPW_ENC_BIT_PACKED;
         p.rl_encoding = KPW_ENC_BIT_PACKED;
         p.has_stats = 1;
-        p.uncompressed_size = (int64_t)plen[2 * ci + 1];
+        p.uncompressed_size = (int64_t)(plen[2 * ci + 1] + ppre[2 * ci + 1]);
         p.compressed_size = (int64_t)pclen[2 * ci + 1];
         p.offset = pcoff[2 * ci + 1];
+        p.dl_byte_length = v2_ ? (int32_t)C.dl_len : 0;
+        p.num_rows = (int32_t)(C.e - C.s);
         p.null_count = (int64_t)C.null_count;
         p.has_min_max = C.has_minmax ? 1 : 0;
         if (C.has_minmax) {
@@ -613,11 +742,21 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         co.num_pages = (int32_t)out.pages.size() - co.first_page;
         out.chunks.push_back(co);
         // single-page regime guard: ColumnWriterV1.accountForValueWritten never cut a page iff
-        // the column's buffered size stayed <= pageSize up to the row-group flush.
-        const uint64_t colmem = (col.phys == KPW_BOOLEAN ? (C.nn + 7) / 8 : C.raw_bytes) + C.dl_len;
-        if (colmem > (uint64_t)props.page_size)
-            return fail(KPW_ERR_UNSUPPORTED, "column '" + col.name + "' would be split into several pages "
-                                             "(pageSize smaller than a column chunk): multi-page chunks are the next round");
+        // the column's buffered size stayed <= pageSize up to the row-group flush;
+        // ColumnWriteStoreV2.sizeCheck cuts once pageSize - usedMem <= (long)(pageSize * 0.1f)
+        // (checked conservatively on the final sizes: no cut can have happened below them).
+        if (!v2_) {
+            const uint64_t colmem = (col.phys == KPW_BOOLEAN ? (C.nn + 7) / 8 : C.raw_bytes) + C.dl_len;
+            if (colmem > (uint64_t)props.page_size)
+                return fail(KPW_ERR_UNSUPPORTED, "column '" + col.name + "' would be split into several pages "
+                                                 "(pageSize smaller than a column chunk): multi-page chunks are the next round");
+        } else {
+            const int64_t tol = (int64_t)((float)props.page_size * 0.1f);
+            const int64_t colmem = (int64_t)C.dl_len + (int64_t)(col.phys == KPW_BOOLEAN ? C.val_len - 4 : C.raw_bytes);
+            if ((int64_t)props.page_size - colmem <= tol)
+                return fail(KPW_ERR_UNSUPPORTED, "column '" + col.name + "' could be split into several v2 pages "
+                                                 "(within 10% of pageSize): multi-page chunks are the next round");
+        }
     }
     out.d_pages = pages_dev_;
     out.pages_len = pages_len_;

@@ -22,6 +22,8 @@ struct PageOut {
     uint64_t offset;            // into the device page buffer
     int64_t null_count;
     int32_t has_min_max;
+    int32_t dl_byte_length = 0; // DataPageV2: uncompressed definition-level bytes at the body start
+    int32_t num_rows = 0;       // DataPageV2
     std::string min, max;       // Statistics.getMinBytes / getMaxBytes
 };
 
@@ -89,6 +91,11 @@ private:
     // snappy
     DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
     DevBuf d_smeta, d_sblob, d_collision, d_dict_order;
+    // v2 (PARQUET_2_0): boolean value streams, planner streams, DELTA streams
+    bool v2_ = false;
+    std::vector<DevBuf> col_cbits;
+    DevBuf d_cbits_ptr, d_streams, d_djobs, d_blk_job, d_blk_min, d_blk_w, d_blk_sz, d_blk_off, d_btot, d_dense, d_pre, d_sfx,
+        d_tile_sfx, d_tile_sfx_off, d_chunk_sfx, d_page_pre;
     hipEvent_t ev_[9] = {};
     hipEvent_t kev_[4] = {};
     std::vector<uint32_t> opt_idx_, bool_idx_;

@@ -203,13 +203,27 @@ int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages,
                 st.nulls = pg.null_count;
                 st.min = pg.min;
                 st.max = pg.max;
-                t.begin(5);
-                t.i32(1, pg.num_values);
-                t.i32(2, pg.encoding);
-                t.i32(3, pg.dl_encoding);
-                t.i32(4, pg.rl_encoding);
-                if (!stats_empty(st)) write_stats(t, 5, st);
-                t.end();
+                if (pg.page_type == KPW_DATA_PAGE_V2) {
+                    // ParquetMetadataConverter.writeDataPageV2Header (is_compressed never set)
+                    t.begin(8);
+                    t.i32(1, pg.num_values);
+                    t.i32(2, (int32_t)pg.null_count);
+                    t.i32(3, pg.num_rows);
+                    t.i32(4, pg.encoding);
+                    t.i32(5, pg.dl_byte_length);
+                    t.i32(6, 0);
+                    if (!stats_empty(st)) write_stats(t, 8, st);
+                    t.end();
+                    m.v2 = true;
+                } else {
+                    t.begin(5);
+                    t.i32(1, pg.num_values);
+                    t.i32(2, pg.encoding);
+                    t.i32(3, pg.dl_encoding);
+                    t.i32(4, pg.rl_encoding);
+                    if (!stats_empty(st)) write_stats(t, 5, st);
+                    t.end();
+                }
                 if (first_data) { m.stats = st; first_data = false; } else merge_stats(m.stats, st);
                 add_count(m.data_stats, pg.encoding);
             }
@@ -221,13 +235,14 @@ int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages,
             st2 = put(pages + (pg.offset - pages_base), (size_t)pg.compressed_size);
             if (st2) return st2;
         }
-        // ColumnChunkPageWriter: rl encodings, dl encodings, data encodings (per page)
+        // ColumnChunkPageWriter: rl encodings, dl encodings, data encodings (per page); v2
+        // pages (writePageV2) record only their data encoding
         for (int p = co.first_page; p < co.first_page + co.num_pages; p++)
             if (b.pages[p].page_type == KPW_DATA_PAGE) add_unique(m.encodings, b.pages[p].rl_encoding);
         for (int p = co.first_page; p < co.first_page + co.num_pages; p++)
             if (b.pages[p].page_type == KPW_DATA_PAGE) add_unique(m.encodings, b.pages[p].dl_encoding);
         for (int p = co.first_page; p < co.first_page + co.num_pages; p++)
-            if (b.pages[p].page_type == KPW_DATA_PAGE) add_unique(m.encodings, b.pages[p].encoding);
+            if (b.pages[p].page_type != KPW_DICTIONARY_PAGE) add_unique(m.encodings, b.pages[p].encoding);
         m.total_uncomp = uncomp;
         m.total_comp = comp;
         rm.total_bytes += uncomp;
@@ -282,7 +297,9 @@ int FileWriter::close()
             if (!stats_empty(m.stats)) write_stats(t, 12, m.stats);
             t.list(13, 12, (uint32_t)(m.dict_stats.size() + m.data_stats.size()));
             for (auto &p : m.dict_stats) { t.begin_elem(); t.i32(1, KPW_DICTIONARY_PAGE); t.i32(2, p.first); t.i32(3, p.second); t.end(); }
-            for (auto &p : m.data_stats) { t.begin_elem(); t.i32(1, KPW_DATA_PAGE); t.i32(2, p.first); t.i32(3, p.second); t.end(); }
+            for (auto &p : m.data_stats) {   // EncodingStats.usesV2Pages -> DATA_PAGE_V2
+                t.begin_elem(); t.i32(1, m.v2 ? KPW_DATA_PAGE_V2 : KPW_DATA_PAGE); t.i32(2, p.first); t.i32(3, p.second); t.end();
+            }
             t.end();
             t.end();
         }

@@ -21,6 +21,7 @@ struct StatsOut {
 
 struct ChunkMeta {
     int phys, codec;
+    bool v2 = false;                              // EncodingStats.usesV2Pages
     std::vector<int> encodings;                   // insertion order, de-duplicated
     std::vector<std::pair<int, int>> dict_stats;  // (encoding, pages)
     std::vector<std::pair<int, int>> data_stats;

@@ -491,8 +491,15 @@ __global__ void k_dict_jobs(ChunkDesc *ch, int nchunks, RleJob *jobs, uint32_t m
 
 // ------------------------------------------------------------------ layout (one block, all chunks)
 
+// Page bodies of every chunk, back to back: [dictionary page][data page].
+//   v1 data page (ColumnWriterV1.writePage): dl = 4-byte length + RLE (optional) | values
+//   v2 data page (ColumnWriterV2.writePage / writePageV2): dl = RLE without length (optional,
+//      stays uncompressed: page_pre) | values (the compressed part); values = 1-byte bit
+//      width + RLE ids (RLE_DICTIONARY), DELTA streams (INT32/INT64/BYTE_ARRAY fallback),
+//      PLAIN (FLOAT/DOUBLE fallback) or 4-byte length + RLE (BOOLEAN)
 __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks, const DevCol *cols, RleJob *jobs, uint64_t *page_off,
-                                                      uint64_t *page_len, uint64_t *tot)
+                                                      uint64_t *page_len, uint64_t *tot, int v2, DeltaJob *djobs,
+                                                      const uint64_t *chunk_sfx, uint64_t *page_pre)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
     uint64_t carry = 0;
@@ -511,7 +518,10 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
                 else dictp = C.dict_bytes;
             }
             if (!C.is_dict || C.fallback) {
-                val = col.phys == 0 ? (uint64_t)(C.nn + 7) / 8 : C.raw_bytes;
+                if (v2 && col.phys == 0) val = 4 + jobs[C.bool_job].total_bytes;
+                else if (v2 && C.dj0 >= 0 && col.phys == 6) val = djobs[C.dj0].total + djobs[C.dj0 + 1].total + chunk_sfx[ci];
+                else if (v2 && C.dj0 >= 0) val = djobs[C.dj0].total;
+                else val = col.phys == 0 ? (uint64_t)(C.nn + 7) / 8 : C.raw_bytes;
                 dictp = 0;
                 if (C.is_dict) {  // do not write ids
                     RleJob &J = jobs[C.id_job];
@@ -520,7 +530,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
             }
             C.val_len = val;
             C.dictpage_len = dictp;
-            body = dictp + (col.optional ? 4 + C.dl_len : 0) + val;
+            const uint64_t lv = col.optional ? (v2 ? 0 : 4) + C.dl_len : 0;
+            body = dictp + lv + val;
         }
         uint64_t t2;
         const uint64_t ex = block_scan_excl<uint64_t, OpSum64>(body, lds, &t2) + carry;
@@ -529,12 +540,26 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
             const DevCol &col = cols[C.col];
             C.body_off = ex;
             const uint64_t dpage = ex + C.dictpage_len;
-            if (col.optional) jobs[C.dl_job].out_off = dpage + 4;
-            if (C.is_dict) jobs[C.id_job].out_off = dpage + (col.optional ? 4 + C.dl_len : 0) + 1;
+            const uint64_t lv = col.optional ? (v2 ? 0 : 4) + C.dl_len : 0;
+            C.val_off = dpage + lv;
+            if (col.optional) jobs[C.dl_job].out_off = dpage + (v2 ? 0 : 4);
+            if (C.is_dict) jobs[C.id_job].out_off = C.val_off + 1;
+            if (v2 && C.bool_job >= 0) jobs[C.bool_job].out_off = C.val_off + 4;
+            if (v2 && C.dj0 >= 0 && C.fallback) {
+                djobs[C.dj0].out_off = C.val_off;
+                if (col.phys == 6) djobs[C.dj0 + 1].out_off = C.val_off + djobs[C.dj0].total;
+            }
             page_off[2 * ci] = ex;
             page_len[2 * ci] = C.dictpage_len;
-            page_off[2 * ci + 1] = dpage;
-            page_len[2 * ci + 1] = body - C.dictpage_len;
+            if (v2) {   // the codec sees only the values; the levels go in front uncompressed
+                page_off[2 * ci + 1] = C.val_off;
+                page_len[2 * ci + 1] = C.val_len;
+                page_pre[2 * ci] = 0;
+                page_pre[2 * ci + 1] = lv;
+            } else {
+                page_off[2 * ci + 1] = dpage;
+                page_len[2 * ci + 1] = body - C.dictpage_len;
+            }
         }
         carry += t2;
     }
@@ -543,19 +568,24 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
 
 // ------------------------------------------------------------------ writers
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_chunk_headers(const ChunkDesc *ch, int nchunks, const DevCol *cols, uint8_t *out)
+__global__ void __launch_bounds__(KPW_BLOCK) k_chunk_headers(const ChunkDesc *ch, int nchunks, const DevCol *cols, uint8_t *out, int v2,
+                                                             const RleJob *jobs)
 {
     const int ci = blockIdx.x * blockDim.x + threadIdx.x;
     if (ci >= nchunks) return;
     const ChunkDesc &C = ch[ci];
     const DevCol &col = cols[C.col];
-    uint8_t *p = out + C.body_off + C.dictpage_len;
-    if (col.optional) {
+    if (col.optional && !v2) {   // v1: 4-byte length in front of the definition levels
+        uint8_t *p = out + C.body_off + C.dictpage_len;
         const uint32_t l = (uint32_t)C.dl_len;
         p[0] = (uint8_t)l; p[1] = (uint8_t)(l >> 8); p[2] = (uint8_t)(l >> 16); p[3] = (uint8_t)(l >> 24);
-        p += 4 + C.dl_len;
     }
+    uint8_t *p = out + C.val_off;
     if (C.is_dict && !C.fallback) p[0] = (uint8_t)C.bw;
+    if (v2 && C.bool_job >= 0) {   // RunLengthBitPackingHybridValuesWriter.getBytes: 4-byte length
+        const uint32_t l = (uint32_t)jobs[C.bool_job].total_bytes;
+        p[0] = (uint8_t)l; p[1] = (uint8_t)(l >> 8); p[2] = (uint8_t)(l >> 16); p[3] = (uint8_t)(l >> 24);
+    }
 }
 
 __global__ void __launch_bounds__(KPW_BLOCK) k_dict_page(const ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
@@ -596,9 +626,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_plain(const ChunkDesc *ch, const 
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
     const DevCol &col = cols[C.col];
-    if ((C.is_dict && !C.fallback) || col.phys == 0) return;
+    if ((C.is_dict && !C.fallback) || col.phys == 0 || C.dj0 >= 0) return;   // dj0: v2 DELTA fallback instead
     const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
-    uint8_t *vout = out + C.body_off + (col.optional ? 4 + C.dl_len : 0);
+    uint8_t *vout = out + C.val_off;
     if (col.phys == 6) {
         uint64_t sz = 0;
         for (int k = 0; k < 8; k++) {
@@ -642,11 +672,11 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_plain_bool(const ChunkDesc *ch, c
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
     const DevCol &col = cols[C.col];
-    if (col.phys != 0) return;
+    if (col.phys != 0 || C.bool_job >= 0) return;   // bool_job: v2 RLE booleans instead
     const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
     if (p0 >= (uint64_t)C.e) return;
     uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
-    const uint64_t base_bit = (C.body_off + (col.optional ? 4 + C.dl_len : 0)) * 8;
+    const uint64_t base_bit = C.val_off * 8;
     for (int k = 0; k < 8; k++) {
         const uint64_t r = p0 + k;
         if (r >= (uint64_t)C.e) break;
@@ -735,12 +765,13 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
 
 void launch_layout(const ChunkArgs &a, RleJob *jobs, uint64_t *page_off, uint64_t *page_len, uint64_t *tot, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_layout, dim3(1), dim3(KPW_BLOCK), 0, s, a.ch, a.nchunks, a.cols, jobs, page_off, page_len, tot);
+    hipLaunchKernelGGL(k_layout, dim3(1), dim3(KPW_BLOCK), 0, s, a.ch, a.nchunks, a.cols, jobs, page_off, page_len, tot, a.v2,
+                       a.djobs_w, a.chunk_sfx, a.page_pre);
 }
 
-void launch_chunk_write(const ChunkArgs &a, uint8_t *out, hipStream_t s)
+void launch_chunk_write(const ChunkArgs &a, const RleJob *jobs, uint8_t *out, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_chunk_headers, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, a.cols, out);
+    hipLaunchKernelGGL(k_chunk_headers, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, a.cols, out, a.v2, jobs);
     hipLaunchKernelGGL(k_dict_page, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
                        a.ent_rec, a.ent_boff, out);
     seg_tile_scan_u64(a.tile_raw, a.tile_raw_off, a.ctile_chunk, a.nctiles, s);

@@ -12,14 +12,18 @@
 // pageSize; verified on the host from the encoded chunk sizes) is
 //   sum over columns of  rl(0) + dl.getBufferedSize() + data.getBufferedSize()
 // = [P[r]-P[s]]                         FallbackValuesWriter.rawDataByteSize / PlainValuesWriter
-// + sum_bool ceil(count/8)              BooleanPlainValuesWriter (ByteBasedBitPackingEncoder)
-// + sum_optional E_s(r)                 RunLengthBitPackingHybridEncoder baos.size() for the
-//                                       definition levels written since the row-group start s.
-// E_s(r) comes from the global RLE parse (E_g, started at record 0) once the local parse
+// + sum_bool ceil(count/8)              v1: BooleanPlainValuesWriter (ByteBasedBitPackingEncoder)
+// + sum_stream E_s(q)                   RunLengthBitPackingHybridEncoder baos.size() of each RLE
+//                                       stream written since the row-group start: the
+//                                       definition levels of optional columns (q = r) and, in
+//                                       v2, the boolean values (q = r, or the value rank r'
+//                                       for an optional column); a width-0 REQUIRED level
+//                                       encoder never emits before toBytes.
+// E_s(q) comes from the global RLE parse (E_g, started at position 0) once the local parse
 // started at s re-synchronises with it (both end an RLE run at the same position; from
 // there on the encoders are in identical states), and from a short local walk before.
 //
-// One wave walks the row groups sequentially; lanes split the optional/boolean columns.
+// One wave walks the row groups sequentially; lanes split the streams / boolean columns.
 #include "kpw_device.h"
 #include "kpw_kernels.h"
 
@@ -117,13 +121,20 @@ __device__ __forceinline__ uint64_t pc_at(const DevCol &c, uint64_t x)
     return (uint64_t)c.pcnt[wi] + (uint64_t)__popcll(m);
 }
 
+// position of record r in stream k (the record itself, or its value rank)
+__device__ __forceinline__ int64_t stream_pos(const PlanArgs &a, const PlanStream &S, int64_t r)
+{
+    return S.rank_col < 0 ? r : (int64_t)pc_at(a.cols[S.rank_col], (uint64_t)r);
+}
+
 __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 {
     const int lane = threadIdx.x;
     uint64_t part = 0;
-    for (int k = lane; k < a.nopt; k += 64) {
-        const DevCol &c = a.cols[a.opt_cols[k]];
-        part += walker_query(W[k], r, c.pres, a.n, a.E + (uint64_t)k * (a.n + 1), a.gend + (uint64_t)k * a.gend_stride);
+    for (int k = lane; k < a.nstreams; k += 64) {
+        const PlanStream &S = a.streams[k];
+        part += walker_query(W[k], stream_pos(a, S, r), S.bits, S.len, a.E + (uint64_t)k * (a.n + 1),
+                             a.gend + (uint64_t)k * a.gend_stride);
     }
     for (int k = lane; k < a.nbool; k += 64) {
         const DevCol &c = a.cols[a.bool_cols[k]];
@@ -134,13 +145,13 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 }
 
 // memSize at record r for one lane, valid only when every walker is past its convergence
-// point (or has no further events): E_s(r) is then O(1) per column.
+// point (or has no further events): E_s(q) is then O(1) per stream.
 __device__ uint64_t eval_mem_lane(const PlanArgs &a, const Walker *W, int64_t s, int64_t r)
 {
     uint64_t m = a.P[r] - a.P[s];
-    for (int k = 0; k < a.nopt; k++) {
+    for (int k = 0; k < a.nstreams; k++) {
         const Walker &w = W[k];
-        m += w.state == 1 ? (uint64_t)((int64_t)a.E[(uint64_t)k * (a.n + 1) + r] + w.delta) : w.eacc;
+        m += w.state == 1 ? (uint64_t)((int64_t)a.E[(uint64_t)k * (a.n + 1) + stream_pos(a, a.streams[k], r)] + w.delta) : w.eacc;
     }
     for (int k = 0; k < a.nbool; k++) {
         const DevCol &c = a.cols[a.bool_cols[k]];
@@ -153,14 +164,14 @@ __device__ uint64_t eval_mem_lane(const PlanArgs &a, const Walker *W, int64_t s,
 __device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walker *W, int64_t r)
 {
     bool ok = true;
-    for (int k = threadIdx.x; k < a.nopt; k += 64)
-        ok = ok && (W[k].state == 2 || (W[k].state == 1 && W[k].conv_pos < r));
+    for (int k = threadIdx.x; k < a.nstreams; k += 64)
+        ok = ok && (W[k].state == 2 || (W[k].state == 1 && W[k].conv_pos < stream_pos(a, a.streams[k], r)));
     return __ballot(!ok) == 0;
 }
 
 __global__ void __launch_bounds__(64) k_plan(PlanArgs a)
 {
-    __shared__ Walker W[MAX_COLS];
+    __shared__ Walker W[MAX_STREAMS];
     const int lane = threadIdx.x;
     const int64_t n = (int64_t)a.n;
     const int64_t T = a.next_rg_size;
@@ -168,9 +179,9 @@ __global__ void __launch_bounds__(64) k_plan(PlanArgs a)
     int32_t nrg = 0;
     int64_t overflow = 0;
     for (;;) {
-        for (int k = lane; k < a.nopt; k += 64) {
+        for (int k = lane; k < a.nstreams; k += 64) {
             Walker w;
-            w.p = s; w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
+            w.p = stream_pos(a, a.streams[k], s); w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
             w.pend_bytes = 0; w.pend_rle = 0; w.grp = 0; w.state = 0;
             W[k] = w;
         }

@@ -1001,7 +1001,11 @@ constexpr uint32_t VT_ABORTED = 0xffffffffu;
     "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", \
     "v254", "v255"
 
-// (gfx950 has no v_movrels/v_movreld: VGPR index mode is the only runtime register index)
+// (gfx950 has no v_movrels/v_movreld: VGPR index mode is the only runtime register index).
+// s_set_gpr_idx_on writes M0, hence the M0 clobber (the compiler warns it reserves M0; nothing
+// in k_snappy_v keeps a value in M0 across these statements).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ uint32_t vt_row(uint32_t r)
 {
     uint32_t x;
@@ -1012,6 +1016,7 @@ __device__ __forceinline__ void vt_set_row(uint32_t r, uint32_t v)
 {
     asm volatile("s_set_gpr_idx_on %1, gpr_idx(DST)\n\tv_mov_b32 v128, %0\n\ts_set_gpr_idx_off" : : "v"(v), "s"(r & 127u) : "m0");
 }
+#pragma clang diagnostic pop
 
 // entry h (< 16384) -> row h>>7, lane (h>>1)&63, half h&1
 struct VTab {
@@ -1202,7 +1207,8 @@ __global__ void __launch_bounds__(64) k_snappy_s_rest(SnappyArgs a)
     k_snappy_s_body<SNAPPY_SEQ_PROBES>(a);
 }
 
-// per page: compressed size = varint(len) + sum of its fragments
+// per page: compressed size = [uncompressed level prefix (v2)] + varint(len) + its fragments
+// (SnappyCompressor emits nothing for an empty input)
 __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_page_sizes(SnappyArgs a, const uint32_t *page_frag0)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
@@ -1212,11 +1218,12 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_page_sizes(SnappyArgs a, c
         uint64_t c = 0;
         if (p < a.npages) {
             const uint64_t len = a.page_len[p];
+            const uint64_t pre = a.page_pre ? a.page_pre[p] : 0;
+            c = pre;
             if (len) {
                 uint32_t v = (uint32_t)len;
-                c = varint_len32(v);
+                uint64_t fo = pre + varint_len32(v);
                 const uint32_t nf = (uint32_t)((len + SNAPPY_FRAG - 1) / SNAPPY_FRAG);
-                uint64_t fo = c;
                 for (uint32_t k = 0; k < nf; k++) {
                     a.frag_coff[page_frag0[p] + k] = fo;
                     fo += a.frag_len[page_frag0[p] + k];
@@ -1237,7 +1244,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_copy(SnappyArgs a)
 {
     const uint32_t f = blockIdx.x;
     const uint32_t pg = a.frag_page[f];
-    uint8_t *dst = a.out + a.page_coff[pg];
+    uint8_t *dst = a.out + a.page_coff[pg] + (a.page_pre ? a.page_pre[pg] : 0);
     if (a.frag_idx[f] == 0 && threadIdx.x == 0) {
         uint32_t v = (uint32_t)a.page_len[pg];
         uint32_t i = 0;
@@ -1245,9 +1252,21 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_copy(SnappyArgs a)
         dst[i] = (uint8_t)v;
     }
     const uint8_t *s = a.frag_out + (uint64_t)f * SNAPPY_FRAG_CAP;
-    uint8_t *d = dst + a.frag_coff[f];
+    uint8_t *d = a.out + a.page_coff[pg] + a.frag_coff[f];
     const uint32_t n = a.frag_len[f];
     for (uint32_t i = threadIdx.x; i < n; i += KPW_BLOCK) d[i] = s[i];
+}
+
+// v2: the level bytes that sit in front of a page's values, copied verbatim ahead of its
+// compressed stream (ColumnChunkPageWriter.writePageV2: header | rl | dl | compressed data)
+__global__ void __launch_bounds__(KPW_BLOCK) k_snappy_prefix(SnappyArgs a)
+{
+    const uint32_t p = blockIdx.x;
+    const uint64_t pre = a.page_pre[p];
+    if (!pre) return;
+    const uint8_t *src = a.in + a.page_off[p] - pre;
+    uint8_t *dst = a.out + a.page_coff[p];
+    for (uint64_t i = threadIdx.x; i < pre; i += KPW_BLOCK) dst[i] = src[i];
 }
 
 // K7: the register-table kernel on every fragment (8 waves/CU, no LDS), then the batched
@@ -1263,6 +1282,7 @@ void launch_snappy_finish(const SnappyArgs &a, const uint32_t *page_frag0, hipSt
 {
     hipLaunchKernelGGL(k_snappy_page_sizes, dim3(1), dim3(KPW_BLOCK), 0, s, a, page_frag0);
     if (a.nfrags) hipLaunchKernelGGL(k_snappy_copy, dim3(a.nfrags), dim3(KPW_BLOCK), 0, s, a);
+    if (a.page_pre && a.npages) hipLaunchKernelGGL(k_snappy_prefix, dim3(a.npages), dim3(KPW_BLOCK), 0, s, a);
 }
 
 }  // namespace kpw

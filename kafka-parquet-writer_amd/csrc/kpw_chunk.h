@@ -29,7 +29,32 @@ struct ChunkArgs {
     uint32_t *collision;           // device flag: a hash-keyed string dictionary failed verification
     const uint32_t *dict_order;    // dictionary chunk tiles, interleaved across chunks
     uint32_t ndict_tiles;
+    int32_t v2;                    // PARQUET_2_0 page layout (levels unprefixed, DELTA fallback, RLE booleans)
+    const DeltaJob *djobs;         // v2: DELTA streams (layout reads their totals)
+    DeltaJob *djobs_w;             // v2: same array (layout sets out_off)
+    const uint64_t *chunk_sfx;     // v2: DELTA_BYTE_ARRAY suffix bytes per chunk
+    uint64_t *page_pre;            // v2: uncompressed level bytes in front of each page's values
 };
+
+// DELTA streams of a batch (k_delta.hip)
+struct DeltaArgs {
+    DeltaJob *jobs;
+    uint32_t njobs;
+    uint32_t nblk;                 // block tiles
+    const uint32_t *blk_job;
+    uint64_t *blk_min, *blk_sz, *blk_off, *btot;
+    uint32_t *blk_w;
+};
+void launch_delta_structure(const DeltaArgs &d, hipStream_t s);
+void launch_delta_write(const DeltaArgs &d, uint8_t *out, hipStream_t s);
+void launch_v2_decide(const ChunkArgs &a, const RleJob *jobs, DeltaJob *djobs, hipStream_t s);
+void launch_v2_dense(const ChunkArgs &a, uint64_t *dense, uint32_t *pre, uint32_t *sfx, uint64_t *tile_sfx, uint64_t *tile_sfx_off,
+                     uint64_t *chunk_sfx, hipStream_t s);
+void launch_dba_suffixes(const ChunkArgs &a, const uint32_t *pre, const DeltaJob *djobs, const uint64_t *tile_sfx_off, uint8_t *out,
+                         hipStream_t s);
+void launch_v2_bool_jobs(const ChunkArgs &a, RleJob *jobs, hipStream_t s);
+void launch_bool_streams(const DevCol *cols, const uint32_t *bool_cols, uint32_t nbool, uint64_t n, uint64_t *const *cbits,
+                         RleJob *jobs, uint32_t job0, PlanStream *streams, uint32_t stream0, hipStream_t s);
 
 inline void seg_tile_scan_u32(const uint32_t *in, uint32_t *out, const uint32_t *seg, uint32_t n, hipStream_t s)
 {
@@ -43,7 +68,7 @@ inline void seg_tile_scan_u64(const uint64_t *in, uint64_t *out, const uint32_t 
 void launch_chunk_stats(const ChunkArgs &a, hipStream_t s);
 void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s);
 void launch_layout(const ChunkArgs &a, RleJob *jobs, uint64_t *page_off, uint64_t *page_len, uint64_t *tot, hipStream_t s);
-void launch_chunk_write(const ChunkArgs &a, uint8_t *out, hipStream_t s);
+void launch_chunk_write(const ChunkArgs &a, const RleJob *jobs, uint8_t *out, hipStream_t s);
 
 // Snappy (K7)
 struct SnappyArgs {
@@ -61,6 +86,7 @@ struct SnappyArgs {
     uint64_t *frag_coff;         // per fragment output offset
     uint8_t *out;                // compressed pages
     uint64_t *tot;               // [0] total compressed bytes
+    const uint64_t *page_pre;    // v2: uncompressed level bytes right before page_off (nullptr: none)
 };
 constexpr uint32_t SNAPPY_FRAG = 65536;
 // per-fragment output slot: max compressed length (32 + n + n/6) rounded up to the 256-byte

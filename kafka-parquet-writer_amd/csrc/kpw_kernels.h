@@ -86,6 +86,18 @@ struct RleScratch {
 
 // Plan / chunk descriptors -------------------------------------------------------------
 
+// One RLE-encoded bit stream whose emitted bytes count in the row-group size check: the
+// definition levels of an optional column (record-indexed presence bits) or, in v2, the
+// values of a boolean column (RunLengthBitPackingHybridValuesWriter: record-indexed value
+// bits when required, rank-indexed compacted bits when optional).
+struct PlanStream {
+    const uint64_t *bits;
+    uint64_t len;                  // stream length (device-set for rank-indexed streams)
+    int32_t rank_col;              // -1: position = record; else position = rank in this column
+    int32_t pad;
+};
+constexpr int MAX_STREAMS = 2 * MAX_COLS;
+
 struct PlanArgs {
     uint64_t n;                    // records in the batch
     int32_t final_flush;           // close(): flush the trailing row group
@@ -93,13 +105,13 @@ struct PlanArgs {
     int64_t next_rg_size;          // nextRowGroupSize
     const uint64_t *P;             // exclusive prefix of raw bytes [n+1]
     const DevCol *cols;
-    const uint32_t *opt_cols;      // indices of optional columns
-    int32_t nopt;
-    int32_t nbool;
+    const PlanStream *streams;     // RLE streams counted by emitted bytes
+    int32_t nstreams;
+    int32_t nbool;                 // boolean columns counted as ceil(values/8) (v1); 0 in v2
     const uint32_t *bool_cols;     // indices of boolean columns
-    const uint32_t *E;             // per optional column k: E[k*(n+1) + r] global emitted dl bytes
-    const uint64_t *gend;          // per optional column k: bitmask of global RLE ends [(n/64+2)]
-    uint64_t gend_stride;          // words per column
+    const uint32_t *E;             // per stream k: E[k*(n+1) + q] global emitted bytes before position q
+    const uint64_t *gend;          // per stream k: bitmask of global RLE ends [(n/64+2)]
+    uint64_t gend_stride;          // words per stream
     // outputs
     int64_t *rg_start;             // [max_rgs]
     int64_t *rg_end;
@@ -136,6 +148,25 @@ struct ChunkDesc {
     uint64_t body_off;             // byte offset of this chunk's uncompressed bodies (dict page, then data page)
     uint64_t dl_scratch, id_scratch;   // offsets of RLE outputs in the rle output scratch
     int32_t dl_job, id_job;
+    // v2 (PARQUET_2_0)
+    int32_t bool_job;              // RLE job of the boolean values (-1 none)
+    int32_t dj0;                   // first DELTA stream (INT: 1, BYTE_ARRAY: 2), -1 none
+    uint64_t val_off;              // absolute offset of the values part of the data page
+};
+
+// One DELTA_BINARY_PACKED stream (k_delta.hip).
+constexpr uint32_t DJ_LONG = 1;      // 64-bit arithmetic (ForLong)
+constexpr uint32_t DJ_U32_SRC = 2;   // source values are u32 (else u64)
+constexpr uint32_t DJ_INACTIVE = 4;  // not written (chunk kept its dictionary)
+struct DeltaJob {
+    const void *vals;              // dense values, rank order
+    uint64_t base;                 // index of value 0
+    uint32_t n;                    // values (device-set)
+    uint32_t flags;
+    uint32_t blk0, nblk;           // block tiles [blk0, blk0+nblk) (host: upper bound, >= 1)
+    uint64_t out_off;              // absolute output offset (device-set by the layout)
+    uint64_t hdr;                  // header bytes (device)
+    uint64_t total;                // header + blocks (device)
 };
 
 // ---------------------------------------------------------------- launch wrappers

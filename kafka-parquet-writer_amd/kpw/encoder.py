@@ -10,8 +10,10 @@ from ._lib import KpwError, load_library, make_schema, _PropsC, BatchInfo
 MiB = 1024 * 1024
 
 
-def props_c(block_size=128 * MiB, page_size=128 * MiB, codec=0, enable_dictionary=True, dictionary_page_size=MiB):
-    return _PropsC(block_size, page_size, dictionary_page_size, 1 if enable_dictionary else 0, codec, 1, 0, 0, 8 * MiB)
+def props_c(block_size=128 * MiB, page_size=128 * MiB, codec=0, enable_dictionary=True, dictionary_page_size=MiB,
+            writer_version=1):
+    return _PropsC(block_size, page_size, dictionary_page_size, 1 if enable_dictionary else 0, codec, writer_version, 0, 0,
+                   8 * MiB)
 
 
 class Encoder:
@@ -61,7 +63,8 @@ class Encoder:
                             dl_encoding=p.dl_encoding, uncompressed_size=p.uncompressed_size,
                             compressed_size=p.compressed_size, offset=p.offset, null_count=p.null_count,
                             has_min_max=p.has_min_max, min=stats[p.min_off:p.min_off + p.min_len],
-                            max=stats[p.max_off:p.max_off + p.max_len]))
+                            max=stats[p.max_off:p.max_off + p.max_len], dl_byte_length=p.dl_byte_length,
+                            num_rows=p.num_rows))
         return out
 
     def chunks(self):

@@ -32,20 +32,23 @@ class ParquetProperties:
     for signature parity and ignored (the output stream is a local path or memory)."""
 
     def __init__(self, hadoop_conf=None, block_size=128 * MiB, compression_codec_name=UNCOMPRESSED,
-                 page_size=128 * MiB, enable_dictionary=True):
+                 page_size=128 * MiB, enable_dictionary=True, writer_version=1):
         self.hadoop_conf = hadoop_conf
         self.block_size = int(block_size)
         self.compression_codec_name = int(compression_codec_name)
         self.page_size = int(page_size)
         self.enable_dictionary = bool(enable_dictionary)
+        # ParquetFile.java:42-50 never sets a writer version (PARQUET_1_0); 2 = PARQUET_2_0,
+        # an explicit opt-in beyond the reference (DataPageV2 + DELTA fallback encodings)
+        self.writer_version = int(writer_version)
 
     def to_c(self):
         # ParquetFile.java:48-50 only ever calls enableDictionaryEncoding(); parquet-mr 1.10.1's
         # builder defaults dictionary encoding to ON, so the reference writes dictionaries
         # even when enableDictionary is false.  Reproduced here on purpose.
         effective_dictionary = 1
-        return _PropsC(self.block_size, self.page_size, MiB, effective_dictionary, self.compression_codec_name, 1, 0,
-                       0, 8 * MiB)
+        return _PropsC(self.block_size, self.page_size, MiB, effective_dictionary, self.compression_codec_name,
+                       self.writer_version, 0, 0, 8 * MiB)
 
 
 def _as_batch(values):

@@ -17,12 +17,14 @@ def to_device(data, offsets):
     return d, o
 
 
-def gpu_encoder_pages(schema, data, offsets, codec=0, block_size=128 * MiB, page_size=128 * MiB, dictionary=True):
+def gpu_encoder_pages(schema, data, offsets, codec=0, block_size=128 * MiB, page_size=128 * MiB, dictionary=True,
+                      writer_version=1):
     """Returns (row_groups, [(rg, col, [page dicts with 'body'])]) from the HIP encoder."""
     import kpw
     import torch
     enc = kpw.Encoder(kpw.Schema(schema.message_name, schema.columns, schema.proto_class), codec=codec,
-                      block_size=block_size, page_size=page_size, enable_dictionary=dictionary)
+                      block_size=block_size, page_size=page_size, enable_dictionary=dictionary,
+                      writer_version=writer_version)
     d, o = to_device(data, offsets)
     torch.cuda.synchronize()
     info = enc.encode(d.data_ptr(), o.data_ptr(), len(offsets) - 1, final=True)
@@ -63,7 +65,8 @@ def compare_pages(schema, data, offsets, **kw):
     """Returns a list of human-readable mismatches (empty = byte-identical pages)."""
     codec = kw.get("codec", 0)
     props = oracle.make_props(block_size=kw.get("block_size", 128 * MiB), page_size=kw.get("page_size", 128 * MiB),
-                              codec=codec, enable_dictionary=kw.get("dictionary", True))
+                              codec=codec, enable_dictionary=kw.get("dictionary", True),
+                              writer_version=kw.get("writer_version", 1))
     fb = oracle.encode_file(schema, data, offsets, props)
     rgs, gpages, info, enc = gpu_encoder_pages(schema, data, offsets, **kw)
     errs = []
@@ -87,20 +90,27 @@ def compare_pages(schema, data, offsets, **kw):
             if g["uncompressed_size"] != h[2] or g["compressed_size"] != h[3]:
                 errs.append("rg %d col %s page %d: sizes gpu (%d,%d) oracle (%d,%d)" % (
                     rg, name, k, g["uncompressed_size"], g["compressed_size"], h[2], h[3]))
-            if ptype == 0:
-                dh = h[5]
-                if (g["num_values"], g["encoding"], g["dl_encoding"]) != (dh[1], dh[2], dh[3]):
-                    errs.append("rg %d col %s page %d: header gpu %r oracle %r" % (
-                        rg, name, k, (g["num_values"], g["encoding"], g["dl_encoding"]), (dh[1], dh[2], dh[3])))
-                st = dh.get(5, {})
+            if ptype in (0, 3):
+                if ptype == 0:
+                    dh = h[5]
+                    got, want = (g["num_values"], g["encoding"], g["dl_encoding"]), (dh[1], dh[2], dh[3])
+                    st = dh.get(5, {})
+                else:   # DataPageHeaderV2
+                    dh = h[8]
+                    got = (g["num_values"], g["null_count"], g["num_rows"], g["encoding"], g["dl_byte_length"], 0)
+                    want = (dh[1], dh[2], dh[3], dh[4], dh[5], dh[6])
+                    st = dh.get(8, {})
+                if got != want:
+                    errs.append("rg %d col %s page %d: header gpu %r oracle %r" % (rg, name, k, got, want))
                 if st.get(3, None) is not None and st.get(3) != g["null_count"]:
                     errs.append("rg %d col %s: null_count gpu %d oracle %d" % (rg, name, g["null_count"], st.get(3)))
                 if 6 in st and (st[6] != g["min"] or st[5] != g["max"]):
                     errs.append("rg %d col %s: min/max gpu %r/%r oracle %r/%r" % (rg, name, g["min"][:20], g["max"][:20],
                                                                                 st[6][:20], st[5][:20]))
             else:
-                if g["num_values"] != h[7][1]:
-                    errs.append("rg %d col %s dict entries gpu %d oracle %d" % (rg, name, g["num_values"], h[7][1]))
+                if (g["num_values"], g["encoding"]) != (h[7][1], h[7][2]):
+                    errs.append("rg %d col %s dict page (entries, encoding) gpu %r oracle %r" % (
+                        rg, name, (g["num_values"], g["encoding"]), (h[7][1], h[7][2])))
             if g["body"] != o["body"]:
                 a, b = g["body"], o["body"]
                 i = next((j for j in range(min(len(a), len(b))) if a[j] != b[j]), min(len(a), len(b)))

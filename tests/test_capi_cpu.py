@@ -45,12 +45,21 @@ def test_create_rejects_bad_schema_without_gpu():
     # null schema
     h = L.kpw_encoder_create(0, None, ctypes.byref(pr), ctypes.byref(st))
     assert not h and st.value == -1
-    # writer version 2 is not reachable from the reference
+    # PARQUET_2_0 is an explicit opt-in and needs the dictionary on (the reference cannot
+    # turn it off); unknown writer versions are rejected
     sc, keep = _lib.make_schema(_schema([("a", 1, 5, 2)]))
-    pr2 = kpw.encoder.props_c()
-    pr2.writer_version = 2
+    pr2 = kpw.encoder.props_c(writer_version=2, enable_dictionary=False)
     h = L.kpw_encoder_create(0, ctypes.byref(sc), ctypes.byref(pr2), ctypes.byref(st))
     assert not h and st.value == -2
+    pr3 = kpw.encoder.props_c(writer_version=3)
+    h = L.kpw_encoder_create(0, ctypes.byref(sc), ctypes.byref(pr3), ctypes.byref(st))
+    assert not h and st.value == -2
+
+
+def test_page_info_layout():
+    """kpw_page_info as declared in include/kpw_gpu.h (the ctypes mirror must match it)."""
+    assert ctypes.sizeof(_lib.PageInfo) == 96
+    assert _lib.PageInfo.min_off.offset == 72 and _lib.PageInfo.num_rows.offset == 88
 
 
 def test_null_handles():

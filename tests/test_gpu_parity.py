@@ -37,6 +37,60 @@ def test_pages_match_oracle(name, kind, param, n, codec, block_size):
     assert not errs, "\n".join(errs[:12])
 
 
+@pytest.mark.parametrize("name,kind,param,n", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("codec", [0, 1], ids=["uncompressed", "snappy"])
+@pytest.mark.parametrize("block_size", [128 * MiB, 64 * 1024], ids=["rg128M", "rg64K"])
+def test_v2_pages_match_oracle(name, kind, param, n, codec, block_size):
+    """A10 / PARQUET_2_0: DataPageV2 headers, unprefixed levels in front of the compressed
+    values, RLE_DICTIONARY, RLE booleans (their RLE bytes in the row-group size check),
+    DELTA_BINARY_PACKED / DELTA_BYTE_ARRAY fallback pages byte-identical to the oracle."""
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, 0xC0FFEE21 + kind, n, param=param)
+    errs = gh.compare_pages(schema, data, offs, codec=codec, block_size=block_size, writer_version=2)
+    assert not errs, "\n".join(errs[:12])
+
+
+@pytest.mark.parametrize("kind,n", [(synth.KIND_HIGHCARD, 40000), (synth.KIND_REC8, 300000)], ids=["highcard", "rec8"])
+def test_v2_delta_fallback_large(kind, n):
+    # uuid/blob fall back to DELTA_BYTE_ARRAY, ts/user_id to DELTA_BINARY_PACKED (many 128-value
+    # blocks, partial last blocks with parquet-mr's stale widths and padding)
+    import pqwalk
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, 5, n)
+    errs = gh.compare_pages(schema, data, offs, codec=1, writer_version=2)
+    assert not errs, "\n".join(errs[:12])
+    fb = oracle.encode_file(schema, data, offs, oracle.make_props(codec=1, writer_version=2))
+    encs = {p["header"][8][4] for p in pqwalk.pages(fb) if p["header"][1] == 3}
+    # highcard: uuid/blob DELTA_BYTE_ARRAY; rec8: ts/user_id DELTA_BINARY_PACKED, price PLAIN
+    assert (7 in encs) if kind == synth.KIND_HIGHCARD else (5 in encs and 0 in encs), encs
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 33, 128, 129, 130, 257, 1000])
+def test_v2_delta_block_edges(n):
+    """Stream lengths around the 128-value block and 32-value miniblock boundaries; the
+    dictionary is forced off by its compression check (all-distinct timestamps/queries)."""
+    cls = protoutil.message_class(synth.SAMPLE)
+    recs = [cls(query="q%07d" % (i * 7919 % 1000003), timestamp=(i * 2654435761) % (1 << 40) - (1 << 39),
+                page_number=(-i if i % 3 else i)).SerializeToString() for i in range(n)]
+    data, offs = synth.pack(recs)
+    for codec in (0, 1):
+        errs = gh.compare_pages(synth.SAMPLE, data, offs, codec=codec, writer_version=2)
+        assert not errs, "\n".join(errs[:12])
+
+
+def test_v2_writer_file_identical():
+    import kpw
+    import pqwalk
+    schema = synth.REC8
+    data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE31, 20000, param=0)
+    props = kpw.ParquetProperties(block_size=256 * 1024, compression_codec_name=1, writer_version=2)
+    fb = gh.gpu_file(schema, data, offs, props, batches=3)
+    ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=256 * 1024, codec=1, writer_version=2))
+    assert fb == ob, pqwalk.first_difference(fb, ob)
+    tbl = pq.read_table(io.BytesIO(fb))
+    assert protoutil.table_columns(tbl, schema) == protoutil.decode_columns(schema, synth.records(data, offs))
+
+
 @pytest.mark.parametrize("dictionary", [True, False])
 def test_dictionary_toggle(dictionary):
     data, offs = synth.generate(synth.KIND_REC8, 11, 5000)
