@@ -35,6 +35,35 @@ __device__ __forceinline__ uint64_t rank_base(const DevCol &c, uint64_t s, uint6
     return pc(x) - pc(s);
 }
 
+// Coalesced chunk-tile layout: thread t of tile T handles records T0 + k*KPW_BLOCK + t,
+// k = 0..7 (one fully used line per wave and k), and gets each record's rank (index among
+// the chunk's non-null values) from the presence popcount prefix instead of a running
+// count.  Used by every per-record kernel whose result does not depend on a thread's
+// records being contiguous.
+__device__ __forceinline__ uint64_t pres_rank(const DevCol &c, uint64_t y)
+{
+    const uint64_t wi = y >> 6;
+    const uint64_t m = (y & 63) ? (c.pres[wi] & ((1ull << (y & 63)) - 1)) : 0ull;
+    return (uint64_t)c.pcnt[wi] + (uint64_t)__popcll(m);
+}
+struct TileRecs {
+    uint64_t t0, e;       // first record of the tile, chunk end
+    uint64_t rank0;       // rank base of the chunk (pres_rank(C.s) or C.s)
+    __device__ __forceinline__ uint64_t rec(int k) const { return t0 + (uint64_t)k * KPW_BLOCK + threadIdx.x; }
+    __device__ __forceinline__ uint64_t rank(const DevCol &c, uint64_t r) const
+    {
+        return (c.optional ? pres_rank(c, r) : r) - rank0;
+    }
+};
+__device__ __forceinline__ TileRecs tile_recs(const ChunkDesc &C, const DevCol &col, uint32_t t, const uint32_t *ctile_first, uint32_t ci)
+{
+    TileRecs T;
+    T.t0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P;
+    T.e = (uint64_t)C.e;
+    T.rank0 = col.optional ? pres_rank(col, (uint64_t)C.s) : (uint64_t)C.s;
+    return T;
+}
+
 __device__ __forceinline__ uint64_t fixed_val(const DevCol &c, uint64_t r)
 {
     return c.vsize == 4 ? (uint64_t)((const uint32_t *)c.vals)[r] : ((const uint64_t *)c.vals)[r];
@@ -85,12 +114,12 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
     const uint32_t ci = ctile_chunk[t];
     ChunkDesc &C = ch[ci];
     const DevCol &col = cols[C.col];
-    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     uint64_t nn = 0, raw = 0;
     uint64_t kmin = ~0ull, kmax = 0;
     for (int k = 0; k < 8; k++) {
-        const uint64_t r = p0 + k;
-        if (r >= (uint64_t)C.e) break;
+        const uint64_t r = T.rec(k);
+        if (r >= T.e) break;
         if (!present_at(col, r)) continue;
         nn++;
         if (col.phys == 6) {
@@ -158,15 +187,16 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_str_minmax(const ChunkDesc *ch, c
     if (col.phys != 6) return;
     const uint64_t data_end = *data_end_p;
     const bool ents = C.is_dict && !C.fallback;
-    const uint64_t q0 = (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    const uint64_t q0 = (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x;   // coalesced (equal strings tie harmlessly)
     uint64_t a = ~0ull, b = ~0ull;
     for (int k = 0; k < 8; k++) {
+        const uint64_t q = q0 + (uint64_t)k * KPW_BLOCK;
         uint64_t r;
         if (ents) {
-            if (q0 + k >= C.dict_n) break;
-            r = ent_rec[C.ent_off + q0 + k];
+            if (q >= C.dict_n) break;
+            r = ent_rec[C.ent_off + q];
         } else {
-            r = (uint64_t)C.s + q0 + k;
+            r = (uint64_t)C.s + q;
             if (r >= (uint64_t)C.e) break;
             if (!present_at(col, r)) continue;
         }
@@ -295,7 +325,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     __syncthreads();
     if (skip) return;
     const DevCol &col = cols[C.col];
-    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     const uint32_t cap = C.ht_cap;
     uint64_t *keys = ht_key + C.ht_off;
     uint32_t *mins = ht_min + C.ht_off;
@@ -305,24 +335,21 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     const bool is_bin = col.phys == 6 && exact;
     for (uint32_t i = threadIdx.x; i < LDS_T; i += KPW_BLOCK) { lkey[i] = HT_EMPTY; lmin[i] = 0xffffffffu; }
     __syncthreads();
-    uint64_t rank0 = p0 < (uint64_t)C.e ? rank_base(col, (uint64_t)C.s, p0) : 0;
     int32_t li[8];
     uint64_t keyv[8];
     uint32_t rk[8];
-    uint32_t npres = 0;
     // phase 1: LDS dedup
     for (int k = 0; k < 8; k++) {
         li[k] = -2;  // not present
-        const uint64_t r = p0 + k;
-        if (r >= (uint64_t)C.e) continue;
+        const uint64_t r = T.rec(k);
+        if (r >= T.e) continue;
         if (!present_at(col, r)) continue;
         uint64_t key;
         if (is_bin) key = r;
         else if (col.phys == 6) key = col.shash[r];
         else key = fixed_val(col, r);
         keyv[k] = key;
-        rk[k] = (uint32_t)(rank0 + npres);
-        npres++;
+        rk[k] = (uint32_t)T.rank(col, r);
         li[k] = -1;  // global path
         if (is_bin || key == HT_EMPTY) continue;
         uint32_t i = (uint32_t)(mix64(key) >> 40) & (LDS_T - 1);
@@ -361,7 +388,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     // phase 3: slots for every value (LDS hit or direct global insert)
     for (int k = 0; k < 8; k++) {
         if (li[k] == -2) continue;
-        const uint64_t r = p0 + k;
+        const uint64_t r = T.rec(k);
         int64_t g;
         if (li[k] >= 0) {
             g = lslot[li[k]] == 0xffffffffu ? -1 : (int64_t)lslot[li[k]];
@@ -382,7 +409,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     }
 }
 
-// count (write=0) / assign (write=1) first occurrences in record order
+// count (write=0) / assign (write=1) first occurrences in record order.  In the coalesced
+// tile layout record order is (k, wave, lane); the write pass ranks a thread's first
+// occurrences with one ballot + one wave scan per k and 32 (k, wave) totals in LDS.
 __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
                                                            const uint32_t *ctile_first, const uint32_t *ht_min, uint32_t *ht_id,
                                                            const uint32_t *slotof, uint32_t *tile_cnt, uint64_t *tile_sz,
@@ -391,28 +420,32 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
 {
     __shared__ uint64_t lds[KPW_BLOCK];
     __shared__ uint32_t ldu[KPW_BLOCK];
+    __shared__ uint32_t wcnt[8][KPW_BLOCK / 64];
+    __shared__ uint64_t wsz[8][KPW_BLOCK / 64];
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
     const bool active = C.is_dict && !C.fallback;
     const DevCol &col = cols[C.col];
-    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
+    const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     uint32_t cnt = 0;
     uint64_t sz = 0;
     uint32_t firsts = 0;  // bitmask over the 8 records
-    if (active && p0 < (uint64_t)C.e) {
-        uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+    uint32_t esz[8];
+    if (active) {
         for (int k = 0; k < 8; k++) {
-            const uint64_t r = p0 + k;
-            if (r >= (uint64_t)C.e) break;
+            esz[k] = 0;
+            const uint64_t r = T.rec(k);
+            if (r >= T.e) break;
             if (!present_at(col, r)) continue;
+            const uint64_t rank = T.rank(col, r);
             const uint32_t slot = slotof[C.ids_off + rank];
             if (ht_min[C.ht_off + slot] == (uint32_t)rank) {
                 firsts |= 1u << k;
                 cnt++;
-                sz += col.phys == 6 ? 4 + col.slen[r] : (uint64_t)col.vsize;
+                esz[k] = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize;
+                sz += esz[k];
             }
-            rank++;
         }
     }
     if (!write) {
@@ -421,25 +454,44 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
         if (threadIdx.x == 0) { tile_cnt[t] = sc; tile_sz[t] = ss; }
         return;
     }
-    uint32_t tc;
-    uint64_t ts;
-    uint32_t eid = block_scan_excl<uint32_t, OpSum32>(cnt, ldu, &tc) + tile_cnt_off[t];
-    uint64_t boff = block_scan_excl<uint64_t, OpSum64>(sz, lds, &ts) + tile_sz_off[t];
-    if (!firsts) return;
-    uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+    if (!active) return;   // block-uniform
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lt = (1ull << lane) - 1;
+    uint32_t lpre[8];
+    uint64_t spre[8];
+#pragma unroll
     for (int k = 0; k < 8; k++) {
-        const uint64_t r = p0 + k;
-        if (r >= (uint64_t)C.e) break;
-        if (!present_at(col, r)) continue;
-        if ((firsts >> k) & 1) {
-            const uint32_t slot = slotof[C.ids_off + rank];
-            ht_id[C.ht_off + slot] = eid;
-            ent_rec[C.ent_off + eid] = r;
-            ent_boff[C.ent_off + eid] = boff;
-            boff += col.phys == 6 ? 4 + col.slen[r] : (uint64_t)col.vsize;
-            eid++;
+        const bool f = (firsts >> k) & 1;
+        const uint64_t m = __ballot(f);
+        lpre[k] = (uint32_t)__popcll(m & lt);
+        uint64_t x = f ? esz[k] : 0, inc = x;   // inclusive wave scan of entry sizes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
         }
-        rank++;
+        spre[k] = inc - x;
+        if (lane == 63) { wcnt[k][w] = (uint32_t)__popcll(m); wsz[k][w] = inc; }
+    }
+    __syncthreads();
+    if (!firsts) return;
+    uint32_t ebase = tile_cnt_off[t];
+    uint64_t bbase = tile_sz_off[t];
+    const int klast = 31 - __clz(firsts);
+    for (int k = 0; k <= klast; k++) {
+        for (int w2 = 0; w2 < KPW_BLOCK / 64; w2++) {
+            if (((firsts >> k) & 1) && w2 == w) {   // my segment (k, w): emit, then keep counting
+                const uint64_t r = T.rec(k);
+                const uint64_t rank = T.rank(col, r);
+                const uint32_t eid = ebase + lpre[k];
+                const uint32_t slot = slotof[C.ids_off + rank];
+                ht_id[C.ht_off + slot] = eid;
+                ent_rec[C.ent_off + eid] = r;
+                ent_boff[C.ent_off + eid] = bbase + spre[k];
+            }
+            ebase += wcnt[k][w2];
+            bbase += wsz[k][w2];
+        }
     }
 }
 
@@ -455,21 +507,18 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, con
     const ChunkDesc &C = ch[ci];
     if (!C.is_dict || C.fallback) return;
     const DevCol &col = cols[C.col];
-    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
-    if (p0 >= (uint64_t)C.e) return;
-    uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+    const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     for (int k = 0; k < 8; k++) {
-        const uint64_t r = p0 + k;
-        if (r >= (uint64_t)C.e) break;
+        const uint64_t r = T.rec(k);
+        if (r >= T.e) break;
         if (!present_at(col, r)) continue;
-        const uint64_t o = C.ids_off + rank;
+        const uint64_t o = C.ids_off + T.rank(col, r);
         const uint32_t id = ht_id[C.ht_off + ids[o]];
         ids[o] = id;
         if (col.phys == 6) {  // verify the hash-keyed dictionary byte-for-byte
             const uint64_t e = ent_rec[C.ent_off + id];
             if (!str_eq(col, data, e, r, data_end)) atomicOr(collision, 1u);
         }
-        rank++;
     }
 }
 
@@ -650,16 +699,19 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_plain(const ChunkDesc *ch, const 
             o += 4 + l;
         }
     } else {
-        if (p0 >= (uint64_t)C.e) return;
-        uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+        const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
         for (int k = 0; k < 8; k++) {
-            const uint64_t r = p0 + k;
-            if (r >= (uint64_t)C.e) break;
+            const uint64_t r = T.rec(k);
+            if (r >= T.e) break;
             if (!present_at(col, r)) continue;
             const uint64_t v = fixed_val(col, r);
-            uint8_t *d = vout + rank * col.vsize;
+            uint8_t *d = vout + T.rank(col, r) * col.vsize;
+            if (col.vsize == 8) {
+                if (((uintptr_t)d & 7) == 0) { *(uint64_t *)d = v; continue; }
+            } else if (col.vsize == 4) {
+                if (((uintptr_t)d & 3) == 0) { *(uint32_t *)d = (uint32_t)v; continue; }
+            }
             for (int i = 0; i < col.vsize; i++) d[i] = (uint8_t)(v >> (8 * i));
-            rank++;
         }
     }
 }
@@ -673,19 +725,16 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_plain_bool(const ChunkDesc *ch, c
     const ChunkDesc &C = ch[ci];
     const DevCol &col = cols[C.col];
     if (col.phys != 0 || C.bool_job >= 0) return;   // bool_job: v2 RLE booleans instead
-    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
-    if (p0 >= (uint64_t)C.e) return;
-    uint64_t rank = rank_base(col, (uint64_t)C.s, p0);
+    const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     const uint64_t base_bit = C.val_off * 8;
     for (int k = 0; k < 8; k++) {
-        const uint64_t r = p0 + k;
-        if (r >= (uint64_t)C.e) break;
+        const uint64_t r = T.rec(k);
+        if (r >= T.e) break;
         if (!present_at(col, r)) continue;
         if ((col.vbits[r >> 6] >> (r & 63)) & 1ull) {
-            const uint64_t bit = base_bit + rank;
+            const uint64_t bit = base_bit + T.rank(col, r);
             atomicOr((uint32_t *)(out + ((bit >> 3) & ~3ull)), 1u << (((bit >> 3) & 3) * 8 + (bit & 7)));
         }
-        rank++;
     }
 }
 

@@ -211,18 +211,17 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_delta_dense(const ChunkDesc *ch, 
     const ChunkDesc &C = ch[ci];
     if (C.dj0 < 0 || !C.fallback) return;
     const DevCol &col = cols[C.col];
-    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
-    if (p0 >= (uint64_t)C.e) return;
-    uint64_t rank = col.optional ? rank_of(col, p0) - rank_of(col, (uint64_t)C.s) : p0 - (uint64_t)C.s;
+    // coalesced tile layout: thread x handles records t0 + x, t0 + x + 256, ...
+    const uint64_t t0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x;
+    const uint64_t rank0 = col.optional ? rank_of(col, (uint64_t)C.s) : (uint64_t)C.s;
     for (int k = 0; k < 8; k++) {
-        const uint64_t r = p0 + k;
+        const uint64_t r = t0 + (uint64_t)k * KPW_BLOCK;
         if (r >= (uint64_t)C.e) break;
         if (col.optional && !((col.pres[r >> 6] >> (r & 63)) & 1ull)) continue;
         uint64_t v;
         if (col.phys == 6) v = r;
         else v = col.vsize == 4 ? (uint64_t)((const uint32_t *)col.vals)[r] : ((const uint64_t *)col.vals)[r];
-        dense[C.ids_off + rank] = v;
-        rank++;
+        dense[C.ids_off + (col.optional ? rank_of(col, r) : r) - rank0] = v;
     }
 }
 
@@ -256,19 +255,19 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dba_lengths(const ChunkDesc *ch, 
     const DevCol &col = cols[C.col];
     uint64_t sum = 0;
     const bool active = C.dj0 >= 0 && C.fallback && col.phys == 6;
-    const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
-    if (active && p0 < (uint64_t)C.e) {
-        uint64_t rank = col.optional ? rank_of(col, p0) - rank_of(col, (uint64_t)C.s) : p0 - (uint64_t)C.s;
+    if (active) {   // coalesced tile layout (the per-tile suffix total is order-independent)
+        const uint64_t t0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x;
+        const uint64_t rank0 = col.optional ? rank_of(col, (uint64_t)C.s) : (uint64_t)C.s;
         for (int k = 0; k < 8; k++) {
-            const uint64_t r = p0 + k;
+            const uint64_t r = t0 + (uint64_t)k * KPW_BLOCK;
             if (r >= (uint64_t)C.e) break;
             if (col.optional && !((col.pres[r >> 6] >> (r & 63)) & 1ull)) continue;
+            const uint64_t rank = (col.optional ? rank_of(col, r) : r) - rank0;
             const uint32_t p = rank ? common_prefix(col, data, dense[C.ids_off + rank - 1], r) : 0u;
             const uint32_t s = col.slen[r] - p;
             pre[C.ids_off + rank] = p;
             sfx[C.ids_off + rank] = s;
             sum += s;
-            rank++;
         }
     }
     sum = block_reduce<uint64_t, OpSum64>(sum, lds);
