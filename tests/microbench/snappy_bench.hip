@@ -65,6 +65,18 @@ static float run(const SnappyArgs &a, int reps)
             hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, 0, a);
             hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, 0, a);
         } else if (KIND == 5) hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, 0, a);
+        else if (KIND == 7) {   // register-resident + scheduled fast path, then the batched LDS kernel
+            hipLaunchKernelGGL(k_snappy_ra, dim3(a.nfrags), dim3(64), 0, 0, a);
+            hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, 0, a);
+        }
+        else if (KIND == 8) {   // windowed register-resident kernel, then the batched LDS kernel
+            hipLaunchKernelGGL(k_snappy_w2, dim3(a.nfrags), dim3(64), 0, 0, a);
+            hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, 0, a);
+        }
+        else if (KIND == 6) {   // register-resident fragment kernel, then the batched LDS kernel
+            hipLaunchKernelGGL(k_snappy_r, dim3(a.nfrags), dim3(64), 0, 0, a);
+            hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, 0, a);
+        }
         else hipLaunchKernelGGL(k_snappy_frag<SEQ>, dim3(a.nfrags), dim3(64), 0, 0, a);
     };
     launch();
@@ -81,17 +93,34 @@ int main(int argc, char **argv)
 {
     const size_t MB = 1 << 20;
     const size_t size = argc > 1 ? (size_t)atoll(argv[1]) * MB : 256 * MB;   // bytes per kind (many pages of 16 MiB)
-    const char *kinds[] = {"ts", "price", "user_id", "ids14", "key16", "json", "defl"};
+    std::vector<std::string> kinds = {"ts", "price", "user_id", "ids14", "key16", "json", "defl"};
+    // "@file": real pages dumped by dump_pages.py (u64 length + bytes each); every page of
+    // at least 1 MiB becomes one kind "pageN", replicated to `size` bytes
+    std::vector<std::vector<uint8_t>> file_pages;
+    if (argc > 2 && argv[2][0] == '@') {
+        kinds.clear();
+        FILE *fp = fopen(argv[2] + 1, "rb");
+        if (!fp) { fprintf(stderr, "cannot open %s\n", argv[2] + 1); return 2; }
+        uint64_t l;
+        for (int i = 0; fread(&l, 8, 1, fp) == 1; i++) {
+            std::vector<uint8_t> b(l);
+            if (fread(b.data(), 1, l, fp) != l) return 2;
+            if (l >= MB) { kinds.push_back("page" + std::to_string(i)); file_pages.push_back(std::move(b)); }
+        }
+        fclose(fp);
+    }
     int bad = 0;
-    for (const char *kind : kinds) {
-        if (argc > 2 && !strstr(argv[2], kind)) continue;   // optional kind filter, e.g. "ts,key16"
-        // pages of 16 MiB (C2 pages are 2-17 MiB)
-        const size_t psz = 16 * MB;
+    for (size_t ki = 0; ki < kinds.size(); ki++) {
+        const char *kind = kinds[ki].c_str();
+        if (argc > 2 && argv[2][0] != '@' && !strstr(argv[2], kind)) continue;   // optional kind filter, e.g. "ts,key16"
+        if (argc > 3 && kinds[ki] != argv[3]) continue;                            // "@file pageN"
+        // pages of 16 MiB (C2 pages are 2-17 MiB), or copies of the real page
+        const size_t psz = file_pages.empty() ? 16 * MB : file_pages[ki].size();
         const size_t npages = (size + psz - 1) / psz;
         std::vector<uint8_t> host;
         std::vector<uint64_t> off, len;
         for (size_t p = 0; p < npages; p++) {
-            std::vector<uint8_t> pg = make_page(kind, psz);
+            std::vector<uint8_t> pg = file_pages.empty() ? make_page(kind, psz) : file_pages[ki];
             off.push_back(host.size()); len.push_back(pg.size());
             host.insert(host.end(), pg.begin(), pg.end());
         }
@@ -137,7 +166,7 @@ int main(int argc, char **argv)
         };
         const double gb = (double)(npages * psz) / 1e9;
         struct V { const char *name; float (*fn)(const SnappyArgs &, int); };
-        V vs[] = {{"s2", run<2, 2>}, {"v+s2", run<2, 4>}};
+        V vs[] = {{"s2", run<2, 2>}, {"v+s2", run<2, 4>}, {"r+s2", run<2, 6>}, {"ra+s2", run<2, 7>}, {"w2+s2", run<2, 8>}};
         {   // how many fragments the register-table kernel gives up on
             (void)run<2, 5>(a, 1);
             std::vector<uint32_t> fl(nf);
