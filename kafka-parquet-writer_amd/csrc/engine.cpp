@@ -87,6 +87,8 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     if (pr->dfs_block_size > 0) return fail(KPW_ERR_UNSUPPORTED, "HDFS padding alignment (next round)");
     props = *pr;
     v2_ = pr->writer_version == 2;
+    // pages cut inside row groups: ColumnWriterV1 page checks + compressed-size row-group checks
+    mp_ = !v2_ && pr->page_size < pr->block_size;
     message_name = schema->message_name;
     proto_class = schema->proto_class ? schema->proto_class : schema->message_name;
     for (int c = 0; c < schema->num_columns; c++) {
@@ -339,6 +341,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), d_gend.as<uint64_t>(), nwords, s);
         launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ne, nstreams, d_scan_tmp.as<uint64_t>(), s);
     }
+    if (mp_) return encode_mp(d_data, d_off, n, ne, final_flush, next_rg_size, hc, nwords, out);
     // ---------------------------------------------------------------- A9 plan
     const int32_t max_rgs = (int32_t)(ne / 100 + 4);
     ENS(d_rg_start, max_rgs * 8); ENS(d_rg_end, max_rgs * 8); ENS(d_plan_out, 64);

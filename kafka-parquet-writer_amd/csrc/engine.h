@@ -47,6 +47,11 @@ struct BatchOut {
     int64_t records_consumed = 0, open_records = 0, open_buffered = 0, invalid_record = -1;
 };
 
+// multi-page regime: one encode of [s, e) -> per column its pages (dictionary page first)
+struct MpRun {
+    std::vector<std::vector<PageOut>> cols;
+};
+
 class DevBuf {
 public:
     void *p = nullptr;
@@ -100,6 +105,17 @@ private:
     hipEvent_t kev_[4] = {};
     std::vector<uint32_t> opt_idx_, bool_idx_;
     int run_rle(std::vector<RleJob> &jobs, uint32_t &nptiles, uint32_t &netiles, RleScratch &sc);
+    // multi-page regime (engine_mp.cpp)
+    bool mp_ = false;
+    int encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
+                  const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out);
+    int mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vector<int64_t>> &cuts);
+    int mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s, int64_t e,
+                    const std::vector<std::vector<int64_t>> &cuts, MpRun &run);
+    int grow_keep(DevBuf &b, size_t bytes, size_t keep);
+    std::vector<DevBuf> mp_sp;
+    DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_flag, mp_dch, mp_dtile_chunk, mp_dtile_first, mp_dtile_count, mp_dtile_raw,
+        mp_dtile_smin, mp_dtile_smax, mp_dtile_cnt, mp_dtile_sz, mp_ssz, mp_spp, mp_cstream, mp_acc;
     uint8_t *pages_dev_ = nullptr;
     uint64_t pages_len_ = 0;
 };

@@ -1,0 +1,524 @@
+// engine_mp.cpp — the multi-page regime: PARQUET_1_0 with pageSize < blockSize.
+//
+// parquet-mr 1.10.1 cuts a column's page inside a row group (ColumnWriterV1
+// .accountForValueWritten), and from then on the row-group size check
+// (InternalParquetRecordWriter.checkBlockSizeReached) counts the flushed pages by their
+// header + compressed bytes (ColumnChunkPageWriter.getMemSize) instead of their raw size.  A
+// row-group boundary therefore depends on the encoded and compressed sizes of the pages
+// before it, so row groups are planned one at a time:
+//
+//   1. k_page_cuts   page cuts of every column from the row-group start s to a horizon h
+//                    (they depend only on s and the values);
+//   2. mp_pipeline   encode [s, h) as pages (statistics, dictionary per column chunk with
+//                    per-page fallback / bit width, RLE, PLAIN, Snappy) -> page bytes;
+//   3. k_plan_mp     the row-group check walk with those page bytes -> end r (or none: h
+//                    doubles and 1-3 repeat);
+//   4. mp_pipeline   encode [s, r) exactly (the last page of every column ends at r) and
+//                    append it to the batch output.
+//
+// The single-page regime (pageSize >= blockSize, the reference default) stays in engine.cpp
+// and plans every row group of a batch in one pass.
+#include <algorithm>
+#include <cstring>
+
+#include "engine.h"
+#include "filewriter.h"
+#include "kpw_chunk.h"
+#include "kpw_scan.h"
+
+namespace kpw {
+
+void launch_snappy_finish(const SnappyArgs &a, const uint32_t *page_frag0, hipStream_t s);
+void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, const uint8_t *data, uint64_t *meta,
+                         uint8_t *blob, hipStream_t s);
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) return fail(KPW_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define ENS(buf, bytes) do { if ((buf).ensure(bytes)) return fail(KPW_ERR_NOMEM, "device allocation failed: " #buf); } while (0)
+
+static inline uint64_t next_pow2_mp(uint64_t x)
+{
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// Grow `b` to hold `bytes`, keeping its first `keep` bytes.
+int Engine::grow_keep(DevBuf &b, size_t bytes, size_t keep)
+{
+    if (bytes <= b.cap && b.p) return KPW_OK;
+    void *np = nullptr;
+    const size_t c = bytes + bytes / 2 + 256;
+    if (hipMalloc(&np, c) != hipSuccess) return fail(KPW_ERR_NOMEM, "device allocation failed: multi-page output");
+    if (keep && b.p) CK(hipMemcpyAsync(np, b.p, keep, hipMemcpyDeviceToDevice, stream));
+    CK(hipStreamSynchronize(stream));
+    if (b.p) (void)hipFree(b.p);
+    b.p = np;
+    b.cap = c;
+    return KPW_OK;
+}
+
+// Page cuts of every column over [s, h).
+int Engine::mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vector<int64_t>> &cuts)
+{
+    const int nc = (int)cols.size();
+    a.s = s;
+    a.h = h;
+    a.cap = (uint32_t)std::min<uint64_t>((uint64_t)(h - s) / 2 + 2, 0xFFFFFFF0ull);
+    ENS(mp_ncuts, nc * 4); ENS(mp_cutpos, (uint64_t)nc * a.cap * 8); ENS(mp_pbytes, (uint64_t)nc * a.cap * 8); ENS(mp_flag, 64);
+    a.ncuts = mp_ncuts.as<uint32_t>();
+    a.cuts = mp_cutpos.as<int64_t>();
+    a.pbytes = mp_pbytes.as<uint64_t>();
+    a.overflow = mp_flag.as<int32_t>();
+    a.out = mp_flag.as<int64_t>() + 1;
+    CK(hipMemsetAsync(mp_flag.p, 0, 64, stream));
+    launch_page_cuts(a, stream);
+    CK(hipGetLastError());
+    std::vector<uint32_t> nct(nc);
+    int32_t ovf = 0;
+    CK(hipMemcpyAsync(nct.data(), mp_ncuts.p, nc * 4, hipMemcpyDeviceToHost, stream));
+    CK(hipMemcpyAsync(&ovf, mp_flag.p, 4, hipMemcpyDeviceToHost, stream));
+    CK(hipStreamSynchronize(stream));
+    if (ovf) return fail(KPW_ERR_DEVICE, "page cut table overflow");
+    cuts.assign(nc, {});
+    for (int c = 0; c < nc; c++) {
+        cuts[c].resize(nct[c]);
+        if (nct[c]) CK(hipMemcpyAsync(cuts[c].data(), mp_cutpos.as<int64_t>() + (uint64_t)c * a.cap, nct[c] * 8ull,
+                                      hipMemcpyDeviceToHost, stream));
+    }
+    CK(hipStreamSynchronize(stream));
+    return KPW_OK;
+}
+
+// Encode the column chunks [s, e) split at `cuts` (page ends <= e).  Result pages are in
+// pages_dev_ (PageOut offsets), grouped per column: optional dictionary page, data pages.
+int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s,
+                        int64_t e, const std::vector<std::vector<int64_t>> &cuts, MpRun &run)
+{
+    hipStream_t st = stream;
+    const int nc = (int)cols.size();
+    run.cols.assign(nc, {});
+    std::vector<ChunkDesc> dch(nc), pg;
+    std::vector<RleJob> ej;
+    uint64_t ht_off = 0, ids_off = 0;
+    std::vector<uint32_t> dtj, dfirst(nc), dcount(nc), ptj, pfirst, pcount;
+    for (int c = 0; c < nc; c++) {
+        ChunkDesc &D = dch[c];
+        memset(&D, 0, sizeof(D));
+        const uint64_t len = (uint64_t)(e - s);
+        D.s = s; D.e = e; D.col = c; D.rg = 0;
+        D.is_dict = cols[c].dict ? 1 : 0;
+        D.smin = ~0ull; D.smax = 0;
+        D.ids_off = ids_off; D.ent_off = ids_off;
+        ids_off += len;
+        if (D.is_dict) {   // no 1 MiB early stop: pages before the fallback page keep their ids
+            D.ht_cap = (uint32_t)next_pow2_mp(std::max<uint64_t>(16, 2 * len));
+            D.ht_off = ht_off;
+            ht_off += D.ht_cap + 1;
+        }
+        D.dl_job = D.id_job = D.bool_job = D.dj0 = -1;
+        D.owner = -1;
+        D.first_page = (int32_t)pg.size();
+        const uint32_t nt = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
+        dfirst[c] = (uint32_t)dtj.size();
+        dcount[c] = nt;
+        dtj.insert(dtj.end(), nt, (uint32_t)c);
+        int64_t q = s;
+        for (size_t i = 0; i <= cuts[c].size(); i++) {
+            const int64_t pe = i < cuts[c].size() ? std::min<int64_t>(cuts[c][i], e) : e;
+            if (pe <= q) continue;
+            ChunkDesc P;
+            memset(&P, 0, sizeof(P));
+            P.s = q; P.e = pe; P.col = c; P.rg = 0;
+            P.is_dict = D.is_dict;
+            P.smin = ~0ull; P.smax = 0;
+            P.owner = c;
+            P.dl_job = P.id_job = P.bool_job = P.dj0 = -1;
+            if (cols[c].optional) {
+                RleJob J;
+                memset(&J, 0, sizeof(J));
+                J.src.kind = 0; J.src.ptr = hc[c].pres; J.src.base = (uint64_t)P.s;
+                J.len = (uint32_t)(pe - q); J.bw = 1;
+                P.dl_job = (int32_t)ej.size();
+                ej.push_back(J);
+            }
+            if (P.is_dict) {
+                RleJob J;
+                memset(&J, 0, sizeof(J));
+                J.src.kind = 1; J.src.ptr = nullptr; J.src.base = 0;   // ptr below, base on the device
+                J.len = (uint32_t)(pe - q); J.bw = 0;
+                P.id_job = (int32_t)ej.size();
+                ej.push_back(J);
+            }
+            const uint32_t pt = (uint32_t)std::max<uint64_t>(1, ((uint64_t)(pe - q) + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
+            pfirst.push_back((uint32_t)ptj.size());
+            pcount.push_back(pt);
+            ptj.insert(ptj.end(), pt, (uint32_t)pg.size());
+            pg.push_back(P);
+            q = pe;
+        }
+        D.npages = (int32_t)pg.size() - D.first_page;
+    }
+    const int npg = (int)pg.size();
+    const uint32_t npt = (uint32_t)ptj.size(), ndt = (uint32_t)dtj.size();
+    std::vector<uint32_t> dorder;
+    {
+        uint32_t maxnt = 0;
+        for (int c = 0; c < nc; c++) if (dch[c].is_dict) maxnt = std::max(maxnt, dcount[c]);
+        for (uint32_t k = 0; k < maxnt; k++)
+            for (int c = 0; c < nc; c++)
+                if (dch[c].is_dict && k < dcount[c]) dorder.push_back(dfirst[c] + k);
+    }
+    // page descriptors use the engine's chunk buffers; dictionary descriptors their own
+    ENS(d_chunks, npg * sizeof(ChunkDesc)); ENS(d_ctile_chunk, npt * 4); ENS(d_ctile_first, npg * 4); ENS(d_ctile_count, npg * 4);
+    ENS(d_tile_raw, npt * 8); ENS(d_tile_raw_off, npt * 8); ENS(d_tile_smin, npt * 8); ENS(d_tile_smax, npt * 8);
+    ENS(d_tile_cnt, npt * 4); ENS(d_tile_sz, npt * 8);
+    ENS(mp_dch, nc * sizeof(ChunkDesc)); ENS(mp_dtile_chunk, ndt * 4); ENS(mp_dtile_first, nc * 4); ENS(mp_dtile_count, nc * 4);
+    ENS(mp_dtile_raw, ndt * 8); ENS(mp_dtile_smin, ndt * 8); ENS(mp_dtile_smax, ndt * 8); ENS(mp_dtile_cnt, ndt * 4);
+    ENS(mp_dtile_sz, ndt * 8); ENS(d_dict_order, std::max<size_t>(1, dorder.size()) * 4);
+    ENS(d_ht_key, std::max<uint64_t>(1, ht_off) * 8); ENS(d_ht_min, std::max<uint64_t>(1, ht_off) * 4);
+    ENS(d_ht_id, std::max<uint64_t>(1, ht_off) * 4);
+    ENS(d_ids, std::max<uint64_t>(1, ids_off) * 4); ENS(d_ent_rec, std::max<uint64_t>(1, ids_off) * 8);
+    ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
+    ENS(d_page_off, 2 * npg * 8); ENS(d_page_len, 2 * npg * 8); ENS(d_page_pre, 2 * npg * 8); ENS(d_tot, 64); ENS(d_collision, 64);
+    for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
+    CK(hipMemcpyAsync(d_ctile_chunk.p, ptj.data(), npt * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(d_ctile_first.p, pfirst.data(), npg * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(d_ctile_count.p, pcount.data(), npg * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(mp_dtile_chunk.p, dtj.data(), ndt * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(mp_dtile_first.p, dfirst.data(), nc * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(mp_dtile_count.p, dcount.data(), nc * 4, hipMemcpyHostToDevice, st));
+    if (!dorder.empty()) CK(hipMemcpyAsync(d_dict_order.p, dorder.data(), dorder.size() * 4, hipMemcpyHostToDevice, st));
+
+    ChunkArgs ap{};
+    ap.ch = d_chunks.as<ChunkDesc>(); ap.nchunks = npg; ap.nctiles = npt; ap.cols = d_cols.as<DevCol>(); ap.data = d_data;
+    ap.ctile_chunk = d_ctile_chunk.as<uint32_t>(); ap.ctile_first = d_ctile_first.as<uint32_t>();
+    ap.ctile_count = d_ctile_count.as<uint32_t>(); ap.tile_raw = d_tile_raw.as<uint64_t>();
+    ap.tile_raw_off = d_tile_raw_off.as<uint64_t>(); ap.tile_smin = d_tile_smin.as<uint64_t>();
+    ap.tile_smax = d_tile_smax.as<uint64_t>(); ap.tile_cnt = d_tile_cnt.as<uint32_t>(); ap.tile_sz = d_tile_sz.as<uint64_t>();
+    ap.ht_key = d_ht_key.as<uint64_t>(); ap.ht_min = d_ht_min.as<uint32_t>(); ap.ht_id = d_ht_id.as<uint32_t>();
+    ap.ids = d_ids.as<uint32_t>(); ap.ent_rec = d_ent_rec.as<uint64_t>(); ap.ent_boff = d_ent_boff.as<uint64_t>();
+    ap.max_dict_bytes = (uint32_t)props.dictionary_page_size;
+    ap.data_end = d_off + n; ap.collision = d_collision.as<uint32_t>();
+    ap.page_pre = d_page_pre.as<uint64_t>();
+    ap.mp = 1;
+    ChunkArgs ad = ap;
+    ad.ch = mp_dch.as<ChunkDesc>(); ad.nchunks = nc; ad.nctiles = ndt;
+    ad.ctile_chunk = mp_dtile_chunk.as<uint32_t>(); ad.ctile_first = mp_dtile_first.as<uint32_t>();
+    ad.ctile_count = mp_dtile_count.as<uint32_t>(); ad.tile_raw = mp_dtile_raw.as<uint64_t>(); ad.tile_raw_off = nullptr;
+    ad.tile_smin = mp_dtile_smin.as<uint64_t>(); ad.tile_smax = mp_dtile_smax.as<uint64_t>();
+    ad.tile_cnt = mp_dtile_cnt.as<uint32_t>(); ad.tile_sz = mp_dtile_sz.as<uint64_t>();
+    ad.max_dict_bytes = 0xFFFFFFFFu;   // the dictPageSize limit is applied per page (k_mp_dict_decide)
+    ad.dict_order = d_dict_order.as<uint32_t>(); ad.ndict_tiles = (uint32_t)dorder.size();
+
+    uint32_t enpt = 0, enet = 0;
+    RleScratch esc{};
+    uint64_t body_tot = 0;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        ap.exact_strings = ad.exact_strings = attempt;
+        CK(hipMemcpyAsync(d_chunks.p, pg.data(), npg * sizeof(ChunkDesc), hipMemcpyHostToDevice, st));
+        CK(hipMemcpyAsync(mp_dch.p, dch.data(), nc * sizeof(ChunkDesc), hipMemcpyHostToDevice, st));
+        CK(hipMemsetAsync(d_collision.p, 0, 4, st));
+        if (ht_off) {
+            CK(hipMemsetAsync(d_ht_key.p, 0xFF, ht_off * 8, st));
+            CK(hipMemsetAsync(d_ht_min.p, 0xFF, ht_off * 4, st));
+        }
+        launch_chunk_stats(ap, st);                          // K6 per page (+ nn, raw bytes)
+        if (!ej.empty()) {
+            int rs = run_rle(ej, enpt, enet, esc);
+            if (rs) return rs;
+        }
+        launch_mp_pages_init(ap.ch, npg, ad.ch, ap.cols, d_jobs.as<RleJob>(), st);
+        launch_dict(ad, d_jobs.as<RleJob>(), st);            // K2 per column chunk
+        launch_page_str_stats(ap, st);
+        launch_mp_dict_decide(ap.ch, npg, ad.ch, ap.cols, ap.ent_rec, ap.ent_boff, (uint32_t)props.dictionary_page_size,
+                              d_jobs.as<RleJob>(), st);
+        CK(hipGetLastError());
+        if (!ej.empty()) launch_rle_structure(d_jobs.as<RleJob>(), (int)ej.size(), enpt, enet, esc, st);
+        launch_mp_satisfy(ap.ch, ad.ch, nc, ap.cols, ap.ent_rec, ap.ent_boff, d_jobs.as<RleJob>(), st);
+        launch_layout(ap, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), st);
+        CK(hipGetLastError());
+        uint32_t coll = 0;
+        CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, st));
+        CK(hipMemcpyAsync(&coll, d_collision.p, 4, hipMemcpyDeviceToHost, st));
+        CK(hipMemcpyAsync(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+        if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+        for (int c = 0; c < nc; c++)
+            if (dch[c].is_dict && dch[c].overflow) return fail(KPW_ERR_DEVICE, "multi-page dictionary table overflow");
+        if (!coll) break;
+        if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
+        for (int c = 0; c < nc; c++) {   // restore the host descriptors for the exact re-run
+            dch[c].nn = 0; dch[c].dict_bytes = 0; dch[c].dict_n = 0; dch[c].fallback = 0; dch[c].overflow = 0;
+        }
+    }
+    ENS(d_body, body_tot + 512);
+    CK(hipMemsetAsync(d_body.p, 0, body_tot + 512, st));
+    launch_mp_dictpage_off(ap.ch, ad.ch, nc, st);
+    launch_dict_page(ad, d_body.as<uint8_t>(), st);
+    launch_chunk_write(ap, d_jobs.as<RleJob>(), d_body.as<uint8_t>(), st);
+    if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), st);
+    CK(hipGetLastError());
+    std::vector<uint64_t> poff(2 * npg), plen(2 * npg), pcoff(2 * npg), pclen(2 * npg);
+    CK(hipMemcpyAsync(poff.data(), d_page_off.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(plen.data(), d_page_len.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    // ---------------------------------------------------------------- K7
+    if (props.codec == KPW_SNAPPY) {
+        std::vector<uint32_t> fpage, fidx, pfrag0(2 * npg);
+        for (int p = 0; p < 2 * npg; p++) {
+            pfrag0[p] = (uint32_t)fpage.size();
+            const uint64_t nf = (plen[p] + SNAPPY_FRAG - 1) / SNAPPY_FRAG;
+            for (uint64_t k = 0; k < nf; k++) { fpage.push_back((uint32_t)p); fidx.push_back((uint32_t)k); }
+        }
+        const uint32_t nf = (uint32_t)fpage.size();
+        ENS(d_frag_page, std::max<uint32_t>(1, nf) * 4); ENS(d_frag_idx, std::max<uint32_t>(1, nf) * 4);
+        ENS(d_frag_out, (uint64_t)std::max<uint32_t>(1, nf) * SNAPPY_FRAG_CAP); ENS(d_frag_len, std::max<uint32_t>(1, nf) * 4);
+        ENS(d_frag_coff, std::max<uint32_t>(1, nf) * 8); ENS(d_page_coff, 2 * npg * 8); ENS(d_page_clen, 2 * npg * 8);
+        ENS(d_page_frag0, 2 * npg * 4);
+        ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * npg * 8 + 64);
+        if (nf) {
+            CK(hipMemcpyAsync(d_frag_page.p, fpage.data(), nf * 4, hipMemcpyHostToDevice, st));
+            CK(hipMemcpyAsync(d_frag_idx.p, fidx.data(), nf * 4, hipMemcpyHostToDevice, st));
+        }
+        CK(hipMemcpyAsync(d_page_frag0.p, pfrag0.data(), 2 * npg * 4, hipMemcpyHostToDevice, st));
+        SnappyArgs sa{};
+        sa.in = d_body.as<uint8_t>(); sa.page_off = d_page_off.as<uint64_t>(); sa.page_len = d_page_len.as<uint64_t>();
+        sa.npages = 2 * npg; sa.nfrags = nf; sa.frag_page = d_frag_page.as<uint32_t>(); sa.frag_idx = d_frag_idx.as<uint32_t>();
+        sa.frag_out = d_frag_out.as<uint8_t>(); sa.frag_len = d_frag_len.as<uint32_t>();
+        sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
+        sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
+        sa.page_pre = nullptr;
+        launch_snappy(sa, st);
+        launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), st);
+        CK(hipGetLastError());
+        uint64_t ctot = 0;
+        CK(hipMemcpyAsync(pcoff.data(), d_page_coff.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
+        CK(hipMemcpyAsync(pclen.data(), d_page_clen.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
+        CK(hipMemcpyAsync(&ctot, d_tot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+        pages_dev_ = d_comp.as<uint8_t>();
+        pages_len_ = ctot;
+    } else {
+        pcoff = poff;
+        pclen = plen;
+        pages_dev_ = d_body.as<uint8_t>();
+        pages_len_ = body_tot;
+    }
+    if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+    // ---------------------------------------------------------------- page metadata
+    CK(hipMemcpyAsync(pg.data(), d_chunks.p, npg * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> smeta(4 * npg, 0);
+    ENS(d_smeta, 4 * npg * 8);
+    launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(), nullptr, st);
+    CK(hipMemcpyAsync(smeta.data(), d_smeta.p, 4 * npg * 8, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    std::vector<std::string> bmin(npg), bmax(npg);
+    {
+        uint64_t blob_len = 0;
+        std::vector<uint64_t> boff(npg);
+        for (int p = 0; p < npg; p++) {
+            boff[p] = blob_len;
+            if (cols[pg[p].col].phys == KPW_BYTE_ARRAY && pg[p].has_minmax) blob_len += smeta[4 * p + 1] + smeta[4 * p + 3];
+        }
+        if (blob_len) {
+            std::vector<uint8_t> blob(blob_len);
+            ENS(d_sblob, blob_len);
+            launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(),
+                                d_sblob.as<uint8_t>(), st);
+            CK(hipMemcpyAsync(blob.data(), d_sblob.p, blob_len, hipMemcpyDeviceToHost, st));
+            CK(hipStreamSynchronize(st));
+            for (int p = 0; p < npg; p++) {
+                if (cols[pg[p].col].phys != KPW_BYTE_ARRAY || !pg[p].has_minmax) continue;
+                const uint64_t l1 = smeta[4 * p + 1], l2 = smeta[4 * p + 3];
+                bmin[p].assign((const char *)blob.data() + boff[p], l1);
+                bmax[p].assign((const char *)blob.data() + boff[p] + l1, l2);
+            }
+        }
+    }
+    for (int p = 0; p < npg; p++) {
+        const ChunkDesc &C = pg[p];
+        const ColInfo &col = cols[C.col];
+        std::vector<PageOut> &out = run.cols[C.col];
+        if (C.dictpage_len) {   // ColumnChunkPageWriter: the dictionary page first
+            PageOut d;
+            d.page_type = KPW_DICTIONARY_PAGE;
+            d.num_values = (int32_t)dch[C.col].dict_n;
+            d.encoding = KPW_ENC_PLAIN_DICTIONARY;
+            d.dl_encoding = d.rl_encoding = 0;
+            d.has_stats = 0;
+            d.uncompressed_size = (int64_t)plen[2 * p];
+            d.compressed_size = (int64_t)pclen[2 * p];
+            d.offset = pcoff[2 * p];
+            d.null_count = 0;
+            d.has_min_max = 0;
+            out.push_back(d);
+        }
+        PageOut q;
+        q.page_type = KPW_DATA_PAGE;
+        q.num_values = (int32_t)(C.e - C.s);
+        q.encoding = (C.is_dict && !C.fallback) ? KPW_ENC_PLAIN_DICTIONARY : KPW_ENC_PLAIN;
+        q.dl_encoding = col.optional ? KPW_ENC_RLE : KPW_ENC_BIT_PACKED;
+        q.rl_encoding = KPW_ENC_BIT_PACKED;
+        q.has_stats = 1;
+        q.uncompressed_size = (int64_t)plen[2 * p + 1];
+        q.compressed_size = (int64_t)pclen[2 * p + 1];
+        q.offset = pcoff[2 * p + 1];
+        q.num_rows = (int32_t)(C.e - C.s);
+        q.null_count = (int64_t)C.null_count;
+        q.has_min_max = C.has_minmax ? 1 : 0;
+        if (C.has_minmax) {
+            if (col.phys == KPW_BYTE_ARRAY) {
+                q.min = bmin[p];
+                q.max = bmax[p];
+            } else {
+                auto unkey = [&](uint64_t k) -> uint64_t {
+                    switch (col.phys) {
+                    case KPW_INT32: return (uint32_t)k ^ 0x80000000u;
+                    case KPW_INT64: return k ^ 0x8000000000000000ull;
+                    case KPW_FLOAT: { uint32_t b = (uint32_t)k; return (b >> 31) ? (b & 0x7fffffffu) : (uint32_t)~b; }
+                    case KPW_DOUBLE: return (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+                    default: return k;
+                    }
+                };
+                auto le = [&](uint64_t v) {
+                    std::string s2;
+                    const int nb = col.phys == KPW_BOOLEAN ? 1 : col.vsize;
+                    for (int i = 0; i < nb; i++) s2.push_back((char)(uint8_t)(v >> (8 * i)));
+                    return s2;
+                };
+                q.min = le(unkey(C.smin));
+                q.max = le(unkey(C.smax));
+            }
+        }
+        out.push_back(q);
+    }
+    return KPW_OK;
+}
+
+int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
+                      const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out)
+{
+    hipStream_t st = stream;
+    const int nc = (int)cols.size();
+    // per BYTE_ARRAY column: exclusive prefix of (4 + len) over present values
+    std::vector<const uint64_t *> sp(nc, nullptr);
+    std::vector<int32_t> cstream(nc, -1);
+    mp_sp.resize(nc);
+    for (size_t k = 0; k < opt_idx_.size(); k++) cstream[opt_idx_[k]] = (int32_t)k;
+    for (int c = 0; c < nc; c++) {
+        if (cols[c].phys != KPW_BYTE_ARRAY) continue;
+        ENS(mp_sp[c], (ne + 1) * 8); ENS(mp_ssz, ne * 4 + 4);
+        launch_str_sizes(d_cols.as<DevCol>(), c, ne, mp_ssz.as<uint32_t>(), st);
+        launch_prefix_raw(mp_ssz.as<uint32_t>(), ne, mp_sp[c].as<uint64_t>(), d_scan_tmp.as<uint64_t>(), st);
+        sp[c] = mp_sp[c].as<uint64_t>();
+    }
+    ENS(mp_spp, nc * sizeof(uint64_t *)); ENS(mp_cstream, nc * 4);
+    CK(hipMemcpyAsync(mp_spp.p, sp.data(), nc * sizeof(uint64_t *), hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(mp_cstream.p, cstream.data(), nc * 4, hipMemcpyHostToDevice, st));
+    uint64_t Ptot = 0;
+    CK(hipMemcpyAsync(&Ptot, d_P.as<uint64_t>() + ne, 8, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+
+    PageCutArgs a{};
+    a.n = ne; a.ncols = nc; a.page_size = props.page_size; a.cols = d_cols.as<DevCol>();
+    a.col_stream = mp_cstream.as<int32_t>(); a.E = d_E.as<uint32_t>(); a.gend = d_gend.as<uint64_t>();
+    a.gend_stride = gend_stride;
+    a.sp = mp_spp.as<const uint64_t *>(); a.next_rg_size = T;
+    if (opt_idx_.empty()) { a.E = nullptr; a.gend = nullptr; }
+
+    uint64_t acc_len = 0;
+    const uint64_t per_rec = std::max<uint64_t>(1, Ptot / ne);
+    int64_t guess = std::max<int64_t>(1000, (int64_t)(2 * (uint64_t)T / per_rec));
+    int64_t s0 = 0;
+    std::vector<std::vector<int64_t>> cuts;
+    MpRun run;
+    auto append = [&](int64_t s, int64_t e) -> int {
+        if (grow_keep(mp_acc, acc_len + pages_len_ + 64, acc_len)) return KPW_ERR_NOMEM;
+        if (pages_len_) CK(hipMemcpyAsync(mp_acc.as<uint8_t>() + acc_len, pages_dev_, pages_len_, hipMemcpyDeviceToDevice, st));
+        out.rgs.push_back(RowGroupOut{s, e - s, (int32_t)out.chunks.size()});
+        for (int c = 0; c < nc; c++) {
+            ChunkOut co;
+            co.column = c;
+            co.first_page = (int32_t)out.pages.size();
+            co.num_values = e - s;
+            co.has_dictionary = 0;
+            for (PageOut p : run.cols[c]) {
+                if (p.page_type == KPW_DICTIONARY_PAGE) co.has_dictionary = 1;
+                p.offset += acc_len;
+                out.pages.push_back(p);
+            }
+            co.num_pages = (int32_t)out.pages.size() - co.first_page;
+            out.chunks.push_back(co);
+        }
+        acc_len += pages_len_;
+        return KPW_OK;
+    };
+    while (s0 < (int64_t)ne) {
+        int64_t h = std::min<int64_t>((int64_t)ne, s0 + guess);
+        int64_t po[2] = {-1, 0};
+        for (;;) {
+            int rs = mp_cuts(a, s0, h, cuts);
+            if (rs) return rs;
+            rs = mp_pipeline(d_data, d_off, n, hc, s0, h, cuts, run);
+            if (rs) return rs;
+            // header + compressed bytes of every cut page (the open page per column is last)
+            std::vector<uint64_t> pb((size_t)nc * a.cap, 0);
+            for (int c = 0; c < nc; c++) {
+                size_t i = 0;
+                for (const PageOut &p : run.cols[c]) {
+                    if (p.page_type == KPW_DICTIONARY_PAGE) continue;
+                    if (i < cuts[c].size()) pb[(size_t)c * a.cap + i] = page_header(p, cols[c].phys).size() + (uint64_t)p.compressed_size;
+                    i++;
+                }
+            }
+            CK(hipMemcpyAsync(mp_pbytes.p, pb.data(), pb.size() * 8, hipMemcpyHostToDevice, st));
+            a.s = s0; a.h = h;
+            launch_plan_mp(a, st);
+            CK(hipGetLastError());
+            CK(hipMemcpyAsync(po, a.out, 16, hipMemcpyDeviceToHost, st));
+            CK(hipStreamSynchronize(st));
+            if (po[0] >= 0 || h == (int64_t)ne) break;
+            h = std::min<int64_t>((int64_t)ne, s0 + 2 * (h - s0));
+        }
+        if (po[0] >= 0) {
+            const int64_t r = po[0];
+            for (auto &v : cuts) v.erase(std::remove_if(v.begin(), v.end(), [r](int64_t x) { return x > r; }), v.end());
+            int rs = mp_pipeline(d_data, d_off, n, hc, s0, r, cuts, run);
+            if (rs) return rs;
+            rs = append(s0, r);
+            if (rs) return rs;
+            guess = std::max<int64_t>(1000, (r - s0) + (r - s0) / 4 + 200);
+            s0 = r;
+            continue;
+        }
+        if (final_flush) {   // [s0, ne) was just encoded with its final pages
+            int rs = append(s0, (int64_t)ne);
+            if (rs) return rs;
+            s0 = (int64_t)ne;
+        } else {
+            out.open_buffered = po[1];
+        }
+        break;
+    }
+    CK(hipStreamSynchronize(st));
+    out.records_consumed = s0;
+    out.open_records = (int64_t)ne - s0;
+    if (final_flush) out.open_buffered = 0;
+    out.d_pages = mp_acc.as<uint8_t>();
+    out.pages_len = acc_len;
+    pages_dev_ = mp_acc.as<uint8_t>();
+    pages_len_ = acc_len;
+    CK(hipEventRecord(ev_[7], st));
+    CK(hipEventSynchronize(ev_[7]));
+    for (int i = 0; i < 10; i++) stage_ms[i] = 0;
+    CK(hipEventElapsedTime(&stage_ms[7], ev_[0], ev_[7]));
+    return KPW_OK;
+}
+
+}  // namespace kpw

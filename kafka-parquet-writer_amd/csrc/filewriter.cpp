@@ -135,6 +135,50 @@ const char *pt_name(int pt)
 
 }  // namespace
 
+std::string page_header(const PageOut &pg, int phys)
+{
+    std::string hdr;
+    TCompact t(hdr);
+    t.i32(1, pg.page_type);
+    t.i32(2, (int32_t)pg.uncompressed_size);
+    t.i32(3, (int32_t)pg.compressed_size);
+    if (pg.page_type == KPW_DICTIONARY_PAGE) {
+        t.begin(7);
+        t.i32(1, pg.num_values);
+        t.i32(2, pg.encoding);
+        t.end();
+    } else {
+        StatsOut st;
+        st.phys = phys;
+        st.has = pg.has_min_max != 0;
+        st.nulls = pg.null_count;
+        st.min = pg.min;
+        st.max = pg.max;
+        if (pg.page_type == KPW_DATA_PAGE_V2) {
+            // ParquetMetadataConverter.writeDataPageV2Header (is_compressed never set)
+            t.begin(8);
+            t.i32(1, pg.num_values);
+            t.i32(2, (int32_t)pg.null_count);
+            t.i32(3, pg.num_rows);
+            t.i32(4, pg.encoding);
+            t.i32(5, pg.dl_byte_length);
+            t.i32(6, 0);
+            if (!stats_empty(st)) write_stats(t, 8, st);
+            t.end();
+        } else {
+            t.begin(5);
+            t.i32(1, pg.num_values);
+            t.i32(2, pg.encoding);
+            t.i32(3, pg.dl_encoding);
+            t.i32(4, pg.rl_encoding);
+            if (!stats_empty(st)) write_stats(t, 5, st);
+            t.end();
+        }
+    }
+    t.stop();
+    return hdr;
+}
+
 FileWriter::FileWriter(const std::vector<ColInfo> &cols, const std::string &message_name, const std::string &proto_class,
                        const kpw_props &props)
     : cols_(cols), message_name_(message_name), proto_class_(proto_class), props_(props) {}
@@ -184,16 +228,8 @@ int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages,
         bool first_data = true;
         for (int p = co.first_page; p < co.first_page + co.num_pages; p++) {
             const PageOut &pg = b.pages[p];
-            std::string hdr;
-            TCompact t(hdr);
-            t.i32(1, pg.page_type);
-            t.i32(2, (int32_t)pg.uncompressed_size);
-            t.i32(3, (int32_t)pg.compressed_size);
+            const std::string hdr = page_header(pg, m.phys);
             if (pg.page_type == KPW_DICTIONARY_PAGE) {
-                t.begin(7);
-                t.i32(1, pg.num_values);
-                t.i32(2, pg.encoding);
-                t.end();
                 add_count(m.dict_stats, pg.encoding);
                 add_unique(m.encodings, pg.encoding);
             } else {
@@ -203,31 +239,10 @@ int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages,
                 st.nulls = pg.null_count;
                 st.min = pg.min;
                 st.max = pg.max;
-                if (pg.page_type == KPW_DATA_PAGE_V2) {
-                    // ParquetMetadataConverter.writeDataPageV2Header (is_compressed never set)
-                    t.begin(8);
-                    t.i32(1, pg.num_values);
-                    t.i32(2, (int32_t)pg.null_count);
-                    t.i32(3, pg.num_rows);
-                    t.i32(4, pg.encoding);
-                    t.i32(5, pg.dl_byte_length);
-                    t.i32(6, 0);
-                    if (!stats_empty(st)) write_stats(t, 8, st);
-                    t.end();
-                    m.v2 = true;
-                } else {
-                    t.begin(5);
-                    t.i32(1, pg.num_values);
-                    t.i32(2, pg.encoding);
-                    t.i32(3, pg.dl_encoding);
-                    t.i32(4, pg.rl_encoding);
-                    if (!stats_empty(st)) write_stats(t, 5, st);
-                    t.end();
-                }
+                if (pg.page_type == KPW_DATA_PAGE_V2) m.v2 = true;
                 if (first_data) { m.stats = st; first_data = false; } else merge_stats(m.stats, st);
                 add_count(m.data_stats, pg.encoding);
             }
-            t.stop();
             uncomp += pg.uncompressed_size + (int64_t)hdr.size();
             comp += pg.compressed_size + (int64_t)hdr.size();
             int st2 = put(hdr.data(), hdr.size());

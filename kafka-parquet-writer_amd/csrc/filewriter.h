@@ -34,6 +34,10 @@ struct RowGroupMeta {
     std::vector<ChunkMeta> chunks;
 };
 
+// Thrift-compact PageHeader of one page exactly as write_row_group emits it
+// (ParquetMetadataConverter.writeDataPageHeader / writeDataPageV2Header / dictionary page).
+std::string page_header(const PageOut &pg, int phys);
+
 class FileWriter {
 public:
     FileWriter(const std::vector<ColInfo> &cols, const std::string &message_name, const std::string &proto_class,

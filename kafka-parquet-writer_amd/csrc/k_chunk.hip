@@ -177,7 +177,7 @@ __global__ void k_chunk_stats_final(ChunkDesc *ch, int nchunks)
 __global__ void __launch_bounds__(KPW_BLOCK) k_str_minmax(const ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
                                                           const uint32_t *ctile_chunk, const uint32_t *ctile_first,
                                                           const uint64_t *ent_rec, uint64_t *tile_smin, uint64_t *tile_smax,
-                                                          const uint64_t *data_end_p)
+                                                          const uint64_t *data_end_p, int mp)
 {
     __shared__ uint64_t li[KPW_BLOCK], la[KPW_BLOCK];
     const uint32_t t = blockIdx.x;
@@ -186,7 +186,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_str_minmax(const ChunkDesc *ch, c
     const DevCol &col = cols[C.col];
     if (col.phys != 6) return;
     const uint64_t data_end = *data_end_p;
-    const bool ents = C.is_dict && !C.fallback;
+    // a page of a multi-page chunk is only part of what its dictionary covers: use its values
+    const bool ents = !mp && C.is_dict && !C.fallback;
     const uint64_t q0 = (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x;   // coalesced (equal strings tie harmlessly)
     uint64_t a = ~0ull, b = ~0ull;
     for (int k = 0; k < 8; k++) {
@@ -529,6 +530,7 @@ __global__ void k_dict_jobs(ChunkDesc *ch, int nchunks, RleJob *jobs, uint32_t m
     ChunkDesc &C = ch[ci];
     if (!C.is_dict) return;
     if (C.dict_bytes > max_dict_bytes || C.overflow) C.fallback = 1;
+    if (C.id_job < 0) return;   // multi-page dictionary descriptor: pages carry the id jobs
     RleJob &J = jobs[C.id_job];
     if (C.fallback) { J.len = 0; J.bw = 0; return; }
     // DictionaryValuesWriter.getBytes: bitWidth = getWidthFromMaxInt(dictSize - 1)
@@ -548,7 +550,7 @@ __global__ void k_dict_jobs(ChunkDesc *ch, int nchunks, RleJob *jobs, uint32_t m
 //      PLAIN (FLOAT/DOUBLE fallback) or 4-byte length + RLE (BOOLEAN)
 __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks, const DevCol *cols, RleJob *jobs, uint64_t *page_off,
                                                       uint64_t *page_len, uint64_t *tot, int v2, DeltaJob *djobs,
-                                                      const uint64_t *chunk_sfx, uint64_t *page_pre)
+                                                      const uint64_t *chunk_sfx, uint64_t *page_pre, int mp)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
     uint64_t carry = 0;
@@ -563,7 +565,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
             if (C.is_dict && !C.fallback) {
                 val = 1 + jobs[C.id_job].total_bytes;
                 // FallbackValuesWriter.getBytes on the first page: isCompressionSatisfying
-                if (!(val + C.dict_bytes < C.raw_bytes)) C.fallback = 1;
+                // (multi-page: decided per chunk by k_mp_satisfy, dictionary page preset)
+                if (mp) dictp = C.dictpage_len;
+                else if (!(val + C.dict_bytes < C.raw_bytes)) C.fallback = 1;
                 else dictp = C.dict_bytes;
             }
             if (!C.is_dict || C.fallback) {
@@ -571,7 +575,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
                 else if (v2 && C.dj0 >= 0 && col.phys == 6) val = djobs[C.dj0].total + djobs[C.dj0 + 1].total + chunk_sfx[ci];
                 else if (v2 && C.dj0 >= 0) val = djobs[C.dj0].total;
                 else val = col.phys == 0 ? (uint64_t)(C.nn + 7) / 8 : C.raw_bytes;
-                dictp = 0;
+                dictp = mp ? C.dictpage_len : 0;
                 if (C.is_dict) {  // do not write ids
                     RleJob &J = jobs[C.id_job];
                     J.n_rle = 0; J.total_groups = 0; J.final_gap_groups = 0; J.total_bytes = 0;
@@ -805,9 +809,19 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
                        a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1);
     hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht_id, a.ids,
                        a.data, a.ent_rec, a.data_end, a.collision);
-    // BYTE_ARRAY statistics need the dictionary outcome (entries stand in for the values)
+    // BYTE_ARRAY statistics need the dictionary outcome (entries stand in for the values);
+    // multi-page dictionary descriptors have no statistics (their pages do)
+    if (a.mp) return;
     hipLaunchKernelGGL(k_str_minmax, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
-                       a.ent_rec, a.tile_smin, a.tile_smax, a.data_end);
+                       a.ent_rec, a.tile_smin, a.tile_smax, a.data_end, 0);
+    hipLaunchKernelGGL(k_str_final, dim3(a.nchunks), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_first, a.ctile_count,
+                       a.tile_smin, a.tile_smax, a.data_end);
+}
+
+void launch_page_str_stats(const ChunkArgs &a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_str_minmax, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
+                       a.ent_rec, a.tile_smin, a.tile_smax, a.data_end, 1);
     hipLaunchKernelGGL(k_str_final, dim3(a.nchunks), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_first, a.ctile_count,
                        a.tile_smin, a.tile_smax, a.data_end);
 }
@@ -815,18 +829,147 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
 void launch_layout(const ChunkArgs &a, RleJob *jobs, uint64_t *page_off, uint64_t *page_len, uint64_t *tot, hipStream_t s)
 {
     hipLaunchKernelGGL(k_layout, dim3(1), dim3(KPW_BLOCK), 0, s, a.ch, a.nchunks, a.cols, jobs, page_off, page_len, tot, a.v2,
-                       a.djobs_w, a.chunk_sfx, a.page_pre);
+                       a.djobs_w, a.chunk_sfx, a.page_pre, a.mp);
 }
 
 void launch_chunk_write(const ChunkArgs &a, const RleJob *jobs, uint8_t *out, hipStream_t s)
 {
     hipLaunchKernelGGL(k_chunk_headers, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, a.cols, out, a.v2, jobs);
-    hipLaunchKernelGGL(k_dict_page, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
-                       a.ent_rec, a.ent_boff, out);
+    if (!a.mp)   // multi-page: the dictionary page is written from the dictionary descriptors
+        hipLaunchKernelGGL(k_dict_page, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
+                           a.ent_rec, a.ent_boff, out);
     seg_tile_scan_u64(a.tile_raw, a.tile_raw_off, a.ctile_chunk, a.nctiles, s);
     hipLaunchKernelGGL(k_plain, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
                        a.tile_raw_off, out);
     hipLaunchKernelGGL(k_plain_bool, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, out);
+}
+
+// ------------------------------------------------------------------ multi-page (v1) dictionary decisions
+//
+// A column chunk's dictionary (first-occurrence ids over the whole chunk) is built on its
+// dictionary descriptor with no size limit; the pages then take parquet-mr's decisions:
+//  * FallbackValuesWriter.checkFallback: the first entry whose dictionaryByteSize pushes the
+//    total past dictPageSize lands in page F; pages before F keep ids, F and later are PLAIN
+//    (fallBackAllValuesTo rewrites F's values);
+//  * DictionaryValuesWriter.getBytes: bit width of page p = width(entries seen by p's end - 1);
+//  * isCompressionSatisfying on the first page only (all pages PLAIN when it fails);
+//  * toDictPageAndClose: entries [0, lastUsedDictionarySize) of the last dictionary page.
+__global__ void k_mp_pages_init(ChunkDesc *pg, int npg, const ChunkDesc *dch, const DevCol *cols, RleJob *jobs)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npg) return;
+    ChunkDesc &C = pg[p];
+    const ChunkDesc &D = dch[C.owner];
+    const DevCol &col = cols[C.col];
+    const uint64_t r0 = col.optional ? pres_rank(col, (uint64_t)D.s) : (uint64_t)D.s;
+    const uint64_t rp = col.optional ? pres_rank(col, (uint64_t)C.s) : (uint64_t)C.s;
+    C.ids_off = D.ids_off + (rp - r0);
+    C.ent_off = D.ent_off;
+    if (C.id_job >= 0) jobs[C.id_job].src.base = C.ids_off;
+}
+
+// bytes of the first k entries (dictionaryByteSize after k insertions)
+__device__ __forceinline__ uint64_t ent_cum(const DevCol &col, const ChunkDesc &D, const uint64_t *ent_rec, const uint64_t *ent_boff,
+                                            uint32_t k)
+{
+    if (!k) return 0;
+    const uint64_t r = ent_rec[D.ent_off + k - 1];
+    return ent_boff[D.ent_off + k - 1] + (col.phys == 6 ? 4u + col.slen[r] : (uint32_t)col.vsize);
+}
+
+__global__ void k_mp_dict_decide(ChunkDesc *pg, int npg, const ChunkDesc *dch, const DevCol *cols, const uint64_t *ent_rec,
+                                 const uint64_t *ent_boff, uint32_t max_dict_bytes, RleJob *jobs)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npg) return;
+    ChunkDesc &C = pg[p];
+    if (!C.is_dict) return;
+    const ChunkDesc &D = dch[C.owner];
+    const DevCol &col = cols[C.col];
+    const uint32_t dn = D.dict_n;
+    // fallback record: smallest k with cum(k) > max -> entry k-1 first occurs at ent_rec[k-1]
+    int64_t xf = -1;
+    if (ent_cum(col, D, ent_rec, ent_boff, dn) > max_dict_bytes) {
+        uint32_t lo = 1, hi = dn;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (ent_cum(col, D, ent_rec, ent_boff, mid) > max_dict_bytes) hi = mid; else lo = mid + 1;
+        }
+        xf = (int64_t)ent_rec[D.ent_off + lo - 1];
+    }
+    // entries first seen before the page end (ent_rec increases with the id)
+    uint32_t lo = 0, hi = dn;
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if ((int64_t)ent_rec[D.ent_off + mid] < C.e) lo = mid + 1; else hi = mid;
+    }
+    C.dict_n = lo;
+    C.dict_bytes = ent_cum(col, D, ent_rec, ent_boff, lo);
+    C.fallback = (xf >= 0 && xf < C.e) ? 1u : 0u;
+    const uint32_t m = lo - 1;
+    C.bw = lo ? (m ? 32 - __clz(m) : 0) : 32;
+    RleJob &J = jobs[C.id_job];
+    J.len = C.fallback ? 0 : C.nn;
+    J.bw = C.fallback ? 0 : C.bw;
+}
+
+// per chunk, after the RLE structure of the pages' id streams
+__global__ void k_mp_satisfy(ChunkDesc *pg, ChunkDesc *dch, int ndch, const DevCol *cols, const uint64_t *ent_rec,
+                             const uint64_t *ent_boff, const RleJob *jobs)
+{
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= ndch) return;
+    ChunkDesc &D = dch[d];
+    if (!D.is_dict) return;
+    const DevCol &col = cols[D.col];
+    ChunkDesc &P0 = pg[D.first_page];
+    if (!P0.fallback) {
+        const uint64_t val = 1 + jobs[P0.id_job].total_bytes;
+        if (!(val + P0.dict_bytes < P0.raw_bytes))
+            for (int p = D.first_page; p < D.first_page + D.npages; p++) pg[p].fallback = 1;
+    }
+    int last = -1;
+    for (int p = D.first_page; p < D.first_page + D.npages; p++) if (!pg[p].fallback) last = p;
+    if (last >= 0 && pg[last].dict_n > 0) {
+        D.dict_n = pg[last].dict_n;
+        D.fallback = 0;
+        P0.dictpage_len = ent_cum(col, D, ent_rec, ent_boff, D.dict_n);
+    } else {
+        D.fallback = 1;
+        P0.dictpage_len = 0;
+    }
+}
+
+__global__ void k_mp_dictpage_off(const ChunkDesc *pg, ChunkDesc *dch, int ndch)
+{
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= ndch) return;
+    dch[d].body_off = pg[dch[d].first_page].body_off;
+}
+
+void launch_mp_pages_init(ChunkDesc *pg, int npg, const ChunkDesc *dch, const DevCol *cols, RleJob *jobs, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mp_pages_init, dim3((npg + 255) / 256), dim3(256), 0, s, pg, npg, dch, cols, jobs);
+}
+void launch_dict_page(const ChunkArgs &a, uint8_t *out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_dict_page, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
+                       a.ent_rec, a.ent_boff, out);
+}
+void launch_mp_dict_decide(ChunkDesc *pg, int npg, const ChunkDesc *dch, const DevCol *cols, const uint64_t *ent_rec,
+                           const uint64_t *ent_boff, uint32_t max_dict_bytes, RleJob *jobs, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mp_dict_decide, dim3((npg + 255) / 256), dim3(256), 0, s, pg, npg, dch, cols, ent_rec, ent_boff,
+                       max_dict_bytes, jobs);
+}
+void launch_mp_satisfy(ChunkDesc *pg, ChunkDesc *dch, int ndch, const DevCol *cols, const uint64_t *ent_rec,
+                       const uint64_t *ent_boff, const RleJob *jobs, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mp_satisfy, dim3((ndch + 255) / 256), dim3(256), 0, s, pg, dch, ndch, cols, ent_rec, ent_boff, jobs);
+}
+void launch_mp_dictpage_off(const ChunkDesc *pg, ChunkDesc *dch, int ndch, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mp_dictpage_off, dim3((ndch + 255) / 256), dim3(256), 0, s, pg, dch, ndch);
 }
 
 }  // namespace kpw

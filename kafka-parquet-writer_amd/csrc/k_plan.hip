@@ -263,4 +263,145 @@ void launch_plan(const PlanArgs &a, hipStream_t s)
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, a);
 }
 
+// ------------------------------------------------------------------ multi-page (v1)
+
+// (4 + len) of present BYTE_ARRAY values, 0 for nulls (input of the per-column size prefix)
+__global__ void __launch_bounds__(256) k_str_sizes(const DevCol *cols, int c, uint64_t n, uint32_t *sz)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    const DevCol &col = cols[c];
+    const bool pres = !col.optional || ((col.pres[r >> 6] >> (r & 63)) & 1ull);
+    sz[r] = pres ? 4u + col.slen[r] : 0u;
+}
+
+// rl(0) + dl + data buffered sizes of column c over the page [q, r):
+// dl = RunLengthBitPackingHybridEncoder bytes emitted since q (walker), data =
+// FallbackValuesWriter.rawDataByteSize / PlainValuesWriter size / boolean bit count.
+__device__ __forceinline__ uint64_t col_data_bytes(const PageCutArgs &a, int c, int64_t q, int64_t r)
+{
+    const DevCol &col = a.cols[c];
+    const uint64_t cnt = col.optional ? pc_at(col, (uint64_t)r) - pc_at(col, (uint64_t)q) : (uint64_t)(r - q);
+    if (col.phys == 0) return (cnt + 7) / 8;
+    if (col.phys == 6) return a.sp[c][r] - a.sp[c][q];
+    return cnt * (uint64_t)col.vsize;
+}
+__device__ __forceinline__ void walker_init(Walker &w, int64_t p)
+{
+    w.p = p; w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
+    w.pend_bytes = 0; w.pend_rle = 0; w.grp = 0; w.state = 0;
+}
+__device__ __forceinline__ uint64_t col_dl_bytes(const PageCutArgs &a, int c, Walker &w, int64_t r)
+{
+    const int k = a.col_stream[c];
+    if (k < 0) return 0;
+    const DevCol &col = a.cols[c];
+    return walker_query(w, r, col.pres, a.n, a.E + (uint64_t)k * (a.n + 1), a.gend + (uint64_t)k * a.gend_stride);
+}
+
+// ColumnWriterV1.accountForValueWritten (estimateNextSizeCheck = true), one thread per
+// column: valueCountForNextSizeCheck starts at 100 (also after a row-group flush); after
+// record x the page holds vc = x - q + 1 values; a check (vc > next) cuts when memSize >
+// pageSize (next = vc / 2, count restarts), else next = (int)(vc + (float)vc * pageSize /
+// memSize) / 2 + 1 in Java float arithmetic.
+__global__ void __launch_bounds__(64) k_page_cuts(PageCutArgs a)
+{
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= a.ncols) return;
+    Walker w;
+    int64_t q = a.s;
+    walker_init(w, q);
+    int32_t next = 100;
+    uint32_t nc = 0;
+    for (;;) {
+        const int64_t x = q + (int64_t)next;
+        if (x >= a.h) break;
+        const int32_t vc = next + 1;
+        const uint64_t mem = col_dl_bytes(a, c, w, x + 1) + col_data_bytes(a, c, q, x + 1);
+        if (mem > (uint64_t)a.page_size) {
+            if (nc < a.cap) a.cuts[(uint64_t)c * a.cap + nc] = x + 1;
+            else atomicOr(a.overflow, 1);
+            nc++;
+            next = vc / 2;
+            q = x + 1;
+            walker_init(w, q);
+        } else {
+            float t = __fmul_rn((float)vc, (float)a.page_size);
+            t = __fdiv_rn(t, (float)mem);
+            const float sf = __fadd_rn((float)vc, t);
+            next = java_f2i(sf) / 2 + 1;
+        }
+    }
+    a.ncuts[c] = nc < a.cap ? nc : a.cap;
+}
+
+// checkBlockSizeReached over one row group from s with the page cuts above: memSize at
+// record count rc = sum over columns of (open page rl+dl+data) + (header + compressed
+// bytes of the pages already flushed to the ColumnChunkPageWriter).  One wave; lanes own
+// columns; r only grows, so each column's page cursor and walker advance monotonically.
+struct MpCol {
+    Walker w;
+    int64_t q;
+    uint64_t pb;
+    uint32_t ci, pad;
+};
+
+__device__ uint64_t mp_mem(const PageCutArgs &a, MpCol *S, int64_t r)
+{
+    uint64_t part = 0;
+    for (int c = threadIdx.x; c < a.ncols; c += 64) {
+        MpCol &m = S[c];
+        const uint32_t nc = a.ncuts[c];
+        while (m.ci < nc && a.cuts[(uint64_t)c * a.cap + m.ci] <= r) {
+            m.pb += a.pbytes[(uint64_t)c * a.cap + m.ci];
+            m.q = a.cuts[(uint64_t)c * a.cap + m.ci];
+            m.ci++;
+            walker_init(m.w, m.q);
+        }
+        part += m.pb + col_dl_bytes(a, c, m.w, r) + col_data_bytes(a, c, m.q, r);
+    }
+    return wave_sum(part);
+}
+
+__global__ void __launch_bounds__(64) k_plan_mp(PageCutArgs a)
+{
+    __shared__ MpCol S[MAX_COLS];
+    for (int c = threadIdx.x; c < a.ncols; c += 64) {
+        walker_init(S[c].w, a.s);
+        S[c].q = a.s; S[c].pb = 0; S[c].ci = 0;
+    }
+    __syncthreads();
+    const int64_t T = a.next_rg_size;
+    const int64_t s = a.s;
+    int64_t rc = 100, cut = -1;
+    while (s + rc <= a.h) {
+        const int64_t M = (int64_t)mp_mem(a, S, s + rc);
+        const int64_t rs = M / rc;
+        if (M > T - 2 * rs) { cut = s + rc; break; }
+        const float qf = __fdiv_rn((float)T, (float)rs);
+        const int64_t est = jadd(rc, java_f2l(qf)) / 2;
+        const int64_t lo = est > 100 ? est : 100;
+        const int64_t hi = jadd(rc, 10000);
+        int64_t nc = lo < hi ? lo : hi;
+        if (nc < rc + 1) nc = rc + 1;
+        rc = nc;
+    }
+    int64_t open_buf = 0;
+    if (cut < 0 && a.h == (int64_t)a.n && s < a.h) open_buf = (int64_t)mp_mem(a, S, a.h);
+    if (threadIdx.x == 0) { a.out[0] = cut; a.out[1] = open_buf; }
+}
+
+void launch_str_sizes(const DevCol *cols, int c, uint64_t n, uint32_t *sz, hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_str_sizes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cols, c, n, sz);
+}
+void launch_page_cuts(const PageCutArgs &a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_page_cuts, dim3((a.ncols + 63) / 64), dim3(64), 0, s, a);
+}
+void launch_plan_mp(const PageCutArgs &a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_plan_mp, dim3(1), dim3(64), 0, s, a);
+}
+
 }  // namespace kpw

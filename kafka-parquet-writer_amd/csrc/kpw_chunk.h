@@ -34,7 +34,20 @@ struct ChunkArgs {
     DeltaJob *djobs_w;             // v2: same array (layout sets out_off)
     const uint64_t *chunk_sfx;     // v2: DELTA_BYTE_ARRAY suffix bytes per chunk
     uint64_t *page_pre;            // v2: uncompressed level bytes in front of each page's values
+    int32_t mp;                    // multi-page regime: descriptors are pages (dictionary decided per chunk)
+    int32_t pad_mp;
 };
+
+// Multi-page (v1): page descriptors `pg` (ChunkArgs of the pages) and dictionary
+// descriptors `dch` (one per column chunk; dictionary kernels run on them).
+void launch_mp_pages_init(ChunkDesc *pg, int npg, const ChunkDesc *dch, const DevCol *cols, RleJob *jobs, hipStream_t s);
+void launch_dict_page(const ChunkArgs &a, uint8_t *out, hipStream_t s);
+void launch_mp_dict_decide(ChunkDesc *pg, int npg, const ChunkDesc *dch, const DevCol *cols, const uint64_t *ent_rec,
+                           const uint64_t *ent_boff, uint32_t max_dict_bytes, RleJob *jobs, hipStream_t s);
+void launch_mp_satisfy(ChunkDesc *pg, ChunkDesc *dch, int ndch, const DevCol *cols, const uint64_t *ent_rec,
+                       const uint64_t *ent_boff, const RleJob *jobs, hipStream_t s);
+void launch_mp_dictpage_off(const ChunkDesc *pg, ChunkDesc *dch, int ndch, hipStream_t s);
+void launch_page_str_stats(const ChunkArgs &a, hipStream_t s);
 
 // DELTA streams of a batch (k_delta.hip)
 struct DeltaArgs {

@@ -120,6 +120,34 @@ struct PlanArgs {
     int64_t *out;                  // [0]=n_rgs [1]=open_start [2]=open_buffered [3]=overflow
 };
 
+// Multi-page (v1, pageSize < blockSize) planning of one row group at a time (k_plan.hip):
+// ColumnWriterV1.accountForValueWritten page cuts per column from the row-group start s up
+// to a horizon h, then InternalParquetRecordWriter.checkBlockSizeReached with the flushed
+// pages' header + compressed bytes (ColumnChunkPageWriter.getMemSize) in memSize.
+struct PageCutArgs {
+    uint64_t n;                    // records in the batch (valid prefix)
+    int64_t s, h;                  // row-group start, horizon (exclusive)
+    int32_t ncols;
+    int32_t pad;
+    int64_t page_size;
+    const DevCol *cols;
+    const int32_t *col_stream;     // per column: definition-level stream (E/gend index) or -1
+    const uint32_t *E;             // as PlanArgs
+    const uint64_t *gend;
+    uint64_t gend_stride;
+    const uint64_t *const *sp;     // per column: exclusive prefix of (4 + len) over present BYTE_ARRAY values
+    uint32_t cap;                  // cut capacity per column
+    uint32_t *ncuts;               // [ncols]
+    int64_t *cuts;                 // [ncols * cap] page ends (exclusive record index), increasing
+    int32_t *overflow;
+    const uint64_t *pbytes;        // k_plan_mp: [ncols * cap] header + compressed bytes of each cut page
+    int64_t next_rg_size;
+    int64_t *out;                  // k_plan_mp: [0] row-group end or -1, [1] memSize at n (open buffered)
+};
+void launch_str_sizes(const DevCol *cols, int c, uint64_t n, uint32_t *sz, hipStream_t s);
+void launch_page_cuts(const PageCutArgs &a, hipStream_t s);
+void launch_plan_mp(const PageCutArgs &a, hipStream_t s);
+
 struct ChunkDesc {
     int64_t s, e;                  // record range in the batch
     int32_t col, rg;
@@ -152,6 +180,11 @@ struct ChunkDesc {
     int32_t bool_job;              // RLE job of the boolean values (-1 none)
     int32_t dj0;                   // first DELTA stream (INT: 1, BYTE_ARRAY: 2), -1 none
     uint64_t val_off;              // absolute offset of the values part of the data page
+    // multi-page (v1): page descriptors point at their column chunk's dictionary descriptor;
+    // a dictionary descriptor lists its pages [first_page, first_page + npages)
+    int32_t owner;                 // page: dictionary descriptor index (-1 single-page regime)
+    int32_t first_page, npages;    // dictionary descriptor: its pages
+    int32_t pad5;
 };
 
 // One DELTA_BINARY_PACKED stream (k_delta.hip).

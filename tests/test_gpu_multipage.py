@@ -1,0 +1,92 @@
+"""GPU parity in the multi-page regime (PARQUET_1_0, pageSize < blockSize): pages cut inside a
+row group by ColumnWriterV1.accountForValueWritten, the dictionary kept across a chunk's pages
+with a per-page bit width, fallback to PLAIN from the page where the dictionary crosses
+dictPageSize, isCompressionSatisfying on the first page only, and row groups cut by a size
+check that counts flushed pages by their header + compressed bytes.  Every page byte-identical
+to the CPU oracle (oracle/oracle_core.c colw_account / check_block_size)."""
+import io
+
+import pyarrow.parquet as pq
+import pytest
+
+import gpu_helpers as gh
+import oracle
+import protoutil
+import synth
+
+pytestmark = pytest.mark.gpu
+KiB = 1024
+MiB = 1024 * 1024
+
+CASES = [
+    ("sample", synth.KIND_SAMPLE, 0, 6000),
+    ("sample_nulls", synth.KIND_SAMPLE, 30, 6000),
+    ("rec8", synth.KIND_REC8, 0, 40000),
+    ("highcard", synth.KIND_HIGHCARD, 0, 6000),
+    ("wide", synth.KIND_WIDE, 0, 1500),
+]
+
+
+@pytest.mark.parametrize("name,kind,param,n", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("codec", [0, 1], ids=["uncompressed", "snappy"])
+@pytest.mark.parametrize("block_size,page_size", [(256 * KiB, 8 * KiB), (128 * MiB, 16 * KiB), (64 * KiB, 1024)],
+                         ids=["rg256K_p8K", "rg128M_p16K", "rg64K_p1K"])
+def test_multipage_matches_oracle(name, kind, param, n, codec, block_size, page_size):
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, 0xC0FFEE41 + kind, n, param=param)
+    errs = gh.compare_pages(schema, data, offs, codec=codec, block_size=block_size, page_size=page_size)
+    assert not errs, "\n".join(errs[:12])
+
+
+def _pairs_records(n):
+    # every query value twice in a row: the first page's dictionary is worth keeping
+    # (isCompressionSatisfying), and the dictionary crosses 1 MiB after ~31k distinct
+    # 30-byte values, many 64 KiB pages into the chunk
+    cls = protoutil.message_class(synth.SAMPLE)
+    recs = [cls(query="query-%024d" % (i // 2), timestamp=1700000000000 + i,
+                page_number=i % 7).SerializeToString() for i in range(n)]
+    return synth.pack(recs)
+
+
+def test_multipage_fallback_mid_chunk():
+    # earlier pages keep PLAIN_DICTIONARY ids (bit width growing page by page), the page where
+    # the dictionary crosses dictPageSize and every later one is PLAIN, and the dictionary page
+    # holds the entries of the last dictionary-encoded page
+    import pqwalk
+    data, offs = _pairs_records(80000)
+    for codec in (0, 1):
+        errs = gh.compare_pages(synth.SAMPLE, data, offs, codec=codec, page_size=64 * KiB)
+        assert not errs, "\n".join(errs[:12])
+    fb = oracle.encode_file(synth.SAMPLE, data, offs, oracle.make_props(codec=1, page_size=64 * KiB))
+    encs = [p["header"][5][2] for p in pqwalk.pages(fb) if p["col"] == 0 and p["header"][1] == 0]
+    assert encs[0] == 2 and encs[-1] == 0, encs   # PLAIN_DICTIONARY first, PLAIN after the fallback
+
+
+@pytest.mark.parametrize("page_size", [64, 300])
+def test_multipage_tiny_pages(page_size):
+    # pages of a handful of values: every size check cuts, next check = valueCount / 2
+    data, offs = synth.generate(synth.KIND_SAMPLE, 3, 3000, param=30)
+    errs = gh.compare_pages(synth.SAMPLE, data, offs, codec=1, block_size=32 * KiB, page_size=page_size)
+    assert not errs, "\n".join(errs[:12])
+
+
+def test_multipage_rowgroups_by_compressed_pages():
+    # 1 MiB pages in 4 MiB row groups: after the first page cuts the row-group check counts
+    # Snappy-compressed pages, so row groups hold more records than raw bytes suggest
+    schema = synth.REC8
+    data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE42, 300000)
+    errs = gh.compare_pages(schema, data, offs, codec=1, block_size=4 * MiB, page_size=1 * MiB)
+    assert not errs, "\n".join(errs[:12])
+
+
+def test_multipage_writer_file_identical():
+    import kpw
+    import pqwalk
+    schema = synth.REC8
+    data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE43, 30000, param=0)
+    props = kpw.ParquetProperties(block_size=256 * 1024, page_size=16 * 1024, compression_codec_name=1)
+    fb = gh.gpu_file(schema, data, offs, props, batches=3)
+    ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=256 * 1024, page_size=16 * 1024, codec=1))
+    assert fb == ob, pqwalk.first_difference(fb, ob)
+    tbl = pq.read_table(io.BytesIO(fb))
+    assert protoutil.table_columns(tbl, schema) == protoutil.decode_columns(schema, synth.records(data, offs))
