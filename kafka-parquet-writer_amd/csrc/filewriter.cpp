@@ -10,6 +10,9 @@
 //  * ColumnMetaData.encodings: insertion order (the JVM HashSet<Encoding> order is identity-
 //    hash based and not reproducible); key-value metadata in java.util.HashMap order;
 //  * created_by "parquet-mr version 1.10.1 (build a89df8f9932b6ef6633d06069e50c9b7970bebd1)".
+#include <thread>
+#include <algorithm>
+#include <cstdlib>
 #include "filewriter.h"
 
 #include <cstring>
@@ -186,6 +189,24 @@ FileWriter::FileWriter(const std::vector<ColInfo> &cols, const std::string &mess
 FileWriter::~FileWriter()
 {
     if (fp_) fclose(fp_);
+    free(mem_);
+}
+
+void par_copy(uint8_t *dst, const uint8_t *src, size_t n)
+{
+    static const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const size_t kMin = 4ull << 20;
+    const unsigned t = (unsigned)std::min<size_t>(hw, n / kMin);
+    if (t <= 1) { memcpy(dst, src, n); return; }
+    std::vector<std::thread> th;
+    th.reserve(t - 1);
+    const size_t per = (n / t + 4095) & ~(size_t)4095;
+    for (unsigned i = 1; i < t; i++) {
+        const size_t a = std::min(n, per * i), b = std::min(n, per * (i + 1));
+        if (b > a) th.emplace_back([=] { memcpy(dst + a, src + a, b - a); });
+    }
+    memcpy(dst, src, std::min(n, per));
+    for (auto &x : th) x.join();
 }
 
 int FileWriter::put(const void *p, size_t n)
@@ -194,7 +215,15 @@ int FileWriter::put(const void *p, size_t n)
     if (fp_) {
         if (fwrite(p, 1, n, fp_) != n) { err_ = "short write"; return KPW_ERR_IO; }
     } else {
-        mem_.insert(mem_.end(), (const uint8_t *)p, (const uint8_t *)p + n);
+        if (mem_len_ + n > mem_cap_) {
+            const size_t c = std::max(mem_len_ + n, mem_cap_ + mem_cap_ / 2 + 4096);
+            uint8_t *q = (uint8_t *)realloc(mem_, c);
+            if (!q) { err_ = "out of host memory"; return KPW_ERR_NOMEM; }
+            mem_ = q;
+            mem_cap_ = c;
+        }
+        par_copy(mem_ + mem_len_, (const uint8_t *)p, n);
+        mem_len_ += n;
     }
     pos_ += (int64_t)n;
     return KPW_OK;

@@ -38,6 +38,9 @@ struct RowGroupMeta {
 // (ParquetMetadataConverter.writeDataPageHeader / writeDataPageV2Header / dictionary page).
 std::string page_header(const PageOut &pg, int phys);
 
+// Host copy split over a few threads for large buffers (page faults and memcpy in parallel).
+void par_copy(uint8_t *dst, const uint8_t *src, size_t n);
+
 class FileWriter {
 public:
     FileWriter(const std::vector<ColInfo> &cols, const std::string &message_name, const std::string &proto_class,
@@ -49,7 +52,8 @@ public:
     int write_row_group(const BatchOut &b, int rg, const uint8_t *pages, uint64_t pages_base);
     int close();                      // footer + magic
     int64_t pos() const { return pos_; }
-    const std::vector<uint8_t> &memory() const { return mem_; }
+    const uint8_t *memory_data() const { return mem_; }
+    size_t memory_size() const { return mem_len_; }
     const std::string &error() const { return err_; }
 
 private:
@@ -58,7 +62,8 @@ private:
     std::string message_name_, proto_class_;
     kpw_props props_;
     FILE *fp_ = nullptr;
-    std::vector<uint8_t> mem_;
+    uint8_t *mem_ = nullptr;        // memory mode: malloc/realloc-grown (large reallocs remap, no copy)
+    size_t mem_len_ = 0, mem_cap_ = 0;
     int64_t pos_ = 0;
     std::vector<RowGroupMeta> rgs_;
     std::string err_;
