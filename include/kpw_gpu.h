@@ -51,7 +51,10 @@ int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64_t *offsets
 /* The WorkerThread size-rotation loop (KafkaProtoParquetWriter.java:277-285,306-308):
  * writes records in order and stops right after the first one for which
  * getDataSize() >= max_file_size.  *n_accepted = records written, *full = 1 if the stop
- * condition fired (the caller then closes this file and opens the next). */
+ * condition fired (the caller then closes this file and opens the next).  The stop point is
+ * found by encoding staged prefixes (segment checks + bisection), identical to the per-record
+ * loop.  pageSize < blockSize (v1 multi-page chunks) returns KPW_ERR_UNSUPPORTED there: use
+ * write + data_size per record.  An invalid record ends the batch as in kpw_writer_write. */
 int kpw_writer_write_until_full(kpw_writer *w, const uint8_t *data, const uint64_t *offsets,
                                 uint64_t n, int64_t max_file_size, uint64_t *n_accepted, int *full);
 

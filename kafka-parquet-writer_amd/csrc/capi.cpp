@@ -286,6 +286,38 @@ static int stage_bytes(kpw_writer *w, const uint8_t *src, uint64_t len)
     return KPW_OK;
 }
 
+// Stage n records (bytes through the pinned slots, offsets on the host).
+static int append_records(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n)
+{
+    const uint64_t bytes = offsets[n] - offsets[0];
+    if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
+    if (grow_stage(w, w->stage_len + bytes)) return KPW_ERR_NOMEM;
+    const uint64_t base = w->stage_len;
+    int st = stage_bytes(w, data + offsets[0], bytes);
+    if (st) return st;
+    const size_t o0 = w->offs.size();
+    w->offs.resize(o0 + n);
+    uint64_t *od = w->offs.data() + o0;
+    const uint64_t delta = base - offsets[0];
+    for (uint64_t i = 1; i <= n; i++) od[i - 1] = offsets[i] + delta;
+    w->num_records += (int64_t)n;
+    return KPW_OK;
+}
+
+// Offsets of every staged record to the device, ordered after the side stream's byte copies.
+static int upload_offsets(kpw_writer *w)
+{
+    const uint64_t n = w->offs.size() - 1;
+    if (w->d_off.ensure((n + 1) * 8) || w->h_off.ensure((n + 1) * 8))
+        return wfail(w, KPW_ERR_NOMEM, "offset staging allocation failed");
+    hipStream_t s = w->eng.stream;
+    memcpy(w->h_off.p, w->offs.data(), (n + 1) * 8);
+    if (hipEventRecord(w->copied, w->copy_stream) != hipSuccess || hipStreamWaitEvent(s, w->copied, 0) != hipSuccess ||
+        hipMemcpyAsync(w->d_off.p, w->h_off.p, (n + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+        return wfail(w, KPW_ERR_DEVICE, "H2D failed");
+    return KPW_OK;
+}
+
 // Encode the staged records: flush every row group parquet-mr would have completed (all of
 // them if final), keep the open row group's records staged.
 static int process(kpw_writer *w, bool final)
@@ -297,13 +329,8 @@ static int process(kpw_writer *w, bool final)
     if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
     if (trace_on()) w->t_enter = now_ms();
     if (grow_stage(w, w->stage_len)) return KPW_ERR_NOMEM;
-    if (w->d_off.ensure((n + 1) * 8) || w->h_off.ensure((n + 1) * 8))
-        return wfail(w, KPW_ERR_NOMEM, "offset staging allocation failed");
+    if (int ust = upload_offsets(w)) return ust;
     hipStream_t s = w->eng.stream;
-    memcpy(w->h_off.p, w->offs.data(), (n + 1) * 8);
-    if (hipEventRecord(w->copied, w->copy_stream) != hipSuccess || hipStreamWaitEvent(s, w->copied, 0) != hipSuccess ||
-        hipMemcpyAsync(w->d_off.p, w->h_off.p, (n + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
-        return wfail(w, KPW_ERR_DEVICE, "H2D failed");
     const double t0 = trace_on() ? (hipStreamSynchronize(s), now_ms()) : 0.0;
     BatchOut out;
     int st = w->eng.encode(w->d_stage[w->cur], w->d_off.as<uint64_t>(), n, final, w->eng.props.block_size, nullptr, out);
@@ -427,18 +454,8 @@ extern "C" int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64
     if (!w || (n && (!data || !offsets))) return KPW_ERR_INVALID_ARG;
     if (w->closed || w->dead) return KPW_ERR_STATE;
     try {
-        const uint64_t bytes = offsets[n] - offsets[0];
-        if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
-        if (grow_stage(w, w->stage_len + bytes)) return KPW_ERR_NOMEM;
-        const uint64_t base = w->stage_len;
-        int st = stage_bytes(w, data + offsets[0], bytes);
+        int st = append_records(w, data, offsets, n);
         if (st) return st;
-        const size_t o0 = w->offs.size();
-        w->offs.resize(o0 + n);
-        uint64_t *od = w->offs.data() + o0;
-        const uint64_t delta = base - offsets[0];
-        for (uint64_t i = 1; i <= n; i++) od[i - 1] = offsets[i] + delta;
-        w->num_records += (int64_t)n;
         if (w->stage_len >= stage_flush_bytes() + (uint64_t)w->eng.props.block_size) return process(w, false);
         return KPW_OK;
     } catch (const std::bad_alloc &) {
@@ -448,13 +465,126 @@ extern "C" int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64
     }
 }
 
+// getDataSize() after the first m staged records, without flushing anything: an encode of
+// [0, m) gives the row groups parquet-mr would have completed by then (their header +
+// compressed bytes follow lastRowGroupEndPos) and the open row group's buffered size.
+static int ds_prefix(kpw_writer *w, uint64_t m, int64_t &ds, BatchOut &out)
+{
+    out = BatchOut();
+    int st = w->eng.encode(w->d_stage[w->cur], w->d_off.as<uint64_t>(), m, false, w->eng.props.block_size, nullptr, out);
+    if (st) return wfail(w, st, w->eng.error());
+    int64_t t = w->last_rg_end;
+    for (size_t r = 0; r < out.rgs.size(); r++) t += w->fw->row_group_size(out, (int)r);
+    ds = t + out.open_buffered;
+    return KPW_OK;
+}
+
+// The WorkerThread loop (KafkaProtoParquetWriter.java:268-285,306-308) over a batch: records
+// are written one at a time and the file is full right after the first record for which
+// getDataSize() >= max_file_size.  Within one row group getDataSize() only grows (raw column
+// sizes and level bytes are appended), and a row-group flush replaces the group's buffered
+// size by its encoded bytes, so the first crossing is found segment by segment: at the last
+// record before each cut, at the cut itself, and by bisection inside the segment that crosses.
+// Every probe is an encode of a staged prefix (row-group cuts are causal: a prefix plans the
+// same cuts).  Multi-page chunks can shrink the buffered size inside a row group (a page cut
+// swaps raw bytes for compressed ones), so that regime keeps the per-record getDataSize() path.
 extern "C" int kpw_writer_write_until_full(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n,
                                            int64_t max_file_size, uint64_t *n_accepted, int *full)
 {
-    (void)data; (void)offsets; (void)n; (void)max_file_size; (void)n_accepted; (void)full;
-    if (!w) return KPW_ERR_INVALID_ARG;
-    w->err = "write_until_full: per-record size rotation on the GPU path is the next round";
-    return KPW_ERR_UNSUPPORTED;
+    if (!w || !n_accepted || !full || (n && (!data || !offsets))) return KPW_ERR_INVALID_ARG;
+    *n_accepted = 0;
+    *full = 0;
+    if (w->closed || w->dead) return KPW_ERR_STATE;
+    if (w->eng.props.writer_version == 1 && w->eng.props.page_size < w->eng.props.block_size) {
+        w->err = "write_until_full: pageSize < blockSize (multi-page chunks) — use write + getDataSize per record";
+        return KPW_ERR_UNSUPPORTED;
+    }
+    try {
+        int st = join_bg(w);
+        if (st) return st;
+        if (!n) return KPW_OK;
+        const uint64_t base = w->offs.size() - 1;
+        st = append_records(w, data, offsets, n);
+        if (st) return st;
+        w->staged_bytes_at_encode = ~0ull;
+        auto truncate = [&](uint64_t keep) {   // keep the first `keep` records of this batch staged
+            w->offs.resize(base + keep + 1);
+            w->stage_len = w->offs.back();
+            w->num_records -= (int64_t)(n - keep);
+        };
+        if ((st = upload_offsets(w))) return st;
+        BatchOut out;
+        int64_t ds_end = 0;
+        if ((st = ds_prefix(w, base + n, ds_end, out))) return st;
+        uint64_t valid = n;
+        if (out.invalid_record >= 0) {
+            if ((uint64_t)out.invalid_record < base) {   // a record staged by an earlier write()
+                truncate(0);
+                return process(w, false);
+            }
+            valid = (uint64_t)out.invalid_record - base;
+            if ((st = ds_prefix(w, base + valid, ds_end, out))) return st;
+        }
+        std::vector<int64_t> cut, end;   // row-group ends (records from the staging start), file pos after each
+        {
+            int64_t e = w->last_rg_end;
+            for (size_t r = 0; r < out.rgs.size(); r++) {
+                e += w->fw->row_group_size(out, (int)r);
+                cut.push_back(out.rgs[r].first_record + out.rgs[r].num_records);
+                end.push_back(e);
+            }
+        }
+        BatchOut tmp;
+        auto ds = [&](uint64_t j, int64_t &v) { return ds_prefix(w, base + j, v, tmp); };
+        // first j in [lo, hi] with ds(j) >= max, given ds(hi) >= max
+        auto bisect = [&](uint64_t lo, uint64_t hi, uint64_t &res) {
+            while (lo < hi) {
+                const uint64_t mid = lo + (hi - lo) / 2;
+                int64_t v = 0;
+                if (int e2 = ds(mid, v)) return e2;
+                if (v >= max_file_size) hi = mid; else lo = mid + 1;
+            }
+            res = lo;
+            return (int)KPW_OK;
+        };
+        uint64_t a = 0, found = 0;
+        for (size_t i = 0; i < cut.size() && !found; i++) {
+            const int64_t b = cut[i] - (int64_t)base;
+            if (b < 1) continue;
+            if ((uint64_t)b - 1 >= a + 1) {
+                int64_t v = 0;
+                if ((st = ds((uint64_t)b - 1, v))) return st;
+                if (v >= max_file_size) {
+                    if ((st = bisect(a + 1, (uint64_t)b - 1, found))) return st;
+                    break;
+                }
+            }
+            if (end[i] >= max_file_size) { found = (uint64_t)b; break; }
+            a = (uint64_t)b;
+        }
+        if (!found && valid >= a + 1 && ds_end >= max_file_size)
+            if ((st = bisect(a + 1, valid, found))) return st;
+        if (found) {
+            truncate(found);
+            *n_accepted = found;
+            *full = 1;
+        } else {
+            truncate(valid);
+            *n_accepted = valid;
+            if (valid < n) {
+                w->failed_record = w->num_records;
+                w->dead = true;
+                w->err = "Invalid proto message received (record " + std::to_string(w->failed_record) + ")";
+                return KPW_ERR_INVALID_PROTO;
+            }
+        }
+        if (w->stage_len >= stage_flush_bytes() + (uint64_t)w->eng.props.block_size) return process(w, false);
+        return KPW_OK;
+    } catch (const std::bad_alloc &) {
+        return wfail(w, KPW_ERR_NOMEM, "host allocation failed");
+    } catch (...) {
+        return wfail(w, KPW_ERR_DEVICE, "unexpected failure");
+    }
 }
 
 extern "C" int64_t kpw_writer_data_size(kpw_writer *w)

@@ -296,6 +296,18 @@ int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages,
     return KPW_OK;
 }
 
+int64_t FileWriter::row_group_size(const BatchOut &b, int rg) const
+{
+    const RowGroupOut &R = b.rgs[rg];
+    int64_t t = 0;
+    for (int c = 0; c < (int)cols_.size(); c++) {
+        const ChunkOut &co = b.chunks[R.first_chunk + c];
+        for (int p = co.first_page; p < co.first_page + co.num_pages; p++)
+            t += (int64_t)page_header(b.pages[p], cols_[c].phys).size() + b.pages[p].compressed_size;
+    }
+    return t;
+}
+
 int FileWriter::close()
 {
     if (closed_) return KPW_OK;

@@ -50,6 +50,8 @@ public:
     // Appends one encoded row group; `pages` is host memory holding the batch's page bodies
     // (indexed by PageOut.offset relative to pages_base).
     int write_row_group(const BatchOut &b, int rg, const uint8_t *pages, uint64_t pages_base);
+    // Bytes write_row_group would append for row group `rg` (page headers + compressed bodies).
+    int64_t row_group_size(const BatchOut &b, int rg) const;
     int close();                      // footer + magic
     int64_t pos() const { return pos_; }
     const uint8_t *memory_data() const { return mem_; }
