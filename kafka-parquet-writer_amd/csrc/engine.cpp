@@ -7,6 +7,8 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "kpw_chunk.h"
@@ -609,8 +611,43 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
         sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
         sa.page_pre = v2_ ? d_page_pre.as<uint64_t>() : nullptr;
+        // Longest-first dispatch.  K7's waves are latency-bound and a fragment's time depends on
+        // its data (one PLAIN int64 fragment of slowly-growing timestamps: ~9 ms; an
+        // incompressible one: ~50 us), so the kernel's tail is set by the long fragments
+        // dispatched last.  Every fragment records its [start, end] clock; the longest duration
+        // seen per (column, page kind, fragment index in the page) in the previous batch ranks
+        // this batch's fragments, longest first (per (column, page kind) when the index is new).
+        // Output is unchanged (fragments are independent; slots are indexed by fragment).
+        const size_t nkind = 2 * cols.size();
+        if (sn_cost_.size() != nkind) sn_cost_.assign(nkind, 0.0);
+        auto kind_of = [&](uint32_t p) { return ((p / 2) % cols.size()) * 2 + (p & 1); };
+        auto fkey = [&](uint32_t f) { return ((uint64_t)kind_of(fpage[f]) << 32) | fidx[f]; };
+        auto cost_of = [&](uint32_t f) {
+            auto it = sn_fcost_.find(fkey(f));
+            return it != sn_fcost_.end() ? it->second : sn_cost_[kind_of(fpage[f])];
+        };
+        bool have_cost = false;
+        for (double c : sn_cost_) have_cost |= c > 0;
+        if (nf) {
+            ENS(d_sprof, (uint64_t)nf * 16);
+            sa.ftime = d_sprof.as<uint64_t>();
+            if (have_cost) {
+                sn_order_.resize(nf);
+                std::vector<std::pair<double, uint32_t>> ranked(nf);
+                for (uint32_t f = 0; f < nf; f++) ranked[f] = {-cost_of(f), f};
+                std::sort(ranked.begin(), ranked.end());
+                for (uint32_t f = 0; f < nf; f++) sn_order_[f] = ranked[f].second;
+                ENS(d_sorder, (uint64_t)nf * 4);
+                CK(hipMemcpyAsync(d_sorder.p, sn_order_.data(), (size_t)nf * 4, hipMemcpyHostToDevice, s));
+                sa.order = d_sorder.as<uint32_t>();
+            }
+        }
         CK(hipEventRecord(kev_[2], s));
         launch_snappy(sa, s);
+        if (nf) {
+            sn_ft_.resize(2 * (size_t)nf);
+            CK(hipMemcpyAsync(sn_ft_.data(), d_sprof.p, sn_ft_.size() * 8, hipMemcpyDeviceToHost, s));
+        }
         CK(hipEventRecord(kev_[3], s));
         launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), s);
         CK(hipGetLastError());
@@ -621,6 +658,34 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         CK(hipMemcpyAsync(pclen.data(), d_page_clen.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
         CK(hipMemcpyAsync(&ctot, d_tot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
+        if (nf) {
+            // per-kind mean duration (fragments handed to k_snappy_s_rest count their short
+            // k_snappy_v attempt); KPW_SNAPPY_PROFILE=<file> also dumps the raw records
+            std::vector<double> mx(nkind, 0.0);
+            sn_fcost_.clear();
+            for (uint32_t f = 0; f < nf; f++) {
+                const uint64_t e = sn_ft_[2 * f + 1] & ~(1ull << 63);
+                const double d = std::max(1.0, (double)(e - sn_ft_[2 * f]));
+                const size_t k = kind_of(fpage[f]);
+                mx[k] = std::max(mx[k], d);
+                double &c = sn_fcost_[fkey(f)];
+                c = std::max(c, d);
+            }
+            for (size_t k = 0; k < nkind; k++)
+                if (mx[k] > 0) sn_cost_[k] = mx[k];
+            static const char *sprof = getenv("KPW_SNAPPY_PROFILE");
+            if (sprof) {
+                if (FILE *fp = fopen(sprof, "wb")) {
+                    // per fragment: page, index in page, page length, column, start, end (bit 63: handed on)
+                    for (uint32_t f = 0; f < nf; f++) {
+                        const uint64_t rec[6] = {fpage[f], fidx[f], plen[fpage[f]], (uint64_t)((fpage[f] / 2) % cols.size()),
+                                                 sn_ft_[2 * f], sn_ft_[2 * f + 1]};
+                        fwrite(rec, 8, 6, fp);
+                    }
+                    fclose(fp);
+                }
+            }
+        }
         pages_dev_ = d_comp.as<uint8_t>();
         pages_len_ = ctot;
     } else {   // uncompressed: a (v2) page body starts at its level prefix

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/kpw_types.h"
@@ -95,7 +96,11 @@ private:
         d_body;
     // snappy
     DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
-    DevBuf d_smeta, d_sblob, d_collision, d_dict_order;
+    DevBuf d_smeta, d_sblob, d_collision, d_dict_order, d_sprof, d_sorder;
+    std::vector<double> sn_cost_;       // K7 mean fragment duration per (column, page kind), previous batch
+    std::unordered_map<uint64_t, double> sn_fcost_;   // per (kind, fragment index)
+    std::vector<uint32_t> sn_order_;
+    std::vector<uint64_t> sn_ft_;
     // v2 (PARQUET_2_0): boolean value streams, planner streams, DELTA streams
     bool v2_ = false;
     std::vector<DevBuf> col_cbits;

@@ -1125,7 +1125,8 @@ __device__ __forceinline__ uint32_t find_match_length_v(VWin &in, const SIn &si,
 __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k_snappy_v(SnappyArgs a)
 {
     const int lane = threadIdx.x;
-    const uint32_t f = blockIdx.x;
+    const uint32_t f = a.order ? a.order[blockIdx.x] : blockIdx.x;
+    if (a.ftime && lane == 0) a.ftime[2 * f] = wall_clock64();
     const uint32_t pg = a.frag_page[f];
     const uint32_t fi = a.frag_idx[f];
     const uint64_t plen = a.page_len[pg];
@@ -1162,7 +1163,7 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k
                 const uint32_t next_ip = ip + (skip++ >> 5);
                 if (next_ip > ip_limit) goto emit_remainder;
                 if (skip > 32 + VT_ABORT) {
-                    if (lane == 0) a.frag_len[f] = VT_ABORTED;
+                    if (lane == 0) { a.frag_len[f] = VT_ABORTED; if (a.ftime) a.ftime[2 * f + 1] = wall_clock64() | (1ull << 63); }
                     return;
                 }
                 const uint32_t cur_s = in.ld32(ip, si, true);
@@ -1199,7 +1200,7 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k
     }
 emit_remainder:
     if (next_emit < ip_end) op = emit_literal(out, op, g, next_emit, ip_end - next_emit, lane);
-    if (lane == 0) a.frag_len[f] = op;
+    if (lane == 0) { a.frag_len[f] = op; if (a.ftime) a.ftime[2 * f + 1] = wall_clock64(); }
 }
 
 // ------------------------------------------------------------------ register-resident variant

@@ -100,6 +100,8 @@ struct SnappyArgs {
     uint8_t *out;                // compressed pages
     uint64_t *tot;               // [0] total compressed bytes
     const uint64_t *page_pre;    // v2: uncompressed level bytes right before page_off (nullptr: none)
+    uint64_t *ftime;             // per fragment [start, end] wall clock of k_snappy_v (nullptr: off)
+    const uint32_t *order;       // k_snappy_v: block b compresses fragment order[b] (nullptr: b)
 };
 constexpr uint32_t SNAPPY_FRAG = 65536;
 // per-fragment output slot: max compressed length (32 + n + n/6) rounded up to the 256-byte
