@@ -76,6 +76,51 @@ __device__ __forceinline__ uint32_t emit_literal(uint8_t *out, uint32_t op, cons
     return op + len;
 }
 
+// emit_literal for the LDS-table kernel (k_snappy_s / k_snappy_s_rest, the fragments the
+// register kernels hand on: mostly incompressible, i.e. one 64 KiB literal)
+__device__ __forceinline__ uint32_t emit_literal_wide(uint8_t *out, uint32_t op, const Src &in, uint32_t lit, uint32_t len, int lane)
+{
+    if (len < 512) return emit_literal(out, op, in, lit, len, lane);
+    {
+        uint32_t n = len - 1;
+        uint32_t base = op++;
+        int count = 0;
+        while (n > 0) { if (lane == 0) out[op] = (uint8_t)(n & 0xff); op++; n >>= 8; count++; }
+        if (lane == 0) out[base] = (uint8_t)((59 + count) << 2);
+    }
+    {
+        // long literal (incompressible stretches): aligned 16-byte loads, 1 KiB per wave step and
+        // four steps in flight, bytes stored to their output positions.  Reads stay inside the
+        // 16-byte blocks that overlap [lit, lit + len): the page buffer starts 256-aligned and is
+        // padded past its last page.
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(1))) v4u g_u4;
+        const uintptr_t src0 = (uintptr_t)(in.p + lit), end = src0 + len;
+        uint8_t *dst = out + op;
+        for (uintptr_t a = (src0 & ~(uintptr_t)15) + 16 * (uintptr_t)lane; a < end; a += 4096) {
+            v4u v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (a + 1024 * u < end) v[u] = *(g_u4 *)(a + 1024 * u);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uintptr_t b0 = a + 1024 * u;
+                if (b0 >= end) break;
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                if (b0 >= src0 && b0 + 16 <= end) {
+#pragma unroll
+                    for (int j = 0; j < 16; j++) dst[b0 - src0 + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 16; j++)
+                        if (b0 + j >= src0 && b0 + j < end) dst[b0 + j - src0] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+                }
+            }
+        }
+        return op + len;
+    }
+}
+
 __device__ __forceinline__ uint32_t emit_copy_lt64(uint8_t *out, uint32_t op, uint32_t offset, uint32_t len, int lane)
 {
     if (len < 12 && offset < 2048) {
@@ -624,7 +669,7 @@ __device__ __forceinline__ uint32_t emit_literal_s(uint8_t *out, uint32_t op, co
         st_word(out, op, ((uint64_t)((len - 1) << 2)) | (b << 8), 1 + len, lane);
         return op + 1 + len;
     }
-    return emit_literal(out, op, g, lit, len, lane);
+    return emit_literal_wide(out, op, g, lit, len, lane);
 }
 
 // matching bytes of [s1..) vs [s2..s2_limit): 8 bytes per scalar step for up to 64 bytes,
@@ -764,7 +809,7 @@ __device__ __forceinline__ void k_snappy_s_body(const SnappyArgs &a)
         }
     }
 emit_remainder:
-    if (next_emit < ip_end) op = emit_literal(out, op, g, next_emit, ip_end - next_emit, lane);
+    if (next_emit < ip_end) op = emit_literal_wide(out, op, g, next_emit, ip_end - next_emit, lane);
     if (lane == 0) a.frag_len[f] = op;
 }
 
