@@ -35,6 +35,35 @@ def log(msg):
         print("[bench] " + msg, file=sys.stderr, flush=True)
 
 
+# SURVEY.md §8(d) configurations that fit one GPU: kind, records per GPU, seed, description.
+# C2 is the headline (BASELINE.json metric); C3 / C4 are extra measurement lines.
+WORKLOADS = {
+    "c2": (1, 100_000_000, 0xC0FFEE02, "C2: Rec8 (8 cols)"),
+    "c3": (3, 10_000_000, 0xC0FFEE03, "C3: Wide telemetry (ts + 199 optional cols, 30% null)"),
+    "c4": (2, 20_000_000, 0xC0FFEE04, "C4: HighCard (ts, uuid, JSON blob, code)"),
+}
+
+
+def decode_out_bytes(schema, n):
+    """K1 algorithmic output bytes: 8 B per 64-bit value, 4 B per 32-bit value, 12 B (offset +
+    length) per string, 1 bit per bool, 1 bit of presence per optional column, 4 B raw size."""
+    import synth
+    per = 4
+    bits = 0
+    for _, _, t, label in schema.columns:
+        if t == synth.BOOL:
+            bits += 1
+        elif t in (synth.STRING, synth.BYTES):
+            per += 12
+        elif t in (synth.INT64, synth.UINT64, synth.DOUBLE, synth.FIXED64, synth.SFIXED64, synth.SINT64):
+            per += 8
+        else:
+            per += 4
+        if label == synth.OPTIONAL:
+            bits += 1
+    return n * per + (bits * n) // 8
+
+
 def cpu_baseline(kind, seed, sample_records, threads):
     """The CPU oracle (a C restatement of parquet-mr 1.10.1's write path, kind "port") on a
     bounded sample of the same workload: `threads` independent files (one per thread, like
@@ -51,7 +80,7 @@ def cpu_baseline(kind, seed, sample_records, threads):
     def work(i):
         try:
             d, o = chunks[i]
-            oracle.encode_file(synth.REC8, d, o, props)
+            oracle.encode_file(synth.SCHEMAS[kind], d, o, props)
         except Exception as e:  # noqa: BLE001
             errs.append(e)
 
@@ -65,8 +94,8 @@ def cpu_baseline(kind, seed, sample_records, threads):
     if errs:
         raise errs[0]
     return dict(value=round(total_bytes / dt / 1e9, 4), unit="GB/s", cores=threads, kind="port",
-                sample="%d Rec8 records (%d per thread, %.1f MB), SNAPPY, 128 MiB row groups, %d threads, %.2f s"
-                       % (per * threads, per, total_bytes / 1e6, threads, dt),
+                sample="%d %s records (%d per thread, %.1f MB), SNAPPY, 128 MiB row groups, %d threads, %.2f s"
+                       % (per * threads, synth.SCHEMAS[kind].message_name.split(".")[-1], per, total_bytes / 1e6, threads, dt),
                 records_per_s=round(per * threads / dt, 1))
 
 
@@ -141,7 +170,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--records", type=int, default=100_000_000, help="records per GPU (C2: 100 M)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
+                    help="SURVEY §8(d) configuration (c2 = the BASELINE.json metric's workload)")
+    ap.add_argument("--records", type=int, default=0, help="records per GPU (default: the workload's, C2: 100 M)")
     ap.add_argument("--codec", type=int, default=1, help="0 UNCOMPRESSED, 1 SNAPPY (C2)")
     ap.add_argument("--cpu-sample", type=int, default=24_000_000,
                     help="records for the CPU baseline sample (~1.5 GB, ~16 s of single-core oracle work)")
@@ -158,16 +189,19 @@ def main():
 
     import kpw
     import synth
-    seed = 0xC0FFEE02 if world == 1 else 0xC0FFEE05 + rank
+    kind, default_records, wseed, wdesc = WORKLOADS[args.workload]
+    schema = synth.SCHEMAS[kind]
+    args.records = args.records or default_records
+    seed = (wseed if world == 1 else 0xC0FFEE05 + rank) if args.workload == "c2" else wseed + 0x100 * rank
     t0 = time.perf_counter()
-    data, offs = synth.generate(synth.KIND_REC8, seed, args.records)
+    data, offs = synth.generate(kind, seed, args.records)
     log("generated %d records (%.2f GB) in %.1fs" % (args.records, len(data) / 1e9, time.perf_counter() - t0))
     d_data = torch.from_numpy(data).to("cuda")
     d_off = torch.from_numpy(offs.view(np.int64)).to("cuda")
     nbytes = int(offs[-1])
     n = args.records
     del data
-    enc = kpw.Encoder(kpw.Schema(synth.REC8.message_name, synth.REC8.columns, synth.REC8.proto_class),
+    enc = kpw.Encoder(kpw.Schema(schema.message_name, schema.columns, schema.proto_class),
                       device=local_rank, codec=args.codec, block_size=128 * MiB, page_size=128 * MiB)
     torch.cuda.synchronize()
 
@@ -207,7 +241,7 @@ def main():
     # K1 decode: algorithmic bytes = record bytes + offsets in; columnar values out
     # (ts 8, user_id 4, status 4, price 8, score 8, key16 8+4, region 8+4 per record,
     #  presence/boolean bits n/8 per optional column + flag bits, raw sizes 4 per record)
-    k1_bytes = nbytes + 8 * (n + 1) + n * (8 + 4 + 4 + 8 + 8 + 12 + 12 + 4) + (5 * n) // 8
+    k1_bytes = nbytes + 8 * (n + 1) + decode_out_bytes(schema, n)
     names = ["decode", "plan", "stats+dict", "rle", "layout+plain+write", "compress", "metadata", "total",
              "k_decode", "k_snappy"]
     stage = dict(zip(names, [round(x, 3) for x in stages]))
@@ -229,14 +263,19 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         threads = args.cpu_threads or min(16, os.cpu_count() or 8)
-        cpu = cpu_baseline(synth.KIND_REC8, seed, args.cpu_sample, threads)
+        sample = args.cpu_sample
+        if args.workload != "c2":   # the same ~1.5 GB of wire bytes as the C2 sample
+            sample = max(threads, int(sample * 62 / max(1.0, nbytes / n)))
+        cpu = cpu_baseline(kind, seed, sample, threads)
     out = {
         "metric": "Parquet encode GB/s + records/sec (whole node) at 1/2/4/8 MI355X vs CPU writer",
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8", "data": "synthetic (counter-based proto2 Rec8 generator; no broker, in-memory record source)",
-        "config": {"workload": "C2: Rec8 (8 cols), %d records/GPU, PLAIN_DICTIONARY + SNAPPY, 128 MiB row groups, "
-                               "128 MiB pages, parquet-mr 1.10.1 v1 semantics" % n,
+        "dtype": "u8", "data": "synthetic (counter-based proto2 %s generator; no broker, in-memory record source)"
+                               % schema.message_name.split(".")[-1],
+        "config": {"workload": "%s, %d records/GPU, PLAIN_DICTIONARY + %s, 128 MiB row groups, "
+                               "128 MiB pages, parquet-mr 1.10.1 v1 semantics"
+                               % (wdesc, n, "SNAPPY" if args.codec else "UNCOMPRESSED"),
                    "records_per_gpu": n, "bytes_per_gpu": nbytes, "row_groups_per_gpu": nrg,
                    "codec": "SNAPPY" if args.codec else "UNCOMPRESSED", "parallelism": "partition-sharded x%d" % world},
         "records_per_s": round(rec_s, 1),
