@@ -72,7 +72,26 @@ __device__ uint64_t walker_query(Walker &w, int64_t r, const uint64_t *pres, uin
         if (w.pend_pos < 0) {
             const int64_t p = w.p;
             if (p + 8 > (int64_t)n) { w.state = 2; break; }
-            const uint32_t x8 = (uint32_t)(bits_window(pres, (uint64_t)p) & 0xffu);
+            const uint64_t x64 = bits_window(pres, (uint64_t)p);
+            const uint32_t x8 = (uint32_t)(x64 & 0xffu);
+            if (x8 != 0 && x8 != 0xffu && p + 7 < r) {
+                // bit-packed groups straight from the 64-bit window: every mixed group that ends
+                // before r is consumed (1 byte, +1 for a new run header every 63 groups) without
+                // reloading; the first group that is not is left to the general path below
+                int64_t q = p;
+                int k = 0;
+                do {
+                    w.eacc += 1 + ((w.grp % 63) == 0 ? 1 : 0);
+                    w.grp++;
+                    q += 8;
+                    k++;
+                    if (k == 8 || q + 8 > (int64_t)n || q + 7 >= r) break;
+                    const uint32_t y8 = (uint32_t)((x64 >> (8 * k)) & 0xffu);
+                    if (y8 == 0 || y8 == 0xffu) break;
+                } while (true);
+                w.p = q;
+                continue;
+            }
             if (x8 == 0 || x8 == 0xffu) {
                 const uint64_t fill = x8 ? ~0ull : 0ull;
                 int64_t pos = p + 8, b = (int64_t)n;
