@@ -23,7 +23,8 @@
 // started at s re-synchronises with it (both end an RLE run at the same position; from
 // there on the encoders are in identical states), and from a short local walk before.
 //
-// One wave walks the row groups sequentially; lanes split the streams / boolean columns.
+// One block walks the row groups sequentially; its 256 threads split the streams / boolean
+// columns (every thread takes the same decisions from block-wide sums).
 #include "kpw_device.h"
 #include "kpw_kernels.h"
 
@@ -146,21 +147,31 @@ __device__ __forceinline__ int64_t stream_pos(const PlanArgs &a, const PlanStrea
     return S.rank_col < 0 ? r : (int64_t)pc_at(a.cols[S.rank_col], (uint64_t)r);
 }
 
+constexpr int PLAN_T = 256;   // k_plan block: four waves, each thread owns streams tid, tid + 256, ...
+
 __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 {
-    const int lane = threadIdx.x;
+    __shared__ uint64_t red[PLAN_T / 64];
+    const int tid = threadIdx.x;
     uint64_t part = 0;
-    for (int k = lane; k < a.nstreams; k += 64) {
+    for (int k = tid; k < a.nstreams; k += PLAN_T) {
         const PlanStream &S = a.streams[k];
         part += walker_query(W[k], stream_pos(a, S, r), S.bits, S.len, a.E + (uint64_t)k * (a.n + 1),
                              a.gend + (uint64_t)k * a.gend_stride);
     }
-    for (int k = lane; k < a.nbool; k += 64) {
+    for (int k = tid; k < a.nbool; k += PLAN_T) {
         const DevCol &c = a.cols[a.bool_cols[k]];
         const uint64_t cnt = c.optional ? pc_at(c, (uint64_t)r) - pc_at(c, (uint64_t)s) : (uint64_t)(r - s);
         part += (cnt + 7) / 8;
     }
-    return wave_sum(part) + (a.P[r] - a.P[s]);
+    part = wave_sum(part);
+    if ((tid & 63) == 0) red[tid >> 6] = part;
+    __syncthreads();   // also publishes the walkers to eval_mem_lane
+    uint64_t tot = 0;
+#pragma unroll
+    for (int i = 0; i < PLAN_T / 64; i++) tot += red[i];
+    __syncthreads();
+    return tot + (a.P[r] - a.P[s]);
 }
 
 // memSize at record r for one lane, valid only when every walker is past its convergence
@@ -183,22 +194,23 @@ __device__ uint64_t eval_mem_lane(const PlanArgs &a, const Walker *W, int64_t s,
 __device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walker *W, int64_t r)
 {
     bool ok = true;
-    for (int k = threadIdx.x; k < a.nstreams; k += 64)
+    for (int k = threadIdx.x; k < a.nstreams; k += PLAN_T)
         ok = ok && (W[k].state == 2 || (W[k].state == 1 && W[k].conv_pos < stream_pos(a, a.streams[k], r)));
-    return __ballot(!ok) == 0;
+    return __syncthreads_and(ok ? 1 : 0) != 0;
 }
 
-__global__ void __launch_bounds__(64) k_plan(PlanArgs a)
+__global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
 {
     __shared__ Walker W[MAX_STREAMS];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
     const int64_t n = (int64_t)a.n;
     const int64_t T = a.next_rg_size;
     int64_t s = 0;
     int32_t nrg = 0;
     int64_t overflow = 0;
     for (;;) {
-        for (int k = lane; k < a.nstreams; k += 64) {
+        for (int k = tid; k < a.nstreams; k += PLAN_T) {
             Walker w;
             w.p = stream_pos(a, a.streams[k], s); w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
             w.pend_bytes = 0; w.pend_rle = 0; w.grp = 0; w.state = 0;
@@ -250,7 +262,7 @@ __global__ void __launch_bounds__(64) k_plan(PlanArgs a)
             rc = nc;
         }
         if (cut) {
-            if (nrg < a.max_rgs) { if (lane == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = r; } }
+            if (nrg < a.max_rgs) { if (tid == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = r; } }
             else overflow = 1;
             nrg++;
             s = r;
@@ -261,13 +273,13 @@ __global__ void __launch_bounds__(64) k_plan(PlanArgs a)
         int64_t open_buf = 0;
         if (s < n) open_buf = (int64_t)eval_mem(a, W, s, n);
         if (a.final_flush && s < n) {
-            if (nrg < a.max_rgs) { if (lane == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = n; } }
+            if (nrg < a.max_rgs) { if (tid == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = n; } }
             else overflow = 1;
             nrg++;
             s = n;
             open_buf = 0;
         }
-        if (lane == 0) {
+        if (tid == 0) {
             a.out[0] = nrg;
             a.out[1] = s;
             a.out[2] = open_buf;
@@ -279,7 +291,7 @@ __global__ void __launch_bounds__(64) k_plan(PlanArgs a)
 
 void launch_plan(const PlanArgs &a, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(PLAN_T), 0, s, a);
 }
 
 // ------------------------------------------------------------------ multi-page (v1)
