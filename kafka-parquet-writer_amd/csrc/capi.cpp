@@ -212,14 +212,18 @@ static int wfail(kpw_writer *w, int st, const std::string &m)
     return st;
 }
 
-// Wait for the previous flush's file assembly; surface its failure.
+// Wait for the previous flush's file assembly; surface its failure.  A failed assembly is
+// fatal even for KPW_ERR_IO: its records were already dropped from staging, so a retried
+// close()/getDataSize() could otherwise "succeed" with rows missing from the file.
 static int join_bg(kpw_writer *w)
 {
     if (w->bg.joinable()) w->bg.join();
     if (w->bg_st) {
         const int st = w->bg_st;
         w->bg_st = KPW_OK;
-        return wfail(w, st, w->bg_err);
+        wfail(w, st, w->bg_err);
+        w->dead = true;
+        return st;
     }
     return KPW_OK;
 }
@@ -331,7 +335,7 @@ static int process(kpw_writer *w, bool final)
     if (grow_stage(w, w->stage_len)) return KPW_ERR_NOMEM;
     if (int ust = upload_offsets(w)) return ust;
     hipStream_t s = w->eng.stream;
-    const double t0 = trace_on() ? (hipStreamSynchronize(s), now_ms()) : 0.0;
+    const double t0 = trace_on() ? ((void)hipStreamSynchronize(s), now_ms()) : 0.0;
     BatchOut out;
     int st = w->eng.encode(w->d_stage[w->cur], w->d_off.as<uint64_t>(), n, final, w->eng.props.block_size, nullptr, out);
     if (st) return wfail(w, st, w->eng.error());
@@ -350,23 +354,32 @@ static int process(kpw_writer *w, bool final)
     if (!out.rgs.empty()) {
         w->bg_out = std::move(out);
         w->bg = std::thread([w] {
-            (void)hipSetDevice(w->eng.device);
-            const double tf = trace_on() ? now_ms() : 0.0;
-            if (hipEventSynchronize(w->d2h_done) != hipSuccess) {
-                w->bg_st = KPW_ERR_DEVICE;
-                w->bg_err = "D2H of pages failed";
-                return;
-            }
-            for (size_t r = 0; r < w->bg_out.rgs.size(); r++) {
-                const int st2 = w->fw->write_row_group(w->bg_out, (int)r, w->host_pages.p, 0);
-                if (st2) {
-                    w->bg_st = st2;
-                    w->bg_err = w->fw->error();
+            // no exception may leave this thread (std::terminate would kill the host process)
+            try {
+                (void)hipSetDevice(w->eng.device);
+                const double tf = trace_on() ? now_ms() : 0.0;
+                if (hipEventSynchronize(w->d2h_done) != hipSuccess) {
+                    w->bg_st = KPW_ERR_DEVICE;
+                    w->bg_err = "D2H of pages failed";
                     return;
                 }
-                w->last_rg_end = w->fw->pos();
+                for (size_t r = 0; r < w->bg_out.rgs.size(); r++) {
+                    const int st2 = w->fw->write_row_group(w->bg_out, (int)r, w->host_pages.p, 0);
+                    if (st2) {
+                        w->bg_st = st2;
+                        w->bg_err = w->fw->error();
+                        return;
+                    }
+                    w->last_rg_end = w->fw->pos();
+                }
+                if (trace_on()) fprintf(stderr, "[kpw] file assembly (d2h wait + write) %.2f ms\n", now_ms() - tf);
+            } catch (const std::bad_alloc &) {
+                w->bg_st = KPW_ERR_NOMEM;
+                w->bg_err = "file assembly: host allocation failed";
+            } catch (...) {
+                w->bg_st = KPW_ERR_DEVICE;
+                w->bg_err = "file assembly failed";
             }
-            if (trace_on()) fprintf(stderr, "[kpw] file assembly (d2h wait + write) %.2f ms\n", now_ms() - tf);
         });
     }
     // keep [records_consumed, valid end) staged

@@ -46,6 +46,8 @@ Engine::~Engine()
 {
     for (auto &e : ev_) if (e) (void)hipEventDestroy(e);
     for (auto &e : kev_) if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamSynchronize(stream);
+    seg_scratch_free(seg_);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -196,6 +198,7 @@ int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, Rle
     sc.job_nrle = r_jnrle.as<uint32_t>();
     sc.job_btot = r_jbtot.as<uint64_t>();
     sc.job_gtot = r_jgtot.as<uint64_t>();
+    sc.seg = &seg_;
     return KPW_OK;
 }
 
@@ -498,6 +501,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     a.collision = d_collision.as<uint32_t>();
     a.dict_order = d_dict_order.as<uint32_t>(); a.ndict_tiles = (uint32_t)dorder.size();
     a.v2 = v2_ ? 1 : 0;
+    a.seg = &seg_;
     // v2 DELTA streams: dense inputs share the chunks' rank-indexed id space (ids_off)
     DeltaArgs dla{};
     ENS(d_page_pre, 2 * nch * 8);
@@ -520,6 +524,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         dla.jobs = d_djobs.as<DeltaJob>(); dla.njobs = (uint32_t)dj.size(); dla.nblk = (uint32_t)dblk_job.size();
         dla.blk_job = d_blk_job.as<uint32_t>(); dla.blk_min = d_blk_min.as<uint64_t>(); dla.blk_w = d_blk_w.as<uint32_t>();
         dla.blk_sz = d_blk_sz.as<uint64_t>(); dla.blk_off = d_blk_off.as<uint64_t>(); dla.btot = d_btot.as<uint64_t>();
+        dla.seg = &seg_;
         a.djobs = dla.jobs; a.djobs_w = dla.jobs; a.chunk_sfx = d_chunk_sfx.as<uint64_t>();
     }
     uint32_t enpt = 0, enet = 0;
@@ -565,7 +570,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, s));
         CK(hipMemcpyAsync(&coll, d_collision.p, 4, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
-        if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+        if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
         if (!coll) break;
         if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
     }
@@ -696,7 +701,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         pages_len_ = body_tot;
     }
     CK(hipEventRecord(ev_[6], s));
-    if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+    if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
     // ---------------------------------------------------------------- metadata
     CK(hipMemcpyAsync(ch.data(), d_chunks.p, nch * sizeof(ChunkDesc), hipMemcpyDeviceToHost, s));
     // binary min/max bytes: gather (offset, len) pairs, then the bytes into one blob

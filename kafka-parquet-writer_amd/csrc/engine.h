@@ -76,10 +76,12 @@ public:
     std::string message_name, proto_class;
     int device = 0;
     hipStream_t stream = nullptr;
-    float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 k_snappy_frag
+    float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 K7 (k_snappy_v + k_snappy_s_rest)
 
 private:
     int fail(int code, const std::string &msg);
+    SegScratch seg_;   // segmented-scan scratch of this handle (freed in ~Engine)
+    bool seg_failed_reset() { const bool f = seg_.failed; seg_.failed = false; return f; }
     std::string err_;
     // decode buffers
     std::vector<DevBuf> col_vals, col_shash, col_spfx, col_soff, col_slen, col_pres, col_vbits, col_pcnt;

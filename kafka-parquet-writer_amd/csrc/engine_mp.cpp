@@ -205,6 +205,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ap.data_end = d_off + n; ap.collision = d_collision.as<uint32_t>();
     ap.page_pre = d_page_pre.as<uint64_t>();
     ap.mp = 1;
+    ap.seg = &seg_;
     ChunkArgs ad = ap;
     ad.ch = mp_dch.as<ChunkDesc>(); ad.nchunks = nc; ad.nctiles = ndt;
     ad.ctile_chunk = mp_dtile_chunk.as<uint32_t>(); ad.ctile_first = mp_dtile_first.as<uint32_t>();
@@ -246,7 +247,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         CK(hipMemcpyAsync(&coll, d_collision.p, 4, hipMemcpyDeviceToHost, st));
         CK(hipMemcpyAsync(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
         CK(hipStreamSynchronize(st));
-        if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+        if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
         for (int c = 0; c < nc; c++)
             if (dch[c].is_dict && dch[c].overflow) return fail(KPW_ERR_DEVICE, "multi-page dictionary table overflow");
         if (!coll) break;
@@ -308,7 +309,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         pages_dev_ = d_body.as<uint8_t>();
         pages_len_ = body_tot;
     }
-    if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+    if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
     // ---------------------------------------------------------------- page metadata
     CK(hipMemcpyAsync(pg.data(), d_chunks.p, npg * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
@@ -423,7 +424,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     uint64_t Ptot = 0;
     CK(hipMemcpyAsync(&Ptot, d_P.as<uint64_t>() + ne, 8, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
-    if (seg_scan_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+    if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
 
     PageCutArgs a{};
     a.n = ne; a.ncols = nc; a.page_size = props.page_size; a.cols = d_cols.as<DevCol>();

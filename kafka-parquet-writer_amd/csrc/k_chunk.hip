@@ -826,8 +826,8 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
     hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
                        a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0);
-    seg_tile_scan_u32(a.tile_cnt, a.tile_cnt, a.ctile_chunk, a.nctiles, s);
-    seg_tile_scan_u64(a.tile_sz, a.tile_sz, a.ctile_chunk, a.nctiles, s);
+    seg_tile_scan_u32(a.tile_cnt, a.tile_cnt, a.ctile_chunk, a.nctiles, a.seg, s);
+    seg_tile_scan_u64(a.tile_sz, a.tile_sz, a.ctile_chunk, a.nctiles, a.seg, s);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
                        a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1);
     hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht_id, a.ids,
@@ -861,7 +861,7 @@ void launch_chunk_write(const ChunkArgs &a, const RleJob *jobs, uint8_t *out, hi
     if (!a.mp)   // multi-page: the dictionary page is written from the dictionary descriptors
         hipLaunchKernelGGL(k_dict_page, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
                            a.ent_rec, a.ent_boff, out);
-    seg_tile_scan_u64(a.tile_raw, a.tile_raw_off, a.ctile_chunk, a.nctiles, s);
+    seg_tile_scan_u64(a.tile_raw, a.tile_raw_off, a.ctile_chunk, a.nctiles, a.seg, s);
     hipLaunchKernelGGL(k_plain, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
                        a.tile_raw_off, out);
     hipLaunchKernelGGL(k_plain_bool, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, out);

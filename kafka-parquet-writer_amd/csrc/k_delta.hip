@@ -397,7 +397,7 @@ void launch_delta_structure(const DeltaArgs &d, hipStream_t s)
     if (!d.nblk) return;
     hipLaunchKernelGGL(k_delta_blocks, dim3(d.nblk), dim3(64), 0, s, (const DeltaJob *)d.jobs, d.blk_job, d.blk_min, d.blk_w,
                        d.blk_sz);
-    seg_tile_scan<uint64_t, OpSum64>(d.blk_sz, d.blk_off, d.blk_job, d.nblk, d.btot, s);
+    seg_tile_scan<uint64_t, OpSum64>(d.blk_sz, d.blk_off, d.blk_job, d.nblk, d.btot, d.seg, s);
     hipLaunchKernelGGL(k_delta_totals, dim3((d.njobs + 255) / 256), dim3(256), 0, s, d.jobs, (int)d.njobs, (const uint64_t *)d.btot);
 }
 
@@ -422,7 +422,7 @@ void launch_v2_dense(const ChunkArgs &a, uint64_t *dense, uint32_t *pre, uint32_
                        a.ctile_first, dense);
     hipLaunchKernelGGL(k_dba_lengths, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, (const ChunkDesc *)a.ch, a.cols, a.data,
                        a.ctile_chunk, a.ctile_first, (const uint64_t *)dense, pre, sfx, tile_sfx);
-    seg_tile_scan<uint64_t, OpSum64>(tile_sfx, tile_sfx_off, a.ctile_chunk, a.nctiles, chunk_sfx, s);
+    seg_tile_scan<uint64_t, OpSum64>(tile_sfx, tile_sfx_off, a.ctile_chunk, a.nctiles, chunk_sfx, a.seg, s);
 }
 
 void launch_dba_suffixes(const ChunkArgs &a, const uint32_t *pre, const DeltaJob *djobs, const uint64_t *tile_sfx_off, uint8_t *out,

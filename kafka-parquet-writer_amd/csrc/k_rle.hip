@@ -373,26 +373,26 @@ void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t
 {
     if (!njobs || !n_ptiles) return;
     hipLaunchKernelGGL(k_rle_bounds, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.last_brk);
-    seg_tile_scan<int64_t, OpMaxI64>(sc.last_brk, sc.prev_brk, sc.ptile_job, n_ptiles, nullptr, s);
+    seg_tile_scan<int64_t, OpMaxI64>(sc.last_brk, sc.prev_brk, sc.ptile_job, n_ptiles, nullptr, sc.seg, s);
     hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.prev_brk,
                        sc.lr_cnt, sc.lr_off, sc.lr_a, sc.lr_b, 0);
     // n_long per job lands in jobs[j].n_long via the job-total pointer trick below
-    seg_tile_scan<uint32_t, OpSum32>(sc.lr_cnt, sc.lr_off, sc.ptile_job, n_ptiles, sc.job_nlong, s);
+    seg_tile_scan<uint32_t, OpSum32>(sc.lr_cnt, sc.lr_off, sc.ptile_job, n_ptiles, sc.job_nlong, sc.seg, s);
     hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.prev_brk,
                        sc.lr_cnt, sc.lr_off, sc.lr_a, sc.lr_b, 1);
     launch_rle_store_counts(jobs_d, njobs, sc.job_nlong, 0, s);
     hipLaunchKernelGGL(k_phase_reduce, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b, sc.emap);
-    seg_tile_scan<uint32_t, OpMapCompose>(sc.emap, sc.emap_pre, sc.etile_job, n_etiles, nullptr, s);
+    seg_tile_scan<uint32_t, OpMapCompose>(sc.emap, sc.emap_pre, sc.etile_job, n_etiles, nullptr, sc.seg, s);
     hipLaunchKernelGGL(k_phase_apply, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b,
                        sc.emap_pre, sc.r_cnt, sc.r_off, sc.r_g, sc.r_b, 0);
-    seg_tile_scan<uint32_t, OpSum32>(sc.r_cnt, sc.r_off, sc.etile_job, n_etiles, sc.job_nrle, s);
+    seg_tile_scan<uint32_t, OpSum32>(sc.r_cnt, sc.r_off, sc.etile_job, n_etiles, sc.job_nrle, sc.seg, s);
     hipLaunchKernelGGL(k_phase_apply, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b,
                        sc.emap_pre, sc.r_cnt, sc.r_off, sc.r_g, sc.r_b, 1);
     launch_rle_store_counts(jobs_d, njobs, sc.job_nrle, 1, s);
     hipLaunchKernelGGL(k_r_sizes, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b,
                        sc.r_bytes, sc.r_groups, sc.et_bytes, sc.et_groups);
-    seg_tile_scan<uint64_t, OpSum64>(sc.et_bytes, sc.et_bytes, sc.etile_job, n_etiles, sc.job_btot, s);
-    seg_tile_scan<uint64_t, OpSum64>(sc.et_groups, sc.et_groups, sc.etile_job, n_etiles, sc.job_gtot, s);
+    seg_tile_scan<uint64_t, OpSum64>(sc.et_bytes, sc.et_bytes, sc.etile_job, n_etiles, sc.job_btot, sc.seg, s);
+    seg_tile_scan<uint64_t, OpSum64>(sc.et_groups, sc.et_groups, sc.etile_job, n_etiles, sc.job_gtot, sc.seg, s);
     hipLaunchKernelGGL(k_r_finalize, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_b, sc.r_bytes,
                        sc.r_groups, sc.et_bytes, sc.et_groups, sc.job_btot, sc.job_gtot, sc.r_boff, sc.r_goff);
 }

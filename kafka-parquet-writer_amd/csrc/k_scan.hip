@@ -231,45 +231,35 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_seg_apply(const T *in, T *out, co
     }
 }
 
-// scratch for the multi-block scans (per-chunk pairs), grown on demand.  Thread-local and
-// per device: writer handles are used by one thread at a time, each encode is blocking, so
-// a thread's scans never overlap.
-struct SegScratch { void *p = nullptr; size_t bytes = 0; };
-static thread_local SegScratch g_seg_scratch[16];
-static thread_local bool g_seg_failed = false;
-
-bool seg_scan_failed_reset()
+void seg_scratch_free(SegScratch &sc)
 {
-    const bool f = g_seg_failed;
-    g_seg_failed = false;
-    return f;
+    if (sc.p) (void)hipFree(sc.p);
+    sc.p = nullptr;
+    sc.bytes = 0;
 }
 
 template <typename T, typename Op>
-void seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, hipStream_t s)
+void seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, SegScratch *sc, hipStream_t s)
 {
     if (!n) return;
     const uint32_t nb = (n + SEG_CH - 1) / SEG_CH;
     const size_t need = (size_t)nb * (sizeof(T) + sizeof(uint32_t)) + 64;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    SegScratch &sc = g_seg_scratch[dev & 15];
-    if (need > sc.bytes) {
-        if (sc.p) { (void)hipStreamSynchronize(s); (void)hipFree(sc.p); }
-        sc.bytes = need * 2;
-        if (hipMalloc(&sc.p, sc.bytes) != hipSuccess) { sc.p = nullptr; sc.bytes = 0; g_seg_failed = true; return; }
+    if (need > sc->bytes) {
+        // earlier scans of this handle may still read the old buffer on `s`
+        if (sc->p) { (void)hipStreamSynchronize(s); (void)hipFree(sc->p); }
+        sc->bytes = need * 2;
+        if (hipMalloc(&sc->p, sc->bytes) != hipSuccess) { sc->p = nullptr; sc->bytes = 0; sc->failed = true; return; }
     }
-    void *g_seg_scratch = sc.p;
-    T *bv = (T *)g_seg_scratch;
-    uint32_t *bh = (uint32_t *)((char *)g_seg_scratch + (((size_t)nb * sizeof(T) + 15) & ~(size_t)15));
+    T *bv = (T *)sc->p;
+    uint32_t *bh = (uint32_t *)((char *)sc->p + (((size_t)nb * sizeof(T) + 15) & ~(size_t)15));
     hipLaunchKernelGGL((k_seg_reduce<T, Op>), dim3(nb), dim3(KPW_BLOCK), 0, s, in, seg, n, bv, bh);
     hipLaunchKernelGGL((k_seg_carry<T, Op>), dim3(1), dim3(64), 0, s, bv, (const uint32_t *)bh, nb);
     hipLaunchKernelGGL((k_seg_apply<T, Op>), dim3(nb), dim3(KPW_BLOCK), 0, s, in, out, seg, n, tot, (const T *)bv);
 }
 
-template void seg_tile_scan<uint32_t, OpSum32>(const uint32_t *, uint32_t *, const uint32_t *, uint32_t, uint32_t *, hipStream_t);
-template void seg_tile_scan<uint64_t, OpSum64>(const uint64_t *, uint64_t *, const uint32_t *, uint32_t, uint64_t *, hipStream_t);
-template void seg_tile_scan<int64_t, OpMaxI64>(const int64_t *, int64_t *, const uint32_t *, uint32_t, int64_t *, hipStream_t);
-template void seg_tile_scan<uint32_t, OpMapCompose>(const uint32_t *, uint32_t *, const uint32_t *, uint32_t, uint32_t *, hipStream_t);
+template void seg_tile_scan<uint32_t, OpSum32>(const uint32_t *, uint32_t *, const uint32_t *, uint32_t, uint32_t *, SegScratch *, hipStream_t);
+template void seg_tile_scan<uint64_t, OpSum64>(const uint64_t *, uint64_t *, const uint32_t *, uint32_t, uint64_t *, SegScratch *, hipStream_t);
+template void seg_tile_scan<int64_t, OpMaxI64>(const int64_t *, int64_t *, const uint32_t *, uint32_t, int64_t *, SegScratch *, hipStream_t);
+template void seg_tile_scan<uint32_t, OpMapCompose>(const uint32_t *, uint32_t *, const uint32_t *, uint32_t, uint32_t *, SegScratch *, hipStream_t);
 
 }  // namespace kpw

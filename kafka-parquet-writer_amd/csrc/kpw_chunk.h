@@ -36,6 +36,7 @@ struct ChunkArgs {
     uint64_t *page_pre;            // v2: uncompressed level bytes in front of each page's values
     int32_t mp;                    // multi-page regime: descriptors are pages (dictionary decided per chunk)
     int32_t pad_mp;
+    SegScratch *seg;               // the handle's segmented-scan scratch
 };
 
 // Multi-page (v1): page descriptors `pg` (ChunkArgs of the pages) and dictionary
@@ -57,6 +58,7 @@ struct DeltaArgs {
     const uint32_t *blk_job;
     uint64_t *blk_min, *blk_sz, *blk_off, *btot;
     uint32_t *blk_w;
+    SegScratch *seg;
 };
 void launch_delta_structure(const DeltaArgs &d, hipStream_t s);
 void launch_delta_write(const DeltaArgs &d, uint8_t *out, hipStream_t s);
@@ -69,13 +71,13 @@ void launch_v2_bool_jobs(const ChunkArgs &a, RleJob *jobs, hipStream_t s);
 void launch_bool_streams(const DevCol *cols, const uint32_t *bool_cols, uint32_t nbool, uint64_t n, uint64_t *const *cbits,
                          RleJob *jobs, uint32_t job0, PlanStream *streams, uint32_t stream0, hipStream_t s);
 
-inline void seg_tile_scan_u32(const uint32_t *in, uint32_t *out, const uint32_t *seg, uint32_t n, hipStream_t s)
+inline void seg_tile_scan_u32(const uint32_t *in, uint32_t *out, const uint32_t *seg, uint32_t n, SegScratch *sc, hipStream_t s)
 {
-    seg_tile_scan<uint32_t, OpSum32>(in, out, seg, n, nullptr, s);
+    seg_tile_scan<uint32_t, OpSum32>(in, out, seg, n, nullptr, sc, s);
 }
-inline void seg_tile_scan_u64(const uint64_t *in, uint64_t *out, const uint32_t *seg, uint32_t n, hipStream_t s)
+inline void seg_tile_scan_u64(const uint64_t *in, uint64_t *out, const uint32_t *seg, uint32_t n, SegScratch *sc, hipStream_t s)
 {
-    seg_tile_scan<uint64_t, OpSum64>(in, out, seg, n, nullptr, s);
+    seg_tile_scan<uint64_t, OpSum64>(in, out, seg, n, nullptr, sc, s);
 }
 
 void launch_chunk_stats(const ChunkArgs &a, hipStream_t s);

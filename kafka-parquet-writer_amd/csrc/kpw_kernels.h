@@ -42,6 +42,15 @@ struct DecodeArgs {
     unsigned long long *err_min;
 };
 
+// Device scratch of the multi-block segmented scans (k_scan.hip), owned by one encoder
+// handle (Engine::seg_) and grown on demand.  Scans of one handle run in order on its own
+// stream, so they share it; handles never share one (concurrent writers, C5).
+struct SegScratch {
+    void *p = nullptr;
+    size_t bytes = 0;
+    bool failed = false;           // an allocation failed since the engine last checked
+};
+
 // Generic RLE/bit-packing hybrid job (one encoded stream).
 struct ValSrcH {
     uint32_t kind, pad;
@@ -82,6 +91,7 @@ struct RleScratch {
     // per job
     uint32_t *job_nlong, *job_nrle;
     uint64_t *job_btot, *job_gtot;
+    SegScratch *seg;               // the handle's segmented-scan scratch
 };
 
 // Plan / chunk descriptors -------------------------------------------------------------

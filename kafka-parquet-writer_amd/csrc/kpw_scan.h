@@ -15,11 +15,10 @@ uint64_t mj_scan_tmp_words(uint64_t len, uint32_t njobs);
 void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, uint64_t *tmp, hipStream_t s);
 void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, uint64_t *tmp, hipStream_t s);
 
-// true if a segmented scan could not allocate its scratch since the last call (the scan was
-// skipped: the caller must fail the encode)
-bool seg_scan_failed_reset();
-
+// Exclusive segmented scan over tile aggregates.  If the scratch cannot grow, the scan is
+// skipped and sc->failed is set: the caller must fail the encode.
 template <typename T, typename Op>
-void seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, hipStream_t s);
+void seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, SegScratch *sc, hipStream_t s);
+void seg_scratch_free(SegScratch &sc);
 
 }  // namespace kpw

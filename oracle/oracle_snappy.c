@@ -19,6 +19,18 @@
  *   - literals: tag (len-1)<<2 when len <= 60, else 60..63 with 1..4 length bytes.
  * Byte identity of this choice to the snappy-java build parquet-mr 1.10.1 resolves is
  * UNPINNED offline (no jar here); every stream is checked by pyarrow's Snappy decoder.
+ *
+ * ATTRIBUTION: the fragment compressor below follows the structure and names of Google
+ * Snappy 1.1.2's snappy.cc (CompressFragment, EmitLiteral, EmitCopy, FindMatchLength;
+ * ip_limit, next_emit, bytes_between_hash_lookups, ...).  Snappy is
+ *   Copyright 2005 and onwards Google Inc.
+ * distributed under the BSD 3-Clause license: redistribution in source and binary forms,
+ * with or without modification, is permitted provided that the copyright notice, this list
+ * of conditions and the disclaimer are retained, and that neither the name of Google Inc.
+ * nor the names of its contributors are used to endorse or promote derived products
+ * without specific prior written permission.  THE SOFTWARE IS PROVIDED "AS IS", WITHOUT
+ * ANY EXPRESS OR IMPLIED WARRANTIES.  It is test infrastructure here: nothing in
+ * libkpw_gpu.so links or includes it.
  */
 #include <stdint.h>
 #include <string.h>

@@ -61,19 +61,27 @@ def oracle_row_groups(fb):
     return out
 
 
+def oracle_props(**kw):
+    return oracle.make_props(block_size=kw.get("block_size", 128 * MiB), page_size=kw.get("page_size", 128 * MiB),
+                             codec=kw.get("codec", 0), enable_dictionary=kw.get("dictionary", True),
+                             writer_version=kw.get("writer_version", 1))
+
+
 def compare_pages(schema, data, offsets, **kw):
     """Returns a list of human-readable mismatches (empty = byte-identical pages)."""
-    codec = kw.get("codec", 0)
-    props = oracle.make_props(block_size=kw.get("block_size", 128 * MiB), page_size=kw.get("page_size", 128 * MiB),
-                              codec=codec, enable_dictionary=kw.get("dictionary", True),
-                              writer_version=kw.get("writer_version", 1))
-    fb = oracle.encode_file(schema, data, offsets, props)
+    fb = oracle.encode_file(schema, data, offsets, oracle_props(**kw))
+    return compare_to_file(schema, data, offsets, fb, **kw)[0]
+
+
+def compare_to_file(schema, data, offsets, fb, **kw):
+    """HIP encoder pages of the batch vs the pages of the oracle file `fb`.
+    Returns (mismatches, batch info)."""
     rgs, gpages, info, enc = gpu_encoder_pages(schema, data, offsets, **kw)
     errs = []
     orgs = oracle_row_groups(fb)
     if [tuple(r) for r in rgs] != [tuple(r) for r in orgs]:
         errs.append("row groups differ: gpu %r oracle %r" % (rgs[:8], orgs[:8]))
-        return errs
+        return errs, info
     op = oracle_pages(fb)
     for rg, col, pl in gpages:
         ol = op.get((rg, col), [])
@@ -116,7 +124,7 @@ def compare_pages(schema, data, offsets, **kw):
                 i = next((j for j in range(min(len(a), len(b))) if a[j] != b[j]), min(len(a), len(b)))
                 errs.append("rg %d col %s page %d type %d: body differs at byte %d (len gpu %d oracle %d): gpu %s oracle %s" % (
                     rg, name, k, ptype, i, len(a), len(b), a[max(0, i - 8):i + 16].hex(), b[max(0, i - 8):i + 16].hex()))
-    return errs
+    return errs, info
 
 
 def gpu_file(schema, data, offsets, props=None, batches=1):

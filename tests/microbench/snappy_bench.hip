@@ -1,4 +1,4 @@
-// snappy_bench.hip — test-infrastructure microbenchmark for K7 (k_snappy_frag) variants.
+// snappy_bench.hip — test-infrastructure microbenchmark for K7 variants.
 //
 // Builds synthetic pages shaped like the C2 workload's columns, compresses them with each
 // search variant (SEQ = sequential probes per literal search before 64-wide batches) and
@@ -6,6 +6,7 @@
 // (oracle/oracle_snappy.c, linked as the checker only).  Prints one line per (page, variant).
 //   make -C tests/microbench && tests/microbench/build/snappy_bench
 #include "../../kafka-parquet-writer_amd/csrc/k_snappy.hip"
+#include "snappy_variants.hip"
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>

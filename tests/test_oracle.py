@@ -19,6 +19,7 @@ import oracle
 import pqwalk
 import protoutil
 import synth
+import wire_cases
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SPEC = json.load(open(os.path.join(HERE, "golden", "spec_vectors.json")))
@@ -176,60 +177,25 @@ def test_delta_byte_array_matches_pyarrow(n):
 
 
 def _sample_msg(**kw):
-    cls = protoutil.message_class(synth.SAMPLE)
-    m = cls()
-    for k, v in kw.items():
-        setattr(m, k, v)
-    return m
+    return wire_cases.sample_msg(**kw)
 
 
-def _varint(v):
-    out = bytearray()
-    v &= (1 << 64) - 1
-    while v >= 0x80:
-        out.append((v & 0x7F) | 0x80)
-        v >>= 7
-    out.append(v)
-    return bytes(out)
-
-
-def _tag(f, wt):
-    return _varint((f << 3) | wt)
+_varint = wire_cases.varint
 
 
 def test_proto_edge_cases_accepted():
     """Unknown fields skipped, last occurrence wins, any field order, 10-byte negative
     int32, unknown groups, known number with a foreign wire type treated as unknown
-    (protobuf-java generated switch-on-tag; TestMessage.java:85-139)."""
-    base = _sample_msg(query="q", timestamp=7).SerializeToString()
-    recs = [
-        base,
-        _sample_msg(query="a", timestamp=1, page_number=-5).SerializeToString(),   # 10-byte varint
-        base + _tag(99, 0) + _varint(12345) + _tag(98, 2) + _varint(3) + b"xyz",  # unknown fields
-        base + _tag(2, 0) + _varint(42),                                         # last wins
-        _tag(4, 0) + _varint(9) + _tag(2, 0) + _varint(3) + _tag(1, 2) + b"\x02hi",  # reordered
-        base + _tag(50, 3) + _tag(51, 0) + _varint(1) + _tag(52, 3) + _tag(53, 5) + b"wxyz" + _tag(52, 4) + _tag(50, 4),  # nested unknown groups
-        base + _tag(3, 2) + b"\x01z",                                           # page_number as LEN: unknown
-        base + _tag(60, 5) + b"abcd" + _tag(61, 1) + b"12345678",                # fixed32/fixed64 unknown
-        _sample_msg(query="", timestamp=0, page_number=0, result_per_page=-1).SerializeToString(),
-    ]
+    (protobuf-java generated switch-on-tag; TestMessage.java:85-139).  The same records go
+    through the HIP decoder in test_gpu_wire.py."""
+    recs = [r for _, r in wire_cases.accepted()]
     data, offs = synth.pack(recs)
     fb = oracle.encode_file(synth.SAMPLE, data, offs)
     _readback(synth.SAMPLE, recs, fb)
 
 
-@pytest.mark.parametrize("bad", [
-    _tag(2, 0) + _varint(1),                                   # missing required query
-    _tag(1, 2) + b"\x05ab",                                    # truncated length-delimited
-    _tag(1, 2) + b"\x01a" + _tag(2, 0) + b"\x80",              # truncated varint
-    _tag(1, 2) + b"\x01a" + _tag(2, 0) + b"\x80" * 10 + b"\x01",  # varint > 10 bytes
-    _tag(1, 2) + b"\x01a" + _tag(2, 0) + _varint(1) + _tag(7, 6),  # wire type 6
-    _tag(1, 2) + b"\x01a" + _tag(2, 0) + _varint(1) + b"\x00",  # field number 0
-    _tag(1, 2) + b"\x01a" + _tag(2, 0) + _varint(1) + _tag(9, 4),  # stray end-group
-    _tag(1, 2) + b"\x01a" + _tag(2, 0) + _varint(1) + _tag(9, 3) + _tag(8, 4),  # mismatched end-group
-    _tag(1, 2) + b"\x01a" + _tag(2, 1) + b"\x01\x02",          # required timestamp as fixed64: unknown -> missing
-])
-def test_proto_invalid_rejected(bad):
+@pytest.mark.parametrize("label,bad", wire_cases.invalid(), ids=[c[0] for c in wire_cases.invalid()])
+def test_proto_invalid_rejected(label, bad):
     w = oracle.OracleWriter(synth.SAMPLE)
     good = _sample_msg(query="x", timestamp=1).SerializeToString()
     w.write(good)
@@ -239,6 +205,51 @@ def test_proto_invalid_rejected(bad):
     assert w.num_records() == 1
     w.close()
     _readback(synth.SAMPLE, [good], w.file_bytes())
+    # google.protobuf's own parser rejects it too (the reference's parseFrom would throw)
+    cls = protoutil.message_class(synth.SAMPLE)
+    with pytest.raises(Exception):
+        m = cls.FromString(bad)
+        if not m.IsInitialized():
+            raise ValueError("missing required")
+
+
+DESC = json.load(open(os.path.join(HERE, "golden", "test_message_descriptor.json")))
+
+
+def _kv(fb):
+    return {kv[1].decode(): kv[2].decode() for kv in pqwalk.footer(fb)[5]}
+
+
+def test_descriptor_fixture_matches_sample_schema():
+    """The schema the tests use for the reference's test message equals the descriptor the
+    reference itself holds (TestMessage.java:750-755 descriptorData, decoded into
+    tests/golden/test_message_descriptor.json by make_descriptor_fixture.py)."""
+    from google.protobuf import descriptor_pb2
+    fdp = descriptor_pb2.FileDescriptorProto.FromString(bytes.fromhex(DESC["file_descriptor_hex"]))
+    assert [[f.name, f.number, f.type, f.label] for f in fdp.message_type[0].field] == DESC["columns"]
+    assert [list(c) for c in synth.SAMPLE.columns] == DESC["columns"]
+    assert synth.SAMPLE.message_name == DESC["message_full_name"]
+    assert synth.SAMPLE.proto_class == DESC["proto_class"]
+
+
+def test_footer_pinned_to_reference_descriptor():
+    """ProtoWriteSupport.init's extra metadata (parquet-protobuf 1.10.1): parquet.proto.class
+    = the message class, parquet.proto.descriptor = TextFormat of descriptor.toProto();
+    ProtoSchemaConverter: schema name = full name, one REQUIRED/OPTIONAL leaf per field with
+    field_id = field number, strings as BINARY/UTF8."""
+    data, offs = synth.generate(synth.KIND_SAMPLE, 3, 200)
+    fb = oracle.encode_file(synth.SAMPLE, data, offs)
+    kv = _kv(fb)
+    assert kv["parquet.proto.descriptor"] == DESC["descriptor_text"]
+    assert kv["parquet.proto.class"] == DESC["proto_class"]
+    assert kv["writer.model.name"] == "protobuf"
+    schema = pqwalk.footer(fb)[2]
+    assert schema[0][4].decode() == DESC["message_full_name"] and schema[0][5] == len(DESC["columns"])
+    phys = {9: 6, 3: 2, 5: 1}   # TYPE_STRING -> BYTE_ARRAY, TYPE_INT64 -> INT64, TYPE_INT32 -> INT32
+    for el, (name, number, ptype, label) in zip(schema[1:], DESC["columns"]):
+        assert el[4].decode() == name and el[9] == number and el[1] == phys[ptype]
+        assert el[3] == (0 if label == 2 else 1)            # REQUIRED / OPTIONAL
+        assert (el.get(6) == 0) == (ptype == 9)             # ConvertedType UTF8 for strings
 
 
 def _chunk_encodings(fb):
