@@ -44,9 +44,21 @@ kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, const kpw_prop
 
 /* n x { parser.parseFrom(value); ParquetFile.write(T) } — KafkaProtoParquetWriter.java:268-277,
  * ParquetFile.java:59-62.  data/offsets are host memory; record i is
- * data[offsets[i] .. offsets[i+1]).  On an invalid record returns KPW_ERR_INVALID_PROTO:
- * the records before it are written, it and the rest are not (kpw_writer_failed_record). */
+ * data[offsets[i] .. offsets[i+1]); the caller may reuse both when the call returns.  Data in a
+ * kpw_host_alloc buffer is DMA'd to the device directly; other memory takes one host copy.
+ * On an invalid record the call returns KPW_ERR_INVALID_PROTO: the records before it are
+ * written, it and the rest are not (kpw_writer_failed_record).  For writes of <= 65536 records
+ * that is reported by this call (the reference throws at parseFrom); larger writes are
+ * validated on the GPU and the error surfaces at the next call (write / getDataSize / close),
+ * with kpw_writer_num_records corrected then.  The writer accepts no records after it;
+ * close() writes the ones before it. */
 int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n);
+
+/* Pinned (page-locked) host memory for record batches: where polled Kafka batches are meant
+ * to land (north_star: "pinned host staging buffers"), so kpw_writer_write can DMA them to
+ * HBM without a host copy.  Thread-safe; any writer handle on any device may read them. */
+void *kpw_host_alloc(uint64_t bytes, int *status);
+void kpw_host_free(void *p);
 
 /* The WorkerThread size-rotation loop (KafkaProtoParquetWriter.java:277-285,306-308):
  * writes records in order and stops right after the first one for which
@@ -58,7 +70,11 @@ int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64_t *offsets
 int kpw_writer_write_until_full(kpw_writer *w, const uint8_t *data, const uint64_t *offsets,
                                 uint64_t n, int64_t max_file_size, uint64_t *n_accepted, int *full);
 
-int64_t kpw_writer_data_size(kpw_writer *w);        /* getDataSize()          ParquetFile.java:77-79 */
+/* getDataSize() — ParquetFile.java:77-79, parquet-mr InternalParquetRecordWriter.getDataSize()
+ * (lastRowGroupEndPos + buffered).  With writes of <= 65536 records (the WorkerThread loop) an
+ * exact host model answers in O(1) and cuts row groups on the host; after a larger write the
+ * staged records are encoded to answer.  -1 on failure (see kpw_writer_failed_record). */
+int64_t kpw_writer_data_size(kpw_writer *w);
 int64_t kpw_writer_num_records(const kpw_writer *w); /* getNumWrittenRecords() ParquetFile.java:81-83 */
 int64_t kpw_writer_creation_time_ms(const kpw_writer *w); /* getCreationDate()  ParquetFile.java:70-72 */
 int kpw_writer_close(kpw_writer *w);                 /* close() (idempotent)   ParquetFile.java:65-68 */

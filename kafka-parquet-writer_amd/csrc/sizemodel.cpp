@@ -1,0 +1,246 @@
+// sizemodel.cpp — host model of getDataSize() for the per-record loop (see sizemodel.h).
+#include "sizemodel.h"
+
+#include <climits>
+#include <cstring>
+
+namespace kpw {
+
+namespace {
+
+// Java (int)f / (long)f: NaN -> 0, saturating, truncation toward zero.
+int32_t java_f2i(float f)
+{
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return INT32_MAX;
+    if (f <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)f;
+}
+int64_t java_f2l(float f)
+{
+    if (f != f) return 0;
+    if (f >= 9223372036854775808.0f) return INT64_MAX;
+    if (f <= -9223372036854775808.0f) return INT64_MIN;
+    return (int64_t)f;
+}
+int64_t jadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }   // Java long overflow
+
+uint32_t varint_len(uint32_t v)
+{
+    uint32_t n = 1;
+    while (v >= 0x80u) { v >>= 7; n++; }
+    return n;
+}
+
+// CodedInputStream.readRawVarint64: at most 10 bytes
+inline bool varint64(const uint8_t *d, uint64_t &pos, uint64_t end, uint64_t &out)
+{
+    uint64_t r = 0;
+    for (int i = 0; i < 10; i++) {
+        if (pos >= end) return false;
+        const uint8_t b = d[pos++];
+        r |= (uint64_t)(b & 0x7f) << (7 * i);
+        if (!(b & 0x80)) { out = r; return true; }
+    }
+    return false;
+}
+
+// skipField for an unknown field whose tag was read (k_decode.hip skip_field rules)
+bool skip_field(const uint8_t *d, uint64_t &pos, uint64_t end, uint32_t tag)
+{
+    uint64_t v;
+    switch (tag & 7) {
+    case 0: return varint64(d, pos, end, v);
+    case 1: if (end - pos < 8) return false; pos += 8; return true;
+    case 2:
+        if (!varint64(d, pos, end, v) || (int32_t)(uint32_t)v < 0 || end - pos < (uint32_t)v) return false;
+        pos += (uint32_t)v;
+        return true;
+    case 5: if (end - pos < 4) return false; pos += 4; return true;
+    case 3: {
+        uint32_t stack[100];
+        int depth = 0;
+        stack[depth++] = tag >> 3;
+        while (depth > 0) {
+            uint64_t t64;
+            if (!varint64(d, pos, end, t64)) return false;
+            const uint32_t t = (uint32_t)t64, w = t & 7;
+            if ((t >> 3) == 0) return false;
+            if (w == 4) {
+                if ((t >> 3) != stack[depth - 1]) return false;
+                depth--;
+            } else if (w == 3) {
+                if (depth >= 100) return false;
+                stack[depth++] = t >> 3;
+            } else if (w == 0) {
+                if (!varint64(d, pos, end, v)) return false;
+            } else if (w == 1) {
+                if (end - pos < 8) return false;
+                pos += 8;
+            } else if (w == 5) {
+                if (end - pos < 4) return false;
+                pos += 4;
+            } else if (w == 2) {
+                if (!varint64(d, pos, end, v) || (int32_t)(uint32_t)v < 0 || end - pos < (uint32_t)v) return false;
+                pos += (uint32_t)v;
+            } else {
+                return false;
+            }
+        }
+        return true;
+    }
+    default: return false;   // END_GROUP at top level, wire types 6 / 7
+    }
+}
+
+}  // namespace
+
+// RunLengthBitPackingHybridEncoder.writeInt (bit width 1), sizes only
+void RleCount::write(uint32_t v)
+{
+    if (v == prev) {
+        ++rc;
+        if (rc >= 8) return;                      // extends the RLE run
+    } else {
+        if (rc >= 8) {                            // writeRleRun: endPreviousBitPackedRun + header + value
+            hdr_open = false;
+            groups = 0;
+            out += varint_len((uint32_t)rc << 1) + 1;
+            rc = 0;
+            nbuf = 0;
+        }
+        rc = 1;
+        prev = v;
+    }
+    if (++nbuf == 8) {                            // writeOrAppendBitPackedRun
+        if (groups >= 63) { hdr_open = false; groups = 0; }
+        if (!hdr_open) { out += 1; hdr_open = true; }
+        out += 1;                                 // 8 values x 1 bit
+        nbuf = 0;
+        rc = 0;
+        ++groups;
+    }
+}
+
+int64_t SizeModel::Col::mem() const
+{
+    // ColumnWriterV1: rl (DevNull) + dl + data buffered sizes
+    return (optional ? dl.out : 0) + (phys == KPW_BOOLEAN ? (data + 7) / 8 : data);
+}
+
+bool SizeModel::init(const std::vector<ColInfo> &cols, const kpw_props &p)
+{
+    if (p.writer_version != 1 || p.page_size < p.block_size || p.dfs_block_size > 0) return false;
+    page_size_ = p.page_size;
+    block_size_ = p.block_size;
+    fmap_.assign(FMAP_SIZE, -1);
+    cols_.clear();
+    for (size_t c = 0; c < cols.size(); c++) {
+        Col k;
+        k.field_number = cols[c].field_number;
+        k.wire_type = cols[c].wire_type;
+        k.phys = cols[c].phys;
+        k.optional = cols[c].optional;
+        k.vsize = cols[c].vsize;
+        cols_.push_back(k);
+        if (cols[c].field_number < FMAP_SIZE) fmap_[cols[c].field_number] = (int16_t)c;
+    }
+    seen_.assign(cols_.size(), 0);
+    raw_.assign(cols_.size(), 0);
+    reset_store();
+    next_mem_check_ = 100;
+    return true;
+}
+
+void SizeModel::reset_store()
+{
+    for (Col &k : cols_) {
+        k.dl = RleCount();
+        k.data = 0;
+        k.value_count = 0;
+        k.next_check = 100;   // props.getMinRowCountForPageSizeCheck()
+    }
+    record_count_ = 0;
+}
+
+// parser.parseFrom(record.value()) validity + presence + raw sizes (K1's rules)
+bool SizeModel::scan(const uint8_t *d, uint64_t len)
+{
+    std::memset(seen_.data(), 0, seen_.size());
+    uint64_t pos = 0;
+    const uint64_t end = len;
+    while (pos < end) {
+        uint64_t t64;
+        if (!varint64(d, pos, end, t64)) return false;
+        const uint32_t tag = (uint32_t)t64, fno = tag >> 3, wt = tag & 7;
+        if (fno == 0) return false;
+        int c = -1;
+        if (fno < (uint32_t)FMAP_SIZE) c = fmap_[fno];
+        else
+            for (size_t k = 0; k < cols_.size(); k++)
+                if ((uint32_t)cols_[k].field_number == fno) { c = (int)k; break; }
+        if (c < 0 || (uint32_t)cols_[c].wire_type != wt) {
+            if (!skip_field(d, pos, end, tag)) return false;
+            continue;
+        }
+        uint64_t v;
+        switch (wt) {
+        case 0: if (!varint64(d, pos, end, v)) return false; raw_[c] = (uint32_t)cols_[c].vsize; break;
+        case 1: if (end - pos < 8) return false; pos += 8; raw_[c] = 8; break;
+        case 5: if (end - pos < 4) return false; pos += 4; raw_[c] = 4; break;
+        default:   // 2: length-delimited (BYTE_ARRAY: 4-byte length + bytes)
+            if (!varint64(d, pos, end, v) || (int32_t)(uint32_t)v < 0 || end - pos < (uint32_t)v) return false;
+            pos += (uint32_t)v;
+            raw_[c] = 4 + (uint32_t)v;
+            break;
+        }
+        seen_[c] = 1;
+    }
+    for (size_t c = 0; c < cols_.size(); c++)
+        if (!seen_[c] && !cols_[c].optional) return false;   // isInitialized: missing required field
+    return true;
+}
+
+int64_t SizeModel::buffered() const
+{
+    int64_t s = 0;
+    for (const Col &k : cols_) s += k.mem();
+    return s;
+}
+
+int SizeModel::add(const uint8_t *rec, uint64_t len)
+{
+    if (!scan(rec, len)) return INVALID;
+    for (size_t c = 0; c < cols_.size(); c++) {
+        Col &k = cols_[c];
+        const bool present = seen_[c] != 0;
+        if (k.optional) k.dl.write(present ? 1u : 0u);
+        if (present) k.data += k.phys == KPW_BOOLEAN ? 1 : raw_[c];
+        // ColumnWriterV1.accountForValueWritten
+        if (++k.value_count > k.next_check) {
+            const int64_t mem = k.mem();
+            if (mem > page_size_) return LEAVE;   // writePage inside the row group
+            float t = (float)k.value_count * (float)page_size_;
+            t = t / (float)mem;
+            k.next_check = java_f2i((float)k.value_count + t) / 2 + 1;
+        }
+    }
+    // InternalParquetRecordWriter.write -> checkBlockSizeReached
+    ++record_count_;
+    if (record_count_ >= next_mem_check_) {
+        const int64_t mem = buffered();
+        const int64_t rec_size = mem / record_count_;
+        if (mem > block_size_ - 2 * rec_size) {
+            reset_store();
+            next_mem_check_ = 100;   // min(max(100, recordCount / 2), 10000) with recordCount reset to 0
+            return CUT;
+        }
+        const int64_t est = jadd(record_count_, java_f2l((float)block_size_ / (float)rec_size)) / 2;
+        const int64_t a = est > 100 ? est : 100;
+        const int64_t b = jadd(record_count_, 10000);
+        next_mem_check_ = a < b ? a : b;
+    }
+    return OK;
+}
+
+}  // namespace kpw

@@ -1,0 +1,74 @@
+// sizemodel.h — exact host model of getDataSize() for the reference's per-record loop.
+//
+// The reference's WorkerThread writes ONE record and then asks ParquetFile.getDataSize()
+// (KafkaProtoParquetWriter.java:277-285,306-308 -> ParquetFile.java:77-79), i.e. parquet-mr
+// 1.10.1 InternalParquetRecordWriter.getDataSize() = lastRowGroupEndPos +
+// columnStore.getBufferedSize().  Answering that from the GPU would re-encode the open row
+// group per record, so the writer keeps this O(columns)-per-record model instead:
+//
+//   - a wire-length scan of each record (the K1 rules: field -> column, wire-type check, last
+//     occurrence wins, unknown fields and groups skipped, 10-byte varints, missing required
+//     -> invalid) giving presence and the raw (plain-equivalent) size of every column;
+//   - per column ColumnWriterV1's buffered size: definition-level RunLengthBitPackingHybrid
+//     encoder bytes emitted so far (counted, no bytes kept) + FallbackValuesWriter
+//     rawDataByteSize / PlainValuesWriter size / BooleanPlainValuesWriter (count+7)/8;
+//   - ColumnWriterV1.accountForValueWritten's sampled page check (a page cut inside the row
+//     group leaves the model: the writer then asks the GPU);
+//   - InternalParquetRecordWriter.checkBlockSizeReached's sampled row-group check with Java's
+//     float/long arithmetic.
+//
+// It decides row-group cuts on the host for this loop; the GPU encodes exactly those records
+// (the encoder's own planner plans the same cut, checked per row group).  Only PARQUET_1_0
+// with single-page chunks is modelled (the reference's configuration: pageSize defaults to
+// blockSize, KafkaProtoParquetWriter.java:473-474); other configurations keep the GPU path.
+#pragma once
+#include <stdint.h>
+#include <vector>
+
+#include "engine.h"
+
+namespace kpw {
+
+// RunLengthBitPackingHybridEncoder(bitWidth 1) byte count: BytesInput size after each
+// writeInt, without the bytes (the header byte of a bit-packed run is reserved when the run
+// opens, as in writeOrAppendBitPackedRun).
+struct RleCount {
+    int64_t out = 0;
+    uint32_t prev = 0;
+    int32_t rc = 0;
+    int32_t nbuf = 0;
+    int32_t groups = 0;
+    bool hdr_open = false;
+    void write(uint32_t v);
+};
+
+class SizeModel {
+public:
+    enum { OK = 0, CUT = 1, INVALID = -1, LEAVE = -2 };
+    // false if the configuration is outside the model (v2, multi-page, HDFS alignment)
+    bool init(const std::vector<ColInfo> &cols, const kpw_props &props);
+    // One record: OK, CUT (a row group ends with this record), INVALID (parseFrom would
+    // throw; nothing changed), LEAVE (a page cut: the model stops tracking this file).
+    int add(const uint8_t *rec, uint64_t len);
+    int64_t buffered() const;               // columnStore.getBufferedSize()
+    int64_t record_count() const { return record_count_; }
+
+private:
+    struct Col {
+        int32_t field_number, wire_type, phys, optional, vsize;
+        RleCount dl;
+        int64_t data = 0;                   // raw bytes (non-boolean) or boolean values
+        int32_t value_count = 0, next_check = 100;
+        int64_t mem() const;
+    };
+    bool scan(const uint8_t *rec, uint64_t len);
+    void reset_store();
+    std::vector<Col> cols_;
+    std::vector<int16_t> fmap_;             // field number (< 1024) -> column
+    std::vector<uint8_t> seen_;
+    std::vector<uint32_t> raw_;
+    int64_t page_size_ = 0, block_size_ = 0;
+    int64_t record_count_ = 0, next_mem_check_ = 100;
+};
+
+}  // namespace kpw

@@ -1,0 +1,1078 @@
+// writer.cpp — kpw_writer_*: the ParquetFile drop-in (include/kpw_gpu.h), PCIe-inclusive.
+//
+// Reference seam: ParquetFile<T> (src/main/java/ir/sahab/kafka/reader/ParquetFile.java:24-100)
+// driven by KafkaProtoParquetWriter.WorkerThread (write per record :277, getDataSize :281-285,
+// 306-308, close :326-337).
+//
+// Pipeline (north_star "pinned staging ... overlapped with encoding of the previous
+// row group"):
+//
+//   caller thread   write(): record bytes -> the fill stage buffer in HBM.  Pinned sources
+//                   (kpw_host_alloc, where polled batches are meant to land) are DMA'd
+//                   directly; other memory goes through pinned 32 MiB slots (one host copy).
+//                   Only the u64 record ends stay on the host.  A full stage buffer is handed
+//                   to the worker as a job and the caller goes on filling the next one.
+//   worker thread   per job: wait for the buffer's copies, upload its offsets, encode on the
+//                   handle's stream (K1..K7), carry the open row group's records to the next
+//                   stage buffer device-to-device, release the buffer, D2H the pages.
+//   assembly thread per job: page headers + bodies + row-group metadata into the file
+//                   (overlaps the next job's encode).
+//
+// Three stage buffers: one encoding, one queued, one filling.  Each starts with a gap of
+// `gap_` bytes where the previous job's open records are placed, so a job's records are
+// contiguous: [carried records | appended records].
+//
+// getDataSize() for the per-record loop: an exact host model of parquet-mr's buffered size and
+// row-group check (sizemodel.h) runs on every record of small writes, so getDataSize() is O(1)
+// and row groups are cut on the host exactly where parquet-mr cuts them; the GPU encodes those
+// records as complete row groups (jobs of kind EXACT).  Large writes (bulk path) leave the
+// model: their cuts are planned on the GPU (jobs of kind PLANNED) and getDataSize() drains the
+// pipeline and encodes what is staged.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/kpw_gpu.h"
+#include "engine.h"
+#include "filewriter.h"
+#include "sizemodel.h"
+
+using namespace kpw;
+
+namespace {
+
+double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// KPW_TRACE=1: per-job timings of the writer pipeline on stderr
+bool trace_on()
+{
+    static const bool v = [] { const char *e = getenv("KPW_TRACE"); return e && *e == '1'; }();
+    return v;
+}
+uint64_t env_mb(const char *name, uint64_t dflt)
+{
+    const char *e = getenv(name);
+    const long long v = e ? atoll(e) : 0;
+    return (uint64_t)(v > 0 ? v : (long long)dflt) << 20;
+}
+// Bytes of appended records per job.  KPW_STAGE_FLUSH_MB overrides.
+uint64_t stage_flush_bytes()
+{
+    static const uint64_t v = env_mb("KPW_STAGE_FLUSH_MB", 1024);
+    return v;
+}
+// Writes of more records than this leave the per-record size model (bulk path).
+uint64_t model_max_batch()
+{
+    static const uint64_t v = [] { const char *e = getenv("KPW_MODEL_MAX_BATCH"); return e ? (uint64_t)atoll(e) : 65536ull; }();
+    return v;
+}
+
+// ---- pinned host allocations handed out by kpw_host_alloc (direct-DMA sources)
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pins;
+
+bool pinned_range(const void *p, size_t n)
+{
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pins.upper_bound((uintptr_t)p);
+    if (it == g_pins.begin()) return false;
+    --it;
+    return (uintptr_t)p >= it->first && (uintptr_t)p + n <= it->first + it->second;
+}
+
+// Page-locked host memory owned by the library.
+struct PinnedBuf {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes)
+    {
+        if (bytes <= cap && p) return 0;
+        if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+        const size_t c = bytes + bytes / 4 + 4096;
+        if (hipHostMalloc((void **)&p, c, hipHostMallocDefault) != hipSuccess) { p = nullptr; return -1; }
+        cap = c;
+        return 0;
+    }
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+};
+
+enum { BUF_FREE = 0, BUF_FILLING = 1, BUF_QUEUED = 2 };
+enum { JOB_PLANNED = 0, JOB_EXACT = 1, JOB_FINAL = 2 };
+
+struct StageBuf {
+    uint8_t *d = nullptr;
+    size_t cap = 0;
+    uint64_t gap = 0;                  // first appended byte; carried records end here
+    uint64_t len = 0;                  // append position
+    std::vector<uint64_t> carry;       // carried record boundaries (worker-written; ncarry+1 or empty)
+    bool carry_in_store = false;       // carried records wait in kpw_writer::carry_store (did not fit the gap)
+    std::vector<uint64_t> ends;        // appended record ends (caller-written)
+    int64_t ncarry_expected = 0;       // carried records, as the caller knows them (EXACT jobs)
+    int64_t first_new_global = 0;      // file record index of the first appended record
+    int state = BUF_FREE;
+    hipEvent_t copied = nullptr;       // recorded on the copy stream after the last append
+};
+
+struct Job {
+    int buf, kind, next;
+    int64_t n_exact;                   // EXACT: records [0, n_exact) of the buffer form complete row groups
+};
+
+}  // namespace
+
+struct kpw_writer {
+    static constexpr int kBufs = 3;
+    static constexpr int kSlots = 4;
+    static constexpr size_t kSlotBytes = 32ull << 20;
+    Engine eng;
+    FileWriter *fw = nullptr;
+    hipStream_t copy_stream = nullptr;
+    StageBuf buf[kBufs];
+    int fill = -1;                     // buffer the caller appends to
+    uint64_t gap_ = 0;
+    // pinned slots for non-pinned sources
+    PinnedBuf slot[kSlots];
+    hipEvent_t slot_ev[kSlots] = {};
+    int cur_slot = 0;
+    uint64_t slot_used = 0, slot_dev = 0;   // pending bytes in the current slot and their device offset
+    hipEvent_t direct_ev = nullptr;
+    // caller-side state
+    int64_t num_records = 0;           // ParquetFile.numWrittenRecords
+    int64_t created_ms = 0;
+    int64_t failed_record = -1;
+    bool closed = false;
+    std::string err;
+    SizeModel model;
+    bool model_on = false;
+    bool dirty = false;                // records appended since the last PLANNED job (model off)
+    bool pending_cut = false;          // an EXACT job may not be in the file yet (lastRowGroupEndPos stale)
+    DevBuf probe_off;                  // write_until_full on the bulk path: offsets of staged prefixes
+    PinnedBuf probe_h;
+    // worker
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Job> q;
+    bool busy = false, stop = false;
+    std::thread worker;
+    int fatal_st = KPW_OK;             // first failure of the pipeline (sticky)
+    std::string fatal_err;
+    bool invalid_seen = false;         // worker found an invalid record (bulk path)
+    int64_t invalid_global = -1;
+    // worker-owned
+    DevBuf d_off, carry_store;
+    PinnedBuf h_off;
+    PinnedBuf host_pages[2];
+    int page_slot = 0;
+    hipEvent_t d2h_ev[2] = {};
+    std::thread assembler;
+    int asm_st = KPW_OK;
+    std::string asm_err;
+    BatchOut asm_out;
+    int64_t last_rg_end = 0;           // InternalParquetRecordWriter.lastRowGroupEndPos (assembly thread)
+    int64_t open_buffered = 0;         // open row group's buffered size after the last PLANNED job
+    double t_encode = 0, t_wait = 0;
+
+    ~kpw_writer();
+    int init_pipeline();
+};
+
+static int wfail(kpw_writer *w, int st, const std::string &m)
+{
+    w->err = m;
+    return st;
+}
+
+// Sticky pipeline failure (any thread).  Device / I/O failures lose records already taken off
+// staging, so every later call reports it (close() cannot retry them).
+static void set_fatal(kpw_writer *w, int st, const std::string &m)
+{
+    std::lock_guard<std::mutex> g(w->mu);
+    if (!w->fatal_st) { w->fatal_st = st; w->fatal_err = m; }
+    w->cv.notify_all();
+}
+
+static int check_fatal(kpw_writer *w)
+{
+    std::lock_guard<std::mutex> g(w->mu);
+    if (w->fatal_st) {
+        w->err = w->fatal_err;
+        return w->fatal_st;
+    }
+    return KPW_OK;
+}
+
+// ---------------------------------------------------------------- stage buffers
+
+static int alloc_buf(kpw_writer *w, StageBuf &b, size_t cap)
+{
+    uint8_t *nd = nullptr;
+    if (hipMalloc((void **)&nd, cap) != hipSuccess) return KPW_ERR_NOMEM;
+    if (b.d) (void)hipFree(b.d);
+    b.d = nd;
+    b.cap = cap;
+    return KPW_OK;
+}
+
+// Take a free buffer for filling (waits while the worker still holds all of them).
+static int acquire_fill(kpw_writer *w)
+{
+    int k = -1;
+    {
+        std::unique_lock<std::mutex> lk(w->mu);
+        for (;;) {
+            for (int i = 0; i < kpw_writer::kBufs; i++)
+                if (w->buf[i].state == BUF_FREE) { k = i; break; }
+            if (k >= 0 || w->fatal_st) break;
+            w->cv.wait(lk);
+        }
+        if (k < 0) return w->fatal_st;
+        w->buf[k].state = BUF_FILLING;
+    }
+    StageBuf &b = w->buf[k];
+    const size_t need = w->gap_ + stage_flush_bytes() + (64ull << 20);
+    if (b.cap < need && alloc_buf(w, b, need)) return wfail(w, KPW_ERR_NOMEM, "device stage buffer allocation failed");
+    b.gap = w->gap_;
+    b.len = w->gap_;
+    b.carry.clear();
+    b.carry_in_store = false;
+    b.ends.clear();
+    b.ncarry_expected = 0;
+    b.first_new_global = w->num_records;
+    w->fill = k;
+    return KPW_OK;
+}
+
+// Issue the H2D of the bytes pending in the current slot.
+static int flush_slot(kpw_writer *w)
+{
+    if (!w->slot_used) return KPW_OK;
+    const int k = w->cur_slot;
+    if (hipMemcpyAsync(w->buf[w->fill].d + w->slot_dev, w->slot[k].p, w->slot_used, hipMemcpyHostToDevice, w->copy_stream) !=
+            hipSuccess ||
+        hipEventRecord(w->slot_ev[k], w->copy_stream) != hipSuccess)
+        return wfail(w, KPW_ERR_DEVICE, "H2D of staged records failed");
+    w->cur_slot = (k + 1) % kpw_writer::kSlots;
+    w->slot_used = 0;
+    return KPW_OK;
+}
+
+// Append record bytes to the fill buffer at its append position.
+static int stage_bytes(kpw_writer *w, const uint8_t *src, uint64_t len)
+{
+    StageBuf &F = w->buf[w->fill];
+    if (pinned_range(src, len)) {
+        // direct DMA from the caller's pinned batch; waited for, so the caller may reuse it
+        if (int st = flush_slot(w)) return st;
+        if (hipMemcpyAsync(F.d + F.len, src, len, hipMemcpyHostToDevice, w->copy_stream) != hipSuccess ||
+            hipEventRecord(w->direct_ev, w->copy_stream) != hipSuccess || hipEventSynchronize(w->direct_ev) != hipSuccess)
+            return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
+        F.len += len;
+        return KPW_OK;
+    }
+    while (len) {
+        if (w->slot_used == 0) {
+            // reuse of this slot waits for its previous DMA
+            if (w->slot[w->cur_slot].p && hipEventSynchronize(w->slot_ev[w->cur_slot]) != hipSuccess)
+                return wfail(w, KPW_ERR_DEVICE, "staging slot wait failed");
+            if (w->slot[w->cur_slot].ensure(kpw_writer::kSlotBytes))
+                return wfail(w, KPW_ERR_NOMEM, "pinned staging allocation failed");
+            w->slot_dev = F.len;
+        }
+        const size_t piece = std::min<uint64_t>(len, kpw_writer::kSlotBytes - w->slot_used);
+        par_copy(w->slot[w->cur_slot].p + w->slot_used, src, piece);
+        w->slot_used += piece;
+        F.len += piece;
+        src += piece;
+        len -= piece;
+        if (w->slot_used == kpw_writer::kSlotBytes)
+            if (int st = flush_slot(w)) return st;
+    }
+    return KPW_OK;
+}
+
+// Make room for `bytes` more in the fill buffer.  Growing moves the buffer, so the worker
+// must not be placing a carry into it: wait for the pipeline to drain first.
+static int drain(kpw_writer *w);
+static int grow_fill(kpw_writer *w, uint64_t bytes)
+{
+    StageBuf &F = w->buf[w->fill];
+    if (F.len + bytes + 64 <= F.cap) return KPW_OK;
+    if (int st = drain(w)) return st;
+    if (int st = flush_slot(w)) return st;
+    if (hipStreamSynchronize(w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "staging sync failed");
+    const size_t cap = std::max<size_t>(F.cap * 2, F.len + bytes + (64ull << 20));
+    uint8_t *nd = nullptr;
+    if (hipMalloc((void **)&nd, cap) != hipSuccess) return wfail(w, KPW_ERR_NOMEM, "device stage buffer allocation failed");
+    if (F.len && hipMemcpy(nd, F.d, F.len, hipMemcpyDeviceToDevice) != hipSuccess) {
+        (void)hipFree(nd);
+        return wfail(w, KPW_ERR_DEVICE, "stage buffer grow copy failed");
+    }
+    (void)hipFree(F.d);
+    F.d = nd;
+    F.cap = cap;
+    return KPW_OK;
+}
+
+// Record boundaries of a buffer's records: carried then appended ([n+1] absolute offsets).
+static void boundaries(const StageBuf &B, std::vector<uint64_t> &hb)
+{
+    hb.clear();
+    if (B.carry.empty()) hb.push_back(B.gap);
+    else hb.insert(hb.end(), B.carry.begin(), B.carry.end());
+    hb.insert(hb.end(), B.ends.begin(), B.ends.end());
+}
+
+// ---------------------------------------------------------------- worker
+
+// A carry that did not fit its buffer's gap waits in carry_store: rebuild the buffer as
+// [carried | appended] (the caller is not appending to it: its job runs, or it drains).
+static int materialize(kpw_writer *w, StageBuf &B)
+{
+    if (!B.carry_in_store) return KPW_OK;
+    hipStream_t s = w->eng.stream;
+    const uint64_t cs = B.carry.back();                 // carried bytes (store offsets start at 0)
+    const uint64_t app = B.len - B.gap;
+    const size_t cap = std::max<size_t>(B.cap, cs + app + w->gap_ + (64ull << 20));
+    uint8_t *nd = nullptr;
+    if (hipMalloc((void **)&nd, cap) != hipSuccess) return KPW_ERR_NOMEM;
+    if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess ||
+        hipMemcpyAsync(nd, w->carry_store.p, cs, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+        (app && hipMemcpyAsync(nd + cs, B.d + B.gap, app, hipMemcpyDeviceToDevice, s) != hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        (void)hipFree(nd);
+        return KPW_ERR_DEVICE;
+    }
+    for (auto &e : B.ends) e = e - B.gap + cs;
+    (void)hipFree(B.d);
+    B.d = nd;
+    B.cap = cap;
+    B.len = cs + app;
+    B.gap = cs;
+    B.carry_in_store = false;
+    return KPW_OK;
+}
+
+// Place records [b0, b1) of buffer `src` (boundaries hb[i0..i1]) in front of buffer `dst`'s
+// appended records.
+static int place_carry(kpw_writer *w, const StageBuf &src, const std::vector<uint64_t> &hb, size_t i0, size_t i1, StageBuf &dst)
+{
+    hipStream_t s = w->eng.stream;
+    const uint64_t b0 = hb[i0], c = hb[i1] - b0;
+    uint64_t at;
+    uint8_t *base;
+    if (c <= dst.gap) {
+        at = dst.gap - c;
+        base = dst.d;
+        dst.carry_in_store = false;
+    } else {
+        if (w->carry_store.ensure(c + 64)) return KPW_ERR_NOMEM;
+        at = 0;
+        base = w->carry_store.as<uint8_t>();
+        dst.carry_in_store = true;
+    }
+    if (c && hipMemcpyAsync(base + at, src.d + b0, c, hipMemcpyDeviceToDevice, s) != hipSuccess) return KPW_ERR_DEVICE;
+    dst.carry.resize(i1 - i0 + 1);
+    for (size_t i = i0; i <= i1; i++) dst.carry[i - i0] = hb[i] - b0 + at;
+    return KPW_OK;
+}
+
+// File assembly of one job on the assembly thread (headers + bodies + metadata).
+static void start_assembly(kpw_writer *w, BatchOut &&out, int slot)
+{
+    w->asm_out = std::move(out);
+    w->assembler = std::thread([w, slot] {
+        // no exception may leave this thread (std::terminate would kill the host process)
+        try {
+            (void)hipSetDevice(w->eng.device);
+            if (hipEventSynchronize(w->d2h_ev[slot]) != hipSuccess) {
+                w->asm_st = KPW_ERR_DEVICE;
+                w->asm_err = "D2H of pages failed";
+                return;
+            }
+            for (size_t r = 0; r < w->asm_out.rgs.size(); r++) {
+                const int st = w->fw->write_row_group(w->asm_out, (int)r, w->host_pages[slot].p, 0);
+                if (st) {
+                    w->asm_st = st;
+                    w->asm_err = w->fw->error();
+                    return;
+                }
+                w->last_rg_end = w->fw->pos();
+            }
+        } catch (const std::bad_alloc &) {
+            w->asm_st = KPW_ERR_NOMEM;
+            w->asm_err = "file assembly: host allocation failed";
+        } catch (...) {
+            w->asm_st = KPW_ERR_DEVICE;
+            w->asm_err = "file assembly failed";
+        }
+    });
+}
+
+static int join_assembly(kpw_writer *w)
+{
+    if (w->assembler.joinable()) w->assembler.join();
+    if (w->asm_st) {
+        const int st = w->asm_st;
+        w->asm_st = KPW_OK;
+        set_fatal(w, st, w->asm_err);
+        return st;
+    }
+    return KPW_OK;
+}
+
+static int run_job(kpw_writer *w, const Job &j)
+{
+    StageBuf &B = w->buf[j.buf];
+    hipStream_t s = w->eng.stream;
+    if (int st = materialize(w, B)) return set_fatal(w, st, "stage buffer rebuild failed"), st;
+    bool after_invalid;
+    {
+        std::lock_guard<std::mutex> g(w->mu);
+        after_invalid = w->invalid_seen;
+    }
+    if (after_invalid) { B.ends.clear(); B.len = B.gap; }   // records behind an invalid one are never written
+    std::vector<uint64_t> hb;
+    boundaries(B, hb);
+    const int64_t nrec = (int64_t)hb.size() - 1;
+    const int64_t ncarry = B.carry.empty() ? 0 : (int64_t)B.carry.size() - 1;
+    const int64_t n_enc = j.kind == JOB_EXACT ? std::min<int64_t>(j.n_exact, nrec) : nrec;
+    const double t0 = now_ms();
+    if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess) return set_fatal(w, KPW_ERR_DEVICE, "stream wait failed"), KPW_ERR_DEVICE;
+    BatchOut out;
+    if (n_enc > 0) {
+        if (w->d_off.ensure((n_enc + 1) * 8) || w->h_off.ensure((n_enc + 1) * 8))
+            return set_fatal(w, KPW_ERR_NOMEM, "offset staging allocation failed"), KPW_ERR_NOMEM;
+        memcpy(w->h_off.p, hb.data(), (n_enc + 1) * 8);
+        if (hipMemcpyAsync(w->d_off.p, w->h_off.p, (n_enc + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+            return set_fatal(w, KPW_ERR_DEVICE, "H2D of offsets failed"), KPW_ERR_DEVICE;
+        // EXACT jobs are encoded non-final: the GPU planner must cut the same single row group
+        // the host size model cut (checked below), so every such row group cross-checks the model
+        const int st = w->eng.encode(B.d, w->d_off.as<uint64_t>(), (uint64_t)n_enc, j.kind == JOB_FINAL,
+                                     w->eng.props.block_size, nullptr, out);
+        if (st) return set_fatal(w, st, w->eng.error()), st;
+    }
+    const double t1 = now_ms();
+    int64_t consumed = out.records_consumed, keep_end = nrec;
+    if (out.invalid_record >= 0) {
+        std::lock_guard<std::mutex> g(w->mu);
+        w->invalid_seen = true;
+        w->invalid_global = B.first_new_global - ncarry + out.invalid_record;
+        keep_end = out.invalid_record;
+        w->cv.notify_all();
+    } else if (j.kind == JOB_EXACT && (consumed != n_enc || out.rgs.size() != 1)) {
+        // the host size model and the GPU planner restate the same cut: a mismatch is a bug
+        set_fatal(w, KPW_ERR_DEVICE, "row-group cut of the size model and the GPU planner differ");
+        return KPW_ERR_DEVICE;
+    }
+    if (j.kind == JOB_FINAL) keep_end = consumed;
+    // open records -> the next buffer (device to device), then this buffer is free
+    if (keep_end > consumed && j.next >= 0) {
+        if (int st = place_carry(w, B, hb, (size_t)consumed, (size_t)keep_end, w->buf[j.next]))
+            return set_fatal(w, st, "carry-over copy failed"), st;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return set_fatal(w, KPW_ERR_DEVICE, "carry-over sync failed"), KPW_ERR_DEVICE;
+    {
+        std::lock_guard<std::mutex> g(w->mu);
+        B.state = BUF_FREE;
+        if (j.kind == JOB_PLANNED) w->open_buffered = out.open_buffered;
+        w->cv.notify_all();
+    }
+    // pages -> host (pinned, double-buffered against the previous job's assembly)
+    if (int st = join_assembly(w)) return st;
+    if (!out.rgs.empty()) {
+        const int slot = w->page_slot;
+        w->page_slot ^= 1;
+        if (out.pages_len) {
+            if (w->host_pages[slot].ensure(out.pages_len))
+                return set_fatal(w, KPW_ERR_NOMEM, "pinned page buffer allocation failed"), KPW_ERR_NOMEM;
+            if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, out.pages_len, hipMemcpyDeviceToHost, s) != hipSuccess)
+                return set_fatal(w, KPW_ERR_DEVICE, "D2H of pages failed"), KPW_ERR_DEVICE;
+        }
+        if (hipEventRecord(w->d2h_ev[slot], s) != hipSuccess) return set_fatal(w, KPW_ERR_DEVICE, "event record failed"), KPW_ERR_DEVICE;
+        start_assembly(w, std::move(out), slot);
+    }
+    w->t_encode += t1 - t0;
+    if (trace_on())
+        fprintf(stderr, "[kpw] job kind=%d records=%lld (carried %lld) encode %.2f ms, total %.2f ms\n", j.kind, (long long)n_enc,
+                (long long)ncarry, t1 - t0, now_ms() - t0);
+    return KPW_OK;
+}
+
+static void worker_main(kpw_writer *w)
+{
+    (void)hipSetDevice(w->eng.device);
+    for (;;) {
+        Job j;
+        {
+            std::unique_lock<std::mutex> lk(w->mu);
+            w->cv.wait(lk, [w] { return w->stop || !w->q.empty(); });
+            if (w->q.empty()) break;   // stop requested and nothing queued
+            j = w->q.front();
+            w->q.pop_front();
+            w->busy = true;
+        }
+        bool failed;
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            failed = w->fatal_st != KPW_OK;
+        }
+        try {
+            if (!failed) (void)run_job(w, j);
+        } catch (const std::bad_alloc &) {
+            set_fatal(w, KPW_ERR_NOMEM, "host allocation failed in the encode worker");
+        } catch (...) {
+            set_fatal(w, KPW_ERR_DEVICE, "encode worker failed");
+        }
+        bool idle;
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            if (w->fatal_st) {   // nothing after a failure is encoded; its buffers are free again
+                for (auto &k : w->buf) if (k.state == BUF_QUEUED) k.state = BUF_FREE;
+                w->buf[j.buf].state = BUF_FREE;
+                w->q.clear();
+            }
+            idle = w->q.empty();
+        }
+        if (idle) (void)join_assembly(w);   // idle implies every queued job is in the file
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            w->busy = false;
+            w->cv.notify_all();
+        }
+    }
+    (void)join_assembly(w);
+}
+
+// Hand the fill buffer to the worker and start filling the next one.
+static int submit(kpw_writer *w, int kind, int64_t n_exact)
+{
+    if (int st = flush_slot(w)) return st;
+    StageBuf &F = w->buf[w->fill];
+    if (hipEventRecord(F.copied, w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "event record failed");
+    const int f = w->fill;
+    const int64_t nrec = F.ncarry_expected + (int64_t)F.ends.size();
+    const bool final_job = kind == JOB_FINAL;
+    int next = -1;
+    if (!final_job) {
+        w->fill = -1;
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            F.state = BUF_QUEUED;
+        }
+        if (int st = acquire_fill(w)) {
+            std::lock_guard<std::mutex> g(w->mu);
+            F.state = BUF_FREE;
+            return st;
+        }
+        next = w->fill;
+        w->buf[next].ncarry_expected = kind == JOB_EXACT ? nrec - n_exact : 0;
+    } else {
+        std::lock_guard<std::mutex> g(w->mu);
+        F.state = BUF_QUEUED;
+        w->fill = -1;
+    }
+    {
+        std::lock_guard<std::mutex> g(w->mu);
+        w->q.push_back(Job{f, kind, next, n_exact});
+        w->cv.notify_all();
+    }
+    if (kind == JOB_PLANNED) w->dirty = false;
+    return KPW_OK;
+}
+
+// Wait until every queued job is encoded and assembled.
+static int drain(kpw_writer *w)
+{
+    std::unique_lock<std::mutex> lk(w->mu);
+    w->cv.wait(lk, [w] { return (w->q.empty() && !w->busy) || w->fatal_st; });
+    if (w->fatal_st) {
+        w->cv.wait(lk, [w] { return w->q.empty() && !w->busy; });
+        w->err = w->fatal_err;
+        return w->fatal_st;
+    }
+    return KPW_OK;
+}
+
+int kpw_writer::init_pipeline()
+{
+    if (hipSetDevice(eng.device) != hipSuccess) return KPW_ERR_DEVICE;
+    if (hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking) != hipSuccess) return KPW_ERR_DEVICE;
+    for (auto &e : slot_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    for (auto &e : d2h_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&direct_ev, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    for (auto &b : buf)
+        if (hipEventCreateWithFlags(&b.copied, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    // the open row group of a job lands in the next buffer's gap (its wire bytes are a small
+    // multiple of its buffered size for every schema but pathological ones; see materialize)
+    gap_ = std::max<uint64_t>(64ull << 20, 2 * (uint64_t)eng.props.block_size) + 4096;
+    model_on = model.init(eng.cols, eng.props);
+    worker = std::thread(worker_main, this);
+    return acquire_fill(this);
+}
+
+kpw_writer::~kpw_writer()
+{
+    if (worker.joinable()) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        worker.join();
+    }
+    if (assembler.joinable()) assembler.join();
+    (void)hipSetDevice(eng.device);
+    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    if (eng.stream) (void)hipStreamSynchronize(eng.stream);
+    for (auto &b : buf) {
+        if (b.d) (void)hipFree(b.d);
+        if (b.copied) (void)hipEventDestroy(b.copied);
+    }
+    for (auto &e : slot_ev) if (e) (void)hipEventDestroy(e);
+    for (auto &e : d2h_ev) if (e) (void)hipEventDestroy(e);
+    if (direct_ev) (void)hipEventDestroy(direct_ev);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    delete fw;
+}
+
+// ---------------------------------------------------------------- C-ABI
+
+extern "C" void *kpw_host_alloc(uint64_t bytes, int *status)
+{
+    void *p = nullptr;
+    if (!bytes || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        if (status) *status = bytes ? KPW_ERR_NOMEM : KPW_ERR_INVALID_ARG;
+        return nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pins[(uintptr_t)p] = bytes;
+    }
+    if (status) *status = KPW_OK;
+    return p;
+}
+
+extern "C" void kpw_host_free(void *p)
+{
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pins.erase((uintptr_t)p);
+    }
+    (void)hipHostFree(p);
+}
+
+extern "C" kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, const kpw_props *props, const char *path, int *status)
+{
+    try {
+        kpw_writer *w = new kpw_writer();
+        int st = w->eng.init(device, schema, props);
+        if (!st) {
+            w->fw = new FileWriter(w->eng.cols, w->eng.message_name, w->eng.proto_class, w->eng.props);
+            st = w->fw->open(path);
+        }
+        if (!st) st = w->init_pipeline();
+        if (st) {
+            if (status) *status = st;
+            delete w;
+            return nullptr;
+        }
+        w->created_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                            std::chrono::system_clock::now().time_since_epoch()).count();
+        if (status) *status = KPW_OK;
+        return w;
+    } catch (const std::bad_alloc &) {
+        if (status) *status = KPW_ERR_NOMEM;
+    } catch (...) {
+        if (status) *status = KPW_ERR_DEVICE;
+    }
+    return nullptr;
+}
+
+// A reported pipeline failure; an invalid record found by the worker (bulk path) also fixes
+// the record count: it and everything after it were never written.
+static int observe_failure(kpw_writer *w)
+{
+    std::lock_guard<std::mutex> g(w->mu);
+    if (w->invalid_seen && w->failed_record < 0) {
+        w->failed_record = w->invalid_global;
+        w->num_records = w->invalid_global;
+    }
+    if (w->fatal_st) {
+        w->err = w->fatal_err;
+        return w->fatal_st;
+    }
+    if (w->failed_record >= 0) {
+        w->err = "Invalid proto message received (record " + std::to_string(w->failed_record) + ")";
+        return KPW_ERR_INVALID_PROTO;
+    }
+    return KPW_OK;
+}
+
+
+// Rewind the fill buffer's append position to `new_len` (records after it were not accepted).
+// Bytes still pending in the current slot are dropped with it; bytes already sent are simply
+// overwritten by later appends (same copy stream, in order).
+static void rewind_fill(kpw_writer *w, uint64_t new_len)
+{
+    StageBuf &F = w->buf[w->fill];
+    if (w->slot_used) w->slot_used = new_len > w->slot_dev ? std::min<uint64_t>(w->slot_used, new_len - w->slot_dev) : 0;
+    F.len = new_len;
+}
+
+// One record through the pinned slot (the size-model path: small writes).
+static int stage_record(kpw_writer *w, const uint8_t *src, uint64_t len)
+{
+    if (w->slot_used + len > kpw_writer::kSlotBytes || w->slot_used == 0) return stage_bytes(w, src, len);
+    StageBuf &F = w->buf[w->fill];
+    memcpy(w->slot[w->cur_slot].p + w->slot_used, src, len);
+    w->slot_used += len;
+    F.len += len;
+    return KPW_OK;
+}
+
+// write / write_until_full with the size model on: records go one by one through the model
+// (O(columns) each) and the slot; an invalid record stops the batch right there (the
+// reference throws at parseFrom, KafkaProtoParquetWriter.java:270-276); a row-group cut hands
+// the fill buffer, which then holds exactly that row group, to the worker.
+static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n, int64_t max_file_size,
+                          uint64_t *n_accepted, int *full)
+{
+    uint64_t i = 0;
+    int rc = KPW_OK;
+    for (; i < n; i++) {
+        const uint8_t *rec = data + offsets[i];
+        const uint64_t len = offsets[i + 1] - offsets[i];
+        const int r = w->model.add(rec, len);
+        if (r == SizeModel::INVALID) {
+            w->failed_record = w->num_records;
+            w->err = "Invalid proto message received (record " + std::to_string(w->failed_record) + ")";
+            rc = KPW_ERR_INVALID_PROTO;
+            break;
+        }
+        if (int st = grow_fill(w, len)) return st;
+        if (int st = stage_record(w, rec, len)) return st;
+        StageBuf &F = w->buf[w->fill];
+        F.ends.push_back(F.len);
+        w->num_records++;
+        if (r == SizeModel::LEAVE) {
+            // a page cut inside the row group (pageSize reached first): the GPU plans from here on
+            w->model_on = false;
+            w->dirty = true;
+            i++;
+            if (max_file_size < 0) {   // plain write: stage the rest on the bulk path
+                const uint64_t bytes = offsets[n] - offsets[i];
+                if (i < n) {
+                    if (int st = grow_fill(w, bytes)) return st;
+                    StageBuf &G = w->buf[w->fill];
+                    const uint64_t delta = G.len - offsets[i];
+                    if (int st = stage_bytes(w, data + offsets[i], bytes)) return st;
+                    for (uint64_t k = i + 1; k <= n; k++) G.ends.push_back(offsets[k] + delta);
+                    w->num_records += (int64_t)(n - i);
+                    i = n;
+                }
+            }
+            break;
+        }
+        if (r == SizeModel::CUT) {
+            const int64_t nrec = F.ncarry_expected + (int64_t)F.ends.size();
+            if (int st = submit(w, JOB_EXACT, nrec)) return st;
+            w->pending_cut = true;
+        }
+        if (max_file_size >= 0) {
+            // getDataSize() = lastRowGroupEndPos + columnStore.getBufferedSize()
+            if (w->pending_cut) {
+                if (int st = drain(w)) return st;
+                w->pending_cut = false;
+            }
+            if (w->last_rg_end + w->model.buffered() >= max_file_size) {
+                i++;
+                if (full) *full = 1;
+                break;
+            }
+        }
+    }
+    if (n_accepted) *n_accepted = i;
+    return rc;
+}
+
+// Bulk write: the whole batch in one copy (direct DMA when the batch is pinned).
+static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n)
+{
+    const uint64_t bytes = offsets[n] - offsets[0];
+    if (int st = grow_fill(w, bytes)) return st;
+    StageBuf &F = w->buf[w->fill];
+    const uint64_t delta = F.len - offsets[0];
+    if (int st = stage_bytes(w, data + offsets[0], bytes)) return st;
+    F.ends.reserve(F.ends.size() + n);
+    for (uint64_t i = 1; i <= n; i++) F.ends.push_back(offsets[i] + delta);
+    w->num_records += (int64_t)n;
+    w->dirty = true;
+    return KPW_OK;
+}
+
+// getDataSize() after the first m records of the (drained) fill buffer, without flushing:
+// an encode of [0, m) gives the row groups parquet-mr would have completed by then (their
+// header + compressed bytes follow lastRowGroupEndPos) and the open row group's buffered size.
+static int ds_prefix(kpw_writer *w, uint64_t m, int64_t &ds, BatchOut &out)
+{
+    out = BatchOut();
+    StageBuf &F = w->buf[w->fill];
+    int st = w->eng.encode(F.d, w->probe_off.as<uint64_t>(), m, false, w->eng.props.block_size, nullptr, out);
+    if (st) return wfail(w, st, w->eng.error());
+    int64_t t = w->last_rg_end;
+    for (size_t r = 0; r < out.rgs.size(); r++) t += w->fw->row_group_size(out, (int)r);
+    ds = t + out.open_buffered;
+    return KPW_OK;
+}
+
+// The WorkerThread rotation loop (KafkaProtoParquetWriter.java:268-285,306-308) on the bulk
+// path: records are written in order and the file is full right after the first record with
+// getDataSize() >= max.  Within a row group getDataSize() only grows and a flush swaps the
+// group's buffered size for its encoded bytes, so the first crossing is found segment by
+// segment (before each planned cut, at the cut) and by bisection inside the crossing segment;
+// each probe encodes a staged prefix (cuts are causal).  Multi-page chunks can shrink the
+// buffered size inside a row group: that regime keeps write + getDataSize per record.
+static int write_until_full_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n,
+                                 int64_t max_file_size, uint64_t *n_accepted, int *full)
+{
+    if (w->eng.props.writer_version == 1 && w->eng.props.page_size < w->eng.props.block_size)
+        return wfail(w, KPW_ERR_UNSUPPORTED, "write_until_full: pageSize < blockSize (multi-page chunks): use write + getDataSize");
+    if (int st = drain(w)) return st;
+    if (int st = flush_slot(w)) return st;
+    if (hipEventRecord(w->buf[w->fill].copied, w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "event record failed");
+    if (int st = materialize(w, w->buf[w->fill])) return wfail(w, st, "stage buffer rebuild failed");
+    StageBuf &F0 = w->buf[w->fill];
+    const uint64_t base = (F0.carry.empty() ? 0 : F0.carry.size() - 1) + F0.ends.size();
+    if (int st = write_bulk(w, data, offsets, n)) return st;
+    if (int st = flush_slot(w)) return st;
+    StageBuf &F = w->buf[w->fill];
+    if (hipEventRecord(F.copied, w->copy_stream) != hipSuccess || hipStreamWaitEvent(w->eng.stream, F.copied, 0) != hipSuccess)
+        return wfail(w, KPW_ERR_DEVICE, "staging order failed");
+    std::vector<uint64_t> hb;
+    boundaries(F, hb);
+    if (w->probe_off.ensure(hb.size() * 8) || w->probe_h.ensure(hb.size() * 8))
+        return wfail(w, KPW_ERR_NOMEM, "offset staging allocation failed");
+    memcpy(w->probe_h.p, hb.data(), hb.size() * 8);
+    if (hipMemcpyAsync(w->probe_off.p, w->probe_h.p, hb.size() * 8, hipMemcpyHostToDevice, w->eng.stream) != hipSuccess)
+        return wfail(w, KPW_ERR_DEVICE, "H2D of offsets failed");
+    auto truncate = [&](uint64_t keep) {   // keep the first `keep` records of this batch staged
+        F.ends.resize(F.ends.size() - (n - keep));
+        rewind_fill(w, F.ends.empty() ? F.gap : F.ends.back());
+        w->num_records -= (int64_t)(n - keep);
+    };
+    BatchOut out;
+    int64_t ds_end = 0;
+    if (int st = ds_prefix(w, base + n, ds_end, out)) return st;
+    uint64_t valid = n;
+    if (out.invalid_record >= 0) {
+        if ((uint64_t)out.invalid_record < base) {   // a record staged by an earlier write(): keep what precedes it
+            truncate(0);
+            const uint64_t keep = (uint64_t)out.invalid_record;
+            const uint64_t nc = F.carry.empty() ? 0 : F.carry.size() - 1;
+            if (keep >= nc) {
+                F.ends.resize(keep - nc);
+            } else {
+                F.ends.clear();
+                F.carry.resize(keep + 1);
+                if (keep == 0) F.carry.clear();
+            }
+            rewind_fill(w, F.ends.empty() ? F.gap : F.ends.back());
+            w->failed_record = F.first_new_global - (int64_t)nc + (int64_t)keep;
+            w->num_records = w->failed_record;
+            return wfail(w, KPW_ERR_INVALID_PROTO,
+                         "Invalid proto message received (record " + std::to_string(w->failed_record) + ")");
+        }
+        valid = (uint64_t)out.invalid_record - base;
+        if (int st = ds_prefix(w, base + valid, ds_end, out)) return st;
+    }
+    std::vector<int64_t> cut, end;   // row-group ends (records from the buffer start), file pos after each
+    {
+        int64_t e = w->last_rg_end;
+        for (size_t r = 0; r < out.rgs.size(); r++) {
+            e += w->fw->row_group_size(out, (int)r);
+            cut.push_back(out.rgs[r].first_record + out.rgs[r].num_records);
+            end.push_back(e);
+        }
+    }
+    BatchOut tmp;
+    auto ds = [&](uint64_t j, int64_t &v) { return ds_prefix(w, base + j, v, tmp); };
+    auto bisect = [&](uint64_t lo, uint64_t hi, uint64_t &res) {   // first j in [lo, hi] with ds(j) >= max
+        while (lo < hi) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            int64_t v = 0;
+            if (int e2 = ds(mid, v)) return e2;
+            if (v >= max_file_size) hi = mid; else lo = mid + 1;
+        }
+        res = lo;
+        return (int)KPW_OK;
+    };
+    uint64_t a = 0, found = 0;
+    for (size_t i = 0; i < cut.size() && !found; i++) {
+        const int64_t b = cut[i] - (int64_t)base;
+        if (b < 1) continue;
+        if ((uint64_t)b - 1 >= a + 1) {
+            int64_t v = 0;
+            if (int st = ds((uint64_t)b - 1, v)) return st;
+            if (v >= max_file_size) {
+                if (int st = bisect(a + 1, (uint64_t)b - 1, found)) return st;
+                break;
+            }
+        }
+        if (end[i] >= max_file_size) { found = (uint64_t)b; break; }
+        a = (uint64_t)b;
+    }
+    if (!found && valid >= a + 1 && ds_end >= max_file_size)
+        if (int st = bisect(a + 1, valid, found)) return st;
+    if (found) {
+        truncate(found);
+        *n_accepted = found;
+        *full = 1;
+    } else {
+        truncate(valid);
+        *n_accepted = valid;
+        if (valid < n) {
+            w->failed_record = w->num_records;
+            w->err = "Invalid proto message received (record " + std::to_string(w->failed_record) + ")";
+            return KPW_ERR_INVALID_PROTO;
+        }
+    }
+    return KPW_OK;
+}
+
+static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n, int64_t max_file_size,
+                       uint64_t *n_accepted, int *full)
+{
+    if (n_accepted) *n_accepted = 0;
+    if (full) *full = 0;
+    if (w->closed) return KPW_ERR_STATE;
+    if (int st = observe_failure(w)) return st;
+    if (!n) return KPW_OK;
+    if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
+    if (w->model_on && n > model_max_batch()) w->model_on = false;   // bulk path: cuts planned on the GPU
+    int rc;
+    if (w->model_on) {
+        rc = write_modelled(w, data, offsets, n, max_file_size, n_accepted, full);
+    } else if (max_file_size >= 0) {
+        rc = write_until_full_bulk(w, data, offsets, n, max_file_size, n_accepted, full);
+    } else {
+        rc = write_bulk(w, data, offsets, n);
+        if (n_accepted && !rc) *n_accepted = n;
+    }
+    if (rc) return rc;
+    StageBuf &F = w->buf[w->fill];
+    if (!w->model_on && F.len - F.gap >= stage_flush_bytes()) return submit(w, JOB_PLANNED, 0);
+    return KPW_OK;
+}
+
+extern "C" int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n)
+{
+    if (!w || (n && (!data || !offsets))) return KPW_ERR_INVALID_ARG;
+    try {
+        return write_entry(w, data, offsets, n, -1, nullptr, nullptr);
+    } catch (const std::bad_alloc &) {
+        set_fatal(w, KPW_ERR_NOMEM, "host staging allocation failed");
+        return KPW_ERR_NOMEM;
+    } catch (...) {
+        set_fatal(w, KPW_ERR_DEVICE, "unexpected failure");
+        return KPW_ERR_DEVICE;
+    }
+}
+
+extern "C" int kpw_writer_write_until_full(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n,
+                                           int64_t max_file_size, uint64_t *n_accepted, int *full)
+{
+    if (!w || !n_accepted || !full || (n && (!data || !offsets)) || max_file_size < 0) return KPW_ERR_INVALID_ARG;
+    try {
+        return write_entry(w, data, offsets, n, max_file_size, n_accepted, full);
+    } catch (const std::bad_alloc &) {
+        set_fatal(w, KPW_ERR_NOMEM, "host allocation failed");
+        return KPW_ERR_NOMEM;
+    } catch (...) {
+        set_fatal(w, KPW_ERR_DEVICE, "unexpected failure");
+        return KPW_ERR_DEVICE;
+    }
+}
+
+// getDataSize() (ParquetFile.java:77-79 -> InternalParquetRecordWriter.getDataSize).
+extern "C" int64_t kpw_writer_data_size(kpw_writer *w)
+{
+    if (!w) return -1;
+    try {
+        if (w->closed) return w->fw->pos();
+        if (observe_failure(w)) return -1;
+        if (w->model_on) {
+            if (w->pending_cut) {
+                if (drain(w)) return -1;
+                w->pending_cut = false;
+            }
+            return w->last_rg_end + w->model.buffered();
+        }
+        if (w->dirty && submit(w, JOB_PLANNED, 0)) return -1;   // encode what is staged (completed row groups flushed)
+        if (drain(w)) return -1;
+        if (observe_failure(w)) return -1;
+        return w->last_rg_end + w->open_buffered;
+    } catch (...) {
+        return -1;
+    }
+}
+
+extern "C" int64_t kpw_writer_num_records(const kpw_writer *w) { return w ? w->num_records : -1; }
+extern "C" int64_t kpw_writer_creation_time_ms(const kpw_writer *w) { return w ? w->created_ms : -1; }
+extern "C" int64_t kpw_writer_failed_record(const kpw_writer *w) { return w ? w->failed_record : -1; }
+extern "C" const char *kpw_writer_last_error(const kpw_writer *w) { return w ? w->err.c_str() : "null handle"; }
+
+// close() (ParquetFile.java:65-68): flush everything staged (after an invalid record: only
+// the records before it), then the footer.  Idempotent.
+extern "C" int kpw_writer_close(kpw_writer *w)
+{
+    if (!w) return KPW_ERR_INVALID_ARG;
+    if (w->closed) return KPW_OK;
+    try {
+        if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            if (w->fatal_st) { w->err = w->fatal_err; return w->fatal_st; }
+        }
+        (void)observe_failure(w);   // an invalid record: only what came before it is flushed
+        if (w->fill >= 0) {
+            if (int st = submit(w, JOB_FINAL, 0)) return st;
+        }
+        if (int st = drain(w)) return st;
+        int st = w->fw->close();
+        if (st) return wfail(w, st, w->fw->error());
+        w->closed = true;
+        if (trace_on()) fprintf(stderr, "[kpw] close: worker encode time %.1f ms\n", w->t_encode);
+        return KPW_OK;
+    } catch (...) {
+        set_fatal(w, KPW_ERR_DEVICE, "close failed");
+        return KPW_ERR_DEVICE;
+    }
+}
+
+extern "C" int kpw_writer_file_bytes(const kpw_writer *w, const uint8_t **bytes, uint64_t *len)
+{
+    if (!w || !bytes || !len) return KPW_ERR_INVALID_ARG;
+    if (!w->closed) return KPW_ERR_STATE;
+    *bytes = w->fw->memory_data();
+    *len = w->fw->memory_size();
+    return KPW_OK;
+}
+
+extern "C" void kpw_writer_free(kpw_writer *w) { delete w; }

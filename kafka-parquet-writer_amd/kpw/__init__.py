@@ -7,8 +7,8 @@ is no CPU fallback: constructing a ParquetFile without the library raises.
 """
 from ._lib import (KpwError, InvalidProtoError, load_library, library_path, Schema, Column,
                    UNCOMPRESSED, SNAPPY)
-from .parquet_file import ParquetFile, ParquetProperties
+from .parquet_file import ParquetFile, ParquetProperties, pinned_empty
 from .encoder import Encoder
 
 __all__ = ["ParquetFile", "ParquetProperties", "Encoder", "Schema", "Column", "KpwError", "InvalidProtoError",
-           "load_library", "library_path", "UNCOMPRESSED", "SNAPPY"]
+           "load_library", "library_path", "UNCOMPRESSED", "SNAPPY", "pinned_empty"]

@@ -14,7 +14,12 @@ Differences forced by the GPU boundary: write() takes the serialized record valu
 (record.value(), KafkaProtoParquetWriter.java:270) instead of a parsed T — parsing is
 kernel K1 — and write_batch() accepts many values at once.  An invalid value raises
 InvalidProtoError, the reference's IllegalStateException path (KPW:271-276); records
-before it stay written.  Instances are not thread-safe (ParquetFile.java:19-20).
+before it stay written, it and the records after it are not.  Writes of <= 65536 records
+(the reference's one-record loop) raise it from that write, like parseFrom; a larger
+write is validated on the GPU and the error is raised by the next call (write,
+get_data_size or close), when get_num_written_records() is also corrected.
+Instances are not thread-safe (ParquetFile.java:19-20); separate instances may be used
+from separate threads (one writer per worker thread, KafkaProtoParquetWriter.java:175-179).
 """
 import ctypes
 import datetime
@@ -61,6 +66,22 @@ def _as_batch(values):
         np.cumsum([len(v) for v in values], out=offsets[1:])
     data = np.frombuffer(b"".join(values), dtype=np.uint8) if values else np.zeros(1, np.uint8)
     return np.ascontiguousarray(data), offsets
+
+
+def pinned_empty(nbytes):
+    """A numpy uint8 array in pinned host memory (kpw_host_alloc): record batches placed here
+    are DMA'd to the GPU by write_batch without a host copy (north_star: polled batches land
+    in pinned staging buffers).  Freed with the array."""
+    import weakref
+    L = load_library()
+    st = ctypes.c_int(0)
+    p = L.kpw_host_alloc(max(1, int(nbytes)), ctypes.byref(st))
+    if not p:
+        raise KpwError(st.value, "kpw_host_alloc(%d)" % nbytes)
+    # views of the array keep it (their .base) alive, so the memory outlives every view
+    arr = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, int(nbytes))).from_address(p))
+    weakref.finalize(arr, L.kpw_host_free, p)
+    return arr
 
 
 class ParquetFile:

@@ -222,14 +222,16 @@ def test_tiny_batches(n):
 
 @pytest.mark.parametrize("kind", [synth.KIND_SAMPLE, synth.KIND_REC8])
 @pytest.mark.parametrize("codec", [0, 1])
-def test_writer_file_identical(kind, codec):
+@pytest.mark.parametrize("n,batches", [(20000, 3), (300000, 2)], ids=["model", "bulk"])
+def test_writer_file_identical(kind, codec, n, batches):
     """The ParquetFile drop-in writes the same file bytes as the oracle, across several
-    write batches (open row groups carried between encoder batches)."""
+    write batches: small batches go through the host size model (row groups cut on the host),
+    batches of > 65536 records through the GPU planner (open row groups carried between jobs)."""
     schema = synth.SCHEMAS[kind]
-    data, offs = synth.generate(kind, 0xC0FFEE01, 20000)
+    data, offs = synth.generate(kind, 0xC0FFEE01, n)
     import kpw
     props = kpw.ParquetProperties(block_size=256 * 1024, compression_codec_name=codec)
-    fb = gh.gpu_file(schema, data, offs, props, batches=3)
+    fb = gh.gpu_file(schema, data, offs, props, batches=batches)
     ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=256 * 1024, codec=codec))
     import pqwalk
     assert fb == ob, pqwalk.first_difference(fb, ob)
@@ -238,14 +240,18 @@ def test_writer_file_identical(kind, codec):
 
 
 def test_invalid_record_cuts_batch():
+    """Small write (size-model path): the write itself raises at the invalid record, like the
+    reference's parseFrom (KafkaProtoParquetWriter.java:270-276)."""
     import kpw
     good = synth.records(*synth.generate(synth.KIND_SAMPLE, 1, 50))
     bad = b"\x10\x01"  # missing required query
     pf = kpw.ParquetFile(None, kpw.Schema(synth.SAMPLE.message_name, synth.SAMPLE.columns))
-    pf.write_batch(good + [bad] + good[:5])
     with pytest.raises(kpw.InvalidProtoError) as e:
-        pf.get_data_size()
+        pf.write_batch(good + [bad] + good[:5])
     assert e.value.record == 50
+    assert pf.get_num_written_records() == 50
+    with pytest.raises(kpw.InvalidProtoError):
+        pf.get_data_size()
     pf.close()
     tbl = pq.read_table(io.BytesIO(pf.file_bytes()))
     assert tbl.num_rows == 50

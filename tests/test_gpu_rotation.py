@@ -109,3 +109,95 @@ def test_multipage_regime_unsupported():
     with pytest.raises(kpw.KpwError):
         pf.write_until_full((data, offs), 1000)
     pf.close()
+
+
+def _writer_lib():
+    import kpw
+    return kpw.load_library()
+
+
+def test_data_size_every_record_200k():
+    """The reference's unchanged WorkerThread loop (KafkaProtoParquetWriter.java:268-285,306-308):
+    ParquetFile.write of ONE record, then getDataSize(), 200 000 times.  Every value equals the
+    oracle's InternalParquetRecordWriter.getDataSize(), row groups are cut on the host by the size
+    model (one GPU encode per row group), and the file is byte-identical."""
+    import ctypes
+    import time
+    import kpw
+    import pqwalk
+    n = 200_000
+    data, offs = synth.generate(synth.KIND_REC8, 47, n)
+    props = kpw.ParquetProperties(block_size=1 * MiB, compression_codec_name=1)
+    pf = kpw.ParquetFile(None, kpw.Schema(synth.REC8.message_name, synth.REC8.columns, synth.REC8.proto_class), props)
+    ow = oracle.OracleWriter(synth.REC8, oracle.make_props(block_size=1 * MiB, codec=1))
+    L, OL = pf._L, oracle.lib()
+    base = data.ctypes.data
+    one = np.zeros(2, dtype=np.uint64)
+    optr = one.ctypes.data
+    got = np.empty(n, dtype=np.int64)
+    want = np.empty(n, dtype=np.int64)
+    t0 = time.perf_counter()
+    for i in range(n):
+        a, b = int(offs[i]), int(offs[i + 1])
+        one[1] = b - a
+        assert L.kpw_writer_write(pf._h, base + a, optr, 1) == 0
+        got[i] = L.kpw_writer_data_size(pf._h)
+    dt = time.perf_counter() - t0
+    for i in range(n):
+        a, b = int(offs[i]), int(offs[i + 1])
+        assert OL.kpwo_write(ow._h, base + a, b - a) == 0
+        want[i] = ow.data_size()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, (int(bad[0]), int(got[bad[0]]), int(want[bad[0]]))
+    assert ow.num_row_groups() >= 8
+    pf.close()
+    ow.close()
+    assert pf.file_bytes() == ow.file_bytes(), pqwalk.first_difference(pf.file_bytes(), ow.file_bytes())
+    assert dt < 30, dt
+
+
+def test_rotation_per_record_model():
+    """write_until_full one record at a time (model path) across files."""
+    data, offs = synth.generate(synth.KIND_REC8, 48, 30000)
+    files = _rotate(synth.REC8, data, offs, 300 * 1024, 32 * 1024, 1, chunk=1)
+    assert sum(1 for _, f in files if f) >= 2
+
+
+def test_bulk_then_per_record():
+    """A bulk write (> 65536 records: GPU-planned cuts) and then one-record writes with
+    getDataSize() after each (the GPU answers from the staged records)."""
+    import kpw
+    import pqwalk
+    data, offs = synth.generate(synth.KIND_SAMPLE, 49, 70200)
+    props = kpw.ParquetProperties(block_size=256 * 1024, compression_codec_name=1)
+    pf = kpw.ParquetFile(None, kpw.Schema(synth.SAMPLE.message_name, synth.SAMPLE.columns, synth.SAMPLE.proto_class),
+                         props)
+    ow = oracle.OracleWriter(synth.SAMPLE, oracle.make_props(block_size=256 * 1024, codec=1))
+    pf.write_batch((data[:int(offs[70000])], offs[:70001]))
+    ow.write_batch(data, offs[:70001])
+    assert pf.get_data_size() == ow.data_size()
+    for i in range(70000, 70200):
+        sub = np.array([0, offs[i + 1] - offs[i]], dtype=np.uint64)
+        seg = data[int(offs[i]):int(offs[i + 1])]
+        pf.write_batch((seg, sub))
+        ow.write_batch(seg, sub)
+        assert pf.get_data_size() == ow.data_size(), i
+    pf.close()
+    ow.close()
+    assert pf.file_bytes() == ow.file_bytes(), pqwalk.first_difference(pf.file_bytes(), ow.file_bytes())
+
+
+def test_pinned_source_bulk():
+    """Batches in kpw_host_alloc memory are DMA'd directly (no host copy); same file bytes."""
+    import kpw
+    import pqwalk
+    data, offs = synth.generate(synth.KIND_REC8, 50, 400000)
+    pin = kpw.pinned_empty(len(data))
+    pin[:] = data
+    props = kpw.ParquetProperties(block_size=2 * MiB, compression_codec_name=1)
+    pf = kpw.ParquetFile(None, kpw.Schema(synth.REC8.message_name, synth.REC8.columns, synth.REC8.proto_class), props)
+    for a, b in ((0, 150000), (150000, 300000), (300000, 400000)):
+        pf.write_batch((pin[int(offs[a]):int(offs[b])], (offs[a:b + 1] - offs[a]).astype(np.uint64)))
+    pf.close()
+    want = oracle.encode_file(synth.REC8, data, offs, oracle.make_props(block_size=2 * MiB, codec=1))
+    assert pf.file_bytes() == want, pqwalk.first_difference(pf.file_bytes(), want)

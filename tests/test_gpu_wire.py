@@ -88,10 +88,10 @@ def test_invalid_record_parquet_file(label, bad):
     pos = 137
     pf = kpw.ParquetFile(None, kpw.Schema(synth.SAMPLE.message_name, synth.SAMPLE.columns, synth.SAMPLE.proto_class),
                          kpw.ParquetProperties(block_size=4096, compression_codec_name=1))
-    pf.write_batch(goods[:pos] + [bad] + goods[pos:])
-    with pytest.raises(kpw.InvalidProtoError) as e:
-        pf.get_data_size()
+    with pytest.raises(kpw.InvalidProtoError) as e:   # small write: raised by the write itself
+        pf.write_batch(goods[:pos] + [bad] + goods[pos:])
     assert e.value.record == pos
+    assert pf.get_num_written_records() == pos
     pf.close()
     got = pf.file_bytes()
     data, offs = synth.pack(goods[:pos])
@@ -127,3 +127,24 @@ def test_c1_one_million_records_uncompressed():
     fb = gh.gpu_file(synth.REC8, data, offs, props, batches=4)
     ob = oracle.encode_file(synth.REC8, data, offs, oracle.make_props(codec=0))
     assert fb == ob, pqwalk.first_difference(fb, ob)
+
+
+@pytest.mark.parametrize("label,bad", INVALID[:3] + INVALID[-2:], ids=[c[0] for c in INVALID[:3] + INVALID[-2:]])
+def test_invalid_record_bulk_write(label, bad):
+    """Bulk path (a write of > 65536 records, validated on the GPU): the error surfaces at the
+    next call with the record index, and the file holds exactly the records before it."""
+    import kpw
+    goods = _goods(100000, seed=9)
+    pos = 70001
+    pf = kpw.ParquetFile(None, kpw.Schema(synth.SAMPLE.message_name, synth.SAMPLE.columns, synth.SAMPLE.proto_class),
+                         kpw.ParquetProperties(block_size=256 * 1024, compression_codec_name=1))
+    pf.write_batch(goods[:pos] + [bad] + goods[pos:])
+    with pytest.raises(kpw.InvalidProtoError) as e:
+        pf.get_data_size()
+    assert e.value.record == pos
+    assert pf.get_num_written_records() == pos
+    pf.close()
+    data, offs = synth.pack(goods[:pos])
+    want = oracle.encode_file(synth.SAMPLE, data, offs, oracle.make_props(block_size=256 * 1024, codec=1))
+    got = pf.file_bytes()
+    assert got == want, pqwalk.first_difference(got, want)
