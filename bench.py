@@ -1,19 +1,38 @@
 #!/usr/bin/env python
-"""bench.py — Parquet encode throughput on MI355X (BASELINE.json metric, config C2).
+"""bench.py — Parquet encode throughput on MI355X, the BASELINE.json metric as defined.
 
-Workload: Rec8 records (proto2, ~62 B), 100 M per GPU, dictionary on,
-SNAPPY, 128 MiB row groups, 128 MiB pages (reference default).  One "step" = one pass of
-the flush path over the whole device-resident batch: K1 decode -> row-group planner ->
-K2 dictionary / K3 RLE / K4 PLAIN / K6 stats -> K7 Snappy, every page of every row group
-produced in HBM (kpw_encoder_encode, final=1).  Record bytes are resident in HBM before
-timing starts; page bytes stay in HBM (the PCIe-inclusive rate is reported separately).
+Metric (BASELINE.md:16-19): serialized record-value bytes consumed (the
+reference's `written.bytes` meter, KafkaProtoParquetWriter.java:115,280) divided by the wall
+time from the first ParquetFile write until the last file is closed.  A step is one complete
+file per writer through the ParquetFile drop-in (kpw_writer_*, writer.cpp): record batches
+start in host memory (pinned, where polled Kafka batches land: north_star), are written in
+poll()-sized batches (500 k records), cross PCIe, are encoded (K1..K7), come back as pages and
+are assembled into an in-memory file (headers, footer).  H2D, encode, D2H and file assembly
+are all inside the timed region.
 
-value = sum over ranks of serialized record-value bytes / max-over-ranks wall time (GB/s,
-the reference's `written.bytes` definition, KafkaProtoParquetWriter.java:115,280).
-Multi-GPU: one process per GPU, each encoding its own partition (weak scaling, no
+Workloads (--workload):
+  c2  Rec8, 100 M records/GPU, PLAIN_DICTIONARY + SNAPPY, 128 MiB row groups (BASELINE metric)
+  c3  Wide telemetry (ts + 199 optional cols, 30% null), 10 M records/GPU
+  c4  HighCard (ts, uuid, JSON blob, code), 20 M records/GPU
+  c5  64-partition topic: 8 partitions per GPU, one writer per partition on its own thread,
+      125 M records/GPU (15.625 M per partition, seed 0xC0FFEE05 + partition)
+Timed steps cycle over two distinct record batches (different seeds) for c2-c4; every step
+opens fresh writers, so nothing an encoder learns (K7's longest-first fragment order) carries
+between steps.
+
+Secondary keys: `resident_encode` (kpw_encoder_encode on a batch already in HBM, the r01
+headline), `roofline` (the dominant kernel, timed with HIP events on the encoder's stream inside
+the timed writer steps; algorithmic bytes per launch), `roofline.pipeline_frac` (sum of
+algorithmic bytes over sum of device time of every encode stage, §8d), a measured device copy
+ceiling, and `cpu_baseline` (the CPU oracle — a C restatement of parquet-mr 1.10.1 — doing the
+same work: host records in -> files out, one file per thread, median of 5 runs).
+
+Multi-GPU: one process per GPU (torchrun), each writing its own partitions (weak scaling, no
 data-path collective).  The barrier/max use torch.distributed (RCCL).
 """
 import argparse
+import ctypes
+import glob
 import json
 import os
 import sys
@@ -28,6 +47,7 @@ import numpy as np  # noqa: E402
 
 MiB = 1024 * 1024
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+POLL_BATCH = 500_000    # records per write call (a poll() batch)
 
 
 def log(msg):
@@ -35,13 +55,27 @@ def log(msg):
         print("[bench] " + msg, file=sys.stderr, flush=True)
 
 
-# SURVEY.md §8(d) configurations that fit one GPU: kind, records per GPU, seed, description.
-# C2 is the headline (BASELINE.json metric); C3 / C4 are extra measurement lines.
+# kind, records per GPU, seed, description
 WORKLOADS = {
-    "c2": (1, 100_000_000, 0xC0FFEE02, "C2: Rec8 (8 cols)"),
-    "c3": (3, 10_000_000, 0xC0FFEE03, "C3: Wide telemetry (ts + 199 optional cols, 30% null)"),
-    "c4": (2, 20_000_000, 0xC0FFEE04, "C4: HighCard (ts, uuid, JSON blob, code)"),
+    "c2": (1, 100_000_000, 0xC0FFEE02, "C2: Rec8 (8 cols), SNAPPY, 128 MiB row groups"),
+    "c3": (3, 10_000_000, 0xC0FFEE03, "C3: Wide telemetry (ts + 199 optional cols, 30% null), SNAPPY"),
+    "c4": (2, 20_000_000, 0xC0FFEE04, "C4: HighCard (ts, uuid, JSON blob, code), SNAPPY"),
+    "c5": (1, 125_000_000, 0xC0FFEE05, "C5: Rec8, 8 partitions per GPU, one writer per partition, SNAPPY"),
 }
+C5_PARTS_PER_GPU = 8
+
+
+def partition_seeds(workload, rank, world):
+    """Record sets of one rank: a list (timed steps cycle over it) of lists of partition seeds
+    (one writer per partition).  Ranks never share a partition (weak scaling, no exchange)."""
+    kind, _, wseed, _ = WORKLOADS[workload]
+    if workload == "c5":   # 64-partition topic: partitions rank*8 .. rank*8+7
+        return [[wseed + rank * C5_PARTS_PER_GPU + p for p in range(C5_PARTS_PER_GPU)]]
+    if workload == "c2":
+        seed = wseed if world == 1 else 0xC0FFEE05 + rank * C5_PARTS_PER_GPU
+    else:
+        seed = wseed + 0x100 * rank
+    return [[seed + 0x1000 * k] for k in range(2)]   # two distinct batches
 
 
 def decode_out_bytes(schema, n):
@@ -64,54 +98,35 @@ def decode_out_bytes(schema, n):
     return n * per + (bits * n) // 8
 
 
-def cpu_baseline(kind, seed, sample_records, threads):
-    """The CPU oracle (a C restatement of parquet-mr 1.10.1's write path, kind "port") on a
-    bounded sample of the same workload: `threads` independent files (one per thread, like
-    the reference's threadCount writers), each encoding sample_records/threads records."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    import synth
-    per = max(1, sample_records // threads)
-    chunks = [synth.generate(kind, seed, per, start=i * per) for i in range(threads)]
-    props = oracle.make_props(codec=oracle.SNAPPY)
-    total_bytes = sum(int(o[-1]) for _, o in chunks)
-    errs = []
-
-    def work(i):
-        try:
-            d, o = chunks[i]
-            oracle.encode_file(synth.SCHEMAS[kind], d, o, props)
-        except Exception as e:  # noqa: BLE001
-            errs.append(e)
-
-    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-    t0 = time.perf_counter()
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    dt = time.perf_counter() - t0
-    if errs:
-        raise errs[0]
-    return dict(value=round(total_bytes / dt / 1e9, 4), unit="GB/s", cores=threads, kind="port",
-                sample="%d %s records (%d per thread, %.1f MB), SNAPPY, 128 MiB row groups, %d threads, %.2f s"
-                       % (per * threads, synth.SCHEMAS[kind].message_name.split(".")[-1], per, total_bytes / 1e6, threads, dt),
-                records_per_s=round(per * threads / dt, 1))
+def column_bytes(schema, n, record_bytes):
+    """Columnar value bytes the chunk kernels read once (fixed-width values, string offset +
+    length + the string bytes themselves, bits): the K2/K4/K6 input."""
+    return decode_out_bytes(schema, n) - 4 * n + max(0, record_bytes - 2 * n * len(schema.columns)) // 2
 
 
-# K7 as launched by launch_snappy (k_snappy.hip): the register-table kernel on every fragment,
-# then the batched LDS kernel on the fragments it gave up on; timed together (one HIP-event
-# pair on the encoder's stream) and reported as one kernel step
-SNAPPY_KERNELS = ("kpw::k_snappy_v", "kpw::k_snappy_s_rest")
-SNAPPY_NAME = "K7 kpw::k_snappy_v + kpw::k_snappy_s_rest"
+def stage_bytes(schema, st):
+    """Algorithmic (compulsory) bytes per encode stage, SURVEY §8d, from a writer's totals.
+    Keys follow kpw_encoder_stage_times: decode, plan, stats+dict, rle, layout+plain+write,
+    compress."""
+    n, rb = st["records"], st["record_bytes"]
+    unc, comp = st["page_bytes_uncompressed"], st["page_bytes_compressed"]
+    cols = column_bytes(schema, n, rb)
+    nopt = sum(1 for c in schema.columns if c[3] == 1)
+    return {
+        "decode": rb + 8 * n + decode_out_bytes(schema, n),                 # K1: wire in, columns out
+        "plan": 4 * n + 8 * n + nopt * n // 8,                              # raw sizes in, prefix out, presence bits
+        "stats_dict": 2 * cols + 4 * n,                                     # K6 + K2: columns in (twice), ids out
+        "rle": 4 * n + nopt * n // 8 + 0,                                   # K3: ids / levels in (packed out counted in layout)
+        "layout_plain_write": cols + unc,                                   # K4: values in, page bodies out
+        "compress": unc + comp,                                             # K7: pages in, compressed out
+    }
 
 
-def pmc_traffic(kernels):
-    """HBM bytes per launch summed over `kernels` from the newest profiles/<tag>_pmc_traffic.json
-    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 FETCH correction;
-    profiles/summarize.py).  Returns (bytes, source file) or (None, None)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+def pmc_traffic(workload, kernels):
+    """HBM bytes per launch summed over `kernels` from the newest profiles/*_<workload>_pmc_traffic.json
+    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload; profiles/summarize.py
+    applies the gfx950 x2 FETCH correction to streaming kernels only).  Returns (bytes, file)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_%s_pmc_traffic.json" % workload)))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -137,16 +152,16 @@ def dist_init(world, local_rank, backend="nccl"):
 def timed_steps(step, steps, warmup, dist=None, sync=lambda: None):
     """W untimed warmup steps, then exactly K timed steps bracketed by barrier + device sync
     on both sides; returns (max-over-ranks elapsed seconds, per-step results)."""
-    for _ in range(warmup):
-        step()
+    for i in range(warmup):
+        step(i)
     sync()
     if dist:
         dist.barrier()
     sync()
     out = []
     t0 = time.perf_counter()
-    for _ in range(steps):
-        out.append(step())
+    for i in range(steps):
+        out.append(step(warmup + i))
     sync()
     if dist:
         dist.barrier()
@@ -165,6 +180,124 @@ def reduce_scalar(x, dist=None, op="sum"):
     return float(t.item())
 
 
+def write_file(kpw, schema, props, data, offs, device, batch=POLL_BATCH):
+    """One ParquetFile through the drop-in: batches straight from (pinned) host memory."""
+    pf = kpw.ParquetFile(None, schema, props, device=device)
+    L, h = pf._L, pf._h
+    base = data.ctypes.data
+    optr = offs.ctypes.data
+    n = len(offs) - 1
+    for a in range(0, n, batch):
+        b = min(n, a + batch)
+        st = L.kpw_writer_write(h, base, optr + 8 * a, b - a)   # absolute offsets into `data`
+        if st:
+            pf._check(st, "write")
+    pf.close()
+    size = L.kpw_writer_file_bytes  # noqa: F841 (file stays in memory; its length is reported)
+    p = ctypes.c_void_p()
+    ln = ctypes.c_uint64()
+    L.kpw_writer_file_bytes(h, ctypes.byref(p), ctypes.byref(ln))
+    return ln.value, pf.pipeline_stats()
+
+
+def copy_ceiling(device, nbytes=2 << 30):
+    """Measured device-to-device copy rate (read + write bytes / time), the practical HBM roof."""
+    import torch
+    src = torch.empty(nbytes, dtype=torch.uint8, device="cuda:%d" % device)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 5
+    del src, dst
+    torch.cuda.empty_cache()
+    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+
+
+def cpu_baseline(kind, seed, sample_records, threads, runs=5):
+    """The CPU oracle (C restatement of parquet-mr 1.10.1's write path, kind "port") doing the
+    same work as a writer step: host record bytes in -> a closed in-memory file out, one file
+    per thread (the reference's threadCount writers).  1 warm-up + `runs` timed runs, median."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import synth
+    per = max(1, sample_records // threads)
+    chunks = [synth.generate(kind, seed, per, start=i * per) for i in range(threads)]
+    props = oracle.make_props(codec=oracle.SNAPPY)
+    total_bytes = sum(int(o[-1]) for _, o in chunks)
+    times = []
+    for r in range(runs + 1):
+        errs = []
+
+        def work(i):
+            try:
+                d, o = chunks[i]
+                oracle.encode_file(synth.SCHEMAS[kind], d, o, props)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        dt = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        if r:
+            times.append(dt)
+    med = float(np.median(times))
+    return dict(value=round(total_bytes / med / 1e9, 4), unit="GB/s", cores=threads, kind="port",
+                sample="%d %s records (%d per thread, %.1f MB), SNAPPY, 128 MiB row groups, one in-memory file per "
+                       "thread, %d threads, median of %d runs (%s s)"
+                       % (per * threads, synth.SCHEMAS[kind].message_name.split(".")[-1], per, total_bytes / 1e6,
+                          threads, runs, ", ".join("%.2f" % t for t in times)),
+                records_per_s=round(per * threads / med, 1))
+
+
+def host_threads():
+    """CPU threads this process may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU
+    box gives one GPU's job a 16-CPU share and sets OMP_NUM_THREADS=16 accordingly)."""
+    n = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(n, omp) if omp > 0 else n
+
+
+def resident_encode(kpw, schema, batches, device, steps=3):
+    """Secondary: kpw_encoder_encode on batches already in HBM (pages stay in HBM), cycling
+    over the distinct batches; returns GB/s and the mean per-stage device ms."""
+    import torch
+    enc = kpw.Encoder(schema, device=device, codec=1, block_size=128 * MiB, page_size=128 * MiB)
+    dev = []
+    for data, offs in batches:
+        dev.append((torch.from_numpy(data).to("cuda"), torch.from_numpy(offs.view(np.int64)).to("cuda"), len(offs) - 1,
+                    int(offs[-1])))
+    torch.cuda.synchronize()
+    enc.encode(dev[0][0].data_ptr(), dev[0][1].data_ptr(), dev[0][2], final=True)   # warm-up
+    acc = np.zeros(10)
+    tot_bytes = 0
+    t0 = time.perf_counter()
+    for i in range(steps):
+        d, o, n, nb = dev[(i + 1) % len(dev)]
+        enc.encode(d.data_ptr(), o.data_ptr(), n, final=True)
+        acc += np.array(enc.stage_times()[:10], dtype=np.float64)
+        tot_bytes += nb
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del dev
+    torch.cuda.empty_cache()
+    names = ["decode", "plan", "stats+dict", "rle", "layout+plain+write", "compress", "metadata", "total", "k_decode",
+             "k7_snappy"]
+    return dict(value=round(tot_bytes / dt / 1e9, 3), unit="GB/s", steps=steps,
+                stage_ms=dict(zip(names, [round(x / steps, 3) for x in acc])))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -172,63 +305,78 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
                     help="SURVEY §8(d) configuration (c2 = the BASELINE.json metric's workload)")
-    ap.add_argument("--records", type=int, default=0, help="records per GPU (default: the workload's, C2: 100 M)")
-    ap.add_argument("--codec", type=int, default=1, help="0 UNCOMPRESSED, 1 SNAPPY (C2)")
+    ap.add_argument("--records", type=int, default=0, help="records per GPU (default: the workload's)")
     ap.add_argument("--cpu-sample", type=int, default=24_000_000,
-                    help="records for the CPU baseline sample (~1.5 GB, ~16 s of single-core oracle work)")
+                    help="records for the CPU baseline sample (C2-equivalent bytes for other workloads)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-resident", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(local_rank)   # torch's HIP runtime first (tests/conftest.py: _torch_hip_first)
+    torch.cuda.init()
     dist = dist_init(world, local_rank)
 
     import kpw
     import synth
     kind, default_records, wseed, wdesc = WORKLOADS[args.workload]
-    schema = synth.SCHEMAS[kind]
-    args.records = args.records or default_records
-    seed = (wseed if world == 1 else 0xC0FFEE05 + rank) if args.workload == "c2" else wseed + 0x100 * rank
+    sschema = synth.SCHEMAS[kind]
+    schema = kpw.Schema(sschema.message_name, sschema.columns, sschema.proto_class)
+    n = args.records or default_records
+    props = kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=kpw.SNAPPY, page_size=128 * MiB)
     t0 = time.perf_counter()
-    data, offs = synth.generate(kind, seed, args.records)
-    log("generated %d records (%.2f GB) in %.1fs" % (args.records, len(data) / 1e9, time.perf_counter() - t0))
-    d_data = torch.from_numpy(data).to("cuda")
-    d_off = torch.from_numpy(offs.view(np.int64)).to("cuda")
-    nbytes = int(offs[-1])
-    n = args.records
-    del data
-    enc = kpw.Encoder(kpw.Schema(schema.message_name, schema.columns, schema.proto_class),
-                      device=local_rank, codec=args.codec, block_size=128 * MiB, page_size=128 * MiB)
-    torch.cuda.synchronize()
+    seeds = partition_seeds(args.workload, rank, world)
+    per = n // len(seeds[0])
+    sets = [[synth.generate(kind, sd, per, alloc=kpw.pinned_empty) for sd in ss] for ss in seeds]
+    n = per * len(seeds[0])
+    set_bytes = [sum(int(o[-1]) for _, o in s) for s in sets]
+    log("generated %d x %d records (%.2f GB each) in pinned host memory in %.1fs"
+        % (len(sets), n, set_bytes[0] / 1e9, time.perf_counter() - t0))
 
-    def step():
-        return enc.encode(d_data.data_ptr(), d_off.data_ptr(), n, final=True)
+    def step(i):
+        s = sets[i % len(sets)]
+        if len(s) == 1:
+            size, st = write_file(kpw, schema, props, s[0][0], s[0][1], local_rank)
+            return [(size, st)], set_bytes[i % len(sets)]
+        res = [None] * len(s)
+        errs = []
 
-    stage_acc = np.zeros(10)
+        def one(k):
+            try:
+                res[k] = write_file(kpw, schema, props, s[k][0], s[k][1], local_rank)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        ts = [threading.Thread(target=one, args=(k,)) for k in range(len(s))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        return res, set_bytes[i % len(sets)]
 
-    def timed():
-        info = step()
-        stage_acc[:] += np.array(enc.stage_times(), dtype=np.float64)[:10]
-        return info
-
-    for _ in range(args.warmup):
-        step()
-    elapsed, infos = timed_steps(timed, args.steps, 0, dist, torch.cuda.synchronize)
-    info = infos[-1]
-    # whole-job units: every rank's own partition
-    total_bytes = reduce_scalar(nbytes * args.steps, dist)
+    elapsed, outs = timed_steps(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    my_bytes = sum(b for _, b in outs)
+    total_bytes = reduce_scalar(my_bytes, dist)
     total_records = reduce_scalar(n * args.steps, dist)
+    # pipeline statistics of every writer of the timed steps
+    agg = {}
+    files = 0
+    for res, _ in outs:
+        for size, st in res:
+            files += 1
+            for k, v in st.items():
+                agg[k] = agg.get(k, 0.0) + v
+    file_bytes = sum(size for res, _ in outs for size, _ in res)
 
-    # per-step page statistics (for algorithmic bytes of the compression kernel)
-    pages = enc.pages()
-    unc = sum(p["uncompressed_size"] for p in pages)
-    comp = sum(p["compressed_size"] for p in pages)
-    stages = (stage_acc / args.steps).tolist()
-    nrg = info.num_row_groups
+    resident = None
+    if not args.no_resident and args.workload != "c5" and rank == 0:
+        resident = resident_encode(kpw, schema, [s[0] for s in sets], local_rank)
+    ceiling = copy_ceiling(local_rank) if rank == 0 else None
 
     if rank != 0:
         if dist:
@@ -238,49 +386,56 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_bytes / elapsed / 1e9
     rec_s = total_records / elapsed
-    # K1 decode: algorithmic bytes = record bytes + offsets in; columnar values out
-    # (ts 8, user_id 4, status 4, price 8, score 8, key16 8+4, region 8+4 per record,
-    #  presence/boolean bits n/8 per optional column + flag bits, raw sizes 4 per record)
-    k1_bytes = nbytes + 8 * (n + 1) + decode_out_bytes(schema, n)
-    names = ["decode", "plan", "stats+dict", "rle", "layout+plain+write", "compress", "metadata", "total",
-             "k_decode", "k_snappy"]
-    stage = dict(zip(names, [round(x, 3) for x in stages]))
-    k_dec_ms = stages[8] if len(stages) > 8 else stages[0]
-    k_sn_ms = stages[9] if len(stages) > 9 else stages[5]
-    # the two kernels timed live with HIP events on the encoder's stream (kpw_encoder_stage_times
-    # [8], [9]); K7 = one launch of the Snappy fragment kernel over all pages of the batch
-    kern = {"kpw::k_decode": (k1_bytes, k_dec_ms, ("kpw::k_decode",)),
-            SNAPPY_NAME: (unc + comp, k_sn_ms, SNAPPY_KERNELS)}
+    jobs = max(1.0, agg.get("jobs", 1.0))
+    # dominant kernel of the timed steps: HIP events around K1 / K7 on the encoder's stream,
+    # averaged per launch (one launch per encode job)
+    k1_bytes = (agg["record_bytes"] + 8 * (agg["records"] + jobs) + decode_out_bytes(sschema, agg["records"])) / jobs
+    k7_bytes = (agg["page_bytes_uncompressed"] + agg["page_bytes_compressed"]) / jobs
+    kern = {"kpw::k_decode": (k1_bytes, agg["k_decode_ms"] / jobs, ("kpw::k_decode",)),
+            "K7 kpw::k_snappy_v + kpw::k_snappy_s_rest": (k7_bytes, agg["k7_snappy_ms"] / jobs,
+                                                         ("kpw::k_snappy_v", "kpw::k_snappy_s_rest"))}
     dom = max(kern, key=lambda k: kern[k][1])
     ab, ams, knames = kern[dom]
     achieved = ab / (ams * 1e-3) / 1e9 if ams > 0 else 0.0
-    traffic, tsrc = pmc_traffic(knames)
+    traffic, tsrc = pmc_traffic(args.workload, knames)
+    sb = stage_bytes(sschema, agg)
+    stage_ms = {"decode": agg["decode_ms"], "plan": agg["plan_ms"], "stats_dict": agg["stats_dict_ms"],
+                "rle": agg["rle_ms"], "layout_plain_write": agg["layout_plain_write_ms"], "compress": agg["compress_ms"]}
+    t_stages = sum(stage_ms.values())
+    pipe = sum(sb.values()) / (t_stages * 1e-3) / 1e9 if t_stages > 0 else 0.0
     roof = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBPS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBPS, 5),
                 traffic=(round(traffic / (ams * 1e-3) / 1e9, 2) if traffic else None),
                 traffic_bytes_per_launch=traffic, traffic_source=tsrc, algorithmic_bytes_per_launch=int(ab),
-                avg_launch_ms=round(ams, 4))
+                avg_launch_ms=round(ams, 4), launches=int(jobs),
+                pipeline_achieved=round(pipe, 2), pipeline_frac=round(pipe / HBM_PEAK_GBPS, 5),
+                pipeline_stage_ms=round(t_stages / jobs, 3),
+                copy_ceiling=ceiling, frac_of_copy_ceiling=round(achieved / ceiling, 5) if ceiling else None)
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
-        threads = args.cpu_threads or min(16, os.cpu_count() or 8)
+        threads = args.cpu_threads or host_threads()
         sample = args.cpu_sample
-        if args.workload != "c2":   # the same ~1.5 GB of wire bytes as the C2 sample
-            sample = max(threads, int(sample * 62 / max(1.0, nbytes / n)))
-        cpu = cpu_baseline(kind, seed, sample, threads)
+        if args.workload not in ("c2", "c5"):   # the same ~1.5 GB of wire bytes as the C2 sample
+            sample = max(threads, int(sample * 62 / max(1.0, set_bytes[0] / n)))
+        cpu = cpu_baseline(kind, wseed, sample, threads)
     out = {
         "metric": "Parquet encode GB/s + records/sec (whole node) at 1/2/4/8 MI355X vs CPU writer",
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8", "data": "synthetic (counter-based proto2 %s generator; no broker, in-memory record source)"
-                               % schema.message_name.split(".")[-1],
-        "config": {"workload": "%s, %d records/GPU, PLAIN_DICTIONARY + %s, 128 MiB row groups, "
-                               "128 MiB pages, parquet-mr 1.10.1 v1 semantics"
-                               % (wdesc, n, "SNAPPY" if args.codec else "UNCOMPRESSED"),
-                   "records_per_gpu": n, "bytes_per_gpu": nbytes, "row_groups_per_gpu": nrg,
-                   "codec": "SNAPPY" if args.codec else "UNCOMPRESSED", "parallelism": "partition-sharded x%d" % world},
+        "dtype": "u8",
+        "data": "synthetic (counter-based proto2 %s generator, pinned host memory; no broker: an in-memory record "
+                "source in poll()-sized batches of %d)" % (sschema.message_name.split(".")[-1], POLL_BATCH),
+        "config": {"workload": "%s, %d records/GPU, PLAIN_DICTIONARY + SNAPPY, 128 MiB row groups, 128 MiB pages, "
+                               "parquet-mr 1.10.1 v1 semantics; ParquetFile drop-in, host bytes -> closed in-memory file "
+                               "(H2D, encode, D2H, file assembly timed)" % (wdesc, n),
+                   "records_per_gpu": n, "bytes_per_gpu_step": set_bytes[0], "files_per_gpu_step": len(sets[0]),
+                   "codec": "SNAPPY", "parallelism": "partition-sharded x%d" % world},
         "records_per_s": round(rec_s, 1),
-        "stage_ms": stage,
-        "pages": {"uncompressed_bytes": int(unc), "compressed_bytes": int(comp), "count": len(pages)},
+        "file_bytes_per_step": int(file_bytes / max(1, args.steps)),
+        "encode_jobs_per_step": round(jobs / args.steps, 2),
+        "worker_encode_wall_ms_per_step": round(agg.get("worker_encode_wall_ms", 0) / args.steps, 2),
+        "stage_ms_per_step": {k: round(v / args.steps, 3) for k, v in stage_ms.items()},
+        "resident_encode": resident,
         "roofline": roof,
         "cpu_baseline": cpu,
     }

@@ -185,6 +185,7 @@ struct kpw_writer {
     int64_t last_rg_end = 0;           // InternalParquetRecordWriter.lastRowGroupEndPos (assembly thread)
     int64_t open_buffered = 0;         // open row group's buffered size after the last PLANNED job
     double t_encode = 0, t_wait = 0;
+    double stats[16] = {0};            // kpw_writer_stats (worker-written; read after drain)
 
     ~kpw_writer();
     int init_pipeline();
@@ -493,6 +494,10 @@ static int run_job(kpw_writer *w, const Job &j)
     }
     // pages -> host (pinned, double-buffered against the previous job's assembly)
     if (int st = join_assembly(w)) return st;
+    for (const PageOut &pg : out.pages) {
+        w->stats[3] += (double)pg.uncompressed_size;
+        w->stats[4] += (double)pg.compressed_size;
+    }
     if (!out.rgs.empty()) {
         const int slot = w->page_slot;
         w->page_slot ^= 1;
@@ -506,6 +511,13 @@ static int run_job(kpw_writer *w, const Job &j)
         start_assembly(w, std::move(out), slot);
     }
     w->t_encode += t1 - t0;
+    if (n_enc > 0) {
+        w->stats[0] += 1;
+        w->stats[1] += (double)n_enc;
+        w->stats[2] += (double)(hb[n_enc] - hb[0]);
+        for (int k = 0; k < 10; k++) w->stats[5 + k] += w->eng.stage_ms[k];
+        w->stats[15] += t1 - t0;
+    }
     if (trace_on())
         fprintf(stderr, "[kpw] job kind=%d records=%lld (carried %lld) encode %.2f ms, total %.2f ms\n", j.kind, (long long)n_enc,
                 (long long)ncarry, t1 - t0, now_ms() - t0);
@@ -1076,3 +1088,12 @@ extern "C" int kpw_writer_file_bytes(const kpw_writer *w, const uint8_t **bytes,
 }
 
 extern "C" void kpw_writer_free(kpw_writer *w) { delete w; }
+
+extern "C" int kpw_writer_stats(kpw_writer *w, double *out, int cap)
+{
+    if (!w || !out || cap <= 0) return 0;
+    if (drain(w)) return 0;
+    const int n = cap < 16 ? cap : 16;
+    for (int i = 0; i < n; i++) out[i] = w->stats[i];
+    return n;
+}

@@ -144,6 +144,15 @@ class ParquetFile:
     def close(self):
         self._check(self._L.kpw_writer_close(self._h), "close")
 
+    def pipeline_stats(self):
+        """kpw_writer_stats: accumulated job / byte counts and per-stage device ms."""
+        arr = (ctypes.c_double * 16)()
+        n = self._L.kpw_writer_stats(self._h, arr, 16)
+        names = ["jobs", "records", "record_bytes", "page_bytes_uncompressed", "page_bytes_compressed",
+                 "decode_ms", "plan_ms", "stats_dict_ms", "rle_ms", "layout_plain_write_ms", "compress_ms",
+                 "metadata_ms", "total_ms", "k_decode_ms", "k7_snappy_ms", "worker_encode_wall_ms"]
+        return dict(zip(names, list(arr[:n])))
+
     def file_bytes(self):
         p = ctypes.c_void_p()
         n = ctypes.c_uint64()

@@ -86,15 +86,17 @@ def lib():
     return _lib
 
 
-def generate(kind, seed, n, start=0, param=0):
-    """Return (data: np.uint8[], offsets: np.uint64[n+1]) for records start..start+n-1."""
+def generate(kind, seed, n, start=0, param=0, alloc=None):
+    """Return (data: np.uint8[], offsets: np.uint64[n+1]) for records start..start+n-1.
+    alloc(nbytes) -> uint8 array to generate into (e.g. kpw.pinned_empty); default numpy."""
     L = lib()
     sizes = np.empty(n, dtype=np.uint32)
     L.synth_sizes(ctypes.c_int(kind), ctypes.c_uint64(seed), ctypes.c_uint64(start), ctypes.c_uint64(n),
                   ctypes.c_int(param), sizes.ctypes.data_as(ctypes.c_void_p))
     offsets = np.zeros(n + 1, dtype=np.uint64)
     np.cumsum(sizes, out=offsets[1:])
-    data = np.empty(int(offsets[-1]), dtype=np.uint8)
+    del sizes
+    data = alloc(int(offsets[-1])) if alloc else np.empty(int(offsets[-1]), dtype=np.uint8)
     L.synth_fill(ctypes.c_int(kind), ctypes.c_uint64(seed), ctypes.c_uint64(start), ctypes.c_uint64(n),
                  ctypes.c_int(param), offsets.ctypes.data_as(ctypes.c_void_p), data.ctypes.data_as(ctypes.c_void_p))
     return data, offsets
