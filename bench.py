@@ -182,18 +182,23 @@ def reduce_scalar(x, dist=None, op="sum"):
 
 def write_file(kpw, schema, props, data, offs, device, batch=POLL_BATCH):
     """One ParquetFile through the drop-in: batches straight from (pinned) host memory."""
+    t0 = time.perf_counter()
     pf = kpw.ParquetFile(None, schema, props, device=device)
     L, h = pf._L, pf._h
     base = data.ctypes.data
     optr = offs.ctypes.data
     n = len(offs) - 1
+    t1 = time.perf_counter()
     for a in range(0, n, batch):
         b = min(n, a + batch)
         st = L.kpw_writer_write(h, base, optr + 8 * a, b - a)   # absolute offsets into `data`
         if st:
             pf._check(st, "write")
+    t2 = time.perf_counter()
     pf.close()
-    size = L.kpw_writer_file_bytes  # noqa: F841 (file stays in memory; its length is reported)
+    if os.environ.get("KPW_TRACE") == "1":
+        print("[bench] writer: open %.1f ms, writes %.1f ms, close %.1f ms" % (
+            (t1 - t0) * 1e3, (t2 - t1) * 1e3, (time.perf_counter() - t2) * 1e3), file=sys.stderr, flush=True)
     p = ctypes.c_void_p()
     ln = ctypes.c_uint64()
     L.kpw_writer_file_bytes(h, ctypes.byref(p), ctypes.byref(ln))

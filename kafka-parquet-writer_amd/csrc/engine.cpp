@@ -13,6 +13,7 @@
 
 #include "kpw_chunk.h"
 #include "kpw_scan.h"
+#include "memcache.h"
 
 namespace kpw {
 
@@ -28,19 +29,21 @@ void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, c
         if (e_ != hipSuccess) return fail(KPW_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// Buffers come from the process-wide cache (memcache.h).  Growing one may replace a block
+// that queued work (e.g. a D2H of the previous job's pages) still reads, so the device is
+// synchronised before the old block goes back to the cache (what hipFree used to imply).
 int DevBuf::ensure(size_t bytes)
 {
     if (bytes <= cap && p) return 0;
-    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    if (p) { (void)hipDeviceSynchronize(); dev_free(p); p = nullptr; cap = 0; }
     size_t c = bytes < 256 ? 256 : bytes + bytes / 8;
-    if (hipMalloc(&p, c) != hipSuccess) { p = nullptr; return -1; }
+    p = dev_alloc(c);
+    if (!p) return -1;
     cap = c;
     return 0;
 }
-DevBuf::~DevBuf()
-{
-    if (p) (void)hipFree(p);
-}
+// owners free their buffers only after synchronising the stream that used them
+DevBuf::~DevBuf() { dev_free(p); }
 
 Engine::~Engine()
 {

@@ -58,6 +58,7 @@ public:
     void *p = nullptr;
     size_t cap = 0;
     int ensure(size_t bytes);
+    void swap(DevBuf &o) { std::swap(p, o.p); std::swap(cap, o.cap); }
     ~DevBuf();
     template <typename T> T *as() const { return (T *)p; }
 };
@@ -71,6 +72,11 @@ public:
                hipStream_t user_stream, BatchOut &out);
     int copy_pages(uint64_t off, uint64_t len, void *host);
     const std::string &error() const { return err_; }
+    // Alternate the page output buffers between encodes, so the previous encode's pages can
+    // still be read (D2H on another stream) while this one runs.  The caller orders this
+    // encode after any reader of the buffers it now gets back (two encodes ago).
+    void swap_page_buffers() { d_body.swap(d_body_alt); d_comp.swap(d_comp_alt); }
+    bool multi_page() const { return mp_; }   // pages accumulate in one buffer (no alternation)
     std::vector<ColInfo> cols;
     kpw_props props{};
     std::string message_name, proto_class;
@@ -99,6 +105,7 @@ private:
     // snappy
     DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
     DevBuf d_smeta, d_sblob, d_collision, d_dict_order, d_sprof, d_sorder;
+    DevBuf d_body_alt, d_comp_alt;
     std::vector<double> sn_cost_;       // K7 mean fragment duration per (column, page kind), previous batch
     std::unordered_map<uint64_t, double> sn_fcost_;   // per (kind, fragment index)
     std::vector<uint32_t> sn_order_;

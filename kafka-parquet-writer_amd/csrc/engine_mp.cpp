@@ -25,6 +25,7 @@
 #include "filewriter.h"
 #include "kpw_chunk.h"
 #include "kpw_scan.h"
+#include "memcache.h"
 
 namespace kpw {
 
@@ -50,12 +51,12 @@ static inline uint64_t next_pow2_mp(uint64_t x)
 int Engine::grow_keep(DevBuf &b, size_t bytes, size_t keep)
 {
     if (bytes <= b.cap && b.p) return KPW_OK;
-    void *np = nullptr;
     const size_t c = bytes + bytes / 2 + 256;
-    if (hipMalloc(&np, c) != hipSuccess) return fail(KPW_ERR_NOMEM, "device allocation failed: multi-page output");
+    void *np = dev_alloc(c);
+    if (!np) return fail(KPW_ERR_NOMEM, "device allocation failed: multi-page output");
     if (keep && b.p) CK(hipMemcpyAsync(np, b.p, keep, hipMemcpyDeviceToDevice, stream));
     CK(hipStreamSynchronize(stream));
-    if (b.p) (void)hipFree(b.p);
+    dev_free(b.p);
     b.p = np;
     b.cap = c;
     return KPW_OK;

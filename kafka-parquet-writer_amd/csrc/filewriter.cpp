@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include "filewriter.h"
+#include "memcache.h"
 
 #include <cstring>
 
@@ -189,7 +190,62 @@ FileWriter::FileWriter(const std::vector<ColInfo> &cols, const std::string &mess
 FileWriter::~FileWriter()
 {
     if (fp_) fclose(fp_);
-    free(mem_);
+    for (auto &c : chunks_) pin_free(c.first);
+    free(flat_);
+}
+
+int FileWriter::reserve(size_t n)
+{
+    while (mem_len_ + n > mem_cap_) {
+        const size_t c = std::max<size_t>(256ull << 20, std::min<size_t>(mem_cap_, 4ull << 30));
+        uint8_t *q = (uint8_t *)pin_alloc(c);
+        if (!q) { err_ = "out of pinned host memory"; return KPW_ERR_NOMEM; }
+        chunks_.push_back({q, c});
+        mem_cap_ += c;
+    }
+    return KPW_OK;
+}
+
+const uint8_t *FileWriter::memory_data()
+{
+    if (chunks_.empty()) return nullptr;
+    if (chunks_.size() == 1) return chunks_[0].first;
+    if (!flat_) {
+        flat_ = (uint8_t *)malloc(mem_len_ ? mem_len_ : 1);
+        if (!flat_) return nullptr;
+        size_t at = 0;
+        for (auto &c : chunks_) {
+            const size_t k = std::min(c.second, mem_len_ - at);
+            par_copy(flat_ + at, c.first, k);
+            at += k;
+            if (at == mem_len_) break;
+        }
+    }
+    return flat_;
+}
+
+int FileWriter::put_device(const uint8_t *d, size_t n, hipStream_t s)
+{
+    if (!n) return KPW_OK;
+    if (int st = reserve(n)) return st;
+    size_t at = mem_len_, base = 0;
+    for (auto &c : chunks_) {
+        if (at < base + c.second) {
+            const size_t off = at - base, k = std::min(n, c.second - off);
+            if (hipMemcpyAsync(c.first + off, d, k, hipMemcpyDeviceToHost, s) != hipSuccess) {
+                err_ = "D2H of a page failed";
+                return KPW_ERR_DEVICE;
+            }
+            d += k;
+            n -= k;
+            at += k;
+            mem_len_ += k;
+            pos_ += (int64_t)k;
+            if (!n) break;
+        }
+        base += c.second;
+    }
+    return KPW_OK;
 }
 
 void par_copy(uint8_t *dst, const uint8_t *src, size_t n)
@@ -215,15 +271,20 @@ int FileWriter::put(const void *p, size_t n)
     if (fp_) {
         if (fwrite(p, 1, n, fp_) != n) { err_ = "short write"; return KPW_ERR_IO; }
     } else {
-        if (mem_len_ + n > mem_cap_) {
-            const size_t c = std::max(mem_len_ + n, mem_cap_ + mem_cap_ / 2 + 4096);
-            uint8_t *q = (uint8_t *)realloc(mem_, c);
-            if (!q) { err_ = "out of host memory"; return KPW_ERR_NOMEM; }
-            mem_ = q;
-            mem_cap_ = c;
+        if (int st = reserve(n)) return st;
+        const uint8_t *src = (const uint8_t *)p;
+        size_t base = 0, left = n;
+        for (auto &c : chunks_) {
+            if (mem_len_ < base + c.second) {
+                const size_t off = mem_len_ - base, k = std::min(left, c.second - off);
+                par_copy(c.first + off, src, k);
+                src += k;
+                left -= k;
+                mem_len_ += k;
+                if (!left) break;
+            }
+            base += c.second;
         }
-        par_copy(mem_ + mem_len_, (const uint8_t *)p, n);
-        mem_len_ += n;
     }
     pos_ += (int64_t)n;
     return KPW_OK;
@@ -238,7 +299,7 @@ int FileWriter::open(const char *path)
     return put("PAR1", 4);  // ParquetFileWriter.start()
 }
 
-int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages, uint64_t pages_base)
+int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages, uint64_t pages_base, hipStream_t d2h)
 {
     const RowGroupOut &R = b.rgs[rg];
     RowGroupMeta rm;
@@ -276,7 +337,8 @@ int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages,
             comp += pg.compressed_size + (int64_t)hdr.size();
             int st2 = put(hdr.data(), hdr.size());
             if (st2) return st2;
-            st2 = put(pages + (pg.offset - pages_base), (size_t)pg.compressed_size);
+            st2 = d2h && !fp_ ? put_device(pages + (pg.offset - pages_base), (size_t)pg.compressed_size, d2h)
+                              : put(pages + (pg.offset - pages_base), (size_t)pg.compressed_size);
             if (st2) return st2;
         }
         // ColumnChunkPageWriter: rl encodings, dl encodings, data encodings (per page); v2

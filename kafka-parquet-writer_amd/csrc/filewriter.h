@@ -3,6 +3,7 @@
 // parquet-mr 1.10.1 ParquetFileWriter + ParquetMetadataConverter as driven by
 // ColumnChunkPageWriteStore.flushToFileWriter (dictionary page first, then data pages).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <cstdio>
 #include <string>
@@ -48,23 +49,31 @@ public:
     ~FileWriter();
     int open(const char *path);       // nullptr = memory
     // Appends one encoded row group; `pages` is host memory holding the batch's page bodies
-    // (indexed by PageOut.offset relative to pages_base).
-    int write_row_group(const BatchOut &b, int rg, const uint8_t *pages, uint64_t pages_base);
+    // (indexed by PageOut.offset relative to pages_base).  With d2h != nullptr (memory mode
+    // only) `pages` is DEVICE memory: the bodies are copied straight into the in-memory file
+    // on that stream (the caller synchronises it before the file is read).
+    int write_row_group(const BatchOut &b, int rg, const uint8_t *pages, uint64_t pages_base, hipStream_t d2h = nullptr);
+    bool memory_mode() const { return fp_ == nullptr; }
     // Bytes write_row_group would append for row group `rg` (page headers + compressed bodies).
     int64_t row_group_size(const BatchOut &b, int rg) const;
     int close();                      // footer + magic
     int64_t pos() const { return pos_; }
-    const uint8_t *memory_data() const { return mem_; }
+    const uint8_t *memory_data();     // contiguous view (built on first use after close)
     size_t memory_size() const { return mem_len_; }
     const std::string &error() const { return err_; }
 
 private:
     int put(const void *p, size_t n);
+    int put_device(const uint8_t *d, size_t n, hipStream_t s);
+    int reserve(size_t n);            // arena room for n more bytes
     std::vector<ColInfo> cols_;
     std::string message_name_, proto_class_;
     kpw_props props_;
     FILE *fp_ = nullptr;
-    uint8_t *mem_ = nullptr;        // memory mode: malloc/realloc-grown (large reallocs remap, no copy)
+    // memory mode: pinned chunks (page bodies arrive by D2H straight into place); `flat_` is a
+    // contiguous copy for memory_data() when there is more than one chunk
+    std::vector<std::pair<uint8_t *, size_t>> chunks_;
+    uint8_t *flat_ = nullptr;
     size_t mem_len_ = 0, mem_cap_ = 0;
     int64_t pos_ = 0;
     std::vector<RowGroupMeta> rgs_;

@@ -7,6 +7,7 @@
 #include "kpw_device.h"
 #include "kpw_kernels.h"
 #include "kpw_scan.h"
+#include "memcache.h"
 
 namespace kpw {
 
@@ -233,7 +234,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_seg_apply(const T *in, T *out, co
 
 void seg_scratch_free(SegScratch &sc)
 {
-    if (sc.p) (void)hipFree(sc.p);
+    dev_free(sc.p);
     sc.p = nullptr;
     sc.bytes = 0;
 }
@@ -246,9 +247,10 @@ void seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot,
     const size_t need = (size_t)nb * (sizeof(T) + sizeof(uint32_t)) + 64;
     if (need > sc->bytes) {
         // earlier scans of this handle may still read the old buffer on `s`
-        if (sc->p) { (void)hipStreamSynchronize(s); (void)hipFree(sc->p); }
+        if (sc->p) { (void)hipStreamSynchronize(s); dev_free(sc->p); }
         sc->bytes = need * 2;
-        if (hipMalloc(&sc->p, sc->bytes) != hipSuccess) { sc->p = nullptr; sc->bytes = 0; sc->failed = true; return; }
+        sc->p = dev_alloc(sc->bytes);
+        if (!sc->p) { sc->bytes = 0; sc->failed = true; return; }
     }
     T *bv = (T *)sc->p;
     uint32_t *bh = (uint32_t *)((char *)sc->p + (((size_t)nb * sizeof(T) + 15) & ~(size_t)15));

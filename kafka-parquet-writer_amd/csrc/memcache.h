@@ -1,0 +1,22 @@
+// memcache.h — process-wide caching allocators for device (HBM) and pinned host memory.
+//
+// A writer is a file (the reference opens one ParquetFile per rotation, and C5 runs many at
+// once), and hipMalloc / hipFree / hipHostMalloc / hipHostFree of its multi-GiB stage, scratch
+// and page buffers cost more than encoding a row group (hipFree also synchronises the whole
+// device).  Freed blocks are kept per device (per size, best fit within 2x) and handed to the
+// next allocation.  A block goes back to the cache only when no queued work can still touch
+// it: the callers free after synchronising the stream that used it (Engine / writer teardown,
+// buffer growth after a sync).
+#pragma once
+#include <stddef.h>
+
+namespace kpw {
+
+void *dev_alloc(size_t bytes);     // on the current device; nullptr on failure
+void dev_free(void *p);            // nullptr ok
+void *pin_alloc(size_t bytes);     // page-locked host memory; nullptr on failure
+void pin_free(void *p);            // nullptr ok
+size_t pin_size(const void *p);    // usable bytes of a pin_alloc block containing p (0 if none)
+bool pin_contains(const void *p, size_t n);   // [p, p+n) inside one live pin_alloc block
+
+}  // namespace kpw

@@ -46,6 +46,7 @@
 #include "../../include/kpw_gpu.h"
 #include "engine.h"
 #include "filewriter.h"
+#include "memcache.h"
 #include "sizemodel.h"
 
 using namespace kpw;
@@ -81,33 +82,27 @@ uint64_t model_max_batch()
     return v;
 }
 
-// ---- pinned host allocations handed out by kpw_host_alloc (direct-DMA sources)
-std::mutex g_pin_mu;
-std::map<uintptr_t, size_t> g_pins;
+// pinned host memory handed out by kpw_host_alloc (or used inside the library): direct-DMA sources
+bool pinned_range(const void *p, size_t n) { return pin_contains(p, n); }
 
-bool pinned_range(const void *p, size_t n)
-{
-    std::lock_guard<std::mutex> g(g_pin_mu);
-    auto it = g_pins.upper_bound((uintptr_t)p);
-    if (it == g_pins.begin()) return false;
-    --it;
-    return (uintptr_t)p >= it->first && (uintptr_t)p + n <= it->first + it->second;
-}
-
-// Page-locked host memory owned by the library.
+// Page-locked host memory owned by the library (from the pinned cache, memcache.h).  Its
+// previous contents are never DMA targets or sources when it grows (callers ensure it).
 struct PinnedBuf {
     uint8_t *p = nullptr;
     size_t cap = 0;
     int ensure(size_t bytes)
     {
         if (bytes <= cap && p) return 0;
-        if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+        pin_free(p);
+        p = nullptr;
+        cap = 0;
         const size_t c = bytes + bytes / 4 + 4096;
-        if (hipHostMalloc((void **)&p, c, hipHostMallocDefault) != hipSuccess) { p = nullptr; return -1; }
+        p = (uint8_t *)pin_alloc(c);
+        if (!p) return -1;
         cap = c;
         return 0;
     }
-    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    ~PinnedBuf() { pin_free(p); }
 };
 
 enum { BUF_FREE = 0, BUF_FILLING = 1, BUF_QUEUED = 2 };
@@ -178,13 +173,19 @@ struct kpw_writer {
     PinnedBuf host_pages[2];
     int page_slot = 0;
     hipEvent_t d2h_ev[2] = {};
+    // memory mode: page bodies go D2H straight into the in-memory file on d2h_stream while
+    // the next job encodes into the engine's other page buffer set
+    hipStream_t d2h_stream = nullptr;
+    hipEvent_t enc_done = nullptr;
+    bool d2h_used[2] = {false, false};
+    uint64_t njobs = 0;
     std::thread assembler;
     int asm_st = KPW_OK;
     std::string asm_err;
     BatchOut asm_out;
     int64_t last_rg_end = 0;           // InternalParquetRecordWriter.lastRowGroupEndPos (assembly thread)
     int64_t open_buffered = 0;         // open row group's buffered size after the last PLANNED job
-    double t_encode = 0, t_wait = 0;
+    double t_encode = 0, t_wait = 0, t_dma = 0, t_acquire = 0, t_slot = 0, t_asm = 0, t_d2h_alloc = 0;
     double stats[16] = {0};            // kpw_writer_stats (worker-written; read after drain)
 
     ~kpw_writer();
@@ -220,9 +221,9 @@ static int check_fatal(kpw_writer *w)
 
 static int alloc_buf(kpw_writer *w, StageBuf &b, size_t cap)
 {
-    uint8_t *nd = nullptr;
-    if (hipMalloc((void **)&nd, cap) != hipSuccess) return KPW_ERR_NOMEM;
-    if (b.d) (void)hipFree(b.d);
+    uint8_t *nd = (uint8_t *)dev_alloc(cap);
+    if (!nd) return KPW_ERR_NOMEM;
+    dev_free(b.d);   // a FREE buffer: its last job synchronised before releasing it
     b.d = nd;
     b.cap = cap;
     return KPW_OK;
@@ -232,6 +233,7 @@ static int alloc_buf(kpw_writer *w, StageBuf &b, size_t cap)
 static int acquire_fill(kpw_writer *w)
 {
     int k = -1;
+    const double ta = trace_on() ? now_ms() : 0.0;
     {
         std::unique_lock<std::mutex> lk(w->mu);
         for (;;) {
@@ -246,6 +248,7 @@ static int acquire_fill(kpw_writer *w)
     StageBuf &b = w->buf[k];
     const size_t need = w->gap_ + stage_flush_bytes() + (64ull << 20);
     if (b.cap < need && alloc_buf(w, b, need)) return wfail(w, KPW_ERR_NOMEM, "device stage buffer allocation failed");
+    if (trace_on()) w->t_acquire += now_ms() - ta;
     b.gap = w->gap_;
     b.len = w->gap_;
     b.carry.clear();
@@ -278,9 +281,11 @@ static int stage_bytes(kpw_writer *w, const uint8_t *src, uint64_t len)
     if (pinned_range(src, len)) {
         // direct DMA from the caller's pinned batch; waited for, so the caller may reuse it
         if (int st = flush_slot(w)) return st;
+        const double ta = trace_on() ? now_ms() : 0.0;
         if (hipMemcpyAsync(F.d + F.len, src, len, hipMemcpyHostToDevice, w->copy_stream) != hipSuccess ||
             hipEventRecord(w->direct_ev, w->copy_stream) != hipSuccess || hipEventSynchronize(w->direct_ev) != hipSuccess)
             return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
+        if (trace_on()) w->t_dma += now_ms() - ta;
         F.len += len;
         return KPW_OK;
     }
@@ -316,25 +321,31 @@ static int grow_fill(kpw_writer *w, uint64_t bytes)
     if (int st = flush_slot(w)) return st;
     if (hipStreamSynchronize(w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "staging sync failed");
     const size_t cap = std::max<size_t>(F.cap * 2, F.len + bytes + (64ull << 20));
-    uint8_t *nd = nullptr;
-    if (hipMalloc((void **)&nd, cap) != hipSuccess) return wfail(w, KPW_ERR_NOMEM, "device stage buffer allocation failed");
+    uint8_t *nd = (uint8_t *)dev_alloc(cap);
+    if (!nd) return wfail(w, KPW_ERR_NOMEM, "device stage buffer allocation failed");
     if (F.len && hipMemcpy(nd, F.d, F.len, hipMemcpyDeviceToDevice) != hipSuccess) {
-        (void)hipFree(nd);
+        dev_free(nd);
         return wfail(w, KPW_ERR_DEVICE, "stage buffer grow copy failed");
     }
-    (void)hipFree(F.d);
+    dev_free(F.d);
     F.d = nd;
     F.cap = cap;
     return KPW_OK;
 }
 
 // Record boundaries of a buffer's records: carried then appended ([n+1] absolute offsets).
+static size_t nbounds(const StageBuf &B) { return (B.carry.empty() ? 1 : B.carry.size()) + B.ends.size(); }
+static void boundaries(const StageBuf &B, uint64_t *hb)
+{
+    size_t k = 0;
+    if (B.carry.empty()) hb[k++] = B.gap;
+    else { memcpy(hb, B.carry.data(), B.carry.size() * 8); k = B.carry.size(); }
+    if (!B.ends.empty()) memcpy(hb + k, B.ends.data(), B.ends.size() * 8);
+}
 static void boundaries(const StageBuf &B, std::vector<uint64_t> &hb)
 {
-    hb.clear();
-    if (B.carry.empty()) hb.push_back(B.gap);
-    else hb.insert(hb.end(), B.carry.begin(), B.carry.end());
-    hb.insert(hb.end(), B.ends.begin(), B.ends.end());
+    hb.resize(nbounds(B));
+    boundaries(B, hb.data());
 }
 
 // ---------------------------------------------------------------- worker
@@ -348,17 +359,17 @@ static int materialize(kpw_writer *w, StageBuf &B)
     const uint64_t cs = B.carry.back();                 // carried bytes (store offsets start at 0)
     const uint64_t app = B.len - B.gap;
     const size_t cap = std::max<size_t>(B.cap, cs + app + w->gap_ + (64ull << 20));
-    uint8_t *nd = nullptr;
-    if (hipMalloc((void **)&nd, cap) != hipSuccess) return KPW_ERR_NOMEM;
+    uint8_t *nd = (uint8_t *)dev_alloc(cap);
+    if (!nd) return KPW_ERR_NOMEM;
     if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess ||
         hipMemcpyAsync(nd, w->carry_store.p, cs, hipMemcpyDeviceToDevice, s) != hipSuccess ||
         (app && hipMemcpyAsync(nd + cs, B.d + B.gap, app, hipMemcpyDeviceToDevice, s) != hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess) {
-        (void)hipFree(nd);
+        dev_free(nd);
         return KPW_ERR_DEVICE;
     }
     for (auto &e : B.ends) e = e - B.gap + cs;
-    (void)hipFree(B.d);
+    dev_free(B.d);
     B.d = nd;
     B.cap = cap;
     B.len = cs + app;
@@ -369,7 +380,7 @@ static int materialize(kpw_writer *w, StageBuf &B)
 
 // Place records [b0, b1) of buffer `src` (boundaries hb[i0..i1]) in front of buffer `dst`'s
 // appended records.
-static int place_carry(kpw_writer *w, const StageBuf &src, const std::vector<uint64_t> &hb, size_t i0, size_t i1, StageBuf &dst)
+static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, size_t i0, size_t i1, StageBuf &dst)
 {
     hipStream_t s = w->eng.stream;
     const uint64_t b0 = hb[i0], c = hb[i1] - b0;
@@ -404,6 +415,7 @@ static void start_assembly(kpw_writer *w, BatchOut &&out, int slot)
                 w->asm_err = "D2H of pages failed";
                 return;
             }
+            const double ta = trace_on() ? now_ms() : 0.0;
             for (size_t r = 0; r < w->asm_out.rgs.size(); r++) {
                 const int st = w->fw->write_row_group(w->asm_out, (int)r, w->host_pages[slot].p, 0);
                 if (st) {
@@ -413,6 +425,7 @@ static void start_assembly(kpw_writer *w, BatchOut &&out, int slot)
                 }
                 w->last_rg_end = w->fw->pos();
             }
+            if (trace_on()) w->t_asm += now_ms() - ta;
         } catch (const std::bad_alloc &) {
             w->asm_st = KPW_ERR_NOMEM;
             w->asm_err = "file assembly: host allocation failed";
@@ -446,18 +459,29 @@ static int run_job(kpw_writer *w, const Job &j)
         after_invalid = w->invalid_seen;
     }
     if (after_invalid) { B.ends.clear(); B.len = B.gap; }   // records behind an invalid one are never written
-    std::vector<uint64_t> hb;
+    // boundaries straight into the pinned offset buffer (also the carry bookkeeping below)
+    const size_t nb = nbounds(B);
+    if (w->h_off.ensure(nb * 8)) return set_fatal(w, KPW_ERR_NOMEM, "offset staging allocation failed"), KPW_ERR_NOMEM;
+    uint64_t *hb = (uint64_t *)w->h_off.p;
     boundaries(B, hb);
-    const int64_t nrec = (int64_t)hb.size() - 1;
+    const int64_t nrec = (int64_t)nb - 1;
     const int64_t ncarry = B.carry.empty() ? 0 : (int64_t)B.carry.size() - 1;
     const int64_t n_enc = j.kind == JOB_EXACT ? std::min<int64_t>(j.n_exact, nrec) : nrec;
     const double t0 = now_ms();
     if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess) return set_fatal(w, KPW_ERR_DEVICE, "stream wait failed"), KPW_ERR_DEVICE;
     BatchOut out;
+    const bool direct = w->fw->memory_mode();
+    const int set = (int)(w->njobs & 1);
+    if (direct && n_enc > 0) {
+        // the page buffers this encode gets back were last read by the D2H of two jobs ago
+        w->eng.swap_page_buffers();
+        for (int k = 0; k < 2; k++)
+            if (w->d2h_used[k] && (k == set || w->eng.multi_page()) && hipStreamWaitEvent(s, w->d2h_ev[k], 0) != hipSuccess)
+                return set_fatal(w, KPW_ERR_DEVICE, "stream wait failed"), KPW_ERR_DEVICE;
+    }
     if (n_enc > 0) {
-        if (w->d_off.ensure((n_enc + 1) * 8) || w->h_off.ensure((n_enc + 1) * 8))
+        if (w->d_off.ensure((n_enc + 1) * 8))
             return set_fatal(w, KPW_ERR_NOMEM, "offset staging allocation failed"), KPW_ERR_NOMEM;
-        memcpy(w->h_off.p, hb.data(), (n_enc + 1) * 8);
         if (hipMemcpyAsync(w->d_off.p, w->h_off.p, (n_enc + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
             return set_fatal(w, KPW_ERR_DEVICE, "H2D of offsets failed"), KPW_ERR_DEVICE;
         // EXACT jobs are encoded non-final: the GPU planner must cut the same single row group
@@ -492,20 +516,38 @@ static int run_job(kpw_writer *w, const Job &j)
         if (j.kind == JOB_PLANNED) w->open_buffered = out.open_buffered;
         w->cv.notify_all();
     }
-    // pages -> host (pinned, double-buffered against the previous job's assembly)
-    if (int st = join_assembly(w)) return st;
     for (const PageOut &pg : out.pages) {
         w->stats[3] += (double)pg.uncompressed_size;
         w->stats[4] += (double)pg.compressed_size;
     }
-    if (!out.rgs.empty()) {
+    if (direct && !out.rgs.empty()) {
+        // memory mode: headers on the host, bodies D2H straight into the file (no host copy)
+        const double ta = trace_on() ? now_ms() : 0.0;
+        if (hipEventRecord(w->enc_done, s) != hipSuccess || hipStreamWaitEvent(w->d2h_stream, w->enc_done, 0) != hipSuccess)
+            return set_fatal(w, KPW_ERR_DEVICE, "event record failed"), KPW_ERR_DEVICE;
+        for (size_t r = 0; r < out.rgs.size(); r++) {
+            if (int st = w->fw->write_row_group(out, (int)r, out.d_pages, 0, w->d2h_stream))
+                return set_fatal(w, st, w->fw->error()), st;
+            w->last_rg_end = w->fw->pos();
+        }
+        if (hipEventRecord(w->d2h_ev[set], w->d2h_stream) != hipSuccess)
+            return set_fatal(w, KPW_ERR_DEVICE, "event record failed"), KPW_ERR_DEVICE;
+        w->d2h_used[set] = true;
+        w->njobs++;
+        if (trace_on()) w->t_asm += now_ms() - ta;
+    } else if (!out.rgs.empty()) {
+        // file mode: pages -> host (pinned, double-buffered against the previous job's
+        // assembly), then headers + bodies written on the assembly thread
+        if (int st = join_assembly(w)) return st;
         const int slot = w->page_slot;
         w->page_slot ^= 1;
         if (out.pages_len) {
+            const double ta = trace_on() ? now_ms() : 0.0;
             if (w->host_pages[slot].ensure(out.pages_len))
                 return set_fatal(w, KPW_ERR_NOMEM, "pinned page buffer allocation failed"), KPW_ERR_NOMEM;
             if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, out.pages_len, hipMemcpyDeviceToHost, s) != hipSuccess)
                 return set_fatal(w, KPW_ERR_DEVICE, "D2H of pages failed"), KPW_ERR_DEVICE;
+            if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
         }
         if (hipEventRecord(w->d2h_ev[slot], s) != hipSuccess) return set_fatal(w, KPW_ERR_DEVICE, "event record failed"), KPW_ERR_DEVICE;
         start_assembly(w, std::move(out), slot);
@@ -559,7 +601,11 @@ static void worker_main(kpw_writer *w)
             }
             idle = w->q.empty();
         }
-        if (idle) (void)join_assembly(w);   // idle implies every queued job is in the file
+        if (idle) {   // idle implies every queued job is in the file
+            (void)join_assembly(w);
+            if (w->d2h_stream && hipStreamSynchronize(w->d2h_stream) != hipSuccess)
+                set_fatal(w, KPW_ERR_DEVICE, "D2H of pages failed");
+        }
         {
             std::lock_guard<std::mutex> g(w->mu);
             w->busy = false;
@@ -628,6 +674,8 @@ int kpw_writer::init_pipeline()
     for (auto &e : d2h_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     if (hipEventCreateWithFlags(&direct_ev, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&enc_done, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    if (hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &b : buf)
         if (hipEventCreateWithFlags(&b.copied, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     // the open row group of a job lands in the next buffer's gap (its wire bytes are a small
@@ -653,12 +701,14 @@ kpw_writer::~kpw_writer()
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     if (eng.stream) (void)hipStreamSynchronize(eng.stream);
     for (auto &b : buf) {
-        if (b.d) (void)hipFree(b.d);
+        dev_free(b.d);
         if (b.copied) (void)hipEventDestroy(b.copied);
     }
     for (auto &e : slot_ev) if (e) (void)hipEventDestroy(e);
     for (auto &e : d2h_ev) if (e) (void)hipEventDestroy(e);
     if (direct_ev) (void)hipEventDestroy(direct_ev);
+    if (d2h_stream) { (void)hipStreamSynchronize(d2h_stream); (void)hipStreamDestroy(d2h_stream); }
+    if (enc_done) (void)hipEventDestroy(enc_done);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     delete fw;
 }
@@ -667,14 +717,10 @@ kpw_writer::~kpw_writer()
 
 extern "C" void *kpw_host_alloc(uint64_t bytes, int *status)
 {
-    void *p = nullptr;
-    if (!bytes || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    void *p = bytes ? pin_alloc(bytes) : nullptr;
+    if (!p) {
         if (status) *status = bytes ? KPW_ERR_NOMEM : KPW_ERR_INVALID_ARG;
         return nullptr;
-    }
-    {
-        std::lock_guard<std::mutex> g(g_pin_mu);
-        g_pins[(uintptr_t)p] = bytes;
     }
     if (status) *status = KPW_OK;
     return p;
@@ -682,12 +728,7 @@ extern "C" void *kpw_host_alloc(uint64_t bytes, int *status)
 
 extern "C" void kpw_host_free(void *p)
 {
-    if (!p) return;
-    {
-        std::lock_guard<std::mutex> g(g_pin_mu);
-        g_pins.erase((uintptr_t)p);
-    }
-    (void)hipHostFree(p);
+    pin_free(p);   // kept pinned for the next kpw_host_alloc
 }
 
 extern "C" kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, const kpw_props *props, const char *path, int *status)
@@ -832,8 +873,10 @@ static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offset
     StageBuf &F = w->buf[w->fill];
     const uint64_t delta = F.len - offsets[0];
     if (int st = stage_bytes(w, data + offsets[0], bytes)) return st;
-    F.ends.reserve(F.ends.size() + n);
-    for (uint64_t i = 1; i <= n; i++) F.ends.push_back(offsets[i] + delta);
+    const size_t m = F.ends.size();
+    F.ends.resize(m + n);   // geometric growth (an exact reserve per call would copy the vector every call)
+    uint64_t *e = F.ends.data() + m;
+    for (uint64_t i = 1; i <= n; i++) e[i - 1] = offsets[i] + delta;
     w->num_records += (int64_t)n;
     w->dirty = true;
     return KPW_OK;
@@ -1070,7 +1113,10 @@ extern "C" int kpw_writer_close(kpw_writer *w)
         int st = w->fw->close();
         if (st) return wfail(w, st, w->fw->error());
         w->closed = true;
-        if (trace_on()) fprintf(stderr, "[kpw] close: worker encode time %.1f ms\n", w->t_encode);
+        if (trace_on())
+            fprintf(stderr, "[kpw] close: worker encode %.1f ms; caller: pinned DMA waits %.1f ms, buffer acquire %.1f ms; "
+                            "worker: page buffer alloc + D2H issue %.1f ms; assembly %.1f ms\n",
+                    w->t_encode, w->t_dma, w->t_acquire, w->t_d2h_alloc, w->t_asm);
         return KPW_OK;
     } catch (...) {
         set_fatal(w, KPW_ERR_DEVICE, "close failed");
