@@ -199,10 +199,7 @@ def write_file(kpw, schema, props, data, offs, device, batch=POLL_BATCH):
     if os.environ.get("KPW_TRACE") == "1":
         print("[bench] writer: open %.1f ms, writes %.1f ms, close %.1f ms" % (
             (t1 - t0) * 1e3, (t2 - t1) * 1e3, (time.perf_counter() - t2) * 1e3), file=sys.stderr, flush=True)
-    p = ctypes.c_void_p()
-    ln = ctypes.c_uint64()
-    L.kpw_writer_file_bytes(h, ctypes.byref(p), ctypes.byref(ln))
-    return ln.value, pf.pipeline_stats()
+    return L.kpw_writer_data_size(h), pf.pipeline_stats()   # after close: the file's length
 
 
 def copy_ceiling(device, nbytes=2 << 30):

@@ -283,6 +283,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     if (ne == 0) {
         out.records_consumed = 0;
         out.open_records = 0;
+        if (on_plan) on_plan(out);
         CK(hipStreamSynchronize(s));
         return KPW_OK;
     }
@@ -379,6 +380,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     out.open_records = (int64_t)ne - po[1];
     out.open_buffered = po[2];
     for (int r = 0; r < nrg; r++) out.rgs.push_back(RowGroupOut{rs[r], re[r] - rs[r], r * nc});
+    if (on_plan) on_plan(out);
     if (nrg == 0) {
         for (int i = 3; i < 8; i++) CK(hipEventRecord(ev_[i], s));
         CK(hipStreamSynchronize(s));

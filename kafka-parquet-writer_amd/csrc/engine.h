@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <functional>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -77,6 +78,11 @@ public:
     // encode after any reader of the buffers it now gets back (two encodes ago).
     void swap_page_buffers() { d_body.swap(d_body_alt); d_comp.swap(d_comp_alt); }
     bool multi_page() const { return mp_; }   // pages accumulate in one buffer (no alternation)
+    // Called once per successful encode as soon as the row-group cuts are known (records_consumed,
+    // open_records, invalid_record set; pages not yet), on the encoding thread; work it queues on
+    // `stream` runs before the rest of the encode.  The writer places the next job's carried
+    // records from here, so the next job can start while this one still encodes.
+    std::function<void(const BatchOut &)> on_plan;
     std::vector<ColInfo> cols;
     kpw_props props{};
     std::string message_name, proto_class;

@@ -512,6 +512,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     out.records_consumed = s0;
     out.open_records = (int64_t)ne - s0;
     if (final_flush) out.open_buffered = 0;
+    if (on_plan) on_plan(out);
     out.d_pages = mp_acc.as<uint8_t>();
     out.pages_len = acc_len;
     pages_dev_ = mp_acc.as<uint8_t>();

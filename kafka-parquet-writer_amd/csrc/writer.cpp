@@ -125,15 +125,33 @@ struct StageBuf {
 struct Job {
     int buf, kind, next;
     int64_t n_exact;                   // EXACT: records [0, n_exact) of the buffer form complete row groups
+    uint64_t seq;                      // submission order (= file order)
 };
 
 }  // namespace
 
+// One encode worker: its own engine (HIP stream, scratch, double-buffered page buffers) and thread.
+struct Worker {
+    Engine *eng = nullptr;
+    DevBuf d_off;                      // device record offsets of the running job
+    PinnedBuf h_off;                   // host record boundaries of the running job (H2D source)
+    hipEvent_t carry_ev = nullptr;     // recorded after this worker placed a job's carried records
+    hipEvent_t enc_done = nullptr;     // recorded after a job's encode (the D2H of its pages waits on it)
+    hipEvent_t d2h_ev[2] = {};         // D2H done, per page buffer set of the engine
+    bool d2h_used[2] = {false, false};
+    uint64_t njobs = 0;
+    bool busy = false;
+    std::thread th;
+};
+
 struct kpw_writer {
-    static constexpr int kBufs = 3;
+    static constexpr int kBufs = 4;    // two encoding, one queued, one filling
     static constexpr int kSlots = 4;
     static constexpr size_t kSlotBytes = 32ull << 20;
-    Engine eng;
+    Engine eng;                        // worker 0's engine (also the caller's, for write_until_full probes)
+    Engine eng1;                       // worker 1's engine
+    int nworkers = 2;
+    Worker wk[2];
     FileWriter *fw = nullptr;
     hipStream_t copy_stream = nullptr;
     StageBuf buf[kBufs];
@@ -145,6 +163,7 @@ struct kpw_writer {
     int cur_slot = 0;
     uint64_t slot_used = 0, slot_dev = 0;   // pending bytes in the current slot and their device offset
     hipEvent_t direct_ev = nullptr;
+    bool direct_pending = false;       // a DMA from the caller's pinned batch is in flight
     // caller-side state
     int64_t num_records = 0;           // ParquetFile.numWrittenRecords
     int64_t created_ms = 0;
@@ -157,39 +176,38 @@ struct kpw_writer {
     bool pending_cut = false;          // an EXACT job may not be in the file yet (lastRowGroupEndPos stale)
     DevBuf probe_off;                  // write_until_full on the bulk path: offsets of staged prefixes
     PinnedBuf probe_h;
-    // worker
+    // job scheduling (under mu): a job starts once the previous job's row-group cuts are known
+    // (its carried records are placed), and appends to the file once the previous job has
     std::mutex mu;
     std::condition_variable cv;
     std::deque<Job> q;
-    bool busy = false, stop = false;
-    std::thread worker;
+    uint64_t next_seq = 0;             // next job's sequence number (caller)
+    uint64_t plan_seq = 0;             // first job whose cuts are not known yet
+    uint64_t asm_seq = 0;              // first job not yet appended to the file
+    hipEvent_t last_carry_ev = nullptr;   // carry placement of job plan_seq - 1
+    int inflight = 0;
+    bool stop = false;
     int fatal_st = KPW_OK;             // first failure of the pipeline (sticky)
     std::string fatal_err;
-    bool invalid_seen = false;         // worker found an invalid record (bulk path)
+    bool invalid_seen = false;         // a worker found an invalid record (bulk path)
     int64_t invalid_global = -1;
-    // worker-owned
-    DevBuf d_off, carry_store;
-    PinnedBuf h_off;
-    PinnedBuf host_pages[2];
+    // shared by the workers, used in job order only
+    DevBuf carry_store;
+    PinnedBuf host_pages[2];           // file mode: pages on the host for the assembly thread
     int page_slot = 0;
-    hipEvent_t d2h_ev[2] = {};
-    // memory mode: page bodies go D2H straight into the in-memory file on d2h_stream while
-    // the next job encodes into the engine's other page buffer set
-    hipStream_t d2h_stream = nullptr;
-    hipEvent_t enc_done = nullptr;
-    bool d2h_used[2] = {false, false};
-    uint64_t njobs = 0;
+    hipEvent_t fd2h_ev[2] = {};
+    hipStream_t d2h_stream = nullptr;  // memory mode: page bodies D2H straight into the in-memory file
     std::thread assembler;
     int asm_st = KPW_OK;
     std::string asm_err;
     BatchOut asm_out;
-    int64_t last_rg_end = 0;           // InternalParquetRecordWriter.lastRowGroupEndPos (assembly thread)
+    int64_t last_rg_end = 0;           // InternalParquetRecordWriter.lastRowGroupEndPos
     int64_t open_buffered = 0;         // open row group's buffered size after the last PLANNED job
-    double t_encode = 0, t_wait = 0, t_dma = 0, t_acquire = 0, t_slot = 0, t_asm = 0, t_d2h_alloc = 0;
-    double stats[16] = {0};            // kpw_writer_stats (worker-written; read after drain)
+    double t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0;
+    double stats[16] = {0};            // kpw_writer_stats (job order; read after drain)
 
     ~kpw_writer();
-    int init_pipeline();
+    int init_pipeline(const kpw_schema *schema, const kpw_props *props);
 };
 
 static int wfail(kpw_writer *w, int st, const std::string &m)
@@ -275,17 +293,17 @@ static int flush_slot(kpw_writer *w)
 }
 
 // Append record bytes to the fill buffer at its append position.
-static int stage_bytes(kpw_writer *w, const uint8_t *src, uint64_t len)
+static int stage_bytes(kpw_writer *w, const uint8_t *src, uint64_t len, bool allow_direct = true)
 {
     StageBuf &F = w->buf[w->fill];
-    if (pinned_range(src, len)) {
-        // direct DMA from the caller's pinned batch; waited for, so the caller may reuse it
+    if (allow_direct && pinned_range(src, len)) {
+        // direct DMA from the caller's pinned batch; the caller waits for it (wait_direct)
+        // before the write returns, so it may reuse the batch
         if (int st = flush_slot(w)) return st;
-        const double ta = trace_on() ? now_ms() : 0.0;
         if (hipMemcpyAsync(F.d + F.len, src, len, hipMemcpyHostToDevice, w->copy_stream) != hipSuccess ||
-            hipEventRecord(w->direct_ev, w->copy_stream) != hipSuccess || hipEventSynchronize(w->direct_ev) != hipSuccess)
+            hipEventRecord(w->direct_ev, w->copy_stream) != hipSuccess)
             return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
-        if (trace_on()) w->t_dma += now_ms() - ta;
+        w->direct_pending = true;
         F.len += len;
         return KPW_OK;
     }
@@ -348,14 +366,14 @@ static void boundaries(const StageBuf &B, std::vector<uint64_t> &hb)
     boundaries(B, hb.data());
 }
 
-// ---------------------------------------------------------------- worker
+// ---------------------------------------------------------------- workers
 
 // A carry that did not fit its buffer's gap waits in carry_store: rebuild the buffer as
-// [carried | appended] (the caller is not appending to it: its job runs, or it drains).
-static int materialize(kpw_writer *w, StageBuf &B)
+// [carried | appended] on stream `s` (the caller is not appending to it: its job runs, or it
+// drains; the store was filled by the previous job, which `s` already waits for).
+static int materialize(kpw_writer *w, StageBuf &B, hipStream_t s)
 {
     if (!B.carry_in_store) return KPW_OK;
-    hipStream_t s = w->eng.stream;
     const uint64_t cs = B.carry.back();                 // carried bytes (store offsets start at 0)
     const uint64_t app = B.len - B.gap;
     const size_t cap = std::max<size_t>(B.cap, cs + app + w->gap_ + (64ull << 20));
@@ -378,11 +396,11 @@ static int materialize(kpw_writer *w, StageBuf &B)
     return KPW_OK;
 }
 
-// Place records [b0, b1) of buffer `src` (boundaries hb[i0..i1]) in front of buffer `dst`'s
-// appended records.
-static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, size_t i0, size_t i1, StageBuf &dst)
+// Place records [hb[i0], hb[i1]) of buffer `src` in front of buffer `dst`'s appended records
+// (on stream s).
+static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, size_t i0, size_t i1, StageBuf &dst,
+                       hipStream_t s)
 {
-    hipStream_t s = w->eng.stream;
     const uint64_t b0 = hb[i0], c = hb[i1] - b0;
     uint64_t at;
     uint8_t *base;
@@ -402,7 +420,8 @@ static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, s
     return KPW_OK;
 }
 
-// File assembly of one job on the assembly thread (headers + bodies + metadata).
+// File mode: headers + bodies + metadata of one job on the assembly thread (overlaps the next
+// job's encode).
 static void start_assembly(kpw_writer *w, BatchOut &&out, int slot)
 {
     w->asm_out = std::move(out);
@@ -410,7 +429,7 @@ static void start_assembly(kpw_writer *w, BatchOut &&out, int slot)
         // no exception may leave this thread (std::terminate would kill the host process)
         try {
             (void)hipSetDevice(w->eng.device);
-            if (hipEventSynchronize(w->d2h_ev[slot]) != hipSuccess) {
+            if (hipEventSynchronize(w->fd2h_ev[slot]) != hipSuccess) {
                 w->asm_st = KPW_ERR_DEVICE;
                 w->asm_err = "D2H of pages failed";
                 return;
@@ -448,11 +467,58 @@ static int join_assembly(kpw_writer *w)
     return KPW_OK;
 }
 
-static int run_job(kpw_writer *w, const Job &j)
+// Append one encoded job to the file, in job order (called in the job's assembly turn).
+static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
 {
+    Engine &E = *W.eng;
+    hipStream_t s = E.stream;
+    if (out.rgs.empty()) return KPW_OK;
+    const double ta = trace_on() ? now_ms() : 0.0;
+    if (w->fw->memory_mode()) {
+        // headers on the host; bodies D2H straight into the in-memory file on d2h_stream, after
+        // this encode; the engine's next-but-one encode reuses these page buffers after d2h_ev
+        if (hipEventRecord(W.enc_done, s) != hipSuccess || hipStreamWaitEvent(w->d2h_stream, W.enc_done, 0) != hipSuccess)
+            return KPW_ERR_DEVICE;
+        for (size_t r = 0; r < out.rgs.size(); r++) {
+            if (int st = w->fw->write_row_group(out, (int)r, out.d_pages, 0, w->d2h_stream)) return st;
+            w->last_rg_end = w->fw->pos();
+        }
+        if (hipEventRecord(W.d2h_ev[set], w->d2h_stream) != hipSuccess) return KPW_ERR_DEVICE;
+        W.d2h_used[set] = true;
+        if (trace_on()) w->t_asm += now_ms() - ta;
+        return KPW_OK;
+    }
+    // file mode: pages -> pinned host buffer (double-buffered against the previous job's
+    // assembly), headers + bodies written on the assembly thread
+    if (int st = join_assembly(w)) return st;
+    const int slot = w->page_slot;
+    w->page_slot ^= 1;
+    if (out.pages_len) {
+        if (w->host_pages[slot].ensure(out.pages_len)) return KPW_ERR_NOMEM;
+        if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, out.pages_len, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return KPW_ERR_DEVICE;
+    }
+    if (hipEventRecord(w->fd2h_ev[slot], s) != hipSuccess) return KPW_ERR_DEVICE;
+    if (hipEventSynchronize(w->fd2h_ev[slot]) != hipSuccess) return KPW_ERR_DEVICE;   // the engine reuses its buffers next
+    if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
+    start_assembly(w, std::move(out), slot);
+    return KPW_OK;
+}
+
+static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
+{
+    Worker &W = w->wk[x];
+    Engine &E = *W.eng;
     StageBuf &B = w->buf[j.buf];
-    hipStream_t s = w->eng.stream;
-    if (int st = materialize(w, B)) return set_fatal(w, st, "stage buffer rebuild failed"), st;
+    hipStream_t s = E.stream;
+    bool planned = false;
+    auto plan_fail = [&](int st, const std::string &m) {
+        set_fatal(w, st, m);
+        return st;
+    };
+    // the previous job's carried records (and a carry_store it filled) come first
+    if (prev_carry && hipStreamWaitEvent(s, prev_carry, 0) != hipSuccess) return plan_fail(KPW_ERR_DEVICE, "stream wait failed");
+    if (int st = materialize(w, B, s)) return plan_fail(st, "stage buffer rebuild failed");
     bool after_invalid;
     {
         std::lock_guard<std::mutex> g(w->mu);
@@ -461,123 +527,122 @@ static int run_job(kpw_writer *w, const Job &j)
     if (after_invalid) { B.ends.clear(); B.len = B.gap; }   // records behind an invalid one are never written
     // boundaries straight into the pinned offset buffer (also the carry bookkeeping below)
     const size_t nb = nbounds(B);
-    if (w->h_off.ensure(nb * 8)) return set_fatal(w, KPW_ERR_NOMEM, "offset staging allocation failed"), KPW_ERR_NOMEM;
-    uint64_t *hb = (uint64_t *)w->h_off.p;
+    if (W.h_off.ensure(nb * 8)) return plan_fail(KPW_ERR_NOMEM, "offset staging allocation failed");
+    uint64_t *hb = (uint64_t *)W.h_off.p;
     boundaries(B, hb);
     const int64_t nrec = (int64_t)nb - 1;
     const int64_t ncarry = B.carry.empty() ? 0 : (int64_t)B.carry.size() - 1;
     const int64_t n_enc = j.kind == JOB_EXACT ? std::min<int64_t>(j.n_exact, nrec) : nrec;
     const double t0 = now_ms();
-    if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess) return set_fatal(w, KPW_ERR_DEVICE, "stream wait failed"), KPW_ERR_DEVICE;
-    BatchOut out;
-    const bool direct = w->fw->memory_mode();
-    const int set = (int)(w->njobs & 1);
-    if (direct && n_enc > 0) {
-        // the page buffers this encode gets back were last read by the D2H of two jobs ago
-        w->eng.swap_page_buffers();
+    if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess) return plan_fail(KPW_ERR_DEVICE, "stream wait failed");
+    const int set = (int)(W.njobs & 1);
+    if (w->fw->memory_mode() && n_enc > 0) {
+        // the page buffers this encode gets back were last read by the D2H of this engine's
+        // job before last
+        E.swap_page_buffers();
         for (int k = 0; k < 2; k++)
-            if (w->d2h_used[k] && (k == set || w->eng.multi_page()) && hipStreamWaitEvent(s, w->d2h_ev[k], 0) != hipSuccess)
-                return set_fatal(w, KPW_ERR_DEVICE, "stream wait failed"), KPW_ERR_DEVICE;
+            if (W.d2h_used[k] && (k == set || E.multi_page()) && hipStreamWaitEvent(s, W.d2h_ev[k], 0) != hipSuccess)
+                return plan_fail(KPW_ERR_DEVICE, "stream wait failed");
     }
+    // the row-group cuts: carried records -> the next buffer, then the next job may start
+    int64_t consumed = 0, keep_end = nrec;
+    auto on_plan = [&](const BatchOut &o) {
+        consumed = o.records_consumed;
+        int64_t inv = -1;
+        if (o.invalid_record >= 0) { keep_end = o.invalid_record; inv = B.first_new_global - ncarry + o.invalid_record; }
+        if (j.kind == JOB_FINAL) keep_end = consumed;
+        int st = KPW_OK;
+        if (keep_end > consumed && j.next >= 0)
+            st = place_carry(w, B, hb, (size_t)consumed, (size_t)keep_end, w->buf[j.next], s);
+        if (!st && hipEventRecord(W.carry_ev, s) != hipSuccess) st = KPW_ERR_DEVICE;
+        std::lock_guard<std::mutex> g(w->mu);
+        if (st) {
+            if (!w->fatal_st) { w->fatal_st = st; w->fatal_err = "carry-over copy failed"; }
+        } else if (inv >= 0) {
+            w->invalid_seen = true;
+            w->invalid_global = inv;
+        }
+        w->last_carry_ev = W.carry_ev;
+        w->plan_seq = j.seq + 1;
+        planned = true;
+        w->cv.notify_all();
+    };
+    BatchOut out;
     if (n_enc > 0) {
-        if (w->d_off.ensure((n_enc + 1) * 8))
-            return set_fatal(w, KPW_ERR_NOMEM, "offset staging allocation failed"), KPW_ERR_NOMEM;
-        if (hipMemcpyAsync(w->d_off.p, w->h_off.p, (n_enc + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
-            return set_fatal(w, KPW_ERR_DEVICE, "H2D of offsets failed"), KPW_ERR_DEVICE;
+        if (W.d_off.ensure((n_enc + 1) * 8)) return plan_fail(KPW_ERR_NOMEM, "offset staging allocation failed");
+        if (hipMemcpyAsync(W.d_off.p, W.h_off.p, (n_enc + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+            return plan_fail(KPW_ERR_DEVICE, "H2D of offsets failed");
         // EXACT jobs are encoded non-final: the GPU planner must cut the same single row group
         // the host size model cut (checked below), so every such row group cross-checks the model
-        const int st = w->eng.encode(B.d, w->d_off.as<uint64_t>(), (uint64_t)n_enc, j.kind == JOB_FINAL,
-                                     w->eng.props.block_size, nullptr, out);
-        if (st) return set_fatal(w, st, w->eng.error()), st;
+        E.on_plan = on_plan;
+        const int st = E.encode(B.d, W.d_off.as<uint64_t>(), (uint64_t)n_enc, j.kind == JOB_FINAL, E.props.block_size, nullptr, out);
+        E.on_plan = nullptr;
+        if (st) return plan_fail(st, E.error());
+    } else {
+        on_plan(out);
     }
+    if (!planned) return plan_fail(KPW_ERR_DEVICE, "encode returned without a plan");
     const double t1 = now_ms();
-    int64_t consumed = out.records_consumed, keep_end = nrec;
-    if (out.invalid_record >= 0) {
-        std::lock_guard<std::mutex> g(w->mu);
-        w->invalid_seen = true;
-        w->invalid_global = B.first_new_global - ncarry + out.invalid_record;
-        keep_end = out.invalid_record;
-        w->cv.notify_all();
-    } else if (j.kind == JOB_EXACT && (consumed != n_enc || out.rgs.size() != 1)) {
+    if (out.invalid_record < 0 && j.kind == JOB_EXACT && (consumed != n_enc || out.rgs.size() != 1))
         // the host size model and the GPU planner restate the same cut: a mismatch is a bug
-        set_fatal(w, KPW_ERR_DEVICE, "row-group cut of the size model and the GPU planner differ");
-        return KPW_ERR_DEVICE;
-    }
-    if (j.kind == JOB_FINAL) keep_end = consumed;
-    // open records -> the next buffer (device to device), then this buffer is free
-    if (keep_end > consumed && j.next >= 0) {
-        if (int st = place_carry(w, B, hb, (size_t)consumed, (size_t)keep_end, w->buf[j.next]))
-            return set_fatal(w, st, "carry-over copy failed"), st;
-    }
-    if (hipStreamSynchronize(s) != hipSuccess) return set_fatal(w, KPW_ERR_DEVICE, "carry-over sync failed"), KPW_ERR_DEVICE;
+        return plan_fail(KPW_ERR_DEVICE, "row-group cut of the size model and the GPU planner differ");
+    if (hipStreamSynchronize(s) != hipSuccess) return plan_fail(KPW_ERR_DEVICE, "encode sync failed");
     {
         std::lock_guard<std::mutex> g(w->mu);
-        B.state = BUF_FREE;
-        if (j.kind == JOB_PLANNED) w->open_buffered = out.open_buffered;
+        B.state = BUF_FREE;   // the carried records were copied out before the rest of the encode
         w->cv.notify_all();
+    }
+    // append to the file in job order
+    {
+        const double ta = trace_on() ? now_ms() : 0.0;
+        std::unique_lock<std::mutex> lk(w->mu);
+        w->cv.wait(lk, [&] { return w->asm_seq == j.seq || w->fatal_st; });
+        if (w->fatal_st) return w->fatal_st;
+        if (trace_on()) w->t_turn += now_ms() - ta;
     }
     for (const PageOut &pg : out.pages) {
         w->stats[3] += (double)pg.uncompressed_size;
         w->stats[4] += (double)pg.compressed_size;
     }
-    if (direct && !out.rgs.empty()) {
-        // memory mode: headers on the host, bodies D2H straight into the file (no host copy)
-        const double ta = trace_on() ? now_ms() : 0.0;
-        if (hipEventRecord(w->enc_done, s) != hipSuccess || hipStreamWaitEvent(w->d2h_stream, w->enc_done, 0) != hipSuccess)
-            return set_fatal(w, KPW_ERR_DEVICE, "event record failed"), KPW_ERR_DEVICE;
-        for (size_t r = 0; r < out.rgs.size(); r++) {
-            if (int st = w->fw->write_row_group(out, (int)r, out.d_pages, 0, w->d2h_stream))
-                return set_fatal(w, st, w->fw->error()), st;
-            w->last_rg_end = w->fw->pos();
-        }
-        if (hipEventRecord(w->d2h_ev[set], w->d2h_stream) != hipSuccess)
-            return set_fatal(w, KPW_ERR_DEVICE, "event record failed"), KPW_ERR_DEVICE;
-        w->d2h_used[set] = true;
-        w->njobs++;
-        if (trace_on()) w->t_asm += now_ms() - ta;
-    } else if (!out.rgs.empty()) {
-        // file mode: pages -> host (pinned, double-buffered against the previous job's
-        // assembly), then headers + bodies written on the assembly thread
-        if (int st = join_assembly(w)) return st;
-        const int slot = w->page_slot;
-        w->page_slot ^= 1;
-        if (out.pages_len) {
-            const double ta = trace_on() ? now_ms() : 0.0;
-            if (w->host_pages[slot].ensure(out.pages_len))
-                return set_fatal(w, KPW_ERR_NOMEM, "pinned page buffer allocation failed"), KPW_ERR_NOMEM;
-            if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, out.pages_len, hipMemcpyDeviceToHost, s) != hipSuccess)
-                return set_fatal(w, KPW_ERR_DEVICE, "D2H of pages failed"), KPW_ERR_DEVICE;
-            if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
-        }
-        if (hipEventRecord(w->d2h_ev[slot], s) != hipSuccess) return set_fatal(w, KPW_ERR_DEVICE, "event record failed"), KPW_ERR_DEVICE;
-        start_assembly(w, std::move(out), slot);
-    }
-    w->t_encode += t1 - t0;
     if (n_enc > 0) {
         w->stats[0] += 1;
         w->stats[1] += (double)n_enc;
         w->stats[2] += (double)(hb[n_enc] - hb[0]);
-        for (int k = 0; k < 10; k++) w->stats[5 + k] += w->eng.stage_ms[k];
+        for (int k = 0; k < 10; k++) w->stats[5 + k] += E.stage_ms[k];
         w->stats[15] += t1 - t0;
+        W.njobs++;
     }
+    if (j.kind == JOB_PLANNED) w->open_buffered = out.open_buffered;
+    w->t_encode += t1 - t0;
     if (trace_on())
-        fprintf(stderr, "[kpw] job kind=%d records=%lld (carried %lld) encode %.2f ms, total %.2f ms\n", j.kind, (long long)n_enc,
-                (long long)ncarry, t1 - t0, now_ms() - t0);
+        fprintf(stderr, "[kpw] job %llu worker %d kind=%d records=%lld (carried %lld) encode %.2f ms\n",
+                (unsigned long long)j.seq, x, j.kind, (long long)n_enc, (long long)ncarry, t1 - t0);
+    if (int st = append_job(w, W, out, set)) return plan_fail(st, "file assembly failed: " + w->fw->error());
+    {
+        std::lock_guard<std::mutex> g(w->mu);
+        w->asm_seq = j.seq + 1;
+        w->cv.notify_all();
+    }
     return KPW_OK;
 }
 
-static void worker_main(kpw_writer *w)
+static void worker_main(kpw_writer *w, int x)
 {
     (void)hipSetDevice(w->eng.device);
+    Worker &W = w->wk[x];
     for (;;) {
         Job j;
+        hipEvent_t prev_carry;
         {
             std::unique_lock<std::mutex> lk(w->mu);
-            w->cv.wait(lk, [w] { return w->stop || !w->q.empty(); });
+            // the next job starts once the previous job's cuts are known
+            w->cv.wait(lk, [w] { return (w->stop && w->q.empty()) || (!w->q.empty() && w->q.front().seq == w->plan_seq); });
             if (w->q.empty()) break;   // stop requested and nothing queued
             j = w->q.front();
             w->q.pop_front();
-            w->busy = true;
+            prev_carry = j.seq ? w->last_carry_ev : nullptr;
+            W.busy = true;
+            w->inflight++;
         }
         bool failed;
         {
@@ -585,37 +650,31 @@ static void worker_main(kpw_writer *w)
             failed = w->fatal_st != KPW_OK;
         }
         try {
-            if (!failed) (void)run_job(w, j);
+            if (!failed) (void)run_job(w, x, j, prev_carry);
         } catch (const std::bad_alloc &) {
-            set_fatal(w, KPW_ERR_NOMEM, "host allocation failed in the encode worker");
+            set_fatal(w, KPW_ERR_NOMEM, "host allocation failed in an encode worker");
         } catch (...) {
             set_fatal(w, KPW_ERR_DEVICE, "encode worker failed");
         }
-        bool idle;
         {
             std::lock_guard<std::mutex> g(w->mu);
-            if (w->fatal_st) {   // nothing after a failure is encoded; its buffers are free again
+            if (w->fatal_st) {
+                // nothing after a failure is encoded: release its buffers, let every job pass
                 for (auto &k : w->buf) if (k.state == BUF_QUEUED) k.state = BUF_FREE;
                 w->buf[j.buf].state = BUF_FREE;
+                for (auto &q : w->q) w->plan_seq = std::max(w->plan_seq, q.seq + 1);
                 w->q.clear();
+                w->plan_seq = std::max(w->plan_seq, j.seq + 1);
+                w->asm_seq = std::max(w->asm_seq, j.seq + 1);
             }
-            idle = w->q.empty();
-        }
-        if (idle) {   // idle implies every queued job is in the file
-            (void)join_assembly(w);
-            if (w->d2h_stream && hipStreamSynchronize(w->d2h_stream) != hipSuccess)
-                set_fatal(w, KPW_ERR_DEVICE, "D2H of pages failed");
-        }
-        {
-            std::lock_guard<std::mutex> g(w->mu);
-            w->busy = false;
+            W.busy = false;
+            w->inflight--;
             w->cv.notify_all();
         }
     }
-    (void)join_assembly(w);
 }
 
-// Hand the fill buffer to the worker and start filling the next one.
+// Hand the fill buffer to the workers and start filling the next one.
 static int submit(kpw_writer *w, int kind, int64_t n_exact)
 {
     if (int st = flush_slot(w)) return st;
@@ -623,9 +682,8 @@ static int submit(kpw_writer *w, int kind, int64_t n_exact)
     if (hipEventRecord(F.copied, w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "event record failed");
     const int f = w->fill;
     const int64_t nrec = F.ncarry_expected + (int64_t)F.ends.size();
-    const bool final_job = kind == JOB_FINAL;
     int next = -1;
-    if (!final_job) {
+    if (kind != JOB_FINAL) {
         w->fill = -1;
         {
             std::lock_guard<std::mutex> g(w->mu);
@@ -645,70 +703,98 @@ static int submit(kpw_writer *w, int kind, int64_t n_exact)
     }
     {
         std::lock_guard<std::mutex> g(w->mu);
-        w->q.push_back(Job{f, kind, next, n_exact});
+        w->q.push_back(Job{f, kind, next, n_exact, w->next_seq++});
         w->cv.notify_all();
     }
     if (kind == JOB_PLANNED) w->dirty = false;
     return KPW_OK;
 }
 
-// Wait until every queued job is encoded and assembled.
+// Wait until every submitted job is encoded and in the file (memory mode: its pages landed).
 static int drain(kpw_writer *w)
 {
-    std::unique_lock<std::mutex> lk(w->mu);
-    w->cv.wait(lk, [w] { return (w->q.empty() && !w->busy) || w->fatal_st; });
+    {
+        std::unique_lock<std::mutex> lk(w->mu);
+        w->cv.wait(lk, [w] { return w->q.empty() && w->inflight == 0; });
+    }
+    // no job runs now: the file-mode assembly thread and the D2H stream are the caller's
+    (void)join_assembly(w);
+    if (w->d2h_stream && hipStreamSynchronize(w->d2h_stream) != hipSuccess) set_fatal(w, KPW_ERR_DEVICE, "D2H of pages failed");
+    std::lock_guard<std::mutex> g(w->mu);
     if (w->fatal_st) {
-        w->cv.wait(lk, [w] { return w->q.empty() && !w->busy; });
         w->err = w->fatal_err;
         return w->fatal_st;
     }
     return KPW_OK;
 }
 
-int kpw_writer::init_pipeline()
+static uint64_t env_workers()
+{
+    const char *e = getenv("KPW_ENCODERS");
+    const long v = e ? atol(e) : 2;
+    return v == 1 ? 1 : 2;
+}
+
+int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
 {
     if (hipSetDevice(eng.device) != hipSuccess) return KPW_ERR_DEVICE;
+    nworkers = (int)env_workers();
+    if (nworkers > 1) {
+        if (int st = eng1.init(eng.device, schema, props)) return st;
+    }
+    wk[0].eng = &eng;
+    wk[1].eng = &eng1;
     if (hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking) != hipSuccess) return KPW_ERR_DEVICE;
+    if (hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &e : slot_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
-    for (auto &e : d2h_ev)
+    for (auto &e : fd2h_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     if (hipEventCreateWithFlags(&direct_ev, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
-    if (hipEventCreateWithFlags(&enc_done, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
-    if (hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &b : buf)
         if (hipEventCreateWithFlags(&b.copied, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    for (int x = 0; x < nworkers; x++) {
+        Worker &W = wk[x];
+        if (hipEventCreateWithFlags(&W.carry_ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&W.enc_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&W.d2h_ev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&W.d2h_ev[1], hipEventDisableTiming) != hipSuccess)
+            return KPW_ERR_DEVICE;
+    }
     // the open row group of a job lands in the next buffer's gap (its wire bytes are a small
     // multiple of its buffered size for every schema but pathological ones; see materialize)
     gap_ = std::max<uint64_t>(64ull << 20, 2 * (uint64_t)eng.props.block_size) + 4096;
     model_on = model.init(eng.cols, eng.props);
-    worker = std::thread(worker_main, this);
+    for (int x = 0; x < nworkers; x++) wk[x].th = std::thread(worker_main, this, x);
     return acquire_fill(this);
 }
 
 kpw_writer::~kpw_writer()
 {
-    if (worker.joinable()) {
-        {
-            std::lock_guard<std::mutex> g(mu);
-            stop = true;
-            cv.notify_all();
-        }
-        worker.join();
+    {
+        std::lock_guard<std::mutex> g(mu);
+        stop = true;
+        cv.notify_all();
     }
+    for (auto &W : wk)
+        if (W.th.joinable()) W.th.join();
     if (assembler.joinable()) assembler.join();
     (void)hipSetDevice(eng.device);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    if (d2h_stream) (void)hipStreamSynchronize(d2h_stream);
     if (eng.stream) (void)hipStreamSynchronize(eng.stream);
+    if (eng1.stream) (void)hipStreamSynchronize(eng1.stream);
     for (auto &b : buf) {
         dev_free(b.d);
         if (b.copied) (void)hipEventDestroy(b.copied);
     }
     for (auto &e : slot_ev) if (e) (void)hipEventDestroy(e);
-    for (auto &e : d2h_ev) if (e) (void)hipEventDestroy(e);
+    for (auto &e : fd2h_ev) if (e) (void)hipEventDestroy(e);
+    for (auto &W : wk) {
+        for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1]}) if (e) (void)hipEventDestroy(e);
+    }
     if (direct_ev) (void)hipEventDestroy(direct_ev);
-    if (d2h_stream) { (void)hipStreamSynchronize(d2h_stream); (void)hipStreamDestroy(d2h_stream); }
-    if (enc_done) (void)hipEventDestroy(enc_done);
+    if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     delete fw;
 }
@@ -740,7 +826,7 @@ extern "C" kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, con
             w->fw = new FileWriter(w->eng.cols, w->eng.message_name, w->eng.proto_class, w->eng.props);
             st = w->fw->open(path);
         }
-        if (!st) st = w->init_pipeline();
+        if (!st) st = w->init_pipeline(schema, props);
         if (st) {
             if (status) *status = st;
             delete w;
@@ -779,6 +865,17 @@ static int observe_failure(kpw_writer *w)
 }
 
 
+// Wait for a direct DMA from the caller's pinned batch (issued by stage_bytes).
+static int wait_direct(kpw_writer *w)
+{
+    if (!w->direct_pending) return KPW_OK;
+    const double ta = trace_on() ? now_ms() : 0.0;
+    w->direct_pending = false;
+    if (hipEventSynchronize(w->direct_ev) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
+    if (trace_on()) w->t_dma += now_ms() - ta;
+    return KPW_OK;
+}
+
 // Rewind the fill buffer's append position to `new_len` (records after it were not accepted).
 // Bytes still pending in the current slot are dropped with it; bytes already sent are simply
 // overwritten by later appends (same copy stream, in order).
@@ -792,7 +889,7 @@ static void rewind_fill(kpw_writer *w, uint64_t new_len)
 // One record through the pinned slot (the size-model path: small writes).
 static int stage_record(kpw_writer *w, const uint8_t *src, uint64_t len)
 {
-    if (w->slot_used + len > kpw_writer::kSlotBytes || w->slot_used == 0) return stage_bytes(w, src, len);
+    if (w->slot_used + len > kpw_writer::kSlotBytes || w->slot_used == 0) return stage_bytes(w, src, len, false);
     StageBuf &F = w->buf[w->fill];
     memcpy(w->slot[w->cur_slot].p + w->slot_used, src, len);
     w->slot_used += len;
@@ -836,6 +933,7 @@ static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *of
                     StageBuf &G = w->buf[w->fill];
                     const uint64_t delta = G.len - offsets[i];
                     if (int st = stage_bytes(w, data + offsets[i], bytes)) return st;
+                    if (int st = wait_direct(w)) return st;
                     for (uint64_t k = i + 1; k <= n; k++) G.ends.push_back(offsets[k] + delta);
                     w->num_records += (int64_t)(n - i);
                     i = n;
@@ -873,13 +971,14 @@ static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offset
     StageBuf &F = w->buf[w->fill];
     const uint64_t delta = F.len - offsets[0];
     if (int st = stage_bytes(w, data + offsets[0], bytes)) return st;
+    // the record ends are rebased while the batch's DMA runs
     const size_t m = F.ends.size();
     F.ends.resize(m + n);   // geometric growth (an exact reserve per call would copy the vector every call)
     uint64_t *e = F.ends.data() + m;
     for (uint64_t i = 1; i <= n; i++) e[i - 1] = offsets[i] + delta;
     w->num_records += (int64_t)n;
     w->dirty = true;
-    return KPW_OK;
+    return wait_direct(w);
 }
 
 // getDataSize() after the first m records of the (drained) fill buffer, without flushing:
@@ -912,7 +1011,7 @@ static int write_until_full_bulk(kpw_writer *w, const uint8_t *data, const uint6
     if (int st = drain(w)) return st;
     if (int st = flush_slot(w)) return st;
     if (hipEventRecord(w->buf[w->fill].copied, w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "event record failed");
-    if (int st = materialize(w, w->buf[w->fill])) return wfail(w, st, "stage buffer rebuild failed");
+    if (int st = materialize(w, w->buf[w->fill], w->eng.stream)) return wfail(w, st, "stage buffer rebuild failed");
     StageBuf &F0 = w->buf[w->fill];
     const uint64_t base = (F0.carry.empty() ? 0 : F0.carry.size() - 1) + F0.ends.size();
     if (int st = write_bulk(w, data, offsets, n)) return st;
