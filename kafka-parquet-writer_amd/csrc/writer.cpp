@@ -105,6 +105,45 @@ struct PinnedBuf {
     ~PinnedBuf() { pin_free(p); }
 };
 
+// Growable u64 array without value-initialisation: the bulk path appends 500 k record ends per
+// write and a zero-fill before overwriting them doubled the caller's memory traffic.
+class U64Vec {
+public:
+    U64Vec() = default;
+    U64Vec(const U64Vec &) = delete;
+    U64Vec &operator=(const U64Vec &) = delete;
+    ~U64Vec() { free(p_); }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    void clear() { n_ = 0; }
+    uint64_t *data() { return p_; }
+    const uint64_t *data() const { return p_; }
+    uint64_t back() const { return p_[n_ - 1]; }
+    uint64_t *begin() { return p_; }
+    uint64_t *end() { return p_ + n_; }
+    // n more entries, uninitialised; returns the first of them
+    uint64_t *grow(size_t n)
+    {
+        if (n_ + n > cap_) {
+            size_t c = std::max<size_t>(cap_ * 2, n_ + n);
+            c = std::max<size_t>(c, 1024);
+            uint64_t *q = (uint64_t *)realloc(p_, c * 8);
+            if (!q) throw std::bad_alloc();
+            p_ = q;
+            cap_ = c;
+        }
+        uint64_t *r = p_ + n_;
+        n_ += n;
+        return r;
+    }
+    void push_back(uint64_t v) { *grow(1) = v; }
+    void resize(size_t n) { if (n <= n_) n_ = n; else grow(n - n_); }
+
+private:
+    uint64_t *p_ = nullptr;
+    size_t n_ = 0, cap_ = 0;
+};
+
 enum { BUF_FREE = 0, BUF_FILLING = 1, BUF_QUEUED = 2 };
 enum { JOB_PLANNED = 0, JOB_EXACT = 1, JOB_FINAL = 2 };
 
@@ -115,7 +154,7 @@ struct StageBuf {
     uint64_t len = 0;                  // append position
     std::vector<uint64_t> carry;       // carried record boundaries (worker-written; ncarry+1 or empty)
     bool carry_in_store = false;       // carried records wait in kpw_writer::carry_store (did not fit the gap)
-    std::vector<uint64_t> ends;        // appended record ends (caller-written)
+    U64Vec ends;                       // appended record ends (caller-written)
     int64_t ncarry_expected = 0;       // carried records, as the caller knows them (EXACT jobs)
     int64_t first_new_global = 0;      // file record index of the first appended record
     int state = BUF_FREE;
@@ -972,9 +1011,7 @@ static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offset
     const uint64_t delta = F.len - offsets[0];
     if (int st = stage_bytes(w, data + offsets[0], bytes)) return st;
     // the record ends are rebased while the batch's DMA runs
-    const size_t m = F.ends.size();
-    F.ends.resize(m + n);   // geometric growth (an exact reserve per call would copy the vector every call)
-    uint64_t *e = F.ends.data() + m;
+    uint64_t *e = F.ends.grow(n);
     for (uint64_t i = 1; i <= n; i++) e[i - 1] = offsets[i] + delta;
     w->num_records += (int64_t)n;
     w->dirty = true;
