@@ -66,6 +66,7 @@ static float run(const SnappyArgs &a, int reps)
             hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, 0, a);
             hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, 0, a);
         } else if (KIND == 5) hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, 0, a);
+        else if (KIND == 9) hipLaunchKernelGGL(k_snappy_vns, dim3(a.nfrags), dim3(64), 0, 0, a);   // timing only
         else if (KIND == 7) {   // register-resident + scheduled fast path, then the batched LDS kernel
             hipLaunchKernelGGL(k_snappy_ra, dim3(a.nfrags), dim3(64), 0, 0, a);
             hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, 0, a);
@@ -167,7 +168,7 @@ int main(int argc, char **argv)
         };
         const double gb = (double)(npages * psz) / 1e9;
         struct V { const char *name; float (*fn)(const SnappyArgs &, int); };
-        V vs[] = {{"s2", run<2, 2>}, {"v+s2", run<2, 4>}, {"r+s2", run<2, 6>}, {"ra+s2", run<2, 7>}, {"w2+s2", run<2, 8>}};
+        V vs[] = {{"s2", run<2, 2>}, {"v+s2", run<2, 4>}, {"r+s2", run<2, 6>}, {"ra+s2", run<2, 7>}, {"w2+s2", run<2, 8>}, {"x-vnostore", run<2, 9>}};
         {   // how many fragments the register-table kernel gives up on
             (void)run<2, 5>(a, 1);
             std::vector<uint32_t> fl(nf);
@@ -179,7 +180,7 @@ int main(int argc, char **argv)
         for (auto &v : vs) {
             CK(hipMemset(d_fout, 0, (size_t)nf * SNAPPY_FRAG_CAP));
             float ms = v.fn(a, 3);
-            uint64_t comp = check(v.name);
+            uint64_t comp = strncmp(v.name, "x-", 2) ? check(v.name) : 0;   // "x-" variants: timing only
             printf("kind=%-8s variant=%-7s frags=%6u ratio=%.3f ms=%8.3f GB/s=%7.2f\n", kind, v.name, nf,
                    (double)comp / (npages * psz), ms, gb / (ms * 1e-3));
             fflush(stdout);

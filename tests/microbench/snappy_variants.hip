@@ -1540,4 +1540,88 @@ __global__ void __launch_bounds__(64, 1) __attribute__((amdgpu_num_vgpr(96))) k_
     if (lane == 0) a.frag_len[f] = op;
 }
 
+// ------------------------------------------------------------------ experiment: k_snappy_v without output stores
+// Timing only (its output is not Snappy): how much of the per-match latency of the serial
+// parse is the emission (per-lane byte stores, which share vmcnt with the window refills).
+__global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k_snappy_vns(SnappyArgs a)
+{
+    const int lane = threadIdx.x;
+    const uint32_t f = a.order ? a.order[blockIdx.x] : blockIdx.x;
+    if (a.ftime && lane == 0) a.ftime[2 * f] = wall_clock64();
+    const uint32_t pg = a.frag_page[f];
+    const uint32_t fi = a.frag_idx[f];
+    const uint64_t plen = a.page_len[pg];
+    const uint64_t fstart = (uint64_t)fi * SNAPPY_FRAG;
+    const uint32_t n = (uint32_t)((plen - fstart) < SNAPPY_FRAG ? (plen - fstart) : SNAPPY_FRAG);
+    const uint8_t *fbase = a.in + a.page_off[pg] + fstart;
+    const Src g{(g_u8 *)fbase};
+    const SIn si{(uint64_t)(uintptr_t)fbase};
+    VWin in;
+    in.abs0 = (const uint8_t *)((uintptr_t)fbase & ~(uintptr_t)3);
+    in.off0 = (uint32_t)((uintptr_t)fbase & 3);
+    in.lane = lane;
+    in.refill(0);
+    VTab T;
+    T.lane = (uint32_t)lane;
+    T.clear();
+    uint32_t tsize = 256;
+    while (tsize < SNAPPY_MAX_TABLE && tsize < n) tsize <<= 1;
+
+    uint8_t *out = a.frag_out + (uint64_t)f * SNAPPY_FRAG_CAP;
+    uint32_t op = 0;
+    int shift = 32;
+    for (uint32_t t = tsize; t > 1; t >>= 1) shift--;
+    const uint32_t ip_end = n;
+    uint32_t next_emit = 0;
+    uint32_t ip = 0;
+    if (n >= 15) {
+        const uint32_t ip_limit = n - 15;
+        ip = 1;
+        for (;;) {
+            uint32_t skip = 32;
+            uint32_t candidate;
+            for (;;) {
+                const uint32_t next_ip = ip + (skip++ >> 5);
+                if (next_ip > ip_limit) goto emit_remainder;
+                if (skip > 32 + VT_ABORT) {
+                    if (lane == 0) { a.frag_len[f] = VT_ABORTED; if (a.ftime) a.ftime[2 * f + 1] = wall_clock64() | (1ull << 63); }
+                    return;
+                }
+                const uint32_t cur_s = in.ld32(ip, si, true);
+                candidate = T.swap(sn_hash(cur_s, shift), ip);
+                if (cur_s == in.ld32(candidate, si, false)) break;
+                ip = next_ip;
+            }
+            {
+                const uint32_t len = ip - next_emit;
+                if (len <= 7) {
+                    const uint64_t b = in.ld64(next_emit, si, false) & ((1ull << (8 * len)) - 1);
+                    (void)b;
+                    op += 1 + len;
+                } else {
+                    op += len + 1 + (len > 60) + (len > 256);
+                }
+            }
+            for (;;) {
+                const uint32_t base = ip;
+                const uint32_t matched = 4 + find_match_length_v(in, si, g, candidate + 4, ip + 4, ip_end, lane);
+                ip += matched;
+                op += 2 + (matched > 11) + 2 * (matched / 64);
+                next_emit = ip;
+                if (ip >= ip_limit) goto emit_remainder;
+                const uint64_t in8 = in.ld64(ip - 1, si, true);   // bytes [ip-1, ip+7)
+                const uint32_t input_lo = (uint32_t)in8;
+                const uint32_t b1 = (uint32_t)(in8 >> 8);
+                T.put(sn_hash(input_lo, shift), ip - 1);
+                candidate = T.swap(sn_hash(b1, shift), ip);
+                if (b1 != in.ld32(candidate, si, false)) break;
+            }
+            ++ip;
+        }
+    }
+emit_remainder:
+    if (next_emit < ip_end) op += ip_end - next_emit + 3;
+    if (lane == 0) { a.frag_len[f] = op; if (a.ftime) a.ftime[2 * f + 1] = wall_clock64(); }
+}
+
 }  // namespace kpw
