@@ -91,7 +91,6 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
         return fail(KPW_ERR_UNSUPPORTED, "PARQUET_2_0 requires the dictionary on (the only setting the reference produces)");
     if (pr->codec != KPW_UNCOMPRESSED && pr->codec != KPW_SNAPPY) return fail(KPW_ERR_UNSUPPORTED, "codec");
     if (pr->block_size <= 0 || pr->page_size <= 0 || pr->dictionary_page_size <= 0) return fail(KPW_ERR_INVALID_ARG, "sizes");
-    if (pr->dfs_block_size > 0) return fail(KPW_ERR_UNSUPPORTED, "HDFS padding alignment (next round)");
     props = *pr;
     v2_ = pr->writer_version == 2;
     // pages cut inside row groups: ColumnWriterV1 page checks + compressed-size row-group checks
@@ -361,6 +360,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     pa.nbool = v2_ ? 0 : (int32_t)nbool; pa.bool_cols = d_bool.as<uint32_t>();
     pa.E = nstreams ? d_E.as<uint32_t>() : nullptr; pa.gend = nstreams ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
     pa.rg_start = d_rg_start.as<int64_t>(); pa.rg_end = d_rg_end.as<int64_t>(); pa.max_rgs = max_rgs;
+    pa.max_cuts = max_cuts;
     pa.out = d_plan_out.as<int64_t>();
     launch_plan(pa, s);
     CK(hipGetLastError());

@@ -83,6 +83,9 @@ public:
     // `stream` runs before the rest of the encode.  The writer places the next job's carried
     // records from here, so the next job can start while this one still encodes.
     std::function<void(const BatchOut &)> on_plan;
+    // > 0: plan at most this many row groups per encode (the rest stays unconsumed, also on a
+    // final flush).  HDFS block alignment re-plans after each row group with the next limit.
+    int32_t max_cuts = 0;
     std::vector<ColInfo> cols;
     kpw_props props{};
     std::string message_name, proto_class;

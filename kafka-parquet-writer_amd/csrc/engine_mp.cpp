@@ -497,6 +497,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
             if (rs) return rs;
             guess = std::max<int64_t>(1000, (r - s0) + (r - s0) / 4 + 200);
             s0 = r;
+            if (max_cuts > 0 && (int32_t)out.rgs.size() >= max_cuts) break;   // re-planned by the caller
             continue;
         }
         if (final_flush) {   // [s0, ne) was just encoded with its final pages

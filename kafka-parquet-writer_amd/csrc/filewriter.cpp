@@ -299,8 +299,39 @@ int FileWriter::open(const char *path)
     return put("PAR1", 4);  // ParquetFileWriter.start()
 }
 
+// ParquetFileWriter 1.10.1 alignment: HadoopOutputFile.supportsBlockSize() (hdfs, webhdfs,
+// viewfs) selects PaddingAlignment(max(dfs block size, rowGroupSize), rowGroupSize,
+// maxPaddingSize); other file systems NoAlignment (dfs_block_size = 0).
+static bool padding_alignment(const kpw_props &p) { return p.dfs_block_size > 0 && p.max_padding_size > 0; }
+static int64_t dfs_block(const kpw_props &p) { return std::max<int64_t>(p.dfs_block_size, p.block_size); }
+
+int64_t FileWriter::next_row_group_size() const
+{
+    if (rgs_.empty() || !padding_alignment(props_)) return props_.block_size;
+    const int64_t bs = dfs_block(props_);
+    const int64_t remaining = bs - pos_ % bs;
+    if (remaining <= props_.max_padding_size) return props_.block_size;   // isPaddingNeeded: the next block starts fresh
+    return std::min<int64_t>(remaining, props_.block_size);
+}
+
+int FileWriter::align_for_row_group()
+{
+    if (!padding_alignment(props_)) return KPW_OK;
+    const int64_t bs = dfs_block(props_);
+    int64_t remaining = bs - pos_ % bs;
+    if (remaining > props_.max_padding_size) return KPW_OK;
+    static const std::vector<uint8_t> zeros(1u << 20, 0);
+    while (remaining > 0) {
+        const size_t k = (size_t)std::min<int64_t>(remaining, (int64_t)zeros.size());
+        if (int st = put(zeros.data(), k)) return st;
+        remaining -= (int64_t)k;
+    }
+    return KPW_OK;
+}
+
 int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages, uint64_t pages_base, hipStream_t d2h)
 {
+    if (int st = align_for_row_group()) return st;   // startBlock
     const RowGroupOut &R = b.rgs[rg];
     RowGroupMeta rm;
     rm.rows = R.num_records;

@@ -58,6 +58,9 @@ public:
     int64_t row_group_size(const BatchOut &b, int rg) const;
     int close();                      // footer + magic
     int64_t pos() const { return pos_; }
+    // InternalParquetRecordWriter.nextRowGroupSize after the row groups written so far:
+    // min(PaddingAlignment.nextRowGroupSize, blockSize); blockSize before the first one
+    int64_t next_row_group_size() const;
     const uint8_t *memory_data();     // contiguous view (built on first use after close)
     size_t memory_size() const { return mem_len_; }
     const std::string &error() const { return err_; }
@@ -66,6 +69,7 @@ private:
     int put(const void *p, size_t n);
     int put_device(const uint8_t *d, size_t n, hipStream_t s);
     int reserve(size_t n);            // arena room for n more bytes
+    int align_for_row_group();        // PaddingAlignment.alignForRowGroup (startBlock)
     std::vector<ColInfo> cols_;
     std::string message_name_, proto_class_;
     kpw_props props_;

@@ -266,6 +266,10 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
             else overflow = 1;
             nrg++;
             s = r;
+            if (a.max_cuts > 0 && nrg >= a.max_cuts) {   // the caller re-plans from s with the next limit
+                if (tid == 0) { a.out[0] = nrg; a.out[1] = s; a.out[2] = 0; a.out[3] = overflow; }
+                break;
+            }
             __syncthreads();
             continue;
         }

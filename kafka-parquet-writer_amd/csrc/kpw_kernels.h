@@ -126,7 +126,7 @@ struct PlanArgs {
     int64_t *rg_start;             // [max_rgs]
     int64_t *rg_end;
     int32_t max_rgs;
-    int32_t pad;
+    int32_t max_cuts;              // > 0: stop after this many cuts (HDFS alignment plans one row group at a time)
     int64_t *out;                  // [0]=n_rgs [1]=open_start [2]=open_buffered [3]=overflow
 };
 

@@ -130,9 +130,10 @@ int64_t SizeModel::Col::mem() const
 
 bool SizeModel::init(const std::vector<ColInfo> &cols, const kpw_props &p)
 {
-    if (p.writer_version != 1 || p.page_size < p.block_size || p.dfs_block_size > 0) return false;
+    if (p.writer_version != 1 || p.page_size < p.block_size) return false;
     page_size_ = p.page_size;
     block_size_ = p.block_size;
+    next_rg_size_ = p.block_size;
     fmap_.assign(FMAP_SIZE, -1);
     cols_.clear();
     for (size_t c = 0; c < cols.size(); c++) {
@@ -230,12 +231,12 @@ int SizeModel::add(const uint8_t *rec, uint64_t len)
     if (record_count_ >= next_mem_check_) {
         const int64_t mem = buffered();
         const int64_t rec_size = mem / record_count_;
-        if (mem > block_size_ - 2 * rec_size) {
+        if (mem > next_rg_size_ - 2 * rec_size) {
             reset_store();
             next_mem_check_ = 100;   // min(max(100, recordCount / 2), 10000) with recordCount reset to 0
             return CUT;
         }
-        const int64_t est = jadd(record_count_, java_f2l((float)block_size_ / (float)rec_size)) / 2;
+        const int64_t est = jadd(record_count_, java_f2l((float)next_rg_size_ / (float)rec_size)) / 2;
         const int64_t a = est > 100 ? est : 100;
         const int64_t b = jadd(record_count_, 10000);
         next_mem_check_ = a < b ? a : b;

@@ -45,13 +45,16 @@ struct RleCount {
 class SizeModel {
 public:
     enum { OK = 0, CUT = 1, INVALID = -1, LEAVE = -2 };
-    // false if the configuration is outside the model (v2, multi-page, HDFS alignment)
+    // false if the configuration is outside the model (v2, multi-page)
     bool init(const std::vector<ColInfo> &cols, const kpw_props &props);
     // One record: OK, CUT (a row group ends with this record), INVALID (parseFrom would
     // throw; nothing changed), LEAVE (a page cut: the model stops tracking this file).
     int add(const uint8_t *rec, uint64_t len);
     int64_t buffered() const;               // columnStore.getBufferedSize()
     int64_t record_count() const { return record_count_; }
+    // nextRowGroupSize for the open row group (HDFS alignment: set after each cut from the
+    // file position; blockSize otherwise)
+    void set_next_rg_size(int64_t t) { next_rg_size_ = t; }
 
 private:
     struct Col {
@@ -67,7 +70,7 @@ private:
     std::vector<int16_t> fmap_;             // field number (< 1024) -> column
     std::vector<uint8_t> seen_;
     std::vector<uint32_t> raw_;
-    int64_t page_size_ = 0, block_size_ = 0;
+    int64_t page_size_ = 0, block_size_ = 0, next_rg_size_ = 0;
     int64_t record_count_ = 0, next_mem_check_ = 100;
 };
 

@@ -190,6 +190,7 @@ struct kpw_writer {
     Engine eng;                        // worker 0's engine (also the caller's, for write_until_full probes)
     Engine eng1;                       // worker 1's engine
     int nworkers = 2;
+    bool aligned = false;              // HDFS PaddingAlignment: row groups planned one at a time (run_job_aligned)
     Worker wk[2];
     FileWriter *fw = nullptr;
     hipStream_t copy_stream = nullptr;
@@ -665,6 +666,115 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
     return KPW_OK;
 }
 
+// HDFS block alignment (props.dfs_block_size > 0: ParquetFileWriter's PaddingAlignment).
+// Each row group's size limit is min(blockSize, bytes left in the HDFS block after the row
+// group before it) (InternalParquetRecordWriter.flushRowGroupToStore: nextRowGroupSize), so a
+// cut depends on the compressed bytes of every row group before it.  One worker; the job's
+// row groups are planned and encoded one at a time (the planner stops after one cut), and
+// each is in the file before the next limit is read from the file position.
+static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
+{
+    Worker &W = w->wk[0];
+    Engine &E = *W.eng;
+    StageBuf &B = w->buf[j.buf];
+    hipStream_t s = E.stream;
+    auto jfail = [&](int st, const std::string &m) {
+        set_fatal(w, st, m);
+        return st;
+    };
+    if (prev_carry && hipStreamWaitEvent(s, prev_carry, 0) != hipSuccess) return jfail(KPW_ERR_DEVICE, "stream wait failed");
+    if (int st = materialize(w, B, s)) return jfail(st, "stage buffer rebuild failed");
+    bool after_invalid;
+    {
+        std::lock_guard<std::mutex> g(w->mu);
+        after_invalid = w->invalid_seen;
+    }
+    if (after_invalid) { B.ends.clear(); B.len = B.gap; }
+    const size_t nb = nbounds(B);
+    if (W.h_off.ensure(nb * 8)) return jfail(KPW_ERR_NOMEM, "offset staging allocation failed");
+    uint64_t *hb = (uint64_t *)W.h_off.p;
+    boundaries(B, hb);
+    const int64_t nrec = (int64_t)nb - 1;
+    const int64_t ncarry = B.carry.empty() ? 0 : (int64_t)B.carry.size() - 1;
+    int64_t lim = j.kind == JOB_EXACT ? std::min<int64_t>(j.n_exact, nrec) : nrec;
+    if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess) return jfail(KPW_ERR_DEVICE, "stream wait failed");
+    if (lim > 0) {
+        if (W.d_off.ensure((lim + 1) * 8)) return jfail(KPW_ERR_NOMEM, "offset staging allocation failed");
+        if (hipMemcpyAsync(W.d_off.p, W.h_off.p, (lim + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+            return jfail(KPW_ERR_DEVICE, "H2D of offsets failed");
+    }
+    {   // file order (one worker: the previous job is in the file already)
+        std::unique_lock<std::mutex> lk(w->mu);
+        w->cv.wait(lk, [&] { return w->asm_seq == j.seq || w->fatal_st; });
+        if (w->fatal_st) return w->fatal_st;
+    }
+    int64_t s0 = 0, inv = -1;
+    if (j.kind == JOB_PLANNED) w->open_buffered = 0;
+    while (s0 < lim) {
+        const int64_t T = w->fw->next_row_group_size();
+        const int set = (int)(W.njobs & 1);
+        if (w->fw->memory_mode()) {
+            E.swap_page_buffers();
+            for (int k = 0; k < 2; k++)
+                if (W.d2h_used[k] && (k == set || E.multi_page()) && hipStreamWaitEvent(s, W.d2h_ev[k], 0) != hipSuccess)
+                    return jfail(KPW_ERR_DEVICE, "stream wait failed");
+        }
+        const double t0 = now_ms();
+        BatchOut out;
+        E.max_cuts = 1;
+        const int st = E.encode(B.d, W.d_off.as<uint64_t>() + s0, (uint64_t)(lim - s0), j.kind == JOB_FINAL, T, nullptr, out);
+        E.max_cuts = 0;
+        if (st) return jfail(st, E.error());
+        W.njobs++;   // page buffer sets alternate per encode
+        if (out.invalid_record >= 0) {
+            // records from the invalid one on are never written (KafkaProtoParquetWriter.java:270-276)
+            lim = s0 + out.invalid_record;
+            inv = B.first_new_global - ncarry + lim;
+        }
+        if (inv < 0 && j.kind == JOB_EXACT && (out.records_consumed != lim - s0 || out.rgs.size() != 1))
+            return jfail(KPW_ERR_DEVICE, "row-group cut of the size model and the GPU planner differ");
+        if (hipStreamSynchronize(s) != hipSuccess) return jfail(KPW_ERR_DEVICE, "encode sync failed");
+        const double t1 = now_ms();
+        for (const PageOut &pg : out.pages) {
+            w->stats[3] += (double)pg.uncompressed_size;
+            w->stats[4] += (double)pg.compressed_size;
+        }
+        w->stats[0] += 1;
+        w->stats[1] += (double)out.records_consumed;
+        w->stats[2] += (double)(hb[s0 + out.records_consumed] - hb[s0]);
+        for (int k = 0; k < 10; k++) w->stats[5 + k] += E.stage_ms[k];
+        w->stats[15] += t1 - t0;
+        w->t_encode += t1 - t0;
+        if (out.rgs.empty()) {   // no cut in [s0, lim): the open row group
+            if (j.kind == JOB_PLANNED) w->open_buffered = out.open_buffered;
+            break;
+        }
+        s0 += out.records_consumed;
+        if (int st2 = append_job(w, W, out, set)) return jfail(st2, "file assembly failed: " + w->fw->error());
+        if (trace_on())
+            fprintf(stderr, "[kpw] job %llu row group at %lld: %lld records, limit %lld, file at %lld\n",
+                    (unsigned long long)j.seq, (long long)(s0 - out.records_consumed), (long long)out.records_consumed,
+                    (long long)T, (long long)w->fw->pos());
+    }
+    // the open row group -> the next buffer; then the next job may start
+    int st = KPW_OK;
+    if (j.kind != JOB_FINAL && lim > s0 && j.next >= 0) st = place_carry(w, B, hb, (size_t)s0, (size_t)lim, w->buf[j.next], s);
+    if (!st && hipEventRecord(W.carry_ev, s) != hipSuccess) st = KPW_ERR_DEVICE;
+    if (!st && hipStreamSynchronize(s) != hipSuccess) st = KPW_ERR_DEVICE;
+    if (st) return jfail(st, "carry-over copy failed");
+    std::lock_guard<std::mutex> g(w->mu);
+    if (inv >= 0) {
+        w->invalid_seen = true;
+        w->invalid_global = inv;
+    }
+    w->last_carry_ev = W.carry_ev;
+    w->plan_seq = j.seq + 1;
+    B.state = BUF_FREE;
+    w->asm_seq = j.seq + 1;
+    w->cv.notify_all();
+    return KPW_OK;
+}
+
 static void worker_main(kpw_writer *w, int x)
 {
     (void)hipSetDevice(w->eng.device);
@@ -689,7 +799,7 @@ static void worker_main(kpw_writer *w, int x)
             failed = w->fatal_st != KPW_OK;
         }
         try {
-            if (!failed) (void)run_job(w, x, j, prev_carry);
+            if (!failed) (void)(w->aligned ? run_job_aligned(w, j, prev_carry) : run_job(w, x, j, prev_carry));
         } catch (const std::bad_alloc &) {
             set_fatal(w, KPW_ERR_NOMEM, "host allocation failed in an encode worker");
         } catch (...) {
@@ -778,6 +888,8 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
 {
     if (hipSetDevice(eng.device) != hipSuccess) return KPW_ERR_DEVICE;
     nworkers = (int)env_workers();
+    aligned = props->dfs_block_size > 0 && props->max_padding_size > 0;
+    if (aligned) nworkers = 1;   // each row group's limit follows the file position after the one before
     if (nworkers > 1) {
         if (int st = eng1.init(eng.device, schema, props)) return st;
     }
@@ -984,6 +1096,12 @@ static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *of
             const int64_t nrec = F.ncarry_expected + (int64_t)F.ends.size();
             if (int st = submit(w, JOB_EXACT, nrec)) return st;
             w->pending_cut = true;
+            if (w->aligned) {
+                // the next row group's limit follows from this one's end in the file
+                if (int st = drain(w)) return st;
+                w->pending_cut = false;
+                w->model.set_next_rg_size(w->fw->next_row_group_size());
+            }
         }
         if (max_file_size >= 0) {
             // getDataSize() = lastRowGroupEndPos + columnStore.getBufferedSize()
@@ -1045,6 +1163,9 @@ static int write_until_full_bulk(kpw_writer *w, const uint8_t *data, const uint6
 {
     if (w->eng.props.writer_version == 1 && w->eng.props.page_size < w->eng.props.block_size)
         return wfail(w, KPW_ERR_UNSUPPORTED, "write_until_full: pageSize < blockSize (multi-page chunks): use write + getDataSize");
+    if (w->aligned)
+        return wfail(w, KPW_ERR_UNSUPPORTED,
+                     "write_until_full: batches over 65536 records with HDFS alignment: use write + getDataSize");
     if (int st = drain(w)) return st;
     if (int st = flush_slot(w)) return st;
     if (hipEventRecord(w->buf[w->fill].copied, w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "event record failed");

@@ -32,12 +32,24 @@ from ._lib import (KpwError, InvalidProtoError, load_library, make_schema, _Prop
 MiB = 1024 * 1024
 
 
+HDFS_SCHEMES = ("hdfs", "webhdfs", "viewfs")   # parquet-mr 1.10.1 HadoopOutputFile.BLOCK_FS_SCHEMES
+
+
 class ParquetProperties:
-    """ParquetFile.ParquetProperties (ParquetFile.java:105-122).  hadoop_conf is accepted
-    for signature parity and ignored (the output stream is a local path or memory)."""
+    """ParquetFile.ParquetProperties (ParquetFile.java:105-122).
+
+    The output stream itself is a local path or memory.  hadoop_conf (a dict of Hadoop
+    configuration keys) only selects parquet-mr's row-group alignment: when fs.defaultFS is on a
+    block file system (the reference writes under new Path(fs.defaultFS, targetDir),
+    KafkaProtoParquetWriter.java:137-141) ParquetFileWriter uses PaddingAlignment with the
+    file system's block size (dfs.blocksize, default 128 MiB) and ParquetWriter's
+    MAX_PADDING_SIZE_DEFAULT (8 MiB): row groups are sized to end at HDFS block boundaries and
+    zero padding fills a block's last <= 8 MiB.  dfs_block_size / max_padding_size set the
+    same explicitly (0 = NoAlignment, a local file system)."""
 
     def __init__(self, hadoop_conf=None, block_size=128 * MiB, compression_codec_name=UNCOMPRESSED,
-                 page_size=128 * MiB, enable_dictionary=True, writer_version=1):
+                 page_size=128 * MiB, enable_dictionary=True, writer_version=1, dfs_block_size=None,
+                 max_padding_size=8 * MiB):
         self.hadoop_conf = hadoop_conf
         self.block_size = int(block_size)
         self.compression_codec_name = int(compression_codec_name)
@@ -46,6 +58,15 @@ class ParquetProperties:
         # ParquetFile.java:42-50 never sets a writer version (PARQUET_1_0); 2 = PARQUET_2_0,
         # an explicit opt-in beyond the reference (DataPageV2 + DELTA fallback encodings)
         self.writer_version = int(writer_version)
+        if dfs_block_size is None:
+            dfs_block_size = 0
+            conf = hadoop_conf if isinstance(hadoop_conf, dict) else {}
+            fs = str(conf.get("fs.defaultFS", ""))
+            scheme = fs.split("://", 1)[0].lower() if "://" in fs else ""
+            if scheme in HDFS_SCHEMES:
+                dfs_block_size = _hadoop_size(conf.get("dfs.blocksize", 128 * MiB))
+        self.dfs_block_size = int(dfs_block_size)
+        self.max_padding_size = int(max_padding_size)
 
     def to_c(self):
         # ParquetFile.java:48-50 only ever calls enableDictionaryEncoding(); parquet-mr 1.10.1's
@@ -53,7 +74,18 @@ class ParquetProperties:
         # even when enableDictionary is false.  Reproduced here on purpose.
         effective_dictionary = 1
         return _PropsC(self.block_size, self.page_size, MiB, effective_dictionary, self.compression_codec_name,
-                       self.writer_version, 0, 0, 8 * MiB)
+                       self.writer_version, 0, self.dfs_block_size, self.max_padding_size)
+
+
+def _hadoop_size(v):
+    """Configuration.getLongBytes: a number with an optional k/m/g/t/p/e suffix (binary)."""
+    if isinstance(v, (int, float)):
+        return int(v)
+    t = str(v).strip().lower()
+    mult = {"k": 1 << 10, "m": 1 << 20, "g": 1 << 30, "t": 1 << 40, "p": 1 << 50, "e": 1 << 60}
+    if t and t[-1] in mult:
+        return int(t[:-1]) * mult[t[-1]]
+    return int(t)
 
 
 def _as_batch(values):

@@ -75,3 +75,19 @@ def test_properties_dictionary_quirk():
     p = kpw.ParquetProperties(enable_dictionary=False)
     assert p.to_c().enable_dictionary == 1
     assert p.to_c().page_size == 128 * 1024 * 1024  # reference default pageSize (KPW:473-474)
+
+
+def test_properties_hdfs_alignment():
+    """fs.defaultFS on a block file system selects PaddingAlignment (HadoopOutputFile
+    BLOCK_FS_SCHEMES) with dfs.blocksize (Configuration.getLongBytes suffixes) and 8 MiB max
+    padding; a local file system NoAlignment (dfs_block_size 0)."""
+    MiB = 1 << 20
+    p = kpw.ParquetProperties(hadoop_conf={"fs.defaultFS": "hdfs://nn:8020"})
+    assert (p.dfs_block_size, p.max_padding_size) == (128 * MiB, 8 * MiB)
+    p = kpw.ParquetProperties(hadoop_conf={"fs.defaultFS": "viewfs://c", "dfs.blocksize": "256m"})
+    assert p.dfs_block_size == 256 * MiB and p.to_c().dfs_block_size == 256 * MiB
+    p = kpw.ParquetProperties(hadoop_conf={"fs.defaultFS": "file:///", "dfs.blocksize": "256m"})
+    assert p.dfs_block_size == 0 and p.to_c().dfs_block_size == 0
+    p = kpw.ParquetProperties(dfs_block_size=3 * MiB, max_padding_size=MiB)
+    c = p.to_c()
+    assert (c.dfs_block_size, c.max_padding_size) == (3 * MiB, MiB)

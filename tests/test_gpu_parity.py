@@ -255,3 +255,75 @@ def test_invalid_record_cuts_batch():
     pf.close()
     tbl = pq.read_table(io.BytesIO(pf.file_bytes()))
     assert tbl.num_rows == 50
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec", [0, 1])
+@pytest.mark.parametrize("n,batches", [(60000, 40), (400000, 2)], ids=["model", "bulk"])
+@pytest.mark.parametrize("dfs,pad", [(384 * 1024, 96 * 1024), (300 * 1024, 32 * 1024), (256 * 1024, 64 * 1024)],
+                         ids=["dfs1.5x", "dfs-odd", "dfs=block"])
+def test_writer_hdfs_alignment(codec, n, batches, dfs, pad):
+    """HDFS PaddingAlignment (ParquetFileWriter 1.10.1; the reference's target file system,
+    KafkaProtoParquetWriter.java:137-141): row-group limits follow the HDFS block position of
+    the previous row group's end, zero padding fills a block tail <= maxPaddingSize.  Many row
+    groups cross many dfs blocks; file bytes identical to the oracle (oracle_core.c
+    align_for_row_group / next_row_group_size), on the size-model and bulk paths."""
+    import kpw
+    schema = synth.REC8
+    data, offs = synth.generate(synth.KIND_REC8, 0xD15C, n)
+    props = kpw.ParquetProperties(block_size=256 * 1024, compression_codec_name=codec, dfs_block_size=dfs,
+                                  max_padding_size=pad)
+    fb = gh.gpu_file(schema, data, offs, props, batches=batches)
+    ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=256 * 1024, codec=codec,
+                                                                   dfs_block_size=dfs, max_padding_size=pad))
+    import pqwalk
+    assert fb == ob, pqwalk.first_difference(fb, ob)
+    fm = pqwalk.footer(fb)
+    assert len(fm[4]) >= 8
+    tbl = pq.read_table(io.BytesIO(fb))
+    assert tbl.num_rows == n
+
+
+@pytest.mark.gpu
+def test_writer_hdfs_data_size_every_record():
+    """getDataSize after every record with HDFS alignment (host size model with the per-row-group
+    limit) equals the oracle's on every record, and the file is identical."""
+    import kpw
+    schema = synth.SAMPLE
+    data, offs = synth.generate(synth.KIND_SAMPLE, 0xA11C, 30000)
+    recs = synth.records(data, offs)
+    props = kpw.ParquetProperties(block_size=64 * 1024, dfs_block_size=100 * 1024, max_padding_size=16 * 1024)
+    pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class), props)
+    ow = oracle.OracleWriter(schema, oracle.make_props(block_size=64 * 1024, dfs_block_size=100 * 1024,
+                                                       max_padding_size=16 * 1024))
+    bad = []
+    for i, r in enumerate(recs):
+        pf.write(r)
+        ow.write(r)
+        a, b = pf.get_data_size(), ow.data_size()
+        if a != b:
+            bad.append((i, a, b))
+            if len(bad) > 5:
+                break
+    assert not bad, bad
+    pf.close()
+    ow.close()
+    assert pf.file_bytes() == ow.file_bytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec", [0, 1])
+def test_writer_hdfs_alignment_multipage(codec):
+    """HDFS alignment with multi-page chunks (pageSize < blockSize: the row-group limit is
+    checked against flushed pages' compressed bytes) — identical file bytes."""
+    import kpw
+    schema = synth.REC8
+    n = 250000
+    data, offs = synth.generate(synth.KIND_REC8, 0x3A6E, n)
+    kw = dict(block_size=512 * 1024, dfs_block_size=700 * 1024, max_padding_size=100 * 1024)
+    props = kpw.ParquetProperties(compression_codec_name=codec, page_size=64 * 1024, **kw)
+    fb = gh.gpu_file(schema, data, offs, props, batches=3)
+    ob = oracle.encode_file(schema, data, offs, oracle.make_props(codec=codec, page_size=64 * 1024, **kw))
+    import pqwalk
+    assert fb == ob, pqwalk.first_difference(fb, ob)
+    assert len(pqwalk.footer(fb)[4]) >= 4
