@@ -166,7 +166,7 @@ int kpw_encoder_copy_pages(kpw_encoder *e, uint64_t off, uint64_t len, void *hos
 /* Timing of the last encode: device milliseconds measured with HIP events on the encoder's
  * stream.  Index order: [0] decode, [1] plan, [2] stats+dictionary, [3] rle,
  * [4] layout+plain+write, [5] compress, [6] metadata, [7] total, [8] k_decode kernel alone,
- * [9] K7 Snappy kernels alone (k_snappy_v + k_snappy_s_rest; 0 when uncompressed).  Returns entries written (<= cap). */
+ * [9] K7 Snappy kernels alone (k_snappy_v, k_snappy_seg, k_snappy_s_rest; 0 when uncompressed).  Returns entries written (<= cap). */
 int kpw_encoder_stage_times(const kpw_encoder *e, float *ms, int cap);
 
 #ifdef __cplusplus

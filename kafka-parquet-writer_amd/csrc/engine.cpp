@@ -652,6 +652,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
                 sa.order = d_sorder.as<uint32_t>();
             }
         }
+        if (seg_args(sa)) return KPW_ERR_NOMEM;
         CK(hipEventRecord(kev_[2], s));
         launch_snappy(sa, s);
         if (nf) {
@@ -846,6 +847,21 @@ int Engine::copy_pages(uint64_t off, uint64_t len, void *host)
     if (!pages_dev_ || off + len > pages_len_) return fail(KPW_ERR_INVALID_ARG, "copy_pages range");
     CK(hipMemcpy(host, pages_dev_ + off, len, hipMemcpyDeviceToHost));
     return KPW_OK;
+}
+
+// k_snappy_seg needs one scratch block per workgroup and runs one workgroup per CU
+int Engine::seg_args(SnappyArgs &sa)
+{
+    static const bool off = [] { const char *e = getenv("KPW_SNAPPY_SEG"); return e && e[0] == '0'; }();
+    if (off || !sa.nfrags) return 0;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    ENS(d_seg_scratch, snappy_seg_scratch_bytes((uint32_t)cus));
+    ENS(d_seg_counter, 64);
+    sa.seg_scratch = d_seg_scratch.as<uint8_t>();
+    sa.seg_counter = d_seg_counter.as<uint32_t>();
+    sa.seg_grid = (uint32_t)cus;
+    return 0;
 }
 
 }  // namespace kpw

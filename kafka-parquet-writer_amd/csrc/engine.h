@@ -11,6 +11,7 @@
 #include "kpw_kernels.h"
 
 namespace kpw {
+struct SnappyArgs;
 
 struct ColInfo {
     std::string name;
@@ -91,7 +92,7 @@ public:
     std::string message_name, proto_class;
     int device = 0;
     hipStream_t stream = nullptr;
-    float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 K7 (k_snappy_v + k_snappy_s_rest)
+    float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 K7 (k_snappy_v, k_snappy_seg, k_snappy_s_rest)
 
 private:
     int fail(int code, const std::string &msg);
@@ -114,6 +115,8 @@ private:
     // snappy
     DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
     DevBuf d_smeta, d_sblob, d_collision, d_dict_order, d_sprof, d_sorder;
+    DevBuf d_seg_scratch, d_seg_counter;   // k_snappy_seg (one scratch block per CU)
+    int seg_args(SnappyArgs &sa);          // fills sa.seg_* (KPW_SNAPPY_SEG=0: sequential kernels only)
     DevBuf d_body_alt, d_comp_alt;
     std::vector<double> sn_cost_;       // K7 mean fragment duration per (column, page kind), previous batch
     std::unordered_map<uint64_t, double> sn_fcost_;   // per (kind, fragment index)

@@ -294,6 +294,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
         sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
         sa.page_pre = nullptr;
+        if (seg_args(sa)) return KPW_ERR_NOMEM;
         launch_snappy(sa, st);
         launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), st);
         CK(hipGetLastError());

@@ -507,6 +507,7 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k
 {
     const int lane = threadIdx.x;
     const uint32_t f = a.order ? a.order[blockIdx.x] : blockIdx.x;
+    if (a.v_only_handed_on && a.frag_len[f] != SEG_ABORTED) return;
     if (a.ftime && lane == 0) a.ftime[2 * f] = wall_clock64();
     const uint32_t pg = a.frag_page[f];
     const uint32_t fi = a.frag_idx[f];
@@ -534,6 +535,7 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k
     const uint32_t ip_end = n;
     uint32_t next_emit = 0;
     uint32_t ip = 0;
+    uint32_t budget = a.v_budget ? a.v_budget : 0xffffffffu;   // decisions before handing over to k_snappy_seg
     if (n >= 15) {
         const uint32_t ip_limit = n - 15;
         ip = 1;
@@ -543,6 +545,10 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k
             for (;;) {
                 const uint32_t next_ip = ip + (skip++ >> 5);
                 if (next_ip > ip_limit) goto emit_remainder;
+                if (!--budget) {
+                    if (lane == 0) { a.frag_len[f] = SEG_TODO; if (a.ftime) a.ftime[2 * f + 1] = wall_clock64() | (1ull << 63); }
+                    return;
+                }
                 if (skip > 32 + VT_ABORT) {
                     if (lane == 0) { a.frag_len[f] = VT_ABORTED; if (a.ftime) a.ftime[2 * f + 1] = wall_clock64() | (1ull << 63); }
                     return;
@@ -563,6 +569,10 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(128))) k
                 }
             }
             for (;;) {
+                if (!--budget) {
+                    if (lane == 0) { a.frag_len[f] = SEG_TODO; if (a.ftime) a.ftime[2 * f + 1] = wall_clock64() | (1ull << 63); }
+                    return;
+                }
                 const uint32_t base = ip;
                 const uint32_t matched = 4 + find_match_length_v(in, si, g, candidate + 4, ip + 4, ip_end, lane);
                 ip += matched;
@@ -652,13 +662,36 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_prefix(SnappyArgs a)
     for (uint64_t i = threadIdx.x; i < pre; i += KPW_BLOCK) dst[i] = src[i];
 }
 
-// K7: the register-table kernel on every fragment (8 waves/CU, no LDS), then the batched
-// LDS kernel on the fragments it gave up on (incompressible data: long literal searches).
-// Other variants measured against these live in tests/microbench/snappy_variants.hip.
+__global__ void k_snappy_seg(SnappyArgs a);
+
+// K7: the segment-parallel kernel (k_snappy_seg.hip) on every fragment, the register-table
+// kernel (8 waves/CU, no LDS) on the fragments it hands on, then the batched LDS kernel on the
+// fragments that one gives up on (incompressible data: long literal searches).  Without
+// seg_scratch the register-table kernel takes every fragment.  Other variants measured against
+// these live in tests/microbench/snappy_variants.hip.
 void launch_snappy(const SnappyArgs &a, hipStream_t s)
 {
     if (!a.nfrags) return;
-    hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, a);
+    if (a.seg_scratch) {
+        // register-table kernel with a decision budget; the fragments that run past it (long
+        // chains of short matches: sequential per-match latency) go to the segment-parallel
+        // kernel; the ones that hands back (rounds, long copies) to k_snappy_v without a budget
+        static const uint32_t vbudget = [] { const char *e = getenv("KPW_SNAPPY_VBUDGET"); return e ? (uint32_t)atoi(e) : 256u; }();
+        SnappyArgs v = a;
+        v.v_budget = vbudget;
+        hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, v);
+        (void)hipMemsetAsync(a.seg_counter, 0, 4, s);
+        SnappyArgs g = a;
+        g.order = nullptr;
+        g.seg_only_marked = vbudget ? 1 : 0;
+        hipLaunchKernelGGL(k_snappy_seg, dim3(a.seg_grid), dim3(1024), 0, s, g);
+        SnappyArgs b = a;
+        b.order = nullptr;
+        b.v_only_handed_on = 1;
+        hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, b);
+    } else {
+        hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, a);
+    }
     hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, s, a);
 }
 

@@ -104,11 +104,22 @@ struct SnappyArgs {
     const uint64_t *page_pre;    // v2: uncompressed level bytes right before page_off (nullptr: none)
     uint64_t *ftime;             // per fragment [start, end] wall clock of k_snappy_v (nullptr: off)
     const uint32_t *order;       // k_snappy_v: block b compresses fragment order[b] (nullptr: b)
+    uint8_t *seg_scratch;        // k_snappy_seg: per-workgroup scratch (nullptr: k_snappy_v on every fragment)
+    uint32_t *seg_counter;       // k_snappy_seg: next fragment slot
+    uint32_t seg_grid;           // k_snappy_seg: workgroups (one per CU)
+    uint32_t v_only_handed_on;   // k_snappy_v: only the fragments k_snappy_seg handed on
+    uint32_t seg_only_marked;    // k_snappy_seg: only the fragments k_snappy_v marked SEG_TODO
+    uint32_t v_budget;           // k_snappy_v: copies before it marks a fragment SEG_TODO (0: no limit)
+    uint64_t *seg_prof;          // k_snappy_seg phase cycle counters (microbench; nullptr: off)
+    volatile uint32_t *seg_dbg;  // k_snappy_seg progress per workgroup (microbench; nullptr: off)
 };
 constexpr uint32_t SNAPPY_FRAG = 65536;
 // per-fragment output slot: max compressed length (32 + n + n/6) rounded up to the 256-byte
 // output window, plus one window of slack for the final partial flush
 constexpr uint32_t SNAPPY_FRAG_CAP = ((32 + SNAPPY_FRAG + SNAPPY_FRAG / 6 + 255) / 256) * 256 + 256;
 void launch_snappy(const SnappyArgs &a, hipStream_t s);
+size_t snappy_seg_scratch_bytes(uint32_t grid);
+constexpr uint32_t SEG_ABORTED = 0xfffffffeu;   // frag_len: k_snappy_seg handed the fragment on
+constexpr uint32_t SEG_TODO = 0xfffffffdu;      // frag_len: k_snappy_v ran past its budget (k_snappy_seg's work)
 
 }  // namespace kpw
