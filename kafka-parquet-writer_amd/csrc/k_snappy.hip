@@ -257,6 +257,7 @@ __device__ __forceinline__ void k_snappy_s_body(const SnappyArgs &a)
     const uint32_t ip_end = n;
     uint32_t next_emit = 0;
     uint32_t ip = 0;
+    uint32_t budget = a.s_budget ? a.s_budget : 0xffffffffu;   // search batches + copies before handing over to k_snappy_seg
     if (n >= 15) {
         const uint32_t ip_limit = n - 15;
         ip = 1;
@@ -264,6 +265,7 @@ __device__ __forceinline__ void k_snappy_s_body(const SnappyArgs &a)
             uint32_t skip = 32;
             uint32_t candidate;
             int nseq = 0;
+            if (!--budget) goto handed_on;
             for (;;) {
                 if (nseq < SEQ) {
                     nseq++;
@@ -321,6 +323,7 @@ __device__ __forceinline__ void k_snappy_s_body(const SnappyArgs &a)
                     break;
                 }
                 if (vmask != ~0ull) goto emit_remainder;
+                if (!--budget) goto handed_on;
                 if (losers && (grp >> lane) <= 1) table[h] = (uint16_t)ipk;
                 ip = ip + skip_sum(skip + 64) - base_f;
                 skip += 64;
@@ -348,6 +351,9 @@ __device__ __forceinline__ void k_snappy_s_body(const SnappyArgs &a)
 emit_remainder:
     if (next_emit < ip_end) op = emit_literal_wide(out, op, g, next_emit, ip_end - next_emit, lane);
     if (lane == 0) a.frag_len[f] = op;
+    return;
+handed_on:   // past the budget: k_snappy_seg compresses the fragment (from its start)
+    if (lane == 0) a.frag_len[f] = SEG_TODO;
 }
 
 // ------------------------------------------------------------------ register-table variant
@@ -673,13 +679,21 @@ void launch_snappy(const SnappyArgs &a, hipStream_t s)
 {
     if (!a.nfrags) return;
     if (a.seg_scratch) {
-        // register-table kernel with a decision budget; the fragments that run past it (long
-        // chains of short matches: sequential per-match latency) go to the segment-parallel
-        // kernel; the ones that hands back (rounds, long copies) to k_snappy_v without a budget
+        // register-table kernel with a decision budget, then the batched LDS kernel on the ones it
+        // gives up on (incompressible) with a budget of search batches; the fragments that run
+        // past either budget (long chains of short matches, or of rare matches between literal
+        // stretches: sequential per-match latency) go to the segment-parallel kernel; the ones
+        // that hands back (rounds, long copies) to k_snappy_v, then k_snappy_s_rest, unbudgeted
         static const uint32_t vbudget = [] { const char *e = getenv("KPW_SNAPPY_VBUDGET"); return e ? (uint32_t)atoi(e) : 256u; }();
+        static const uint32_t sbudget = [] { const char *e = getenv("KPW_SNAPPY_SBUDGET"); return e ? (uint32_t)atoi(e) : 128u; }();
         SnappyArgs v = a;
         v.v_budget = vbudget;
         hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, v);
+        if (vbudget && sbudget) {   // the batched LDS kernel on the incompressible ones, also with a budget
+            SnappyArgs r = a;
+            r.s_budget = sbudget;
+            hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, s, r);
+        }
         (void)hipMemsetAsync(a.seg_counter, 0, 4, s);
         SnappyArgs g = a;
         g.order = nullptr;

@@ -109,7 +109,8 @@ struct SnappyArgs {
     uint32_t seg_grid;           // k_snappy_seg: workgroups (one per CU)
     uint32_t v_only_handed_on;   // k_snappy_v: only the fragments k_snappy_seg handed on
     uint32_t seg_only_marked;    // k_snappy_seg: only the fragments k_snappy_v marked SEG_TODO
-    uint32_t v_budget;           // k_snappy_v: copies before it marks a fragment SEG_TODO (0: no limit)
+    uint32_t v_budget;           // k_snappy_v: decisions before it marks a fragment SEG_TODO (0: no limit)
+    uint32_t s_budget;           // k_snappy_s_rest: search batches + copies before SEG_TODO (0: no limit)
     uint64_t *seg_prof;          // k_snappy_seg phase cycle counters (microbench; nullptr: off)
     volatile uint32_t *seg_dbg;  // k_snappy_seg progress per workgroup (microbench; nullptr: off)
 };

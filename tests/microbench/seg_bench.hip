@@ -181,6 +181,31 @@ int main(int argc, char **argv)
             }
         }
         bad += mism;
+        if (mode) {   // the routed pipeline kernel by kernel (launch_snappy's sequence)
+            hipEvent_t ev[5];
+            for (auto &e : ev) CK(hipEventCreate(&e));
+            SnappyArgs v = a; v.v_budget = getenv("KPW_SNAPPY_VBUDGET") ? (uint32_t)atoi(getenv("KPW_SNAPPY_VBUDGET")) : 256u;
+            SnappyArgs g = a; g.seg_only_marked = v.v_budget ? 1 : 0;
+            SnappyArgs b = a; b.v_only_handed_on = 1;
+            SnappyArgs r = a; r.s_budget = getenv("KPW_SNAPPY_SBUDGET") ? (uint32_t)atoi(getenv("KPW_SNAPPY_SBUDGET")) : 128u;
+            CK(hipEventRecord(ev[0]));
+            hipLaunchKernelGGL(k_snappy_v, dim3(nf), dim3(64), 0, 0, v);
+            if (v.v_budget && r.s_budget) hipLaunchKernelGGL(k_snappy_s_rest, dim3(nf), dim3(64), 0, 0, r);
+            CK(hipEventRecord(ev[1]));
+            CK(hipMemset(d_cnt, 0, 4));
+            hipLaunchKernelGGL(k_snappy_seg, dim3(cus), dim3(1024), 0, 0, g);
+            CK(hipEventRecord(ev[2]));
+            hipLaunchKernelGGL(k_snappy_v, dim3(nf), dim3(64), 0, 0, b);
+            CK(hipEventRecord(ev[3]));
+            hipLaunchKernelGGL(k_snappy_s_rest, dim3(nf), dim3(64), 0, 0, a);
+            CK(hipEventRecord(ev[4]));
+            CK(hipEventSynchronize(ev[4]));
+            float m[4];
+            for (int i = 0; i < 4; i++) CK(hipEventElapsedTime(&m[i], ev[i], ev[i + 1]));
+            std::vector<uint32_t> fl2(nf);
+            CK(hipMemcpy(fl2.data(), d_flen, nf * 4, hipMemcpyDeviceToHost));
+            printf("routed: v(budget %u) + s_rest(budget) %.3f ms | seg %.3f ms | v(rest) %.3f ms | s_rest %.3f ms\n", v.v_budget, m[0], m[1], m[2], m[3]);
+        }
         hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
         CK(hipEventRecord(e0));
         for (int r = 0; r < reps; r++) launch_snappy(a, 0);
