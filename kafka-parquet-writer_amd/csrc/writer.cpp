@@ -514,9 +514,12 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
     hipStream_t s = E.stream;
     if (out.rgs.empty()) return KPW_OK;
     const double ta = trace_on() ? now_ms() : 0.0;
-    if (w->fw->memory_mode()) {
+    static const bool per_page_d2h = [] { const char *e = getenv("KPW_D2H_PER_PAGE"); return e && e[0] == '1'; }();
+    if (w->fw->memory_mode() && per_page_d2h) {
         // headers on the host; bodies D2H straight into the in-memory file on d2h_stream, after
-        // this encode; the engine's next-but-one encode reuses these page buffers after d2h_ev
+        // this encode; the engine's next-but-one encode reuses these page buffers after d2h_ev.
+        // (Measured: ROCm runs these per-page D2H copies as blit kernels that take CUs from the
+        // encode; the default below is one DMA per job plus host copies.)
         if (hipEventRecord(W.enc_done, s) != hipSuccess || hipStreamWaitEvent(w->d2h_stream, W.enc_done, 0) != hipSuccess)
             return KPW_ERR_DEVICE;
         for (size_t r = 0; r < out.rgs.size(); r++) {
@@ -528,8 +531,9 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
         if (trace_on()) w->t_asm += now_ms() - ta;
         return KPW_OK;
     }
-    // file mode: pages -> pinned host buffer (double-buffered against the previous job's
-    // assembly), headers + bodies written on the assembly thread
+    // pages -> pinned host buffer in one D2H (double-buffered against the previous job's
+    // assembly), headers + bodies written on the assembly thread (file: fwrite; in-memory file:
+    // parallel host copies into the pinned arena)
     if (int st = join_assembly(w)) return st;
     const int slot = w->page_slot;
     w->page_slot ^= 1;
@@ -542,6 +546,8 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
     if (hipEventSynchronize(w->fd2h_ev[slot]) != hipSuccess) return KPW_ERR_DEVICE;   // the engine reuses its buffers next
     if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
     start_assembly(w, std::move(out), slot);
+    // HDFS alignment: the next row group's size limit depends on where this one ends in the file
+    if (w->aligned) return join_assembly(w);
     return KPW_OK;
 }
 
