@@ -12,7 +12,8 @@
 //       one null per column per record, doubles/floats observed through
 //       doubleToLongBits/floatToIntBits (NaN canonicalised).
 //
-// Layout: one lane per record, 256-record blocks; each wave covers 64 consecutive records
+// Layout: one lane per record, 256-record blocks whose bytes are staged in LDS (coalesced
+// 16-byte loads; varints decoded from 8-byte reads); each wave covers 64 consecutive records
 // so presence / boolean bits are produced with one __ballot per column per wave
 // (word w of a bitmask = records [64w, 64w+64)).  Fixed-width values are stored record-
 // indexed (SoA, coalesced per wave), strings as (absolute offset, length) into the batch
@@ -22,30 +23,72 @@
 
 namespace kpw {
 
-__device__ __forceinline__ bool rd_varint64(const uint8_t *d, uint64_t &pos, uint64_t end, uint64_t &out)
+// Byte sources: the block's record bytes staged in LDS (GSrc for blocks whose bytes do not
+// fit).  Positions are absolute offsets into the batch; 8-byte reads may run past the record
+// (callers mask), never past the staged range + 16 or the batch end.
+struct GSrc {
+    const uint8_t *d;
+    uint64_t end;   // batch end
+    __device__ __forceinline__ uint8_t b(uint64_t p) const { return d[p]; }
+    __device__ __forceinline__ uint64_t w64(uint64_t p) const { return ldu64(d, p, end); }
+};
+struct LSrc {
+    const uint32_t *w;   // LDS words holding bytes [base, ...)
+    uint64_t base;       // 4-aligned
+    __device__ __forceinline__ uint8_t b(uint64_t p) const
+    {
+        const uint32_t o = (uint32_t)(p - base);
+        return (uint8_t)(w[o >> 2] >> (8 * (o & 3)));
+    }
+    __device__ __forceinline__ uint64_t w64(uint64_t p) const
+    {
+        const uint32_t o = (uint32_t)(p - base), i = o >> 2, s = o & 3;
+        const uint32_t a0 = w[i], a1 = w[i + 1], a2 = w[i + 2];
+        return (uint64_t)__builtin_amdgcn_alignbyte(a1, a0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(a2, a1, s) << 32);
+    }
+};
+
+// protobuf varint: 8 bytes at once (one load, the stop byte found with ctz), byte loop only for
+// 9- and 10-byte varints
+template <class Src>
+__device__ __forceinline__ bool rd_varint64(const Src &S, uint64_t &pos, uint64_t end, uint64_t &out)
 {
+    if (pos >= end) return false;
+    const uint64_t w = S.w64(pos);
+    const uint64_t stop = ~w & 0x8080808080808080ull;
+    if (stop) {
+        const uint32_t len = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
+        if (len > end - pos) return false;
+        uint64_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) v |= ((w >> i) & (0x7full << (7 * i)));
+        out = len == 8 ? v : (v & ((1ull << (7 * len)) - 1));
+        pos += len;
+        return true;
+    }
     uint64_t r = 0;
 #pragma unroll 1
     for (int i = 0; i < 10; i++) {
         if (pos >= end) return false;
-        uint8_t b = d[pos++];
-        r |= (uint64_t)(b & 0x7f) << (7 * i);
-        if (!(b & 0x80)) { out = r; return true; }
+        const uint8_t c = S.b(pos++);
+        r |= (uint64_t)(c & 0x7f) << (7 * i);
+        if (!(c & 0x80)) { out = r; return true; }
     }
     return false;
 }
 
 // Skip one unknown field whose tag has already been read. Groups are skipped
 // iteratively with a bounded stack (protobuf-java recursion limit 100).
-__device__ bool skip_field(const uint8_t *d, uint64_t &pos, uint64_t end, uint32_t tag)
+template <class Src>
+__device__ bool skip_field(const Src &S, uint64_t &pos, uint64_t end, uint32_t tag)
 {
     uint32_t wt = tag & 7;
     uint64_t v;
     switch (wt) {
-    case 0: return rd_varint64(d, pos, end, v);
+    case 0: return rd_varint64(S, pos, end, v);
     case 1: if (end - pos < 8) return false; pos += 8; return true;
     case 2:
-        if (!rd_varint64(d, pos, end, v)) return false;
+        if (!rd_varint64(S, pos, end, v)) return false;
         if ((int32_t)(uint32_t)v < 0) return false;
         if (end - pos < (uint32_t)v) return false;
         pos += (uint32_t)v;
@@ -58,7 +101,7 @@ __device__ bool skip_field(const uint8_t *d, uint64_t &pos, uint64_t end, uint32
 #pragma unroll 1
         while (depth > 0) {
             uint64_t t64;
-            if (!rd_varint64(d, pos, end, t64)) return false;
+            if (!rd_varint64(S, pos, end, t64)) return false;
             uint32_t t = (uint32_t)t64;
             if ((t >> 3) == 0) return false;
             uint32_t w = t & 7;
@@ -69,13 +112,13 @@ __device__ bool skip_field(const uint8_t *d, uint64_t &pos, uint64_t end, uint32
                 if (depth >= 100) return false;
                 stack[depth++] = t >> 3;
             } else if (w == 0) {
-                if (!rd_varint64(d, pos, end, v)) return false;
+                if (!rd_varint64(S, pos, end, v)) return false;
             } else if (w == 1) {
                 if (end - pos < 8) return false; pos += 8;
             } else if (w == 5) {
                 if (end - pos < 4) return false; pos += 4;
             } else if (w == 2) {
-                if (!rd_varint64(d, pos, end, v)) return false;
+                if (!rd_varint64(S, pos, end, v)) return false;
                 if ((int32_t)(uint32_t)v < 0) return false;
                 if (end - pos < (uint32_t)v) return false;
                 pos += (uint32_t)v;
@@ -100,88 +143,138 @@ __device__ __forceinline__ uint32_t canon_float(uint32_t b)
     return b;
 }
 
+// 64-bit hash of a value's bytes (the dictionary key of BYTE_ARRAY columns; the same function
+// as bytes_hash in kpw_device.h, through a byte source)
+template <class Src>
+__device__ __forceinline__ uint64_t src_bytes_hash(const Src &S, uint64_t off, uint32_t len)
+{
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ len;
+    for (uint32_t k = 0; k < len; k += 8) {
+        const uint64_t w = S.w64(off + k) & tail_mask(len - k);
+        h = (h ^ w) * 0xff51afd7ed558ccdull;
+        h ^= h >> 29;
+    }
+    return mix64(h);
+}
+
+// Parse record r from source S.  Returns false on an invalid record.
+template <class Src>
+__device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *cols, const int16_t *fmap, const Src &S, uint64_t r,
+                                             uint64_t pos, uint64_t end, uint64_t *seen, uint64_t *bval)
+{
+#pragma unroll 1
+    while (pos < end) {
+        uint64_t t64;
+        if (!rd_varint64(S, pos, end, t64)) return false;
+        const uint32_t tag = (uint32_t)t64;
+        const uint32_t fno = tag >> 3, wt = tag & 7;
+        if (fno == 0) return false;
+        int c = -1;
+        if (fno < FMAP_SIZE) c = fmap[fno];
+        else {
+            for (int k = 0; k < a.ncols; k++) if ((uint32_t)a.cols[k].field_number == fno) { c = k; break; }
+        }
+        const DevCol *col = nullptr;
+        if (c >= 0) col = c < 64 ? &cols[c] : &a.cols[c];
+        if (c < 0 || (uint32_t)col->wire_type != wt) {
+            if (!skip_field(S, pos, end, tag)) return false;
+            continue;
+        }
+        uint64_t v = 0;
+        if (wt == 0) {
+            if (!rd_varint64(S, pos, end, v)) return false;
+            switch (col->proto_type) {
+            case 5: case 13: v = (uint32_t)v; break;                                            // int32/uint32
+            case 17: { uint32_t u = (uint32_t)v; v = (uint32_t)((u >> 1) ^ (0u - (u & 1))); break; }  // sint32
+            case 18: v = (v >> 1) ^ (0ull - (v & 1)); break;                                   // sint64
+            case 8: v = v != 0; break;                                                          // bool
+            default: break;
+            }
+        } else if (wt == 1) {
+            if (end - pos < 8) return false;
+            v = S.w64(pos);
+            pos += 8;
+            if (col->phys == 5) v = canon_double(v);
+        } else if (wt == 5) {
+            if (end - pos < 4) return false;
+            v = S.w64(pos) & 0xffffffffull;
+            pos += 4;
+            if (col->phys == 4) v = canon_float((uint32_t)v);
+        } else {  // wt == 2
+            uint64_t l;
+            if (!rd_varint64(S, pos, end, l)) return false;
+            if ((int32_t)(uint32_t)l < 0 || end - pos < (uint32_t)l) return false;
+            col->soff[r] = pos;
+            col->slen[r] = (uint32_t)l;
+            // first 16 bytes, zero padded: exact compares for short strings (stats,
+            // dictionary verification) without touching the batch bytes again
+            col->spfx[2 * r] = l ? S.w64(pos) & tail_mask(l) : 0ull;
+            col->spfx[2 * r + 1] = l > 8 ? S.w64(pos + 8) & tail_mask(l - 8) : 0ull;
+            if (col->dict) col->shash[r] = src_bytes_hash(S, pos, (uint32_t)l);
+            pos += (uint32_t)l;
+        }
+        if (col->phys == 0) {
+            if (v) bval[c >> 6] |= 1ull << (c & 63); else bval[c >> 6] &= ~(1ull << (c & 63));
+        } else if (col->vsize == 4) {
+            ((uint32_t *)col->vals)[r] = (uint32_t)v;
+        } else if (col->vsize == 8) {
+            ((uint64_t *)col->vals)[r] = v;
+        }
+        seen[c >> 6] |= 1ull << (c & 63);
+    }
+    return true;
+}
+
+// Tile kernel: one block = 256 consecutive records.  When the block's bytes fit K1_LDS bytes
+// they are staged into LDS with coalesced 16-byte loads and every lane parses its record from
+// LDS; wider records (C3-like rows of > 128 bytes) parse straight from global memory.
+constexpr uint32_t K1_LDS = 24576;
+
 __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
 {
     __shared__ int16_t fmap[FMAP_SIZE];
     __shared__ DevCol cols[64];   // first 64 columns cached; rest read from global
+    __shared__ uint4 stage[K1_LDS / 16 + 2];
     for (int i = threadIdx.x; i < FMAP_SIZE; i += blockDim.x) fmap[i] = a.fmap[i];
     const int ncached = a.ncols < 64 ? a.ncols : 64;
     for (int i = threadIdx.x; i < ncached; i += blockDim.x) cols[i] = a.cols[i];
-    __syncthreads();
 
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x;
+    const uint64_t r = r0 + threadIdx.x;
     const bool valid = r < a.n;
     const uint64_t data_end = a.off[a.n];
+    const uint64_t rl = r0 + blockDim.x < a.n ? r0 + blockDim.x : a.n;
+    const uint64_t B0 = a.off[r0], B1 = a.off[rl];
+    const uint64_t S0 = B0 & ~15ull;                          // 16-aligned staging start
+    const bool staged = B1 - S0 <= K1_LDS;
+    if (staged) {
+        // [S0, B1) + 16 bytes of read padding; nothing at or past the batch end is read (the
+        // caller's buffer may end there): the 16-byte piece holding it is copied byte by byte
+        const uint64_t lim = (B1 + 16 + 15) & ~15ull;
+        const uint4 *src = (const uint4 *)(a.data + S0);
+        const uint32_t nv = (uint32_t)((lim - S0) >> 4);
+        for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) {
+            const uint64_t p = S0 + 16ull * i;
+            if (p + 16 <= data_end) {
+                stage[i] = src[i];
+            } else {
+                uint32_t q[4] = {0, 0, 0, 0};
+                for (uint32_t k = 0; k < 16 && p + k < data_end; k++) q[k >> 2] |= (uint32_t)a.data[p + k] << (8 * (k & 3));
+                stage[i] = uint4{q[0], q[1], q[2], q[3]};
+            }
+        }
+    }
+    __syncthreads();
+
     uint64_t seen[4] = {0, 0, 0, 0};
     uint64_t bval[4] = {0, 0, 0, 0};   // boolean values (by column)
     bool bad = false;
     uint32_t raw = 0;
 
     if (valid) {
-        const uint8_t *d = a.data;
-        uint64_t pos = a.off[r], end = a.off[r + 1];
-#pragma unroll 1
-        while (pos < end) {
-            uint64_t t64;
-            if (!rd_varint64(d, pos, end, t64)) { bad = true; break; }
-            const uint32_t tag = (uint32_t)t64;
-            const uint32_t fno = tag >> 3, wt = tag & 7;
-            if (fno == 0) { bad = true; break; }
-            int c = -1;
-            if (fno < FMAP_SIZE) c = fmap[fno];
-            else {
-                for (int k = 0; k < a.ncols; k++) if ((uint32_t)a.cols[k].field_number == fno) { c = k; break; }
-            }
-            const DevCol *col = nullptr;
-            if (c >= 0) col = c < 64 ? &cols[c] : &a.cols[c];
-            if (c < 0 || (uint32_t)col->wire_type != wt) {
-                if (!skip_field(d, pos, end, tag)) { bad = true; break; }
-                continue;
-            }
-            uint64_t v = 0;
-            if (wt == 0) {
-                if (!rd_varint64(d, pos, end, v)) { bad = true; break; }
-                switch (col->proto_type) {
-                case 5: case 13: v = (uint32_t)v; break;                                            // int32/uint32
-                case 17: { uint32_t u = (uint32_t)v; v = (uint32_t)((u >> 1) ^ (0u - (u & 1))); break; }  // sint32
-                case 18: v = (v >> 1) ^ (0ull - (v & 1)); break;                                   // sint64
-                case 8: v = v != 0; break;                                                          // bool
-                default: break;
-                }
-            } else if (wt == 1) {
-                if (end - pos < 8) { bad = true; break; }
-                v = 0;
-                for (int i = 0; i < 8; i++) v |= (uint64_t)d[pos + i] << (8 * i);
-                pos += 8;
-                if (col->phys == 5) v = canon_double(v);
-            } else if (wt == 5) {
-                if (end - pos < 4) { bad = true; break; }
-                v = 0;
-                for (int i = 0; i < 4; i++) v |= (uint64_t)d[pos + i] << (8 * i);
-                pos += 4;
-                if (col->phys == 4) v = canon_float((uint32_t)v);
-            } else {  // wt == 2
-                uint64_t l;
-                if (!rd_varint64(d, pos, end, l)) { bad = true; break; }
-                if ((int32_t)(uint32_t)l < 0 || end - pos < (uint32_t)l) { bad = true; break; }
-                col->soff[r] = pos;
-                col->slen[r] = (uint32_t)l;
-                // first 16 bytes, zero padded: exact compares for short strings (stats,
-                // dictionary verification) without touching the batch bytes again
-                col->spfx[2 * r] = l ? ldu64(d, pos, data_end) & tail_mask(l) : 0ull;
-                col->spfx[2 * r + 1] = l > 8 ? ldu64(d, pos + 8, data_end) & tail_mask(l - 8) : 0ull;
-                if (col->dict) col->shash[r] = bytes_hash(d, pos, (uint32_t)l, data_end);
-                pos += (uint32_t)l;
-            }
-            if (col->phys == 0) {
-                if (v) bval[c >> 6] |= 1ull << (c & 63); else bval[c >> 6] &= ~(1ull << (c & 63));
-            } else if (col->vsize == 4) {
-                ((uint32_t *)col->vals)[r] = (uint32_t)v;
-            } else if (col->vsize == 8) {
-                ((uint64_t *)col->vals)[r] = v;
-            }
-            seen[c >> 6] |= 1ull << (c & 63);
-        }
+        const uint64_t pos = a.off[r], end = a.off[r + 1];
+        if (staged) bad = !parse_record(a, cols, fmap, LSrc{(const uint32_t *)stage, S0}, r, pos, end, seen, bval);
+        else bad = !parse_record(a, cols, fmap, GSrc{a.data, data_end}, r, pos, end, seen, bval);
         if (!bad) {
             for (int c = 0; c < a.ncols; c++) {
                 const DevCol *col = c < 64 ? &cols[c] : &a.cols[c];
