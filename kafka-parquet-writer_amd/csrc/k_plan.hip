@@ -166,7 +166,7 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
     }
     part = wave_sum(part);
     if ((tid & 63) == 0) red[tid >> 6] = part;
-    __syncthreads();   // also publishes the walkers to eval_mem_lane
+    __syncthreads();   // also publishes the walkers to eval_mem_points
     uint64_t tot = 0;
 #pragma unroll
     for (int i = 0; i < PLAN_T / 64; i++) tot += red[i];
@@ -174,21 +174,39 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
     return tot + (a.P[r] - a.P[s]);
 }
 
-// memSize at record r for one lane, valid only when every walker is past its convergence
-// point (or has no further events): E_s(q) is then O(1) per stream.
-__device__ uint64_t eval_mem_lane(const PlanArgs &a, const Walker *W, int64_t s, int64_t r)
+// memSize at the 64 clamp-step check points s + rc + 10000*j, valid only when every walker is
+// past its convergence point (or has no further events): E_s(q) is then one lookup per stream.
+// The block splits (point, stream) pairs: lane j of every wave owns point j, wave g the streams
+// g, g + 4, ... (independent loads, no walking), and the four partial sums meet in LDS; every
+// lane j returns the memSize of point j.
+__device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, int64_t s, int64_t rc)
 {
-    uint64_t m = a.P[r] - a.P[s];
-    for (int k = 0; k < a.nstreams; k++) {
-        const Walker &w = W[k];
-        m += w.state == 1 ? (uint64_t)((int64_t)a.E[(uint64_t)k * (a.n + 1) + stream_pos(a, a.streams[k], r)] + w.delta) : w.eacc;
+    __shared__ uint64_t red[PLAN_T];
+    constexpr int NW = PLAN_T / 64;
+    const int tid = threadIdx.x;
+    const int j = tid & 63, g = tid >> 6;
+    const int64_t r = s + rc + 10000 * (int64_t)j;
+    uint64_t part = 0;
+    if (r <= (int64_t)a.n) {
+        if (g == 0) part = a.P[r] - a.P[s];
+        for (int k = g; k < a.nstreams; k += NW) {
+            const Walker &w = W[k];
+            part += w.state == 1 ? (uint64_t)((int64_t)a.E[(uint64_t)k * (a.n + 1) + stream_pos(a, a.streams[k], r)] + w.delta)
+                                 : w.eacc;
+        }
+        for (int k = g; k < a.nbool; k += NW) {
+            const DevCol &c = a.cols[a.bool_cols[k]];
+            const uint64_t cnt = c.optional ? pc_at(c, (uint64_t)r) - pc_at(c, (uint64_t)s) : (uint64_t)(r - s);
+            part += (cnt + 7) / 8;
+        }
     }
-    for (int k = 0; k < a.nbool; k++) {
-        const DevCol &c = a.cols[a.bool_cols[k]];
-        const uint64_t cnt = c.optional ? pc_at(c, (uint64_t)r) - pc_at(c, (uint64_t)s) : (uint64_t)(r - s);
-        m += (cnt + 7) / 8;
-    }
-    return m;
+    red[tid] = part;
+    __syncthreads();
+    uint64_t tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) tot += red[i * 64 + j];
+    __syncthreads();
+    return tot;
 }
 
 __device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walker *W, int64_t r)
@@ -219,15 +237,16 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
         __syncthreads();
         int64_t rc = 100;
         bool cut = false;
+        bool clamp = true;   // the previous decision took the recordCount + 10000 clamp
         int64_t r = 0;
         while (s + rc <= n) {
             // Far from the cut every next check is recordCount + 10000 (the clamp): once the
-            // walkers are converged, lanes evaluate memSize at the next 64 clamp-step check
-            // points and the scalar replay below takes parquet-mr's decisions over them,
-            // stopping where a decision leaves the clamp path (or cuts).
-            if (walkers_converged(a, W, s + rc)) {
-                const int64_t rcj = rc + 10000 * (int64_t)lane;
-                const uint64_t Mj = (s + rcj <= n) ? eval_mem_lane(a, W, s, s + rcj) : 0;
+            // walkers are converged, the block evaluates memSize at the next 64 clamp-step
+            // check points and the scalar replay below takes parquet-mr's decisions over them,
+            // stopping where a decision leaves the clamp path (or cuts).  Near the cut (the
+            // estimate halves the distance each check) one point at a time is cheaper.
+            if (clamp && walkers_converged(a, W, s + rc)) {
+                const uint64_t Mj = eval_mem_points(a, W, s, rc);
                 bool left = false;
                 for (int j = 0; j < 64; j++) {
                     const int64_t rcv = rc + 10000 * (int64_t)j;
@@ -243,7 +262,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
                     const int64_t hi = jadd(rcv, 10000);
                     int64_t nc = lo < hi ? lo : hi;
                     if (nc < rcv + 1) nc = rcv + 1;
-                    if (nc != rcv + 10000) { rc = nc; left = true; break; }
+                    if (nc != rcv + 10000) { rc = nc; left = true; clamp = false; break; }
                 }
                 if (cut) break;
                 if (!left) rc += 10000 * 64;
@@ -259,6 +278,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
             const int64_t hi = jadd(rc, 10000);
             int64_t nc = lo < hi ? lo : hi;
             if (nc < rc + 1) nc = rc + 1;
+            clamp = nc == rc + 10000;
             rc = nc;
         }
         if (cut) {
