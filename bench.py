@@ -196,10 +196,14 @@ def write_file(kpw, schema, props, data, offs, device, batch=POLL_BATCH):
             pf._check(st, "write")
     t2 = time.perf_counter()
     pf.close()
+    t3 = time.perf_counter()
+    res = L.kpw_writer_data_size(h), pf.pipeline_stats()   # after close: the file's length
+    pf.__del__()   # the writer (and its in-memory file) is released inside the step
     if os.environ.get("KPW_TRACE") == "1":
-        print("[bench] writer: open %.1f ms, writes %.1f ms, close %.1f ms" % (
-            (t1 - t0) * 1e3, (t2 - t1) * 1e3, (time.perf_counter() - t2) * 1e3), file=sys.stderr, flush=True)
-    return L.kpw_writer_data_size(h), pf.pipeline_stats()   # after close: the file's length
+        print("[bench] writer: open %.1f ms, writes %.1f ms, close %.1f ms, free %.1f ms" % (
+            (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (time.perf_counter() - t3) * 1e3),
+            file=sys.stderr, flush=True)
+    return res
 
 
 def copy_ceiling(device, nbytes=2 << 30):

@@ -483,8 +483,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     ENS(d_chunks, nch * sizeof(ChunkDesc)); ENS(d_ctile_chunk, nct * 4); ENS(d_ctile_first, nch * 4); ENS(d_ctile_count, nch * 4);
     ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
     ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8);
-    ENS(d_ht_key, std::max<uint64_t>(1, ht_off) * 8); ENS(d_ht_min, std::max<uint64_t>(1, ht_off) * 4);
-    ENS(d_ht_id, std::max<uint64_t>(1, ht_off) * 4);
+    ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
     ENS(d_ids, std::max<uint64_t>(1, ids_off) * 4); ENS(d_ent_rec, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_page_off, 2 * nch * 8); ENS(d_page_len, 2 * nch * 8); ENS(d_tot, 64);
@@ -499,7 +498,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     a.ctile_count = d_ctile_count.as<uint32_t>(); a.tile_raw = d_tile_raw.as<uint64_t>();
     a.tile_raw_off = d_tile_raw_off.as<uint64_t>(); a.tile_smin = d_tile_smin.as<uint64_t>();
     a.tile_smax = d_tile_smax.as<uint64_t>(); a.tile_cnt = d_tile_cnt.as<uint32_t>(); a.tile_sz = d_tile_sz.as<uint64_t>();
-    a.ht_key = d_ht_key.as<uint64_t>(); a.ht_min = d_ht_min.as<uint32_t>(); a.ht_id = d_ht_id.as<uint32_t>();
+    a.ht = d_ht.as<HtSlot>();
     a.ids = d_ids.as<uint32_t>(); a.ent_rec = d_ent_rec.as<uint64_t>(); a.ent_boff = d_ent_boff.as<uint64_t>();
     a.max_dict_bytes = (uint32_t)props.dictionary_page_size;
     a.data_end = d_off + n;
@@ -541,10 +540,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         a.exact_strings = attempt;
         CK(hipMemcpyAsync(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
         CK(hipMemsetAsync(d_collision.p, 0, 4, s));
-        if (ht_off) {
-            CK(hipMemsetAsync(d_ht_key.p, 0xFF, ht_off * 8, s));
-            CK(hipMemsetAsync(d_ht_min.p, 0xFF, ht_off * 4, s));
-        }
+        if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), s));
         if (v2_ && !dj.empty()) CK(hipMemcpyAsync(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), hipMemcpyHostToDevice, s));
         // ------------------------------------------------------------ K6 + K2
         launch_chunk_stats(a, s);

@@ -110,7 +110,7 @@ private:
         d_jobs;
     // chunks
     DevBuf d_chunks, d_ctile_chunk, d_ctile_first, d_ctile_count, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
-        d_tile_cnt, d_tile_sz, d_ht_key, d_ht_min, d_ht_id, d_ids, d_ent_rec, d_ent_boff, d_page_off, d_page_len, d_tot,
+        d_tile_cnt, d_tile_sz, d_ht, d_ids, d_ent_rec, d_ent_boff, d_page_off, d_page_len, d_tot,
         d_body;
     // snappy
     DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;

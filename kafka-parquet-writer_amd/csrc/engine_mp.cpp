@@ -180,8 +180,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ENS(mp_dch, nc * sizeof(ChunkDesc)); ENS(mp_dtile_chunk, ndt * 4); ENS(mp_dtile_first, nc * 4); ENS(mp_dtile_count, nc * 4);
     ENS(mp_dtile_raw, ndt * 8); ENS(mp_dtile_smin, ndt * 8); ENS(mp_dtile_smax, ndt * 8); ENS(mp_dtile_cnt, ndt * 4);
     ENS(mp_dtile_sz, ndt * 8); ENS(d_dict_order, std::max<size_t>(1, dorder.size()) * 4);
-    ENS(d_ht_key, std::max<uint64_t>(1, ht_off) * 8); ENS(d_ht_min, std::max<uint64_t>(1, ht_off) * 4);
-    ENS(d_ht_id, std::max<uint64_t>(1, ht_off) * 4);
+    ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
     ENS(d_ids, std::max<uint64_t>(1, ids_off) * 4); ENS(d_ent_rec, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_page_off, 2 * npg * 8); ENS(d_page_len, 2 * npg * 8); ENS(d_page_pre, 2 * npg * 8); ENS(d_tot, 64); ENS(d_collision, 64);
@@ -200,7 +199,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ap.ctile_count = d_ctile_count.as<uint32_t>(); ap.tile_raw = d_tile_raw.as<uint64_t>();
     ap.tile_raw_off = d_tile_raw_off.as<uint64_t>(); ap.tile_smin = d_tile_smin.as<uint64_t>();
     ap.tile_smax = d_tile_smax.as<uint64_t>(); ap.tile_cnt = d_tile_cnt.as<uint32_t>(); ap.tile_sz = d_tile_sz.as<uint64_t>();
-    ap.ht_key = d_ht_key.as<uint64_t>(); ap.ht_min = d_ht_min.as<uint32_t>(); ap.ht_id = d_ht_id.as<uint32_t>();
+    ap.ht = d_ht.as<HtSlot>();
     ap.ids = d_ids.as<uint32_t>(); ap.ent_rec = d_ent_rec.as<uint64_t>(); ap.ent_boff = d_ent_boff.as<uint64_t>();
     ap.max_dict_bytes = (uint32_t)props.dictionary_page_size;
     ap.data_end = d_off + n; ap.collision = d_collision.as<uint32_t>();
@@ -224,10 +223,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         CK(hipMemcpyAsync(d_chunks.p, pg.data(), npg * sizeof(ChunkDesc), hipMemcpyHostToDevice, st));
         CK(hipMemcpyAsync(mp_dch.p, dch.data(), nc * sizeof(ChunkDesc), hipMemcpyHostToDevice, st));
         CK(hipMemsetAsync(d_collision.p, 0, 4, st));
-        if (ht_off) {
-            CK(hipMemsetAsync(d_ht_key.p, 0xFF, ht_off * 8, st));
-            CK(hipMemsetAsync(d_ht_min.p, 0xFF, ht_off * 4, st));
-        }
+        if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), st));
         launch_chunk_stats(ap, st);                          // K6 per page (+ nn, raw bytes)
         if (!ej.empty()) {
             int rs = run_rle(ej, enpt, enet, esc);

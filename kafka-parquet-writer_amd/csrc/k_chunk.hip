@@ -260,38 +260,38 @@ constexpr uint64_t HT_EMPTY = ~0ull;
 // the table is full / the chunk already fell back.  Plain loads are used where a stale
 // value is harmless: keys only go EMPTY -> key (a stale EMPTY just leads to a CAS that
 // returns the real key), and recorded ranks only decrease.
-__device__ __forceinline__ int64_t global_insert(ChunkDesc &C, uint64_t *keys, uint32_t *mins, uint32_t cap, uint64_t key,
+__device__ __forceinline__ int64_t global_insert(ChunkDesc &C, HtSlot *tab, uint32_t cap, uint64_t key,
                                                  uint64_t h, uint32_t rank, uint32_t esize, uint32_t max_dict_bytes,
                                                  bool is_bin, const DevCol &col, const uint8_t *data, uint64_t r,
                                                  uint64_t data_end)
 {
     if (!is_bin && key == HT_EMPTY) {
         const uint32_t slot = cap;  // reserved slot for the sentinel value
-        if (atomicCAS((unsigned long long *)&keys[slot], (unsigned long long)HT_EMPTY, 0ull) == HT_EMPTY) {
+        if (atomicCAS((unsigned long long *)&tab[slot].key, (unsigned long long)HT_EMPTY, 0ull) == HT_EMPTY) {
             const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
             atomicAdd(&C.dict_n, 1u);
             if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (mins[slot] > rank) atomicMin(&mins[slot], rank);
+        if (tab[slot].min > rank) atomicMin(&tab[slot].min, rank);
         return slot;
     }
     uint32_t i = (uint32_t)(h & (cap - 1));
     for (uint32_t probe = 0; probe < cap; probe++) {
-        uint64_t cur = keys[i];
+        uint64_t cur = tab[i].key;
         if (cur == HT_EMPTY) {
-            const unsigned long long old = atomicCAS((unsigned long long *)&keys[i], (unsigned long long)HT_EMPTY, (unsigned long long)key);
+            const unsigned long long old = atomicCAS((unsigned long long *)&tab[i].key, (unsigned long long)HT_EMPTY, (unsigned long long)key);
             if (old == HT_EMPTY) {
                 const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
                 atomicAdd(&C.dict_n, 1u);
                 if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicMin(&mins[i], rank);
+                atomicMin(&tab[i].min, rank);
                 return i;
             }
             cur = old;
         }
         const bool eq = is_bin ? str_eq(col, data, cur, r, data_end) : cur == key;
         if (eq) {
-            if (mins[i] > rank) atomicMin(&mins[i], rank);
+            if (tab[i].min > rank) atomicMin(&tab[i].min, rank);
             return i;
         }
         i = (i + 1) & (cap - 1);
@@ -308,7 +308,7 @@ constexpr uint32_t LDS_PROBES = 32;
 
 __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
                                                            const uint32_t *order, const uint32_t *ctile_chunk, const uint32_t *ctile_first,
-                                                           uint64_t *ht_key, uint32_t *ht_min, uint32_t *slotof, uint32_t max_dict_bytes,
+                                                           HtSlot *ht, uint32_t *slotof, uint32_t max_dict_bytes,
                                                            int exact, const uint64_t *data_end_p)
 {
     __shared__ uint64_t lkey[LDS_T];
@@ -328,8 +328,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     const DevCol &col = cols[C.col];
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     const uint32_t cap = C.ht_cap;
-    uint64_t *keys = ht_key + C.ht_off;
-    uint32_t *mins = ht_min + C.ht_off;
+    HtSlot *tab = ht + C.ht_off;
     // BYTE_ARRAY keys: the 64-bit hash computed by K1 (verified byte-for-byte afterwards in
     // k_dict_ids); `exact` re-runs with byte comparisons after a detected hash collision
     // (then the LDS stage is skipped: every value goes straight to the global table).
@@ -377,7 +376,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
         if (key == HT_EMPTY) continue;
         const uint64_t r = lrec[i];
         const uint32_t esize = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize;
-        const int64_t g = global_insert(C, keys, mins, cap, key, mix64(key), lmin[i], esize, max_dict_bytes, false, col, data, r,
+        const int64_t g = global_insert(C, tab, cap, key, mix64(key), lmin[i], esize, max_dict_bytes, false, col, data, r,
                                         data_end);
         lslot[i] = g < 0 ? 0xffffffffu : (uint32_t)g;
         if (g < 0 && !__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -399,7 +398,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
             uint32_t esize;
             if (is_bin) { h = bytes_hash(data, col.soff[r], col.slen[r], data_end); esize = 4 + col.slen[r]; }
             else { h = mix64(keyv[k]); esize = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize; }
-            g = global_insert(C, keys, mins, cap, keyv[k], h, rk[k], esize, max_dict_bytes, is_bin, col, data, r, data_end);
+            g = global_insert(C, tab, cap, keyv[k], h, rk[k], esize, max_dict_bytes, is_bin, col, data, r, data_end);
             if (g < 0 && !__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 atomicOr(&C.overflow, 1u);
                 __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -414,7 +413,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
 // tile layout record order is (k, wave, lane); the write pass ranks a thread's first
 // occurrences with one ballot + one wave scan per k and 32 (k, wave) totals in LDS.
 __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
-                                                           const uint32_t *ctile_first, const uint32_t *ht_min, uint32_t *ht_id,
+                                                           const uint32_t *ctile_first, HtSlot *ht,
                                                            const uint32_t *slotof, uint32_t *tile_cnt, uint64_t *tile_sz,
                                                            const uint32_t *tile_cnt_off, const uint64_t *tile_sz_off,
                                                            uint64_t *ent_rec, uint64_t *ent_boff, int write)
@@ -441,7 +440,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
             if (!present_at(col, r)) continue;
             const uint64_t rank = T.rank(col, r);
             const uint32_t slot = slotof[C.ids_off + rank];
-            if (ht_min[C.ht_off + slot] == (uint32_t)rank) {
+            if (ht[C.ht_off + slot].min == (uint32_t)rank) {
                 firsts |= 1u << k;
                 cnt++;
                 esz[k] = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize;
@@ -486,7 +485,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
                 const uint64_t rank = T.rank(col, r);
                 const uint32_t eid = ebase + lpre[k];
                 const uint32_t slot = slotof[C.ids_off + rank];
-                ht_id[C.ht_off + slot] = eid;
+                ht[C.ht_off + slot].id = eid;
                 ent_rec[C.ent_off + eid] = r;
                 ent_boff[C.ent_off + eid] = bbase + spre[k];
             }
@@ -498,7 +497,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
 
 // slot -> id for every value (overwrites slotof in place); sets id-job width/length
 __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
-                                                        const uint32_t *ctile_first, const uint32_t *ht_id, uint32_t *ids,
+                                                        const uint32_t *ctile_first, const HtSlot *ht, uint32_t *ids,
                                                         const uint8_t *data, const uint64_t *ent_rec, const uint64_t *data_end_p,
                                                         uint32_t *collision)
 {
@@ -514,7 +513,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, con
         if (r >= T.e) break;
         if (!present_at(col, r)) continue;
         const uint64_t o = C.ids_off + T.rank(col, r);
-        const uint32_t id = ht_id[C.ht_off + ids[o]];
+        const uint32_t id = ht[C.ht_off + ids[o]].id;
         ids[o] = id;
         if (col.phys == 6) {  // verify the hash-keyed dictionary byte-for-byte
             const uint64_t e = ent_rec[C.ent_off + id];
@@ -822,15 +821,15 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
 {
     if (a.ndict_tiles)
         hipLaunchKernelGGL(k_dict_insert, dim3(a.ndict_tiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order,
-                           a.ctile_chunk, a.ctile_first, a.ht_key, a.ht_min, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
+                           a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
     hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
-                       a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0);
+                       a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0);
     seg_tile_scan_u32(a.tile_cnt, a.tile_cnt, a.ctile_chunk, a.nctiles, a.seg, s);
     seg_tile_scan_u64(a.tile_sz, a.tile_sz, a.ctile_chunk, a.nctiles, a.seg, s);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
-                       a.ht_min, a.ht_id, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1);
-    hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht_id, a.ids,
+                       a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1);
+    hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht, a.ids,
                        a.data, a.ent_rec, a.data_end, a.collision);
     // BYTE_ARRAY statistics need the dictionary outcome (entries stand in for the values);
     // multi-page dictionary descriptors have no statistics (their pages do)

@@ -7,6 +7,15 @@
 
 namespace kpw {
 
+// One dictionary hash-table slot: key, first rank and entry id share a 16-byte slot, so a probe
+// (key compare + atomicMin of the rank) and the later id lookups touch one cache line.  An
+// all-0xFF fill is the empty table (key HT_EMPTY, rank UINT32_MAX).
+struct HtSlot {
+    uint64_t key;
+    uint32_t min;
+    uint32_t id;
+};
+
 struct ChunkArgs {
     ChunkDesc *ch;
     int32_t nchunks;
@@ -19,8 +28,7 @@ struct ChunkArgs {
     uint64_t *tile_raw, *tile_raw_off, *tile_smin, *tile_smax;
     uint32_t *tile_cnt;
     uint64_t *tile_sz;
-    uint64_t *ht_key;
-    uint32_t *ht_min, *ht_id;
+    HtSlot *ht;                    // dictionary hash tables (per chunk at ChunkDesc::ht_off)
     uint32_t *ids;
     uint64_t *ent_rec, *ent_boff;
     uint32_t max_dict_bytes;
