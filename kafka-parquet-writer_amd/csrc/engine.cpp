@@ -4,6 +4,7 @@
 // them -> per column chunk: dictionary page (if any) + one data page, compressed.
 // Host syncs per batch: decode error index, row-group plan, page layout, (snappy sizes),
 // chunk metadata — all small; every byte of record/page data stays in HBM.
+#include <chrono>
 #include "engine.h"
 
 #include <algorithm>
@@ -47,11 +48,16 @@ DevBuf::~DevBuf() { dev_free(p); }
 
 Engine::~Engine()
 {
+    const bool tr = getenv("KPW_TRACE") && getenv("KPW_TRACE")[0] == '1' && stream;
+    const auto t0 = std::chrono::steady_clock::now();
     for (auto &e : ev_) if (e) (void)hipEventDestroy(e);
     for (auto &e : kev_) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamSynchronize(stream);
     seg_scratch_free(seg_);
     if (stream) (void)hipStreamDestroy(stream);
+    if (tr)
+        fprintf(stderr, "[kpw] engine free: events+stream %.1f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
 int Engine::fail(int code, const std::string &msg)

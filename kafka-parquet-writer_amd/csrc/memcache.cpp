@@ -24,6 +24,8 @@ std::mutex g_mu;
 Pool g_dev[64];
 Pool g_pin;
 std::map<uintptr_t, size_t> g_pin_live;     // live pinned blocks (pin_contains)
+std::map<void *, int> g_dev_of;             // device of every block dev_alloc handed out
+                                            // (hipPointerGetAttributes per free cost ~0.3 ms)
 
 // best fit within 2x (and never more than 1 GiB of slack)
 void *take(Pool &p, size_t bytes)
@@ -64,27 +66,26 @@ void *dev_alloc(size_t bytes)
     void *q = nullptr;
     if (hipMalloc(&q, bytes) != hipSuccess) {
         (void)hipGetLastError();
-        trim(p, 0, [](void *b) { (void)hipFree(b); });   // give the idle blocks back and retry
+        trim(p, 0, [](void *b) { g_dev_of.erase(b); (void)hipFree(b); });   // give the idle blocks back and retry
         if (hipMalloc(&q, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
     }
     p.size_[q] = bytes;
+    g_dev_of[q] = dev;
     return q;
 }
 
 void dev_free(void *q)
 {
     if (!q) return;
-    hipPointerAttribute_t attr;
-    int dev = 0;
-    if (hipPointerGetAttributes(&attr, q) == hipSuccess) dev = attr.device;
-    else (void)hipGetLastError();
     std::lock_guard<std::mutex> g(g_mu);
-    Pool &p = g_dev[dev & 63];
+    auto d = g_dev_of.find(q);
+    if (d == g_dev_of.end()) { (void)hipFree(q); return; }   // not ours
+    Pool &p = g_dev[d->second];
     auto it = p.size_.find(q);
-    if (it == p.size_.end()) { (void)hipFree(q); return; }   // not ours
+    if (it == p.size_.end()) { (void)hipFree(q); return; }
     p.free_.emplace(it->second, q);
     p.free_bytes += it->second;
-    trim(p, kDevCacheCap, [](void *b) { (void)hipFree(b); });
+    trim(p, kDevCacheCap, [](void *b) { g_dev_of.erase(b); (void)hipFree(b); });
 }
 
 void *pin_alloc(size_t bytes)

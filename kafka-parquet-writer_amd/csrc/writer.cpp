@@ -106,13 +106,16 @@ struct PinnedBuf {
 };
 
 // Growable u64 array without value-initialisation: the bulk path appends 500 k record ends per
-// write and a zero-fill before overwriting them doubled the caller's memory traffic.
+// write and a zero-fill before overwriting them doubled the caller's memory traffic.  Storage
+// comes from the pinned cache (memcache.h): a stage buffer's ends reach ~140 MB, and malloc'd
+// arrays of that size were page-faulted in by every new writer and unmapped by every free
+// (~45 ms per file).
 class U64Vec {
 public:
     U64Vec() = default;
     U64Vec(const U64Vec &) = delete;
     U64Vec &operator=(const U64Vec &) = delete;
-    ~U64Vec() { free(p_); }
+    ~U64Vec() { pin_free(p_); }
     size_t size() const { return n_; }
     bool empty() const { return n_ == 0; }
     void clear() { n_ = 0; }
@@ -126,9 +129,11 @@ public:
     {
         if (n_ + n > cap_) {
             size_t c = std::max<size_t>(cap_ * 2, n_ + n);
-            c = std::max<size_t>(c, 1024);
-            uint64_t *q = (uint64_t *)realloc(p_, c * 8);
+            c = std::max<size_t>(c, 1u << 20);
+            uint64_t *q = (uint64_t *)pin_alloc(c * 8);
             if (!q) throw std::bad_alloc();
+            if (n_) memcpy(q, p_, n_ * 8);
+            pin_free(p_);
             p_ = q;
             cap_ = c;
         }
@@ -928,6 +933,8 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
 
 kpw_writer::~kpw_writer()
 {
+    const double tf0 = trace_on() ? now_ms() : 0.0;
+    double tf[5] = {0, 0, 0, 0, 0};
     {
         std::lock_guard<std::mutex> g(mu);
         stop = true;
@@ -936,11 +943,13 @@ kpw_writer::~kpw_writer()
     for (auto &W : wk)
         if (W.th.joinable()) W.th.join();
     if (assembler.joinable()) assembler.join();
+    if (trace_on()) tf[0] = now_ms();
     (void)hipSetDevice(eng.device);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     if (d2h_stream) (void)hipStreamSynchronize(d2h_stream);
     if (eng.stream) (void)hipStreamSynchronize(eng.stream);
     if (eng1.stream) (void)hipStreamSynchronize(eng1.stream);
+    if (trace_on()) tf[1] = now_ms();
     for (auto &b : buf) {
         dev_free(b.d);
         if (b.copied) (void)hipEventDestroy(b.copied);
@@ -951,9 +960,16 @@ kpw_writer::~kpw_writer()
         for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1]}) if (e) (void)hipEventDestroy(e);
     }
     if (direct_ev) (void)hipEventDestroy(direct_ev);
+    if (trace_on()) tf[2] = now_ms();
     if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (trace_on()) tf[3] = now_ms();
     delete fw;
+    if (trace_on()) {
+        tf[4] = now_ms();
+        fprintf(stderr, "[kpw] free: joins %.1f ms, syncs %.1f ms, buffers+events %.1f ms, streams %.1f ms, file %.1f ms\n",
+                tf[0] - tf0, tf[1] - tf[0], tf[2] - tf[1], tf[3] - tf[2], tf[4] - tf[3]);
+    }
 }
 
 // ---------------------------------------------------------------- C-ABI
@@ -1126,6 +1142,23 @@ static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *of
     return rc;
 }
 
+// e[i] = offsets[i + 1] + delta for i < n, split over a few host threads for large batches
+// (one poll() batch is 500 k records: 4 MB in and out, which one core streams no faster than
+// the batch's own DMA)
+static void rebase_ends(uint64_t *e, const uint64_t *offsets, uint64_t n, uint64_t delta)
+{
+    static const unsigned hw = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 2));
+    const uint64_t kMin = 128 * 1024;
+    const unsigned t = (unsigned)std::min<uint64_t>(hw, n / kMin);
+    auto run = [=](uint64_t a, uint64_t b) { for (uint64_t i = a; i < b; i++) e[i] = offsets[i + 1] + delta; };
+    if (t <= 1) { run(0, n); return; }
+    std::thread th[4];
+    const uint64_t per = (n + t - 1) / t;
+    for (unsigned i = 1; i < t; i++) th[i] = std::thread(run, std::min(n, per * i), std::min(n, per * (i + 1)));
+    run(0, std::min(n, per));
+    for (unsigned i = 1; i < t; i++) th[i].join();
+}
+
 // Bulk write: the whole batch in one copy (direct DMA when the batch is pinned).
 static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n)
 {
@@ -1135,8 +1168,7 @@ static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offset
     const uint64_t delta = F.len - offsets[0];
     if (int st = stage_bytes(w, data + offsets[0], bytes)) return st;
     // the record ends are rebased while the batch's DMA runs
-    uint64_t *e = F.ends.grow(n);
-    for (uint64_t i = 1; i <= n; i++) e[i - 1] = offsets[i] + delta;
+    rebase_ends(F.ends.grow(n), offsets, n, delta);
     w->num_records += (int64_t)n;
     w->dirty = true;
     return wait_direct(w);
