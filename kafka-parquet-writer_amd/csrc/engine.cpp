@@ -582,7 +582,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
     }
     // +512: K7 reads its input through 256-byte register windows that may run past the last page
-    ENS(d_body, body_tot + 512);
+    ENS(d_body, body_tot + 512 + 4096);   // + 4 KiB: the writer D2Hs whole 4 KiB units
     CK(hipMemsetAsync(d_body.p, 0, body_tot + 512, s));
     launch_chunk_write(a, d_jobs.as<RleJob>(), d_body.as<uint8_t>(), s);
     if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), s);
@@ -610,7 +610,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         ENS(d_frag_out, (uint64_t)std::max<uint32_t>(1, nf) * SNAPPY_FRAG_CAP); ENS(d_frag_len, std::max<uint32_t>(1, nf) * 4);
         ENS(d_frag_coff, std::max<uint32_t>(1, nf) * 8); ENS(d_page_coff, 2 * nch * 8); ENS(d_page_clen, 2 * nch * 8);
         ENS(d_page_frag0, 2 * nch * 4);
-        ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * nch * 8 + 64);
+        ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * nch * 8 + 64 + 4096);
         if (nf) {
             CK(hipMemcpyAsync(d_frag_page.p, fpage.data(), nf * 4, hipMemcpyHostToDevice, s));
             CK(hipMemcpyAsync(d_frag_idx.p, fidx.data(), nf * 4, hipMemcpyHostToDevice, s));

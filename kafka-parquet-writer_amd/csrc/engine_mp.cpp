@@ -253,7 +253,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             dch[c].nn = 0; dch[c].dict_bytes = 0; dch[c].dict_n = 0; dch[c].fallback = 0; dch[c].overflow = 0;
         }
     }
-    ENS(d_body, body_tot + 512);
+    ENS(d_body, body_tot + 512 + 4096);   // + 4 KiB: the writer D2Hs whole 4 KiB units
     CK(hipMemsetAsync(d_body.p, 0, body_tot + 512, st));
     launch_mp_dictpage_off(ap.ch, ad.ch, nc, st);
     launch_dict_page(ad, d_body.as<uint8_t>(), st);
@@ -277,7 +277,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         ENS(d_frag_out, (uint64_t)std::max<uint32_t>(1, nf) * SNAPPY_FRAG_CAP); ENS(d_frag_len, std::max<uint32_t>(1, nf) * 4);
         ENS(d_frag_coff, std::max<uint32_t>(1, nf) * 8); ENS(d_page_coff, 2 * npg * 8); ENS(d_page_clen, 2 * npg * 8);
         ENS(d_page_frag0, 2 * npg * 4);
-        ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * npg * 8 + 64);
+        ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * npg * 8 + 64 + 4096);
         if (nf) {
             CK(hipMemcpyAsync(d_frag_page.p, fpage.data(), nf * 4, hipMemcpyHostToDevice, st));
             CK(hipMemcpyAsync(d_frag_idx.p, fidx.data(), nf * 4, hipMemcpyHostToDevice, st));
@@ -438,7 +438,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     std::vector<std::vector<int64_t>> cuts;
     MpRun run;
     auto append = [&](int64_t s, int64_t e) -> int {
-        if (grow_keep(mp_acc, acc_len + pages_len_ + 64, acc_len)) return KPW_ERR_NOMEM;
+        if (grow_keep(mp_acc, acc_len + pages_len_ + 64 + 4096, acc_len)) return KPW_ERR_NOMEM;
         if (pages_len_) CK(hipMemcpyAsync(mp_acc.as<uint8_t>() + acc_len, pages_dev_, pages_len_, hipMemcpyDeviceToDevice, st));
         out.rgs.push_back(RowGroupOut{s, e - s, (int32_t)out.chunks.size()});
         for (int c = 0; c < nc; c++) {

@@ -182,6 +182,8 @@ struct Worker {
     hipEvent_t carry_ev = nullptr;     // recorded after this worker placed a job's carried records
     hipEvent_t enc_done = nullptr;     // recorded after a job's encode (the D2H of its pages waits on it)
     hipEvent_t d2h_ev[2] = {};         // D2H done, per page buffer set of the engine
+    hipStream_t up = nullptr;          // record offsets H2D (a copy-only stream: the DMA engine
+    hipEvent_t up_ev = nullptr;        // serves it; on the engine stream it ran as a blit kernel)
     bool d2h_used[2] = {false, false};
     uint64_t njobs = 0;
     bool busy = false;
@@ -248,7 +250,7 @@ struct kpw_writer {
     BatchOut asm_out;
     int64_t last_rg_end = 0;           // InternalParquetRecordWriter.lastRowGroupEndPos
     int64_t open_buffered = 0;         // open row group's buffered size after the last PLANNED job
-    double t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0;
+    double t_open = 0, t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0;
     double stats[16] = {0};            // kpw_writer_stats (job order; read after drain)
 
     ~kpw_writer();
@@ -542,17 +544,33 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
     if (int st = join_assembly(w)) return st;
     const int slot = w->page_slot;
     w->page_slot ^= 1;
+    // (on the copy-only d2h_stream: the DMA engine serves it; on the engine stream ROCm ran it
+    // as a blit kernel holding CUs for the whole PCIe transfer)
+    if (hipEventRecord(W.enc_done, s) != hipSuccess || hipStreamWaitEvent(w->d2h_stream, W.enc_done, 0) != hipSuccess)
+        return KPW_ERR_DEVICE;
     if (out.pages_len) {
-        if (w->host_pages[slot].ensure(out.pages_len)) return KPW_ERR_NOMEM;
-        if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, out.pages_len, hipMemcpyDeviceToHost, s) != hipSuccess)
+        // a whole number of 4 KiB (the engine's page buffer is padded past its last page): an
+        // unaligned length made ROCm fall back to a blit kernel
+        const uint64_t len = (out.pages_len + 4095) & ~(uint64_t)4095;
+        if (w->host_pages[slot].ensure(len)) return KPW_ERR_NOMEM;
+        if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, len, hipMemcpyDeviceToHost, w->d2h_stream) != hipSuccess)
             return KPW_ERR_DEVICE;
     }
-    if (hipEventRecord(w->fd2h_ev[slot], s) != hipSuccess) return KPW_ERR_DEVICE;
+    if (hipEventRecord(w->fd2h_ev[slot], w->d2h_stream) != hipSuccess) return KPW_ERR_DEVICE;
     if (hipEventSynchronize(w->fd2h_ev[slot]) != hipSuccess) return KPW_ERR_DEVICE;   // the engine reuses its buffers next
     if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
     start_assembly(w, std::move(out), slot);
     // HDFS alignment: the next row group's size limit depends on where this one ends in the file
     if (w->aligned) return join_assembly(w);
+    return KPW_OK;
+}
+
+// Record offsets of a job: H2D on the worker's copy stream, ordered before the encode on `s`.
+static int upload_offsets(Worker &W, size_t bytes, hipStream_t s)
+{
+    if (hipMemcpyAsync(W.d_off.p, W.h_off.p, bytes, hipMemcpyHostToDevice, W.up) != hipSuccess ||
+        hipEventRecord(W.up_ev, W.up) != hipSuccess || hipStreamWaitEvent(s, W.up_ev, 0) != hipSuccess)
+        return KPW_ERR_DEVICE;
     return KPW_OK;
 }
 
@@ -621,7 +639,7 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
     BatchOut out;
     if (n_enc > 0) {
         if (W.d_off.ensure((n_enc + 1) * 8)) return plan_fail(KPW_ERR_NOMEM, "offset staging allocation failed");
-        if (hipMemcpyAsync(W.d_off.p, W.h_off.p, (n_enc + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+        if (upload_offsets(W, (n_enc + 1) * 8, s))
             return plan_fail(KPW_ERR_DEVICE, "H2D of offsets failed");
         // EXACT jobs are encoded non-final: the GPU planner must cut the same single row group
         // the host size model cut (checked below), so every such row group cross-checks the model
@@ -665,10 +683,13 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
     }
     if (j.kind == JOB_PLANNED) w->open_buffered = out.open_buffered;
     w->t_encode += t1 - t0;
-    if (trace_on())
-        fprintf(stderr, "[kpw] job %llu worker %d kind=%d records=%lld (carried %lld) encode %.2f ms\n",
-                (unsigned long long)j.seq, x, j.kind, (long long)n_enc, (long long)ncarry, t1 - t0);
+    const double tq = trace_on() ? now_ms() : 0.0;
     if (int st = append_job(w, W, out, set)) return plan_fail(st, "file assembly failed: " + w->fw->error());
+    if (trace_on())
+        fprintf(stderr, "[kpw] job %llu worker %d kind=%d records=%lld (carried %lld) encode %.2f ms; at %.1f: start, "
+                        "encoded %.1f, turn %.1f, appended %.1f\n",
+                (unsigned long long)j.seq, x, j.kind, (long long)n_enc, (long long)ncarry, t1 - t0, t0 - w->t_open,
+                t1 - w->t_open, tq - w->t_open, now_ms() - w->t_open);
     {
         std::lock_guard<std::mutex> g(w->mu);
         w->asm_seq = j.seq + 1;
@@ -711,7 +732,7 @@ static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
     if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess) return jfail(KPW_ERR_DEVICE, "stream wait failed");
     if (lim > 0) {
         if (W.d_off.ensure((lim + 1) * 8)) return jfail(KPW_ERR_NOMEM, "offset staging allocation failed");
-        if (hipMemcpyAsync(W.d_off.p, W.h_off.p, (lim + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+        if (upload_offsets(W, (lim + 1) * 8, s))
             return jfail(KPW_ERR_DEVICE, "H2D of offsets failed");
     }
     {   // file order (one worker: the previous job is in the file already)
@@ -920,7 +941,9 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
         if (hipEventCreateWithFlags(&W.carry_ev, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&W.enc_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&W.d2h_ev[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&W.d2h_ev[1], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&W.d2h_ev[1], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&W.up_ev, hipEventDisableTiming) != hipSuccess ||
+            hipStreamCreateWithFlags(&W.up, hipStreamNonBlocking) != hipSuccess)
             return KPW_ERR_DEVICE;
     }
     // the open row group of a job lands in the next buffer's gap (its wire bytes are a small
@@ -957,7 +980,8 @@ kpw_writer::~kpw_writer()
     for (auto &e : slot_ev) if (e) (void)hipEventDestroy(e);
     for (auto &e : fd2h_ev) if (e) (void)hipEventDestroy(e);
     for (auto &W : wk) {
-        for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1]}) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1], W.up_ev}) if (e) (void)hipEventDestroy(e);
+        if (W.up) { (void)hipStreamSynchronize(W.up); (void)hipStreamDestroy(W.up); }
     }
     if (direct_ev) (void)hipEventDestroy(direct_ev);
     if (trace_on()) tf[2] = now_ms();
@@ -1005,6 +1029,7 @@ extern "C" kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, con
             delete w;
             return nullptr;
         }
+        w->t_open = now_ms();
         w->created_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
                             std::chrono::system_clock::now().time_since_epoch()).count();
         if (status) *status = KPW_OK;
@@ -1394,6 +1419,7 @@ extern "C" int kpw_writer_close(kpw_writer *w)
 {
     if (!w) return KPW_ERR_INVALID_ARG;
     if (w->closed) return KPW_OK;
+    const double t_close = now_ms();
     try {
         if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
         {
@@ -1408,6 +1434,8 @@ extern "C" int kpw_writer_close(kpw_writer *w)
         int st = w->fw->close();
         if (st) return wfail(w, st, w->fw->error());
         w->closed = true;
+        if (trace_on())
+            fprintf(stderr, "[kpw] close: entered at %.1f, footer done at %.1f ms\n", t_close - w->t_open, now_ms() - w->t_open);
         if (trace_on())
             fprintf(stderr, "[kpw] close: worker encode %.1f ms; caller: pinned DMA waits %.1f ms, buffer acquire %.1f ms; "
                             "worker: page buffer alloc + D2H issue %.1f ms; assembly %.1f ms\n",
