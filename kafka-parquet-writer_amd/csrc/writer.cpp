@@ -182,8 +182,6 @@ struct Worker {
     hipEvent_t carry_ev = nullptr;     // recorded after this worker placed a job's carried records
     hipEvent_t enc_done = nullptr;     // recorded after a job's encode (the D2H of its pages waits on it)
     hipEvent_t d2h_ev[2] = {};         // D2H done, per page buffer set of the engine
-    hipStream_t up = nullptr;          // record offsets H2D (a copy-only stream: the DMA engine
-    hipEvent_t up_ev = nullptr;        // serves it; on the engine stream it ran as a blit kernel)
     bool d2h_used[2] = {false, false};
     uint64_t njobs = 0;
     bool busy = false;
@@ -415,6 +413,7 @@ static void boundaries(const StageBuf &B, std::vector<uint64_t> &hb)
 
 // ---------------------------------------------------------------- workers
 
+
 // A carry that did not fit its buffer's gap waits in carry_store: rebuild the buffer as
 // [carried | appended] on stream `s` (the caller is not appending to it: its job runs, or it
 // drains; the store was filled by the previous job, which `s` already waits for).
@@ -544,19 +543,15 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
     if (int st = join_assembly(w)) return st;
     const int slot = w->page_slot;
     w->page_slot ^= 1;
-    // (on the copy-only d2h_stream: the DMA engine serves it; on the engine stream ROCm ran it
-    // as a blit kernel holding CUs for the whole PCIe transfer)
-    if (hipEventRecord(W.enc_done, s) != hipSuccess || hipStreamWaitEvent(w->d2h_stream, W.enc_done, 0) != hipSuccess)
-        return KPW_ERR_DEVICE;
+    // One DMA on the engine stream.  (Measured alternatives, tests/microbench/copy_ab.sh: the
+    // same copy on a separate D2H stream, or a 32-workgroup copy kernel there, which alone reaches
+    // 54 GB/s, both cost 10-12 % end to end.)
     if (out.pages_len) {
-        // a whole number of 4 KiB (the engine's page buffer is padded past its last page): an
-        // unaligned length made ROCm fall back to a blit kernel
-        const uint64_t len = (out.pages_len + 4095) & ~(uint64_t)4095;
-        if (w->host_pages[slot].ensure(len)) return KPW_ERR_NOMEM;
-        if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, len, hipMemcpyDeviceToHost, w->d2h_stream) != hipSuccess)
+        if (w->host_pages[slot].ensure(out.pages_len)) return KPW_ERR_NOMEM;
+        if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, out.pages_len, hipMemcpyDeviceToHost, s) != hipSuccess)
             return KPW_ERR_DEVICE;
     }
-    if (hipEventRecord(w->fd2h_ev[slot], w->d2h_stream) != hipSuccess) return KPW_ERR_DEVICE;
+    if (hipEventRecord(w->fd2h_ev[slot], s) != hipSuccess) return KPW_ERR_DEVICE;
     if (hipEventSynchronize(w->fd2h_ev[slot]) != hipSuccess) return KPW_ERR_DEVICE;   // the engine reuses its buffers next
     if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
     start_assembly(w, std::move(out), slot);
@@ -565,13 +560,11 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
     return KPW_OK;
 }
 
-// Record offsets of a job: H2D on the worker's copy stream, ordered before the encode on `s`.
+// Record offsets of a job: H2D on the engine stream, before the encode.  (A per-worker copy
+// stream measured 3-5 % slower end to end: tests/microbench/copy_ab.sh.)
 static int upload_offsets(Worker &W, size_t bytes, hipStream_t s)
 {
-    if (hipMemcpyAsync(W.d_off.p, W.h_off.p, bytes, hipMemcpyHostToDevice, W.up) != hipSuccess ||
-        hipEventRecord(W.up_ev, W.up) != hipSuccess || hipStreamWaitEvent(s, W.up_ev, 0) != hipSuccess)
-        return KPW_ERR_DEVICE;
-    return KPW_OK;
+    return hipMemcpyAsync(W.d_off.p, W.h_off.p, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
 }
 
 static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
@@ -941,9 +934,7 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
         if (hipEventCreateWithFlags(&W.carry_ev, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&W.enc_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&W.d2h_ev[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&W.d2h_ev[1], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&W.up_ev, hipEventDisableTiming) != hipSuccess ||
-            hipStreamCreateWithFlags(&W.up, hipStreamNonBlocking) != hipSuccess)
+            hipEventCreateWithFlags(&W.d2h_ev[1], hipEventDisableTiming) != hipSuccess)
             return KPW_ERR_DEVICE;
     }
     // the open row group of a job lands in the next buffer's gap (its wire bytes are a small
@@ -980,8 +971,7 @@ kpw_writer::~kpw_writer()
     for (auto &e : slot_ev) if (e) (void)hipEventDestroy(e);
     for (auto &e : fd2h_ev) if (e) (void)hipEventDestroy(e);
     for (auto &W : wk) {
-        for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1], W.up_ev}) if (e) (void)hipEventDestroy(e);
-        if (W.up) { (void)hipStreamSynchronize(W.up); (void)hipStreamDestroy(W.up); }
+        for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1]}) if (e) (void)hipEventDestroy(e);
     }
     if (direct_ev) (void)hipEventDestroy(direct_ev);
     if (trace_on()) tf[2] = now_ms();
