@@ -157,10 +157,12 @@ __device__ __forceinline__ uint64_t src_bytes_hash(const Src &S, uint64_t off, u
     return mix64(h);
 }
 
-// Parse record r from source S.  Returns false on an invalid record.
+// Parse record r from source S.  Returns false on an invalid record.  `cols` holds every
+// column (LDS copy); *raw accumulates the plain-equivalent bytes of the present values (a
+// repeated field replaces its earlier occurrence: last one wins).
 template <class Src>
 __device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *cols, const int16_t *fmap, const Src &S, uint64_t r,
-                                             uint64_t pos, uint64_t end, uint64_t *seen, uint64_t *bval)
+                                             uint64_t pos, uint64_t end, uint64_t *seen, uint64_t *bval, uint32_t *raw)
 {
 #pragma unroll 1
     while (pos < end) {
@@ -174,12 +176,12 @@ __device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *
         else {
             for (int k = 0; k < a.ncols; k++) if ((uint32_t)a.cols[k].field_number == fno) { c = k; break; }
         }
-        const DevCol *col = nullptr;
-        if (c >= 0) col = c < 64 ? &cols[c] : &a.cols[c];
+        const DevCol *col = c >= 0 ? &cols[c] : nullptr;
         if (c < 0 || (uint32_t)col->wire_type != wt) {
             if (!skip_field(S, pos, end, tag)) return false;
             continue;
         }
+        const bool again = (seen[c >> 6] >> (c & 63)) & 1;
         uint64_t v = 0;
         if (wt == 0) {
             if (!rd_varint64(S, pos, end, v)) return false;
@@ -204,6 +206,8 @@ __device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *
             uint64_t l;
             if (!rd_varint64(S, pos, end, l)) return false;
             if ((int32_t)(uint32_t)l < 0 || end - pos < (uint32_t)l) return false;
+            if (again) *raw -= 4 + col->slen[r];
+            *raw += 4 + (uint32_t)l;
             col->soff[r] = pos;
             col->slen[r] = (uint32_t)l;
             // first 16 bytes, zero padded: exact compares for short strings (stats,
@@ -213,6 +217,7 @@ __device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *
             if (col->dict) col->shash[r] = src_bytes_hash(S, pos, (uint32_t)l);
             pos += (uint32_t)l;
         }
+        if (col->phys != 0 && col->phys != 6 && !again) *raw += (uint32_t)col->vsize;
         if (col->phys == 0) {
             if (v) bval[c >> 6] |= 1ull << (c & 63); else bval[c >> 6] &= ~(1ull << (c & 63));
         } else if (col->vsize == 4) {
@@ -227,17 +232,27 @@ __device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *
 
 // Tile kernel: one block = 256 consecutive records.  When the block's bytes fit K1_LDS bytes
 // they are staged into LDS with coalesced 16-byte loads and every lane parses its record from
-// LDS; wider records (C3-like rows of > 128 bytes) parse straight from global memory.
+// LDS; wider records (C3-like rows of > 96 bytes) parse straight from global memory.  Every
+// column descriptor is copied to LDS (dynamic: ncols * 96 bytes), so a wide schema's fields
+// never wait on a global descriptor load.
 constexpr uint32_t K1_LDS = 24576;
 
 __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
 {
     __shared__ int16_t fmap[FMAP_SIZE];
-    __shared__ DevCol cols[64];   // first 64 columns cached; rest read from global
     __shared__ uint4 stage[K1_LDS / 16 + 2];
+    __shared__ uint64_t reqm[MAX_COLS / 64];     // required (non-optional) columns
+    extern __shared__ DevCol cols[];             // [ncols]
     for (int i = threadIdx.x; i < FMAP_SIZE; i += blockDim.x) fmap[i] = a.fmap[i];
-    const int ncached = a.ncols < 64 ? a.ncols : 64;
-    for (int i = threadIdx.x; i < ncached; i += blockDim.x) cols[i] = a.cols[i];
+    for (int i = threadIdx.x; i < a.ncols; i += blockDim.x) cols[i] = a.cols[i];
+    if (threadIdx.x < MAX_COLS / 64) {
+        uint64_t m = 0;
+        for (int k = 0; k < 64; k++) {
+            const int c = (int)threadIdx.x * 64 + k;
+            if (c < a.ncols && !a.cols[c].optional) m |= 1ull << k;
+        }
+        reqm[threadIdx.x] = m;
+    }
 
     const uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x;
     const uint64_t r = r0 + threadIdx.x;
@@ -273,20 +288,10 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
 
     if (valid) {
         const uint64_t pos = a.off[r], end = a.off[r + 1];
-        if (staged) bad = !parse_record(a, cols, fmap, LSrc{(const uint32_t *)stage, S0}, r, pos, end, seen, bval);
-        else bad = !parse_record(a, cols, fmap, GSrc{a.data, data_end}, r, pos, end, seen, bval);
-        if (!bad) {
-            for (int c = 0; c < a.ncols; c++) {
-                const DevCol *col = c < 64 ? &cols[c] : &a.cols[c];
-                const bool pr = (seen[c >> 6] >> (c & 63)) & 1;
-                if (!pr) {
-                    if (!col->optional) { bad = true; break; }
-                    continue;
-                }
-                if (col->phys == 6) raw += 4 + col->slen[r];
-                else if (col->phys != 0) raw += (uint32_t)col->vsize;
-            }
-        }
+        if (staged) bad = !parse_record(a, cols, fmap, LSrc{(const uint32_t *)stage, S0}, r, pos, end, seen, bval, &raw);
+        else bad = !parse_record(a, cols, fmap, GSrc{a.data, data_end}, r, pos, end, seen, bval, &raw);
+        // a missing required field (isInitialized)
+        for (int k = 0; k < MAX_COLS / 64 && !bad; k++) bad = (seen[k] & reqm[k]) != reqm[k];
         if (bad) atomicMin(a.err_min, (unsigned long long)r);
         a.raw[r] = bad ? 0 : raw;
     }
@@ -296,7 +301,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
     // lane 0 of a wave lying wholly past n must not write (bitmasks hold n/64+2 words)
     const bool lane0 = (threadIdx.x & 63) == 0 && r < a.n;
     for (int c = 0; c < a.ncols; c++) {
-        const DevCol *col = c < 64 ? &cols[c] : &a.cols[c];
+        const DevCol *col = &cols[c];
         const bool pr = valid && !bad && ((seen[c >> 6] >> (c & 63)) & 1);
         if (col->optional) {
             uint64_t m = __ballot(pr);
@@ -313,7 +318,7 @@ void launch_decode(const DecodeArgs &a, hipStream_t s)
 {
     if (a.n == 0) return;
     const uint64_t blocks = (a.n + KPW_BLOCK - 1) / KPW_BLOCK;
-    hipLaunchKernelGGL(k_decode, dim3((unsigned)blocks), dim3(KPW_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(k_decode, dim3((unsigned)blocks), dim3(KPW_BLOCK), (size_t)a.ncols * sizeof(DevCol), s, a);
 }
 
 }  // namespace kpw
