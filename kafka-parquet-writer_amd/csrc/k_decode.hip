@@ -157,13 +157,91 @@ __device__ __forceinline__ uint64_t src_bytes_hash(const Src &S, uint64_t off, u
     return mix64(h);
 }
 
+// One value of column c (tag already consumed, wire type matches): decode, store, account.
+template <class Src>
+__device__ __forceinline__ bool parse_value(const DevCol *col, int c, uint32_t wt, const Src &S, uint64_t &pos, uint64_t end,
+                                            uint64_t r, uint64_t *seen, uint64_t *bval, uint32_t *raw)
+{
+    const bool again = (seen[c >> 6] >> (c & 63)) & 1;
+    uint64_t v = 0;
+    if (wt == 0) {
+        if (!rd_varint64(S, pos, end, v)) return false;
+        switch (col->proto_type) {
+        case 5: case 13: v = (uint32_t)v; break;                                            // int32/uint32
+        case 17: { uint32_t u = (uint32_t)v; v = (uint32_t)((u >> 1) ^ (0u - (u & 1))); break; }  // sint32
+        case 18: v = (v >> 1) ^ (0ull - (v & 1)); break;                                   // sint64
+        case 8: v = v != 0; break;                                                          // bool
+        default: break;
+        }
+    } else if (wt == 1) {
+        if (end - pos < 8) return false;
+        v = S.w64(pos);
+        pos += 8;
+        if (col->phys == 5) v = canon_double(v);
+    } else if (wt == 5) {
+        if (end - pos < 4) return false;
+        v = S.w64(pos) & 0xffffffffull;
+        pos += 4;
+        if (col->phys == 4) v = canon_float((uint32_t)v);
+    } else {  // wt == 2
+        uint64_t l;
+        if (!rd_varint64(S, pos, end, l)) return false;
+        if ((int32_t)(uint32_t)l < 0 || end - pos < (uint32_t)l) return false;
+        if (again) *raw -= 4 + col->slen[r];
+        *raw += 4 + (uint32_t)l;
+        col->soff[r] = pos;
+        col->slen[r] = (uint32_t)l;
+        // first 16 bytes, zero padded: exact compares for short strings (stats,
+        // dictionary verification) without touching the batch bytes again
+        col->spfx[2 * r] = l ? S.w64(pos) & tail_mask(l) : 0ull;
+        col->spfx[2 * r + 1] = l > 8 ? S.w64(pos + 8) & tail_mask(l - 8) : 0ull;
+        if (col->dict) col->shash[r] = src_bytes_hash(S, pos, (uint32_t)l);
+        pos += (uint32_t)l;
+    }
+    if (col->phys != 0 && col->phys != 6 && !again) *raw += (uint32_t)col->vsize;
+    if (col->phys == 0) {
+        if (v) bval[c >> 6] |= 1ull << (c & 63); else bval[c >> 6] &= ~(1ull << (c & 63));
+    } else if (col->vsize == 4) {
+        ((uint32_t *)col->vals)[r] = (uint32_t)v;
+    } else if (col->vsize == 8) {
+        ((uint64_t *)col->vals)[r] = v;
+    }
+    seen[c >> 6] |= 1ull << (c & 63);
+    return true;
+}
+
 // Parse record r from source S.  Returns false on an invalid record.  `cols` holds every
 // column (LDS copy); *raw accumulates the plain-equivalent bytes of the present values (a
 // repeated field replaces its earlier occurrence: last one wins).
+//
+// Lockstep pass first: protobuf-java writes the known fields in field-number order, so the
+// lanes of a wave walk the columns in that order (`order`) together, each taking its record's
+// next field when it is that column's.  The lanes holding column c then store c's values in
+// the same instruction (coalesced per wave; a free-running loop has every lane at a different
+// column after the first null, and every store touches its own cache line).  Whatever the pass
+// leaves (unknown fields, another order, repeats) the general loop parses from there.
 template <class Src>
-__device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *cols, const int16_t *fmap, const Src &S, uint64_t r,
-                                             uint64_t pos, uint64_t end, uint64_t *seen, uint64_t *bval, uint32_t *raw)
+__device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *cols, const int16_t *fmap, const uint8_t *order,
+                                             const Src &S, uint64_t r, uint64_t pos, uint64_t end, uint64_t *seen,
+                                             uint64_t *bval, uint32_t *raw)
 {
+    for (int k = 0; k < a.ncols; k++) {
+        if (pos >= end) break;
+        const int c = order[k];
+        const DevCol *col = &cols[c];
+        const uint64_t w = S.w64(pos);
+        // the expected tag: field number and wire type of column c, as a 1- or 2-byte varint
+        const uint32_t t = ((uint32_t)col->field_number << 3) | (uint32_t)col->wire_type;
+        uint32_t tl;
+        if (t < 0x80) { if ((uint32_t)(w & 0xff) != t) continue; tl = 1; }
+        else if (t < 0x4000) {
+            if ((uint32_t)(w & 0xffff) != ((t & 0x7f) | 0x80 | ((t >> 7) << 8))) continue;
+            tl = 2;
+        } else break;   // longer tags: the general loop
+        if (end - pos < tl) break;
+        pos += tl;
+        if (!parse_value(col, c, (uint32_t)col->wire_type, S, pos, end, r, seen, bval, raw)) return false;
+    }
 #pragma unroll 1
     while (pos < end) {
         uint64_t t64;
@@ -181,51 +259,7 @@ __device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *
             if (!skip_field(S, pos, end, tag)) return false;
             continue;
         }
-        const bool again = (seen[c >> 6] >> (c & 63)) & 1;
-        uint64_t v = 0;
-        if (wt == 0) {
-            if (!rd_varint64(S, pos, end, v)) return false;
-            switch (col->proto_type) {
-            case 5: case 13: v = (uint32_t)v; break;                                            // int32/uint32
-            case 17: { uint32_t u = (uint32_t)v; v = (uint32_t)((u >> 1) ^ (0u - (u & 1))); break; }  // sint32
-            case 18: v = (v >> 1) ^ (0ull - (v & 1)); break;                                   // sint64
-            case 8: v = v != 0; break;                                                          // bool
-            default: break;
-            }
-        } else if (wt == 1) {
-            if (end - pos < 8) return false;
-            v = S.w64(pos);
-            pos += 8;
-            if (col->phys == 5) v = canon_double(v);
-        } else if (wt == 5) {
-            if (end - pos < 4) return false;
-            v = S.w64(pos) & 0xffffffffull;
-            pos += 4;
-            if (col->phys == 4) v = canon_float((uint32_t)v);
-        } else {  // wt == 2
-            uint64_t l;
-            if (!rd_varint64(S, pos, end, l)) return false;
-            if ((int32_t)(uint32_t)l < 0 || end - pos < (uint32_t)l) return false;
-            if (again) *raw -= 4 + col->slen[r];
-            *raw += 4 + (uint32_t)l;
-            col->soff[r] = pos;
-            col->slen[r] = (uint32_t)l;
-            // first 16 bytes, zero padded: exact compares for short strings (stats,
-            // dictionary verification) without touching the batch bytes again
-            col->spfx[2 * r] = l ? S.w64(pos) & tail_mask(l) : 0ull;
-            col->spfx[2 * r + 1] = l > 8 ? S.w64(pos + 8) & tail_mask(l - 8) : 0ull;
-            if (col->dict) col->shash[r] = src_bytes_hash(S, pos, (uint32_t)l);
-            pos += (uint32_t)l;
-        }
-        if (col->phys != 0 && col->phys != 6 && !again) *raw += (uint32_t)col->vsize;
-        if (col->phys == 0) {
-            if (v) bval[c >> 6] |= 1ull << (c & 63); else bval[c >> 6] &= ~(1ull << (c & 63));
-        } else if (col->vsize == 4) {
-            ((uint32_t *)col->vals)[r] = (uint32_t)v;
-        } else if (col->vsize == 8) {
-            ((uint64_t *)col->vals)[r] = v;
-        }
-        seen[c >> 6] |= 1ull << (c & 63);
+        if (!parse_value(col, c, wt, S, pos, end, r, seen, bval, raw)) return false;
     }
     return true;
 }
@@ -242,9 +276,16 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
     __shared__ int16_t fmap[FMAP_SIZE];
     __shared__ uint4 stage[K1_LDS / 16 + 2];
     __shared__ uint64_t reqm[MAX_COLS / 64];     // required (non-optional) columns
+    __shared__ uint8_t order[MAX_COLS];          // columns by field number (the wire order)
     extern __shared__ DevCol cols[];             // [ncols]
     for (int i = threadIdx.x; i < FMAP_SIZE; i += blockDim.x) fmap[i] = a.fmap[i];
-    for (int i = threadIdx.x; i < a.ncols; i += blockDim.x) cols[i] = a.cols[i];
+    for (int i = threadIdx.x; i < a.ncols; i += blockDim.x) {
+        cols[i] = a.cols[i];
+        const int f = a.cols[i].field_number;
+        int rank = 0;   // field numbers are distinct
+        for (int k = 0; k < a.ncols; k++) rank += a.cols[k].field_number < f;
+        order[rank] = (uint8_t)i;
+    }
     if (threadIdx.x < MAX_COLS / 64) {
         uint64_t m = 0;
         for (int k = 0; k < 64; k++) {
@@ -288,8 +329,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
 
     if (valid) {
         const uint64_t pos = a.off[r], end = a.off[r + 1];
-        if (staged) bad = !parse_record(a, cols, fmap, LSrc{(const uint32_t *)stage, S0}, r, pos, end, seen, bval, &raw);
-        else bad = !parse_record(a, cols, fmap, GSrc{a.data, data_end}, r, pos, end, seen, bval, &raw);
+        if (staged) bad = !parse_record(a, cols, fmap, order, LSrc{(const uint32_t *)stage, S0}, r, pos, end, seen, bval, &raw);
+        else bad = !parse_record(a, cols, fmap, order, GSrc{a.data, data_end}, r, pos, end, seen, bval, &raw);
         // a missing required field (isInitialized)
         for (int k = 0; k < MAX_COLS / 64 && !bad; k++) bad = (seen[k] & reqm[k]) != reqm[k];
         if (bad) atomicMin(a.err_min, (unsigned long long)r);
