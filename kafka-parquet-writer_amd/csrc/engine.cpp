@@ -252,13 +252,11 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             if (ci.dict) { ENS(col_shash[c], n * 8); d.shash = col_shash[c].as<uint64_t>(); }
         }
         if (ci.optional) {
-            ENS(col_pres[c], nwords * 8); ENS(col_pcnt[c], (nwords + 1) * 4);
-            CK(hipMemsetAsync(col_pres[c].p, 0, nwords * 8, s));
+            ENS(col_pres[c], nwords * 8); ENS(col_pcnt[c], (nwords + 1) * 4);   // K1 writes every word
             d.pres = col_pres[c].as<uint64_t>(); d.pcnt = col_pcnt[c].as<uint32_t>();
         }
         if (ci.phys == KPW_BOOLEAN) {
             ENS(col_vbits[c], nwords * 8);
-            CK(hipMemsetAsync(col_vbits[c].p, 0, nwords * 8, s));
             d.vbits = col_vbits[c].as<uint64_t>();
         }
     }
@@ -269,6 +267,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     DecodeArgs da;
     da.data = d_data; da.off = d_off; da.n = n; da.cols = d_cols.as<DevCol>(); da.ncols = nc; da.pad = 0;
     da.fmap = d_fmap.as<int16_t>(); da.raw = d_raw.as<uint32_t>(); da.err_min = d_err.as<unsigned long long>();
+    da.nwords = nwords;
     CK(hipEventRecord(kev_[0], s));
     launch_decode(da, s);
     CK(hipEventRecord(kev_[1], s));

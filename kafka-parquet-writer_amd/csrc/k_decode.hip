@@ -295,6 +295,15 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
         reqm[threadIdx.x] = m;
     }
 
+    if (blockIdx.x == 0) {   // bitmask words past the last record's word (the waves write the rest)
+        const uint64_t w0 = (a.n + 63) / 64;
+        for (uint64_t i = threadIdx.x; i < (uint64_t)a.ncols * (a.nwords - w0); i += blockDim.x) {
+            const DevCol &col = a.cols[i / (a.nwords - w0)];
+            const uint64_t w = w0 + i % (a.nwords - w0);
+            if (col.optional) col.pres[w] = 0;
+            if (col.phys == 0) col.vbits[w] = 0;
+        }
+    }
     const uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x;
     const uint64_t r = r0 + threadIdx.x;
     const bool valid = r < a.n;

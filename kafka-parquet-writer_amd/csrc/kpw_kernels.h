@@ -40,6 +40,7 @@ struct DecodeArgs {
     const int16_t *fmap;   // field number -> column (-1), size FMAP_SIZE
     uint32_t *raw;         // per record: raw (plain-equivalent) bytes of non-boolean present values
     unsigned long long *err_min;
+    uint64_t nwords;       // words of every presence / boolean bitmask (K1 zeroes those past n)
 };
 
 // Device scratch of the multi-block segmented scans (k_scan.hip), owned by one encoder
