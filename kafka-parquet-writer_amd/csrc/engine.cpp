@@ -415,9 +415,14 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             C.ent_off = ids_off;
             ids_off += len;
             if (C.is_dict) {
-                // >= 4x the most entries a dictionary can hold before its 1 MiB fallback
-                // (262145 four-byte entries), so probe chains stay short until fallback
-                C.ht_cap = (uint32_t)std::min<uint64_t>(next_pow2(std::max<uint64_t>(16, 2 * len)), 1u << 20);
+                // >= 2x the most entries the dictionary can hold before its fallback
+                // (dictionaryByteSize > dictPageSize: entries of >= 4 / 8 bytes), so probe
+                // chains stay short until the fallback; a table that fills anyway means more
+                // entries than that, i.e. a fallback (overflow)
+                const uint64_t esz = (cols[c].phys == KPW_INT64 || cols[c].phys == KPW_DOUBLE) ? 8 : 4;
+                const uint64_t maxent = (uint64_t)props.dictionary_page_size / esz + 1;
+                C.ht_cap = (uint32_t)std::min<uint64_t>(next_pow2(std::max<uint64_t>(16, 2 * std::min<uint64_t>(len, maxent))),
+                                                        1u << 20);
                 C.ht_off = ht_off;
                 ht_off += C.ht_cap + 1;
             }
