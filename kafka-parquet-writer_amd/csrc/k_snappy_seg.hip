@@ -44,6 +44,7 @@ constexpr uint32_t SG_MAXR = 64;
 constexpr uint32_t SG_MAXLEN = 512;
 constexpr uint32_t SG_RECS = 16;         // copies per segment (each >= 4 bytes, starting inside it)
 constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the whole workgroup
+constexpr uint32_t SG_PB = 4;            // search probes in flight per parse step
 
 enum : uint32_t { MS = 0, MP = 1, MT = 2 };
 struct PS {
@@ -270,13 +271,44 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
             if (in.ld32(ipe) != in.ld32(c)) { st = PS{MS, ipe + 1, 32, ipe}; continue; }
             base = ipe; lit = false;
         } else {
-            const uint32_t ip = st.ip;
-            const uint32_t next_ip = ip + (st.skip >> 5);
-            if (next_ip > ip_limit) { st = st_T(st.ne); break; }
-            c = S.cand[ip];
-            o.own |= 1ull << (ip - sk);
-            if (in.ld32(ip) != in.ld32(c)) { st.ip = next_ip; st.skip++; continue; }
-            base = ip; lit = true;
+            // SG_PB probes of the search at once: their positions (ip += skip++ >> 5) do not
+            // depend on the data, so the cand -> data load chains of the next SG_PB decisions
+            // overlap; the first probe that matches is the one the sequential loop takes, and
+            // every probe up to it is inserted (the same state as SG_PB sequential steps)
+            uint32_t q[SG_PB], cc[SG_PB], d[SG_PB], e[SG_PB];
+            bool v[SG_PB];
+            uint32_t ipk = st.ip, skk = st.skip;
+            bool alive = true, term = false;
+#pragma unroll
+            for (int k = 0; k < (int)SG_PB; k++) {
+                const bool inseg = ipk < sk1;
+                const uint32_t nx = ipk + (skk >> 5);
+                v[k] = alive && inseg && nx <= ip_limit;
+                term |= alive && inseg && nx > ip_limit;   // the sequential loop stops before probing
+                alive = v[k];
+                q[k] = v[k] ? ipk : st.ip;                 // (an always-valid address when unused)
+                if (v[k]) { ipk = nx; skk++; }
+            }
+#pragma unroll
+            for (int k = 0; k < (int)SG_PB; k++) cc[k] = S.cand[q[k]];
+#pragma unroll
+            for (int k = 0; k < (int)SG_PB; k++) { d[k] = in.ld32(q[k]); e[k] = in.ld32(cc[k]); }
+            int hit = -1;
+#pragma unroll
+            for (int k = (int)SG_PB - 1; k >= 0; k--)
+                if (v[k] && d[k] == e[k]) hit = k;
+#pragma unroll
+            for (int k = 0; k < (int)SG_PB; k++)
+                if (v[k] && (hit < 0 || k <= hit)) o.own |= 1ull << (q[k] - sk);
+            if (hit < 0) {
+                if (term) { st = st_T(st.ne); break; }
+                st.ip = ipk; st.skip = skk;
+                continue;
+            }
+            base = q[0]; c = cc[0];
+#pragma unroll
+            for (int k = 1; k < (int)SG_PB; k++) if (hit == k) { base = q[k]; c = cc[k]; }
+            lit = true;
         }
         const uint32_t len = 4 + sg_fml(in, c + 4, base + 4, n, SG_MAXLEN);
         if (len > SG_MAXLEN) { o.lng = true; break; }
