@@ -114,6 +114,14 @@ struct FIn {
 __device__ __forceinline__ uint32_t sg_fml(const FIn &in, uint32_t s1, uint32_t s2, uint32_t limit, uint32_t cap)
 {
     uint32_t m = 0;
+    while (s2 + m + 16 <= limit) {   // 16 bytes per step: both words' loads in flight together
+        const uint64_t x0 = in.ld64(s1 + m) ^ in.ld64(s2 + m);
+        const uint64_t x1 = in.ld64(s1 + m + 8) ^ in.ld64(s2 + m + 8);
+        if (x0) return m + ((uint32_t)__builtin_ctzll(x0) >> 3);
+        if (x1) return m + 8 + ((uint32_t)__builtin_ctzll(x1) >> 3);
+        m += 16;
+        if (m > cap) return m;
+    }
     while (s2 + m + 8 <= limit) {
         const uint64_t x = in.ld64(s1 + m) ^ in.ld64(s2 + m);
         if (x) return m + ((uint32_t)__builtin_ctzll(x) >> 3);
