@@ -64,6 +64,12 @@ public:
     const uint8_t *memory_data();     // contiguous view (built on first use after close)
     size_t memory_size() const { return mem_len_; }
     const std::string &error() const { return err_; }
+    // Memory mode: while deferring, page bodies of >= 256 KiB are only placed (arena room and
+    // position taken); run_deferred() then copies all of them in one parallel sweep (a job's
+    // bodies are ~64 pieces of a few MB: one memcpy thread per piece left the last job's
+    // assembly on the writer's tail).  The source memory must stay valid until then.
+    void defer_copies(bool on) { defer_ = on && fp_ == nullptr; }
+    void run_deferred();
 
 private:
     int put(const void *p, size_t n);
@@ -83,6 +89,9 @@ private:
     std::vector<RowGroupMeta> rgs_;
     std::string err_;
     bool closed_ = false;
+    bool defer_ = false;
+    struct Piece { uint8_t *dst; const uint8_t *src; size_t n; };
+    std::vector<Piece> deferred_;
 };
 
 }  // namespace kpw
