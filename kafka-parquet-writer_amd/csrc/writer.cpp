@@ -45,6 +45,7 @@
 
 #include "../../include/kpw_gpu.h"
 #include "engine.h"
+#include "kpw_scan.h"
 #include "filewriter.h"
 #include "memcache.h"
 #include "sizemodel.h"
@@ -177,8 +178,11 @@ struct Job {
 // One encode worker: its own engine (HIP stream, scratch, double-buffered page buffers) and thread.
 struct Worker {
     Engine *eng = nullptr;
-    DevBuf d_off;                      // device record offsets of the running job
-    PinnedBuf h_off;                   // host record boundaries of the running job (H2D source)
+    DevBuf d_off;                      // device record offsets of the running job ([0] = 0, then offs)
+    PinnedBuf h_off;                   // host record boundaries of the running job
+    PinnedBuf h_len;                   // u32 record lengths (H2D source: half the bytes of offsets)
+    DevBuf d_len, d_tmp;               // device lengths, prefix-scan scratch
+    const uint64_t *offs = nullptr;    // device record offsets handed to the engine
     hipEvent_t carry_ev = nullptr;     // recorded after this worker placed a job's carried records
     hipEvent_t enc_done = nullptr;     // recorded after a job's encode (the D2H of its pages waits on it)
     hipEvent_t d2h_ev[2] = {};         // D2H done, per page buffer set of the engine
@@ -411,6 +415,21 @@ static void boundaries(const StageBuf &B, std::vector<uint64_t> &hb)
     boundaries(B, hb.data());
 }
 
+// fn(a, b) over [0, n) split over up to 4 host threads (for large n)
+template <class Fn>
+static void par_for(uint64_t n, Fn fn)
+{
+    static const unsigned hw = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 2));
+    const uint64_t kMin = 128 * 1024;
+    const unsigned t = (unsigned)std::min<uint64_t>(hw, n / kMin);
+    if (t <= 1) { fn(0, n); return; }
+    std::thread th[4];
+    const uint64_t per = (n + t - 1) / t;
+    for (unsigned i = 1; i < t; i++) th[i] = std::thread(fn, std::min(n, per * i), std::min(n, per * (i + 1)));
+    fn(0, std::min(n, per));
+    for (unsigned i = 1; i < t; i++) th[i].join();
+}
+
 // ---------------------------------------------------------------- workers
 
 
@@ -565,11 +584,29 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
     return KPW_OK;
 }
 
-// Record offsets of a job: H2D on the engine stream, before the encode.  (A per-worker copy
-// stream measured 3-5 % slower end to end: tests/microbench/copy_ab.sh.)
-static int upload_offsets(Worker &W, size_t bytes, hipStream_t s)
+// Record offsets of a job (`count` boundaries in W.h_off) onto the device, on the engine stream
+// before the encode.  PCIe is the writer's ceiling, so they cross as u32 lengths
+// (lens[0] = the first boundary) and a prefix scan rebuilds the u64 offsets in HBM.  (A per-worker
+// copy stream measured 3-5 % slower end to end: profiles/r02d_copy_paths.md.)
+static int upload_offsets(Worker &W, size_t count, hipStream_t s)
 {
-    return hipMemcpyAsync(W.d_off.p, W.h_off.p, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
+    const uint64_t *hb = (const uint64_t *)W.h_off.p;
+    if (hb[0] >= (1ull << 32)) {   // a carried prefix of >= 4 GiB: plain u64 offsets
+        if (W.d_off.ensure(count * 8)) return KPW_ERR_NOMEM;
+        W.offs = W.d_off.as<uint64_t>();
+        return hipMemcpyAsync(W.d_off.p, hb, count * 8, hipMemcpyHostToDevice, s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
+    }
+    if (W.h_len.ensure(count * 4) || W.d_len.ensure(count * 4) || W.d_off.ensure((count + 1) * 8) ||
+        W.d_tmp.ensure(mj_scan_tmp_words(count, 1) * 8 + 64))
+        return KPW_ERR_NOMEM;
+    uint32_t *len = (uint32_t *)W.h_len.p;
+    len[0] = (uint32_t)hb[0];
+    par_for(count - 1, [=](uint64_t a, uint64_t b) { for (uint64_t i = a; i < b; i++) len[i + 1] = (uint32_t)(hb[i + 1] - hb[i]); });
+    if (hipMemcpyAsync(W.d_len.p, len, count * 4, hipMemcpyHostToDevice, s) != hipSuccess) return KPW_ERR_DEVICE;
+    launch_prefix_raw(W.d_len.as<uint32_t>(), count, W.d_off.as<uint64_t>(), W.d_tmp.as<uint64_t>(), s);
+    if (hipGetLastError() != hipSuccess) return KPW_ERR_DEVICE;
+    W.offs = W.d_off.as<uint64_t>() + 1;   // P[k + 1] = boundary k
+    return KPW_OK;
 }
 
 static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
@@ -636,13 +673,11 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
     };
     BatchOut out;
     if (n_enc > 0) {
-        if (W.d_off.ensure((n_enc + 1) * 8)) return plan_fail(KPW_ERR_NOMEM, "offset staging allocation failed");
-        if (upload_offsets(W, (n_enc + 1) * 8, s))
-            return plan_fail(KPW_ERR_DEVICE, "H2D of offsets failed");
+        if (int st2 = upload_offsets(W, (size_t)n_enc + 1, s)) return plan_fail(st2, "H2D of offsets failed");
         // EXACT jobs are encoded non-final: the GPU planner must cut the same single row group
         // the host size model cut (checked below), so every such row group cross-checks the model
         E.on_plan = on_plan;
-        const int st = E.encode(B.d, W.d_off.as<uint64_t>(), (uint64_t)n_enc, j.kind == JOB_FINAL, E.props.block_size, nullptr, out);
+        const int st = E.encode(B.d, W.offs, (uint64_t)n_enc, j.kind == JOB_FINAL, E.props.block_size, nullptr, out);
         E.on_plan = nullptr;
         if (st) return plan_fail(st, E.error());
     } else {
@@ -729,9 +764,7 @@ static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
     int64_t lim = j.kind == JOB_EXACT ? std::min<int64_t>(j.n_exact, nrec) : nrec;
     if (hipStreamWaitEvent(s, B.copied, 0) != hipSuccess) return jfail(KPW_ERR_DEVICE, "stream wait failed");
     if (lim > 0) {
-        if (W.d_off.ensure((lim + 1) * 8)) return jfail(KPW_ERR_NOMEM, "offset staging allocation failed");
-        if (upload_offsets(W, (lim + 1) * 8, s))
-            return jfail(KPW_ERR_DEVICE, "H2D of offsets failed");
+        if (int st2 = upload_offsets(W, (size_t)lim + 1, s)) return jfail(st2, "H2D of offsets failed");
     }
     {   // file order (one worker: the previous job is in the file already)
         std::unique_lock<std::mutex> lk(w->mu);
@@ -752,7 +785,7 @@ static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
         const double t0 = now_ms();
         BatchOut out;
         E.max_cuts = 1;
-        const int st = E.encode(B.d, W.d_off.as<uint64_t>() + s0, (uint64_t)(lim - s0), j.kind == JOB_FINAL, T, nullptr, out);
+        const int st = E.encode(B.d, W.offs + s0, (uint64_t)(lim - s0), j.kind == JOB_FINAL, T, nullptr, out);
         E.max_cuts = 0;
         if (st) return jfail(st, E.error());
         W.njobs++;   // page buffer sets alternate per encode
@@ -1167,16 +1200,7 @@ static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *of
 // the batch's own DMA)
 static void rebase_ends(uint64_t *e, const uint64_t *offsets, uint64_t n, uint64_t delta)
 {
-    static const unsigned hw = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 2));
-    const uint64_t kMin = 128 * 1024;
-    const unsigned t = (unsigned)std::min<uint64_t>(hw, n / kMin);
-    auto run = [=](uint64_t a, uint64_t b) { for (uint64_t i = a; i < b; i++) e[i] = offsets[i + 1] + delta; };
-    if (t <= 1) { run(0, n); return; }
-    std::thread th[4];
-    const uint64_t per = (n + t - 1) / t;
-    for (unsigned i = 1; i < t; i++) th[i] = std::thread(run, std::min(n, per * i), std::min(n, per * (i + 1)));
-    run(0, std::min(n, per));
-    for (unsigned i = 1; i < t; i++) th[i].join();
+    par_for(n, [=](uint64_t a, uint64_t b) { for (uint64_t i = a; i < b; i++) e[i] = offsets[i + 1] + delta; });
 }
 
 // Bulk write: the whole batch in one copy (direct DMA when the batch is pinned).
