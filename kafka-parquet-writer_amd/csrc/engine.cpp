@@ -130,7 +130,7 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     for (auto &e : ev_) CK(hipEventCreate(&e));
     for (auto &e : kev_) CK(hipEventCreate(&e));
     const size_t nc = cols.size();
-    col_vals.resize(nc); col_shash.resize(nc); col_soff.resize(nc); col_slen.resize(nc); col_pres.resize(nc); col_vbits.resize(nc); col_pcnt.resize(nc);
+    col_vals.resize(nc); col_shash.resize(nc); col_spfx.resize(nc); col_soff.resize(nc); col_slen.resize(nc); col_pres.resize(nc); col_vbits.resize(nc); col_pcnt.resize(nc);
     col_cbits.resize(bool_idx_.size());
     std::vector<int16_t> fmap(FMAP_SIZE, -1);
     for (size_t c = 0; c < nc; c++)
@@ -247,8 +247,8 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         d.field_number = ci.field_number; d.vsize = ci.vsize; d.dict = ci.dict;
         if (ci.vsize) { ENS(col_vals[c], n * ci.vsize); d.vals = col_vals[c].p; }
         if (ci.phys == KPW_BYTE_ARRAY) {
-            ENS(col_soff[c], n * 8); ENS(col_slen[c], n * 4);
-            d.soff = col_soff[c].as<uint64_t>(); d.slen = col_slen[c].as<uint32_t>();
+            ENS(col_soff[c], n * 8); ENS(col_slen[c], n * 4); ENS(col_spfx[c], n * 16);
+            d.soff = col_soff[c].as<uint64_t>(); d.slen = col_slen[c].as<uint32_t>(); d.spfx = col_spfx[c].as<uint64_t>();
             if (ci.dict) { ENS(col_shash[c], n * 8); d.shash = col_shash[c].as<uint64_t>(); }
         }
         if (ci.optional) {

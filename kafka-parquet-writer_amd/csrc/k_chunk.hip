@@ -83,16 +83,24 @@ __device__ __forceinline__ uint64_t order_key(int phys, uint64_t v)
 
 // ------------------------------------------------------------------ K6 stats + sizes
 
-// BYTE_ARRAY compare / equality of records a and b, straight from the batch bytes (8-byte
-// loads).  Unsigned lexicographic order, shorter first on a common prefix (BinaryStatistics).
+// BYTE_ARRAY compare / equality of records a and b through the 16-byte prefix arrays; the
+// batch bytes are read only when both values are longer than 16 bytes with equal prefixes.
+// Unsigned lexicographic order, shorter first on a common prefix (BinaryStatistics).
 __device__ __forceinline__ int str_cmp(const DevCol &col, const uint8_t *data, uint64_t a, uint64_t b, uint64_t data_end)
 {
-    return bytes_cmp(data, col.soff[a], col.slen[a], col.soff[b], col.slen[b], data_end);
+    const uint64_t a0 = col.spfx[2 * a], b0 = col.spfx[2 * b];
+    if (a0 != b0) return __builtin_bswap64(a0) < __builtin_bswap64(b0) ? -1 : 1;
+    const uint64_t a1 = col.spfx[2 * a + 1], b1 = col.spfx[2 * b + 1];
+    if (a1 != b1) return __builtin_bswap64(a1) < __builtin_bswap64(b1) ? -1 : 1;
+    const uint32_t la = col.slen[a], lb = col.slen[b];
+    if (la <= 16 || lb <= 16) return la == lb ? 0 : (la < lb ? -1 : 1);
+    return bytes_cmp(data, col.soff[a] + 16, la - 16, col.soff[b] + 16, lb - 16, data_end);
 }
 __device__ __forceinline__ bool str_eq(const DevCol &col, const uint8_t *data, uint64_t a, uint64_t b, uint64_t data_end)
 {
     const uint32_t la = col.slen[a];
-    return la == col.slen[b] && bytes_cmp(data, col.soff[a], la, col.soff[b], la, data_end) == 0;
+    if (la != col.slen[b] || col.spfx[2 * a] != col.spfx[2 * b] || col.spfx[2 * a + 1] != col.spfx[2 * b + 1]) return false;
+    return la <= 16 || bytes_cmp(data, col.soff[a] + 16, la - 16, col.soff[b] + 16, la - 16, data_end) == 0;
 }
 
 __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,

@@ -191,6 +191,10 @@ __device__ __forceinline__ bool parse_value(const DevCol *col, int c, uint32_t w
         *raw += 4 + (uint32_t)l;
         col->soff[r] = pos;
         col->slen[r] = (uint32_t)l;
+        // first 16 bytes, zero padded: exact compares for short strings (stats,
+        // dictionary verification) without touching the batch bytes again
+        col->spfx[2 * r] = l ? S.w64(pos) & tail_mask(l) : 0ull;
+        col->spfx[2 * r + 1] = l > 8 ? S.w64(pos + 8) & tail_mask(l - 8) : 0ull;
         if (col->dict) col->shash[r] = src_bytes_hash(S, pos, (uint32_t)l);
         pos += (uint32_t)l;
     }

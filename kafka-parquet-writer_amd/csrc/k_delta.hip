@@ -225,28 +225,29 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_delta_dense(const ChunkDesc *ch, 
     }
 }
 
-// common leading bytes of BYTE_ARRAY values a and b (8 bytes per step from the batch)
-__device__ __forceinline__ uint32_t common_prefix(const DevCol &col, const uint8_t *data, uint64_t a, uint64_t b,
-                                                  uint64_t data_end)
+// common leading bytes of BYTE_ARRAY values a and b (the 16-byte prefix words first)
+__device__ __forceinline__ uint32_t common_prefix(const DevCol &col, const uint8_t *data, uint64_t a, uint64_t b)
 {
     const uint32_t la = col.slen[a], lb = col.slen[b];
     const uint32_t m = la < lb ? la : lb;
-    const uint64_t oa = col.soff[a], ob = col.soff[b];
-    for (uint32_t i = 0; i < m; i += 8) {
-        const uint64_t x = (ldu64(data, oa + i, data_end) ^ ldu64(data, ob + i, data_end)) & tail_mask(m - i);
-        if (x) return i + ((uint32_t)__builtin_ctzll(x) >> 3);
+    uint32_t i = 0;
+    for (int w = 0; w < 2 && i < m; w++) {
+        const uint64_t x = col.spfx[2 * a + w] ^ col.spfx[2 * b + w];
+        if (x) { const uint32_t c = i + ((uint32_t)__builtin_ctzll(x) >> 3); return c < m ? c : m; }
+        i += 8;
     }
-    return m;
+    if (i >= m) return m;
+    const uint8_t *pa = data + col.soff[a], *pb = data + col.soff[b];
+    while (i < m && pa[i] == pb[i]) i++;
+    return i;
 }
 
 // DeltaByteArrayWriter.writeBytes for every value of a BYTE_ARRAY fallback chunk: prefix
 // length with the previous value (pre), suffix length (sfx); per chunk tile the suffix bytes
 __global__ void __launch_bounds__(KPW_BLOCK) k_dba_lengths(const ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
                                                           const uint32_t *ctile_chunk, const uint32_t *ctile_first,
-                                                          const uint64_t *dense, uint32_t *pre, uint32_t *sfx, uint64_t *tile_sfx,
-                                                          const uint64_t *data_end_p)
+                                                          const uint64_t *dense, uint32_t *pre, uint32_t *sfx, uint64_t *tile_sfx)
 {
-    const uint64_t data_end = *data_end_p;
     __shared__ uint64_t lds[KPW_BLOCK];
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
@@ -262,7 +263,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dba_lengths(const ChunkDesc *ch, 
             if (r >= (uint64_t)C.e) break;
             if (col.optional && !((col.pres[r >> 6] >> (r & 63)) & 1ull)) continue;
             const uint64_t rank = (col.optional ? rank_of(col, r) : r) - rank0;
-            const uint32_t p = rank ? common_prefix(col, data, dense[C.ids_off + rank - 1], r, data_end) : 0u;
+            const uint32_t p = rank ? common_prefix(col, data, dense[C.ids_off + rank - 1], r) : 0u;
             const uint32_t s = col.slen[r] - p;
             pre[C.ids_off + rank] = p;
             sfx[C.ids_off + rank] = s;
@@ -420,7 +421,7 @@ void launch_v2_dense(const ChunkArgs &a, uint64_t *dense, uint32_t *pre, uint32_
     hipLaunchKernelGGL(k_delta_dense, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, (const ChunkDesc *)a.ch, a.cols, a.ctile_chunk,
                        a.ctile_first, dense);
     hipLaunchKernelGGL(k_dba_lengths, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, (const ChunkDesc *)a.ch, a.cols, a.data,
-                       a.ctile_chunk, a.ctile_first, (const uint64_t *)dense, pre, sfx, tile_sfx, a.data_end);
+                       a.ctile_chunk, a.ctile_first, (const uint64_t *)dense, pre, sfx, tile_sfx);
     seg_tile_scan<uint64_t, OpSum64>(tile_sfx, tile_sfx_off, a.ctile_chunk, a.nctiles, chunk_sfx, a.seg, s);
 }
 

@@ -27,6 +27,7 @@ struct DevCol {
     uint64_t *vbits;       // BOOLEAN: value bits [nwords]
     uint32_t *pcnt;        // optional: exclusive prefix popcount of pres per word [nwords+1]
     uint64_t *shash;       // BYTE_ARRAY: 64-bit hash of the value bytes (dictionary key)
+    uint64_t *spfx;        // BYTE_ARRAY: first 16 value bytes, zero padded (2 words per record)
 };
 
 struct DecodeArgs {
