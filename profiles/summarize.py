@@ -66,14 +66,20 @@ def main(tag, workload):
                  "--steps 2 --warmup 1; every pass also runs the resident-encode leg).  FETCH is raw except for "
                  "the 16 B/lane streaming kernels %s (x2, MI355X_MICROARCH.md HBM section).\n\n"
                  % (tag, workload, sorted(STREAMING_16B)))
-        fo.write("| kernel | calls | total ms | avg ms | % | FETCH GB/launch | WRITE GB/launch |\n")
-        fo.write("|---|---|---|---|---|---|---|\n")
+        fo.write("Counter GB/s = (FETCH + WRITE bytes per launch) / average launch time, i.e. the HBM traffic a "
+                 "kernel actually moves, against the 8.0 TB/s HBM peak (MI355X_MICROARCH.md); the algorithmic "
+                 "roofline of the dominant kernel (K7) is in the bench line's `roofline` object.\n\n")
+        fo.write("| kernel | calls | total ms | avg ms | % | FETCH GB/launch | WRITE GB/launch | counter GB/s | of 8 TB/s |\n")
+        fo.write("|---|---|---|---|---|---|---|---|---|\n")
         for r in rows[:40]:
             k = short(r["Name"])
             t = traffic.get(k, {})
-            fo.write("| `%s` | %s | %.3f | %.3f | %s | %s | %s |\n" % (
-                k, r["Calls"], float(r["TotalDurationNs"]) / 1e6, float(r["AverageNs"]) / 1e6, r["Percentage"][:5],
-                "%.3f" % (t["fetch_bytes"] / 1e9) if t else "-", "%.3f" % (t["write_bytes"] / 1e9) if t else "-"))
+            avg_ms = float(r["AverageNs"]) / 1e6
+            rate = (t["traffic_bytes"] / (avg_ms * 1e-3) / 1e9) if t and avg_ms > 0 else None
+            fo.write("| `%s` | %s | %.3f | %.3f | %s | %s | %s | %s | %s |\n" % (
+                k, r["Calls"], float(r["TotalDurationNs"]) / 1e6, avg_ms, r["Percentage"][:5],
+                "%.3f" % (t["fetch_bytes"] / 1e9) if t else "-", "%.3f" % (t["write_bytes"] / 1e9) if t else "-",
+                "%.0f" % rate if rate is not None else "-", "%.1f %%" % (rate / 80.0) if rate is not None else "-"))
         if bench:
             fo.write("\nBench line of the trace pass (profiler attached):\n\n```\n%s\n```\n" % bench)
     print("wrote profiles/%s_{kernel_stats.csv,pmc_traffic.json,summary.md}" % name)
