@@ -386,7 +386,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     out.open_buffered = po[2];
     for (int r = 0; r < nrg; r++) out.rgs.push_back(RowGroupOut{rs[r], re[r] - rs[r], r * nc});
     if (on_plan) on_plan(out);
-    if (nrg == 0) {
+    if (nrg == 0 || plan_only) {   // plan_only: cuts + open buffered size, no pages (out.rgs carry no chunks)
         for (int i = 3; i < 8; i++) CK(hipEventRecord(ev_[i], s));
         CK(hipStreamSynchronize(s));
         return KPW_OK;

@@ -79,6 +79,9 @@ public:
     // encode after any reader of the buffers it now gets back (two encodes ago).
     void swap_page_buffers() { d_body.swap(d_body_alt); d_comp.swap(d_comp_alt); }
     bool multi_page() const { return mp_; }   // pages accumulate in one buffer (no alternation)
+    // Single-page regime only: encode() stops after the row-group planner (records_consumed,
+    // open_buffered and the cut positions; no chunks, pages or statistics)
+    bool plan_only = false;
     // Called once per successful encode as soon as the row-group cuts are known (records_consumed,
     // open_records, invalid_record set; pages not yet), on the encoding thread; work it queues on
     // `stream` runs before the rest of the encode.  The writer places the next job's carried

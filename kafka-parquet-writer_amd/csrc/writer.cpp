@@ -1306,7 +1306,22 @@ static int write_until_full_bulk(kpw_writer *w, const uint8_t *data, const uint6
         }
     }
     BatchOut tmp;
-    auto ds = [&](uint64_t j, int64_t &v) { return ds_prefix(w, base + j, v, tmp); };
+    // getDataSize() after record j of this batch, j inside the segment that follows `seg_end`
+    // (the file position after the row groups cut before it): the cuts before j are causal, so
+    // they are the ones already known and only the open row group's buffered size is new; a
+    // plan-only encode of the prefix (K1 + planner, no dictionary / RLE / pages / Snappy) gives
+    // it.  (Each probe used to encode the whole staged prefix in full.)
+    int64_t seg_end = w->last_rg_end;
+    auto ds = [&](uint64_t j, int64_t &v) {
+        tmp = BatchOut();
+        StageBuf &G = w->buf[w->fill];
+        w->eng.plan_only = true;
+        const int st = w->eng.encode(G.d, w->probe_off.as<uint64_t>(), base + j, false, w->eng.props.block_size, nullptr, tmp);
+        w->eng.plan_only = false;
+        if (st) return wfail(w, st, w->eng.error());
+        v = seg_end + tmp.open_buffered;
+        return (int)KPW_OK;
+    };
     auto bisect = [&](uint64_t lo, uint64_t hi, uint64_t &res) {   // first j in [lo, hi] with ds(j) >= max
         while (lo < hi) {
             const uint64_t mid = lo + (hi - lo) / 2;
@@ -1331,6 +1346,7 @@ static int write_until_full_bulk(kpw_writer *w, const uint8_t *data, const uint6
         }
         if (end[i] >= max_file_size) { found = (uint64_t)b; break; }
         a = (uint64_t)b;
+        seg_end = end[i];
     }
     if (!found && valid >= a + 1 && ds_end >= max_file_size)
         if (int st = bisect(a + 1, valid, found)) return st;

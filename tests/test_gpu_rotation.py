@@ -201,3 +201,13 @@ def test_pinned_source_bulk():
     pf.close()
     want = oracle.encode_file(synth.REC8, data, offs, oracle.make_props(block_size=2 * MiB, codec=1))
     assert pf.file_bytes() == want, pqwalk.first_difference(pf.file_bytes(), want)
+
+
+@pytest.mark.parametrize("codec", [0, 1], ids=["uncompressed", "snappy"])
+def test_rotation_bulk_path(codec):
+    """write_until_full with poll()-sized batches of > 65536 records (the GPU-planned bulk path:
+    one full encode per call, plan-only probes inside the crossing row group) against the
+    oracle's record-at-a-time loop: same records per file, byte-identical files."""
+    data, offs = synth.generate(synth.KIND_REC8, 45, 330000)
+    files = _rotate(synth.REC8, data, offs, 3 * MiB, 256 * 1024, codec, chunk=100000, max_files=6)
+    assert sum(1 for _, f in files if f) >= 2
