@@ -26,11 +26,26 @@ namespace kpw {
 // Byte sources: the block's record bytes staged in LDS (GSrc for blocks whose bytes do not
 // fit).  Positions are absolute offsets into the batch; 8-byte reads may run past the record
 // (callers mask), never past the staged range + 16 or the batch end.
+// GSrc keeps a 16-byte window of the lane's record in registers (8-aligned): consecutive reads
+// of a record's fields mostly fall inside it, so a wide row (C3: ~200 fields of a few bytes)
+// takes about half the dependent global loads of an 8-byte load per read.
 struct GSrc {
     const uint8_t *d;
     uint64_t end;   // batch end
+    uint64_t wpos = ~0ull, lo = 0, hi = 0;
     __device__ __forceinline__ uint8_t b(uint64_t p) const { return d[p]; }
-    __device__ __forceinline__ uint64_t w64(uint64_t p) const { return ldu64(d, p, end); }
+    __device__ __forceinline__ uint64_t w64(uint64_t p)
+    {
+        if (p < wpos || p - wpos > 8) {
+            const uint64_t a = p & ~7ull;
+            if (a + 16 > end) return ldu64(d, p, end);   // the batch's last bytes: bounded loads
+            lo = *(const uint64_t *)(d + a);
+            hi = *(const uint64_t *)(d + a + 8);
+            wpos = a;
+        }
+        const uint32_t sh = (uint32_t)(p - wpos) * 8;
+        return sh == 0 ? lo : sh == 64 ? hi : ((lo >> sh) | (hi << (64 - sh)));
+    }
 };
 struct LSrc {
     const uint32_t *w;   // LDS words holding bytes [base, ...)
@@ -51,7 +66,7 @@ struct LSrc {
 // protobuf varint: 8 bytes at once (one load, the stop byte found with ctz), byte loop only for
 // 9- and 10-byte varints
 template <class Src>
-__device__ __forceinline__ bool rd_varint64(const Src &S, uint64_t &pos, uint64_t end, uint64_t &out)
+__device__ __forceinline__ bool rd_varint64(Src &S, uint64_t &pos, uint64_t end, uint64_t &out)
 {
     if (pos >= end) return false;
     const uint64_t w = S.w64(pos);
@@ -80,7 +95,7 @@ __device__ __forceinline__ bool rd_varint64(const Src &S, uint64_t &pos, uint64_
 // Skip one unknown field whose tag has already been read. Groups are skipped
 // iteratively with a bounded stack (protobuf-java recursion limit 100).
 template <class Src>
-__device__ bool skip_field(const Src &S, uint64_t &pos, uint64_t end, uint32_t tag)
+__device__ bool skip_field(Src &S, uint64_t &pos, uint64_t end, uint32_t tag)
 {
     uint32_t wt = tag & 7;
     uint64_t v;
@@ -146,7 +161,7 @@ __device__ __forceinline__ uint32_t canon_float(uint32_t b)
 // 64-bit hash of a value's bytes (the dictionary key of BYTE_ARRAY columns; the same function
 // as bytes_hash in kpw_device.h, through a byte source)
 template <class Src>
-__device__ __forceinline__ uint64_t src_bytes_hash(const Src &S, uint64_t off, uint32_t len)
+__device__ __forceinline__ uint64_t src_bytes_hash(Src &S, uint64_t off, uint32_t len)
 {
     uint64_t h = 0x9E3779B97F4A7C15ull ^ len;
     for (uint32_t k = 0; k < len; k += 8) {
@@ -159,7 +174,7 @@ __device__ __forceinline__ uint64_t src_bytes_hash(const Src &S, uint64_t off, u
 
 // One value of column c (tag already consumed, wire type matches): decode, store, account.
 template <class Src>
-__device__ __forceinline__ bool parse_value(const DevCol *col, int c, uint32_t wt, const Src &S, uint64_t &pos, uint64_t end,
+__device__ __forceinline__ bool parse_value(const DevCol *col, int c, uint32_t wt, Src &S, uint64_t &pos, uint64_t end,
                                             uint64_t r, uint64_t *seen, uint64_t *bval, uint32_t *raw)
 {
     const bool again = (seen[c >> 6] >> (c & 63)) & 1;
@@ -222,7 +237,7 @@ __device__ __forceinline__ bool parse_value(const DevCol *col, int c, uint32_t w
 // leaves (unknown fields, another order, repeats) the general loop parses from there.
 template <class Src>
 __device__ __forceinline__ bool parse_record(const DecodeArgs &a, const DevCol *cols, const int16_t *fmap, const uint8_t *order,
-                                             const Src &S, uint64_t r, uint64_t pos, uint64_t end, uint64_t *seen,
+                                             Src &S, uint64_t r, uint64_t pos, uint64_t end, uint64_t *seen,
                                              uint64_t *bval, uint32_t *raw)
 {
     for (int k = 0; k < a.ncols; k++) {
@@ -338,8 +353,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_decode(DecodeArgs a)
 
     if (valid) {
         const uint64_t pos = a.off[r], end = a.off[r + 1];
-        if (staged) bad = !parse_record(a, cols, fmap, order, LSrc{(const uint32_t *)stage, S0}, r, pos, end, seen, bval, &raw);
-        else bad = !parse_record(a, cols, fmap, order, GSrc{a.data, data_end}, r, pos, end, seen, bval, &raw);
+        if (staged) {
+            LSrc src{(const uint32_t *)stage, S0};
+            bad = !parse_record(a, cols, fmap, order, src, r, pos, end, seen, bval, &raw);
+        } else {
+            GSrc src{a.data, data_end};
+            bad = !parse_record(a, cols, fmap, order, src, r, pos, end, seen, bval, &raw);
+        }
         // a missing required field (isInitialized)
         for (int k = 0; k < MAX_COLS / 64 && !bad; k++) bad = (seen[k] & reqm[k]) != reqm[k];
         if (bad) atomicMin(a.err_min, (unsigned long long)r);
