@@ -664,7 +664,6 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
 // after a fragment's last round on gfx950 (a barrier issue in the compiled code, not reproduced
 // with the counters in; tests/microbench/seg_bench.hip SEG_DEBUG=2)
 __global__ void __launch_bounds__(1024) k_snappy_seg(SnappyArgs a) { k_snappy_seg_t<true>(a); }
-__global__ void __launch_bounds__(1024) k_snappy_seg_prof(SnappyArgs a) { k_snappy_seg_t<true>(a); }
 
 size_t snappy_seg_scratch_bytes(uint32_t grid) { return (size_t)grid * SEG_SCRATCH_BYTES; }
 

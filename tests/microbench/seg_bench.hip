@@ -93,7 +93,7 @@ int main(int argc, char **argv)
             CK(hipDeviceSynchronize());
             if (getenv("SEG_DEBUG")[0] == '2') hipLaunchKernelGGL(k_snappy_seg, dim3(cus), dim3(1024), 0, 0, c);
             else if (getenv("SEG_DEBUG")[0] == '3') { c.v_budget = 256; hipLaunchKernelGGL(k_snappy_v, dim3(nf), dim3(64), 0, 0, c); c.v_budget = 0; c.seg_only_marked = 1; hipLaunchKernelGGL(k_snappy_seg, dim3(cus), dim3(1024), 0, 0, c); }
-            else hipLaunchKernelGGL(k_snappy_seg_prof, dim3(cus), dim3(1024), 0, 0, c);
+            else hipLaunchKernelGGL(k_snappy_seg, dim3(cus), dim3(1024), 0, 0, c);
             for (int it = 0; it < 100; it++) {
                 usleep(100000);
                 int busy = 0;
@@ -128,7 +128,7 @@ int main(int argc, char **argv)
                 uint64_t *d_prof; CK(hipMalloc(&d_prof, 128)); CK(hipMemset(d_prof, 0, 128));
                 SnappyArgs c = b; c.seg_prof = d_prof;
                 CK(hipMemset(d_cnt, 0, 4));
-                hipLaunchKernelGGL(k_snappy_seg_prof, dim3(cus), dim3(1024), 0, 0, c);
+                hipLaunchKernelGGL(k_snappy_seg, dim3(cus), dim3(1024), 0, 0, c);
                 CK(hipDeviceSynchronize());
                 uint64_t pr[16]; CK(hipMemcpy(pr, d_prof, 128, hipMemcpyDeviceToHost));
                 const double fr = pr[6] ? (double)pr[6] : 1;
