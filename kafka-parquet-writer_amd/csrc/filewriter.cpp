@@ -291,9 +291,51 @@ void par_copy(uint8_t *dst, const uint8_t *src, size_t n)
     for (auto &x : th) x.join();
 }
 
+int FileWriter::asm_put(const void *p, size_t n, bool dev)
+{
+    if (!n) return KPW_OK;
+    if (asm_segs_.empty() && asm_len_ == 0) asm_start_ = mem_len_;
+    if (dev) {
+        asm_segs_.push_back({asm_len_, (uint64_t)(uintptr_t)p, (uint32_t)n, 1u});
+    } else {
+        asm_segs_.push_back({asm_len_, (uint64_t)asm_blob_.size(), (uint32_t)n, 0u});
+        asm_blob_.append((const char *)p, n);
+    }
+    asm_len_ += n;
+    if (int st = reserve(n)) return st;
+    mem_len_ += n;
+    pos_ += (int64_t)n;
+    return KPW_OK;
+}
+
+int FileWriter::take_asm(std::string &blob, std::vector<AsmSeg> &segs, uint64_t &total,
+                         std::vector<std::pair<uint8_t *, size_t>> &spans)
+{
+    blob.swap(asm_blob_);
+    segs.swap(asm_segs_);
+    total = asm_len_;
+    spans.clear();
+    size_t at = asm_start_, left = asm_len_, base = 0;
+    for (auto &c : chunks_) {
+        if (!left) break;
+        if (at < base + c.second) {
+            const size_t off = at - base, k = std::min(left, c.second - off);
+            spans.push_back({c.first + off, k});
+            at += k;
+            left -= k;
+        }
+        base += c.second;
+    }
+    asm_blob_.clear();
+    asm_segs_.clear();
+    asm_len_ = 0;
+    return left ? KPW_ERR_DEVICE : KPW_OK;
+}
+
 int FileWriter::put(const void *p, size_t n)
 {
     if (!n) return KPW_OK;
+    if (dev_asm_) return asm_put(p, n, false);
     if (fp_) {
         if (fwrite(p, 1, n, fp_) != n) { err_ = "short write"; return KPW_ERR_IO; }
     } else {
@@ -396,7 +438,8 @@ int FileWriter::write_row_group(const BatchOut &b, int rg, const uint8_t *pages,
             comp += pg.compressed_size + (int64_t)hdr.size();
             int st2 = put(hdr.data(), hdr.size());
             if (st2) return st2;
-            st2 = d2h && !fp_ ? put_device(pages + (pg.offset - pages_base), (size_t)pg.compressed_size, d2h)
+            st2 = dev_asm_ ? asm_put(pages + (pg.offset - pages_base), (size_t)pg.compressed_size, true)
+                  : d2h && !fp_ ? put_device(pages + (pg.offset - pages_base), (size_t)pg.compressed_size, d2h)
                               : put(pages + (pg.offset - pages_base), (size_t)pg.compressed_size);
             if (st2) return st2;
         }

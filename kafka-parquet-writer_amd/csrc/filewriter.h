@@ -70,6 +70,15 @@ public:
     // assembly on the writer's tail).  The source memory must stay valid until then.
     void defer_copies(bool on) { defer_ = on && fp_ == nullptr; }
     void run_deferred();
+    // Memory mode, device assembly: while on, write_row_group (with `pages` = the DEVICE page
+    // buffer) only records the job's bytes as segments — header / padding bytes into a host blob,
+    // page bodies as device ranges — and takes their room in the in-memory file; take_asm()
+    // hands them over with the file spans they fill.  The caller gathers them into one device
+    // buffer and DMAs it straight into those spans (no host copy of the page bodies).
+    struct AsmSeg { uint64_t dst; uint64_t src; uint32_t len; uint32_t dev; };   // dst: from the job's first byte
+    void device_assembly(bool on) { dev_asm_ = on && fp_ == nullptr; }
+    int take_asm(std::string &blob, std::vector<AsmSeg> &segs, uint64_t &total,
+                 std::vector<std::pair<uint8_t *, size_t>> &spans);
 
 private:
     int put(const void *p, size_t n);
@@ -90,6 +99,11 @@ private:
     std::string err_;
     bool closed_ = false;
     bool defer_ = false;
+    bool dev_asm_ = false;
+    std::string asm_blob_;
+    std::vector<AsmSeg> asm_segs_;
+    uint64_t asm_start_ = 0, asm_len_ = 0;   // the job's range in the in-memory file
+    int asm_put(const void *p, size_t n, bool dev);
     struct Piece { uint8_t *dst; const uint8_t *src; size_t n; };
     std::vector<Piece> deferred_;
 };

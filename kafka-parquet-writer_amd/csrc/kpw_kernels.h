@@ -226,5 +226,12 @@ void launch_rle_events(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, con
                        uint8_t *ev, uint64_t *gend, uint64_t gend_stride, hipStream_t s);
 
 void launch_plan(const PlanArgs &a, hipStream_t s);
+// k_asm.hip: one job's file bytes gathered in HBM (pieces of <= 64 KiB: dst offset in `out`,
+// src = device address (dev) or offset into the host-built header blob)
+struct AsmPiece {
+    uint64_t dst, src;
+    uint32_t len, dev;
+};
+void launch_asm_gather(const AsmPiece *pc, uint32_t npieces, const uint8_t *blob, uint8_t *out, hipStream_t s);
 
 }  // namespace kpw

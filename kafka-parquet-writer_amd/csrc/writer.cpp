@@ -187,6 +187,8 @@ struct Worker {
     hipEvent_t enc_done = nullptr;     // recorded after a job's encode (the D2H of its pages waits on it)
     hipEvent_t d2h_ev[2] = {};         // D2H done, per page buffer set of the engine
     bool d2h_used[2] = {false, false};
+    PinnedBuf h_asm;                   // device assembly: header blob + pieces (H2D source)
+    DevBuf d_asm_in, d_asm_out;        // device assembly: blob + pieces, the job's file bytes
     uint64_t njobs = 0;
     bool busy = false;
     std::thread th;
@@ -561,10 +563,49 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
         if (trace_on()) w->t_asm += now_ms() - ta;
         return KPW_OK;
     }
-    // pages -> pinned host buffer in one D2H (double-buffered against the previous job's
-    // assembly), headers + bodies written on the assembly thread (file: fwrite; in-memory file:
-    // parallel host copies into the pinned arena)
     if (int st = join_assembly(w)) return st;
+    if (w->fw->memory_mode()) {
+        // in-memory file: headers on the host, the job's bytes gathered in HBM (k_asm.hip) and
+        // DMA'd straight into the file's pinned chunks; no host thread touches the page bodies
+        w->fw->device_assembly(true);
+        int st = KPW_OK;
+        for (size_t r = 0; r < out.rgs.size() && !st; r++) st = w->fw->write_row_group(out, (int)r, out.d_pages, 0);
+        w->fw->device_assembly(false);
+        std::string blob;
+        std::vector<FileWriter::AsmSeg> segs;
+        std::vector<std::pair<uint8_t *, size_t>> spans;
+        uint64_t total = 0;
+        const int st2 = w->fw->take_asm(blob, segs, total, spans);
+        if (st) return st;
+        if (st2) return st2;
+        std::vector<AsmPiece> pcs;
+        pcs.reserve(segs.size() + total / 65536 + 1);
+        for (const auto &g : segs)
+            for (uint32_t o = 0; o < g.len; o += 65536)
+                pcs.push_back({g.dst + o, g.src + o, std::min<uint32_t>(65536u, g.len - o), g.dev});
+        const size_t bb = (blob.size() + 15) & ~(size_t)15, pb = pcs.size() * sizeof(AsmPiece);
+        if (W.h_asm.ensure(bb + pb) || W.d_asm_in.ensure(bb + pb + 16) || W.d_asm_out.ensure(total + 64)) return KPW_ERR_NOMEM;
+        memcpy(W.h_asm.p, blob.data(), blob.size());
+        memcpy(W.h_asm.p + bb, pcs.data(), pb);
+        if (hipMemcpyAsync(W.d_asm_in.p, W.h_asm.p, bb + pb, hipMemcpyHostToDevice, s) != hipSuccess) return KPW_ERR_DEVICE;
+        launch_asm_gather((const AsmPiece *)(W.d_asm_in.as<uint8_t>() + bb), (uint32_t)pcs.size(), W.d_asm_in.as<uint8_t>(),
+                          W.d_asm_out.as<uint8_t>(), s);
+        if (hipGetLastError() != hipSuccess) return KPW_ERR_DEVICE;
+        uint64_t at = 0;
+        for (const auto &sp : spans) {
+            if (hipMemcpyAsync(sp.first, W.d_asm_out.as<uint8_t>() + at, sp.second, hipMemcpyDeviceToHost, s) != hipSuccess)
+                return KPW_ERR_DEVICE;
+            at += sp.second;
+        }
+        const int slot = w->page_slot;
+        if (hipEventRecord(w->fd2h_ev[slot], s) != hipSuccess) return KPW_ERR_DEVICE;
+        if (hipEventSynchronize(w->fd2h_ev[slot]) != hipSuccess) return KPW_ERR_DEVICE;   // page buffers are reused next
+        w->last_rg_end = w->fw->pos();
+        if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
+        return KPW_OK;
+    }
+    // file mode: pages -> pinned host buffer in one D2H (double-buffered against the previous
+    // job's assembly), headers + bodies written by fwrite on the assembly thread
     const int slot = w->page_slot;
     w->page_slot ^= 1;
     // One DMA on the engine stream.  (Measured alternatives, tests/microbench/copy_ab.sh: the
