@@ -248,32 +248,6 @@ int FileWriter::put_device(const uint8_t *d, size_t n, hipStream_t s)
     return KPW_OK;
 }
 
-void FileWriter::run_deferred()
-{
-    if (deferred_.empty()) return;
-    size_t total = 0;
-    for (auto &q : deferred_) total += q.n;
-    static const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const unsigned t = (unsigned)std::max<size_t>(1, std::min<size_t>(hw, total / (4ull << 20)));
-    // thread i copies bytes [i*per, (i+1)*per) of the concatenated pieces
-    const size_t per = (total + t - 1) / t;
-    auto work = [this, per](unsigned i) {
-        size_t at = 0;
-        const size_t lo = per * i, hi = per * (i + 1);
-        for (auto &q : deferred_) {
-            const size_t a = std::max(lo, at), b = std::min(hi, at + q.n);
-            if (a < b) memcpy(q.dst + (a - at), q.src + (a - at), b - a);
-            at += q.n;
-            if (at >= hi) break;
-        }
-    };
-    std::vector<std::thread> th;
-    for (unsigned i = 1; i < t; i++) th.emplace_back(work, i);
-    work(0);
-    for (auto &x : th) x.join();
-    deferred_.clear();
-}
-
 void par_copy(uint8_t *dst, const uint8_t *src, size_t n)
 {
     static const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
@@ -342,12 +316,10 @@ int FileWriter::put(const void *p, size_t n)
         if (int st = reserve(n)) return st;
         const uint8_t *src = (const uint8_t *)p;
         size_t base = 0, left = n;
-        const bool later = defer_ && n >= (256u << 10);
         for (auto &c : chunks_) {
             if (mem_len_ < base + c.second) {
                 const size_t off = mem_len_ - base, k = std::min(left, c.second - off);
-                if (later) deferred_.push_back({c.first + off, src, k});
-                else par_copy(c.first + off, src, k);
+                par_copy(c.first + off, src, k);
                 src += k;
                 left -= k;
                 mem_len_ += k;

@@ -64,12 +64,6 @@ public:
     const uint8_t *memory_data();     // contiguous view (built on first use after close)
     size_t memory_size() const { return mem_len_; }
     const std::string &error() const { return err_; }
-    // Memory mode: while deferring, page bodies of >= 256 KiB are only placed (arena room and
-    // position taken); run_deferred() then copies all of them in one parallel sweep (a job's
-    // bodies are ~64 pieces of a few MB: one memcpy thread per piece left the last job's
-    // assembly on the writer's tail).  The source memory must stay valid until then.
-    void defer_copies(bool on) { defer_ = on && fp_ == nullptr; }
-    void run_deferred();
     // Memory mode, device assembly: while on, write_row_group (with `pages` = the DEVICE page
     // buffer) only records the job's bytes as segments — header / padding bytes into a host blob,
     // page bodies as device ranges — and takes their room in the in-memory file; take_asm()
@@ -98,14 +92,11 @@ private:
     std::vector<RowGroupMeta> rgs_;
     std::string err_;
     bool closed_ = false;
-    bool defer_ = false;
     bool dev_asm_ = false;
     std::string asm_blob_;
     std::vector<AsmSeg> asm_segs_;
     uint64_t asm_start_ = 0, asm_len_ = 0;   // the job's range in the in-memory file
     int asm_put(const void *p, size_t n, bool dev);
-    struct Piece { uint8_t *dst; const uint8_t *src; size_t n; };
-    std::vector<Piece> deferred_;
 };
 
 }  // namespace kpw

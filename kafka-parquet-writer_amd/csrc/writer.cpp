@@ -487,8 +487,8 @@ static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, s
     return KPW_OK;
 }
 
-// File mode: headers + bodies + metadata of one job on the assembly thread (overlaps the next
-// job's encode).
+// File mode: headers + bodies + metadata of one job on the assembly thread (fwrite; overlaps
+// the next job's encode).  In-memory files are assembled in HBM instead (append_job).
 static void start_assembly(kpw_writer *w, BatchOut &&out, int slot)
 {
     w->asm_out = std::move(out);
@@ -502,19 +502,14 @@ static void start_assembly(kpw_writer *w, BatchOut &&out, int slot)
                 return;
             }
             const double ta = trace_on() ? now_ms() : 0.0;
-            w->fw->defer_copies(true);   // headers now, the job's page bodies in one parallel sweep
             for (size_t r = 0; r < w->asm_out.rgs.size(); r++) {
                 const int st = w->fw->write_row_group(w->asm_out, (int)r, w->host_pages[slot].p, 0);
                 if (st) {
-                    w->fw->run_deferred();
-                    w->fw->defer_copies(false);
                     w->asm_st = st;
                     w->asm_err = w->fw->error();
                     return;
                 }
             }
-            w->fw->run_deferred();
-            w->fw->defer_copies(false);
             w->last_rg_end = w->fw->pos();
             if (trace_on()) w->t_asm += now_ms() - ta;
         } catch (const std::bad_alloc &) {

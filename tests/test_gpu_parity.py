@@ -327,3 +327,24 @@ def test_writer_hdfs_alignment_multipage(codec):
     import pqwalk
     assert fb == ob, pqwalk.first_difference(fb, ob)
     assert len(pqwalk.footer(fb)[4]) >= 4
+
+
+@pytest.mark.parametrize("n,batches", [(20000, 3), (300000, 2)], ids=["model", "bulk"])
+def test_writer_local_file_identical(tmp_path, n, batches):
+    """File mode (a path instead of an in-memory file: pages D2H to pinned staging, fwrite on the
+    assembly thread) writes the same bytes as the oracle."""
+    import kpw
+    schema = synth.REC8
+    data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE07, n)
+    props = kpw.ParquetProperties(block_size=256 * 1024, compression_codec_name=1)
+    path = str(tmp_path / "part-0.parquet")
+    pf = kpw.ParquetFile(path, kpw.Schema(schema.message_name, schema.columns, schema.proto_class), props)
+    step = (n + batches - 1) // batches
+    for i in range(0, n, step):
+        j = min(n, i + step)
+        pf.write_batch((data[int(offs[i]):int(offs[j])], offs[i:j + 1] - offs[i]))
+    pf.close()
+    fb = open(path, "rb").read()
+    ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=256 * 1024, codec=1))
+    import pqwalk
+    assert fb == ob, pqwalk.first_difference(fb, ob)
