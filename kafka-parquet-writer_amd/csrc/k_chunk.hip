@@ -263,7 +263,8 @@ constexpr uint64_t HT_EMPTY = ~0ull;
 __device__ __forceinline__ int64_t global_insert(ChunkDesc &C, HtSlot *tab, uint32_t cap, uint64_t key,
                                                  uint64_t h, uint32_t rank, uint32_t esize, uint32_t max_dict_bytes,
                                                  bool is_bin, const DevCol &col, const uint8_t *data, uint64_t r,
-                                                 uint64_t data_end)
+                                                 uint64_t data_end, uint32_t *acc_n = nullptr,
+                                                 unsigned long long *acc_b = nullptr)
 {
     if (!is_bin && key == HT_EMPTY) {
         const uint32_t slot = cap;  // reserved slot for the sentinel value
@@ -281,9 +282,14 @@ __device__ __forceinline__ int64_t global_insert(ChunkDesc &C, HtSlot *tab, uint
         if (cur == HT_EMPTY) {
             const unsigned long long old = atomicCAS((unsigned long long *)&tab[i].key, (unsigned long long)HT_EMPTY, (unsigned long long)key);
             if (old == HT_EMPTY) {
-                const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
-                atomicAdd(&C.dict_n, 1u);
-                if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (acc_n) {   // block-local totals, added to the chunk once per tile
+                    atomicAdd(acc_n, 1u);
+                    atomicAdd(acc_b, (unsigned long long)esize);
+                } else {
+                    const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, (unsigned long long)esize) + esize;
+                    atomicAdd(&C.dict_n, 1u);
+                    if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 atomicMin(&tab[i].min, rank);
                 return i;
             }
@@ -315,6 +321,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     __shared__ uint32_t lmin[LDS_T];
     __shared__ uint32_t lslot[LDS_T];
     __shared__ uint64_t lrec[LDS_T];
+    __shared__ uint32_t acc_n;
+    __shared__ unsigned long long acc_b;
     const uint64_t data_end = *data_end_p;
     const uint32_t t = order[blockIdx.x];
     const uint32_t ci = ctile_chunk[t];
@@ -334,6 +342,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     // (then the LDS stage is skipped: every value goes straight to the global table).
     const bool is_bin = col.phys == 6 && exact;
     for (uint32_t i = threadIdx.x; i < LDS_T; i += KPW_BLOCK) { lkey[i] = HT_EMPTY; lmin[i] = 0xffffffffu; }
+    if (threadIdx.x == 0) { acc_n = 0; acc_b = 0; }
     __syncthreads();
     int32_t li[8];
     uint64_t keyv[8];
@@ -377,7 +386,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
         const uint64_t r = lrec[i];
         const uint32_t esize = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize;
         const int64_t g = global_insert(C, tab, cap, key, mix64(key), lmin[i], esize, max_dict_bytes, false, col, data, r,
-                                        data_end);
+                                        data_end, &acc_n, &acc_b);
         lslot[i] = g < 0 ? 0xffffffffu : (uint32_t)g;
         if (g < 0 && !__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
             atomicOr(&C.overflow, 1u);
@@ -385,6 +394,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
         }
     }
     __syncthreads();
+    // the tile's new entries: two chunk-wide atomics per tile instead of two per entry (a
+    // high-cardinality tile would otherwise serialise 4096 atomics on one address)
+    if (threadIdx.x == 0 && acc_n) {
+        const unsigned long long nb = atomicAdd((unsigned long long *)&C.dict_bytes, acc_b) + acc_b;
+        atomicAdd(&C.dict_n, acc_n);
+        if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // phase 3: slots for every value (LDS hit or direct global insert)
     for (int k = 0; k < 8; k++) {
         if (li[k] == -2) continue;
