@@ -318,9 +318,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
                                                            int exact, const uint64_t *data_end_p)
 {
     __shared__ uint64_t lkey[LDS_T];
-    __shared__ uint32_t lmin[LDS_T];
-    __shared__ uint32_t lslot[LDS_T];
-    __shared__ uint64_t lrec[LDS_T];
+    __shared__ uint32_t lmin[LDS_T];   // phase 1: first rank per key; phase 2 on: its global slot
+    __shared__ uint16_t lrec[LDS_T];   // first record of the key, relative to the tile (28 KiB per block in all)
     __shared__ uint32_t acc_n;
     __shared__ unsigned long long acc_b;
     const uint64_t data_end = *data_end_p;
@@ -368,7 +367,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
                 const unsigned long long old = atomicCAS((unsigned long long *)&lkey[i], (unsigned long long)HT_EMPTY,
                                                          (unsigned long long)key);
                 cur = old == HT_EMPTY ? key : old;
-                if (old == HT_EMPTY) lrec[i] = r;
+                if (old == HT_EMPTY) lrec[i] = (uint16_t)(r - T.t0);
             }
             if (cur == key) {
                 atomicMin(&lmin[i], rk[k]);
@@ -383,11 +382,11 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     for (uint32_t i = threadIdx.x; i < LDS_T; i += KPW_BLOCK) {
         const uint64_t key = lkey[i];
         if (key == HT_EMPTY) continue;
-        const uint64_t r = lrec[i];
+        const uint64_t r = T.t0 + lrec[i];
         const uint32_t esize = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize;
         const int64_t g = global_insert(C, tab, cap, key, mix64(key), lmin[i], esize, max_dict_bytes, false, col, data, r,
                                         data_end, &acc_n, &acc_b);
-        lslot[i] = g < 0 ? 0xffffffffu : (uint32_t)g;
+        lmin[i] = g < 0 ? 0xffffffffu : (uint32_t)g;   // this thread owns slot i in phase 2
         if (g < 0 && !__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
             atomicOr(&C.overflow, 1u);
             __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -407,7 +406,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
         const uint64_t r = T.rec(k);
         int64_t g;
         if (li[k] >= 0) {
-            g = lslot[li[k]] == 0xffffffffu ? -1 : (int64_t)lslot[li[k]];
+            g = lmin[li[k]] == 0xffffffffu ? -1 : (int64_t)lmin[li[k]];
         } else {
             if (__hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
             uint64_t h;
