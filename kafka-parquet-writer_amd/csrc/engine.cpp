@@ -414,18 +414,6 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             C.ids_off = ids_off;
             C.ent_off = ids_off;
             ids_off += len;
-            if (C.is_dict) {
-                // >= 2x the most entries the dictionary can hold before its fallback
-                // (dictionaryByteSize > dictPageSize: entries of >= 4 / 8 bytes), so probe
-                // chains stay short until the fallback; a table that fills anyway means more
-                // entries than that, i.e. a fallback (overflow)
-                const uint64_t esz = (cols[c].phys == KPW_INT64 || cols[c].phys == KPW_DOUBLE) ? 8 : 4;
-                const uint64_t maxent = (uint64_t)props.dictionary_page_size / esz + 1;
-                C.ht_cap = (uint32_t)std::min<uint64_t>(next_pow2(std::max<uint64_t>(16, 2 * std::min<uint64_t>(len, maxent))),
-                                                        1u << 20);
-                C.ht_off = ht_off;
-                ht_off += C.ht_cap + 1;
-            }
             C.dl_job = C.id_job = -1;
             if (cols[c].optional) {
                 RleJob J;
@@ -477,6 +465,36 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         }
     }
     const uint32_t nct = (uint32_t)ctj.size();
+    // Dictionary hash tables.  Full size: >= 2x the most entries the dictionary can hold before
+    // its fallback (dictionaryByteSize > dictPageSize: entries of >= 4 / 8 bytes), so probe
+    // chains stay short until the fallback; a table that fills anyway means more entries than
+    // that, i.e. a fallback (overflow).  Hinted: 4x the entries the column's chunks reached in
+    // the previous encode (dict_hint_), with a probe limit; a hinted table that hits the limit
+    // flags a retry and the chunk phase is redone at full size, so the hint never changes bytes.
+    // Low-cardinality columns (C3: 199 of 200) then fill and touch kilobytes instead of MiBs.
+    auto assign_tables = [&](bool hinted) {
+        ht_off = 0;
+        for (int ci = 0; ci < nch; ci++) {
+            ChunkDesc &C = ch[ci];
+            if (!C.is_dict) continue;
+            const int c = C.col;
+            const uint64_t len = (uint64_t)(C.e - C.s);
+            const uint64_t esz = (cols[c].phys == KPW_INT64 || cols[c].phys == KPW_DOUBLE) ? 8 : 4;
+            const uint64_t maxent = (uint64_t)props.dictionary_page_size / esz + 1;
+            uint64_t cap = std::min<uint64_t>(next_pow2(std::max<uint64_t>(16, 2 * std::min<uint64_t>(len, maxent))), 1u << 20);
+            C.ht_plim = 0;
+            if (hinted && dict_hint_[c]) {
+                const uint64_t hc = next_pow2(std::max<uint64_t>(256, 4ull * dict_hint_[c]));
+                if (hc < cap) { cap = hc; C.ht_plim = 64; }
+            }
+            C.ht_cap = (uint32_t)cap;
+            C.ht_off = ht_off;
+            ht_off += cap + 1;
+        }
+    };
+    if (dict_hint_.size() != (size_t)nc) dict_hint_.assign(nc, 0);
+    static const bool hints_off = [] { const char *e = getenv("KPW_DICT_HINTS"); return e && e[0] == '0'; }();
+    assign_tables(!hints_off);
     // Dictionary insertion order: tile k of every dictionary chunk before tile k+1 of any, so
     // each chunk is scanned roughly in record order and a chunk that crosses the 1 MiB
     // fallback threshold stops after a few tiles instead of inserting all of its values.
@@ -546,10 +564,11 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     uint64_t body_tot = 0;
     // BYTE_ARRAY dictionaries are keyed by a 64-bit hash and verified byte-for-byte; a
     // verified collision re-runs the chunk phase with byte comparisons (exact_strings).
-    for (int attempt = 0; attempt < 2; attempt++) {
-        a.exact_strings = attempt;
+    // A hint-sized table that overflowed (flag word 1) re-runs the phase at full size.
+    for (bool exact = false;;) {
+        a.exact_strings = exact ? 1 : 0;
         CK(hipMemcpyAsync(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
-        CK(hipMemsetAsync(d_collision.p, 0, 4, s));
+        CK(hipMemsetAsync(d_collision.p, 0, 8, s));
         if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), s));
         if (v2_ && !dj.empty()) CK(hipMemcpyAsync(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), hipMemcpyHostToDevice, s));
         // ------------------------------------------------------------ K6 + K2
@@ -577,13 +596,20 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         CK(hipEventRecord(ev_[4], s));
         // ------------------------------------------------------------ layout
         launch_layout(a, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), s);
-        uint32_t coll = 0;
+        uint32_t flags[2] = {0, 0};
         CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, s));
-        CK(hipMemcpyAsync(&coll, d_collision.p, 4, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(flags, d_collision.p, 8, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
-        if (!coll) break;
-        if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
+        if (flags[1]) {
+            assign_tables(false);
+            ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
+            a.ht = d_ht.as<HtSlot>();
+            continue;
+        }
+        if (!flags[0]) break;
+        if (exact) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
+        exact = true;
     }
     // +512: K7 reads its input through 256-byte register windows that may run past the last page
     ENS(d_body, body_tot + 512 + 4096);   // + 4 KiB: the writer D2Hs whole 4 KiB units
@@ -722,6 +748,19 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(), nullptr, s);
     CK(hipMemcpyAsync(smeta.data(), d_smeta.p, 4 * nch * 8, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
+    {   // next encode's table hints: the most entries of each column's chunks, none after a fallback
+        std::vector<uint32_t> most(nc, 0);
+        std::vector<char> seen(nc, 0), fell(nc, 0);
+        for (int ci = 0; ci < nch; ci++) {
+            const ChunkDesc &C = ch[ci];
+            if (!cols[C.col].dict) continue;
+            seen[C.col] = 1;
+            if (!C.is_dict || C.fallback || C.overflow) fell[C.col] = 1;
+            else most[C.col] = std::max(most[C.col], C.dict_n);
+        }
+        for (int c = 0; c < nc; c++)
+            if (seen[c]) dict_hint_[c] = fell[c] ? 0 : std::max<uint32_t>(1, most[c]);
+    }
     std::vector<std::string> bmin(nch), bmax(nch);
     {
         uint64_t blob_len = 0;

@@ -104,6 +104,7 @@ private:
     std::string err_;
     // decode buffers
     std::vector<DevBuf> col_vals, col_shash, col_spfx, col_soff, col_slen, col_pres, col_vbits, col_pcnt;
+    std::vector<uint32_t> dict_hint_;  // per column: most dictionary entries in the previous encode (0: none)
     DevBuf d_cols, d_fmap, d_raw, d_P, d_err, d_scan_tmp, d_opt, d_bool;
     // planning
     DevBuf d_ev, d_E, d_gend, d_rg_start, d_rg_end, d_plan_out;

@@ -277,7 +277,8 @@ __device__ __forceinline__ int64_t global_insert(ChunkDesc &C, HtSlot *tab, uint
         return slot;
     }
     uint32_t i = (uint32_t)(h & (cap - 1));
-    for (uint32_t probe = 0; probe < cap; probe++) {
+    const uint32_t plim = C.ht_plim ? C.ht_plim : cap;   // hint-sized table: a long chain flags a retry
+    for (uint32_t probe = 0; probe < plim; probe++) {
         uint64_t cur = tab[i].key;
         if (cur == HT_EMPTY) {
             const unsigned long long old = atomicCAS((unsigned long long *)&tab[i].key, (unsigned long long)HT_EMPTY, (unsigned long long)key);
@@ -537,12 +538,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, con
     }
 }
 
-__global__ void k_dict_jobs(ChunkDesc *ch, int nchunks, RleJob *jobs, uint32_t max_dict_bytes)
+__global__ void k_dict_jobs(ChunkDesc *ch, int nchunks, RleJob *jobs, uint32_t max_dict_bytes, uint32_t *retry)
 {
     const int ci = blockIdx.x * blockDim.x + threadIdx.x;
     if (ci >= nchunks) return;
     ChunkDesc &C = ch[ci];
     if (!C.is_dict) return;
+    if (C.overflow && C.ht_plim) atomicOr(retry, 1u);   // hint-sized table too small: the host redoes the phase
     if (C.dict_bytes > max_dict_bytes || C.overflow) C.fallback = 1;
     if (C.id_job < 0) return;   // multi-page dictionary descriptor: pages carry the id jobs
     RleJob &J = jobs[C.id_job];
@@ -837,7 +839,8 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
     if (a.ndict_tiles)
         hipLaunchKernelGGL(k_dict_insert, dim3(a.ndict_tiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order,
                            a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
-    hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes);
+    hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes,
+                       a.collision + 1);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
                        a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0);
     seg_tile_scan_u32(a.tile_cnt, a.tile_cnt, a.ctile_chunk, a.nctiles, a.seg, s);

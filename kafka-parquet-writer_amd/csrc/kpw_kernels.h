@@ -173,7 +173,7 @@ struct ChunkDesc {
     // hash table
     uint64_t ht_off;               // slot offset
     uint32_t ht_cap;               // power of two
-    uint32_t pad2;
+    uint32_t ht_plim;              // probe limit of a hint-sized table (0: none, full-size table)
     uint64_t ids_off;              // ids array offset (nn entries)
     uint64_t ent_off;              // dictionary entries array offset (first-occurrence value index)
     // stats

@@ -18,13 +18,15 @@ def to_device(data, offsets):
 
 
 def gpu_encoder_pages(schema, data, offsets, codec=0, block_size=128 * MiB, page_size=128 * MiB, dictionary=True,
-                      writer_version=1):
-    """Returns (row_groups, [(rg, col, [page dicts with 'body'])]) from the HIP encoder."""
+                      writer_version=1, enc=None):
+    """Returns (row_groups, [(rg, col, [page dicts with 'body'])]) from the HIP encoder
+    (a fresh one, or `enc` to reuse an encoder across batches)."""
     import kpw
     import torch
-    enc = kpw.Encoder(kpw.Schema(schema.message_name, schema.columns, schema.proto_class), codec=codec,
-                      block_size=block_size, page_size=page_size, enable_dictionary=dictionary,
-                      writer_version=writer_version)
+    if enc is None:
+        enc = kpw.Encoder(kpw.Schema(schema.message_name, schema.columns, schema.proto_class), codec=codec,
+                          block_size=block_size, page_size=page_size, enable_dictionary=dictionary,
+                          writer_version=writer_version)
     d, o = to_device(data, offsets)
     torch.cuda.synchronize()
     info = enc.encode(d.data_ptr(), o.data_ptr(), len(offsets) - 1, final=True)

@@ -348,3 +348,35 @@ def test_writer_local_file_identical(tmp_path, n, batches):
     ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=256 * 1024, codec=1))
     import pqwalk
     assert fb == ob, pqwalk.first_difference(fb, ob)
+
+
+def _card_batch(n, card, seed):
+    """SampleMessage records whose four columns each take `card` distinct values."""
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, card, n)
+    recs = []
+    for i in range(n):
+        v = int(k[i])
+        q = b"k%09d" % v
+        rec = b"\x0a" + _varint(len(q)) + q + b"\x10" + _varint(1_700_000_000_000 + v)
+        if i % 5:
+            rec += b"\x18" + _varint(v)
+        if i % 3:
+            rec += b"\x20" + _varint((v * 7) % card)
+        recs.append(rec)
+    return synth.pack(recs)
+
+
+def test_dictionary_table_hints_across_encodes():
+    """One encoder over batches whose cardinality jumps: each encode sizes its dictionary hash
+    tables from the previous one's entry counts (engine.cpp assign_tables); a table that turns
+    out too small is redone at full size.  Every batch must stay byte-identical to the oracle
+    (including a jump past the 1 MiB dictionary fallback)."""
+    import kpw
+    enc = kpw.Encoder(kpw.Schema(synth.SAMPLE.message_name, synth.SAMPLE.columns, synth.SAMPLE.proto_class), codec=1,
+                      block_size=128 * gh.MiB, page_size=128 * gh.MiB, enable_dictionary=True, writer_version=1)
+    for j, card in enumerate((40, 30000, 40, 150000, 3000)):
+        data, offs = _card_batch(200_000, card, 77 + j)
+        fb = oracle.encode_file(synth.SAMPLE, data, offs, gh.oracle_props(codec=1))
+        errs, _ = gh.compare_to_file(synth.SAMPLE, data, offs, fb, codec=1, enc=enc)
+        assert not errs, ("batch %d (card %d): " % (j, card)) + "\n".join(errs[:12])
