@@ -1254,6 +1254,30 @@ static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offset
     return wait_direct(w);
 }
 
+// Plain bulk write: a batch that would take the fill buffer past the job size is split there
+// and the full buffer submitted first, so jobs stay at stage_flush_bytes() and the buffer never
+// has to grow (grow_fill drains the pipeline and copies the buffer: C3's 690 MB poll batches
+// did that on every second batch).
+static int write_bulk_split(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n)
+{
+    const uint64_t flush = stage_flush_bytes();
+    while (n) {
+        const StageBuf &F = w->buf[w->fill];
+        const uint64_t used = F.len - F.gap;
+        const uint64_t room = used < flush ? flush - used : 0;
+        // largest k with offsets[k] - offsets[0] <= room
+        uint64_t k = (uint64_t)(std::upper_bound(offsets, offsets + n + 1, offsets[0] + room) - offsets) - 1;
+        if (k >= n) return write_bulk(w, data, offsets, n);
+        if (k == 0 && used == 0) k = 1;   // one record larger than a job: the buffer grows
+        if (k)
+            if (int st = write_bulk(w, data, offsets, k)) return st;
+        if (int st = submit(w, JOB_PLANNED, 0)) return st;
+        offsets += k;
+        n -= k;
+    }
+    return KPW_OK;
+}
+
 // getDataSize() after the first m records of the (drained) fill buffer, without flushing:
 // an encode of [0, m) gives the row groups parquet-mr would have completed by then (their
 // header + compressed bytes follow lastRowGroupEndPos) and the open row group's buffered size.
@@ -1418,7 +1442,7 @@ static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offse
     } else if (max_file_size >= 0) {
         rc = write_until_full_bulk(w, data, offsets, n, max_file_size, n_accepted, full);
     } else {
-        rc = write_bulk(w, data, offsets, n);
+        rc = write_bulk_split(w, data, offsets, n);
         if (n_accepted && !rc) *n_accepted = n;
     }
     if (rc) return rc;

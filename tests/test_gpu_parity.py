@@ -380,3 +380,38 @@ def test_dictionary_table_hints_across_encodes():
         fb = oracle.encode_file(synth.SAMPLE, data, offs, gh.oracle_props(codec=1))
         errs, _ = gh.compare_to_file(synth.SAMPLE, data, offs, fb, codec=1, enc=enc)
         assert not errs, ("batch %d (card %d): " % (j, card)) + "\n".join(errs[:12])
+
+
+_SPLIT_CHILD = r"""
+import sys
+sys.path[:0] = sys.argv[1].split(":")
+import kpw, oracle, pqwalk, synth
+schema = synth.REC8
+n = 600_000
+data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE09, n)
+props = kpw.ParquetProperties(block_size=1 << 20, compression_codec_name=1)
+pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class), props)
+for i in range(0, n, 150_000):
+    j = min(n, i + 150_000)
+    pf.write_batch((data[int(offs[i]):int(offs[j])], offs[i:j + 1] - offs[i]))
+pf.close()
+fb = pf.file_bytes()
+ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=1 << 20, codec=1))
+assert fb == ob, pqwalk.first_difference(fb, ob)
+print("split ok", len(fb))
+"""
+
+
+def test_writer_batches_split_at_job_size():
+    """Bulk batches larger than the room left in the fill buffer are split at the job size
+    (writer.cpp write_bulk_split) instead of growing the buffer.  With 2 MiB jobs each ~9 MB
+    batch spans several jobs and row groups cross job boundaries; the file must not change.
+    Runs in a child process: the job size is read once per process (KPW_STAGE_FLUSH_MB)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = ":".join(os.path.join(root, d) for d in ("synth", "oracle", "tests", "kafka-parquet-writer_amd", ""))
+    env = dict(os.environ, KPW_STAGE_FLUSH_MB="2")
+    r = subprocess.run([sys.executable, "-c", _SPLIT_CHILD, paths], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "split ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
