@@ -1254,17 +1254,17 @@ static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offset
     return wait_direct(w);
 }
 
-// Plain bulk write: a batch that would take the fill buffer past the job size is split there
-// and the full buffer submitted first, so jobs stay at stage_flush_bytes() and the buffer never
-// has to grow (grow_fill drains the pipeline and copies the buffer: C3's 690 MB poll batches
-// did that on every second batch).
+// Plain bulk write: a batch that does not fit the fill buffer's capacity (gap + job size +
+// 64 MiB) is split where it stops fitting and the full buffer is submitted first, so the buffer
+// never has to grow (grow_fill drains the pipeline and copies the buffer: C3's 690 MB poll
+// batches did that on every second batch).  Batches that fit are appended whole, as before
+// (jobs end at the first batch that reaches the job size).
 static int write_bulk_split(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n)
 {
-    const uint64_t flush = stage_flush_bytes();
     while (n) {
         const StageBuf &F = w->buf[w->fill];
         const uint64_t used = F.len - F.gap;
-        const uint64_t room = used < flush ? flush - used : 0;
+        const uint64_t room = F.cap > F.len + 64 ? F.cap - F.len - 64 : 0;
         // largest k with offsets[k] - offsets[0] <= room
         uint64_t k = (uint64_t)(std::upper_bound(offsets, offsets + n + 1, offsets[0] + room) - offsets) - 1;
         if (k >= n) return write_bulk(w, data, offsets, n);

@@ -387,12 +387,12 @@ import sys
 sys.path[:0] = sys.argv[1].split(":")
 import kpw, oracle, pqwalk, synth
 schema = synth.REC8
-n = 600_000
+n = 2_400_000
 data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE09, n)
 props = kpw.ParquetProperties(block_size=1 << 20, compression_codec_name=1)
 pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class), props)
-for i in range(0, n, 150_000):
-    j = min(n, i + 150_000)
+for i in range(0, n, 1_200_000):
+    j = min(n, i + 1_200_000)
     pf.write_batch((data[int(offs[i]):int(offs[j])], offs[i:j + 1] - offs[i]))
 pf.close()
 fb = pf.file_bytes()
@@ -403,10 +403,11 @@ print("split ok", len(fb))
 
 
 def test_writer_batches_split_at_job_size():
-    """Bulk batches larger than the room left in the fill buffer are split at the job size
-    (writer.cpp write_bulk_split) instead of growing the buffer.  With 2 MiB jobs each ~9 MB
-    batch spans several jobs and row groups cross job boundaries; the file must not change.
-    Runs in a child process: the job size is read once per process (KPW_STAGE_FLUSH_MB)."""
+    """Bulk batches larger than the room left in the fill buffer (gap + job size + 64 MiB) are
+    split where they stop fitting (writer.cpp write_bulk_split) instead of growing the buffer.
+    With 2 MiB jobs the buffers hold ~130 MiB, so each ~74 MB batch is split; row groups cross
+    the job boundaries and the file must not change.  Runs in a child process: the job size is
+    read once per process (KPW_STAGE_FLUSH_MB)."""
     import os
     import subprocess
     import sys
