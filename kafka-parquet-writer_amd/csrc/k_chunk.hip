@@ -113,14 +113,20 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
     ChunkDesc &C = ch[ci];
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];   // by value: loaded once, not after every store
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     uint64_t nn = 0, raw = 0;
     uint64_t kmin = ~0ull, kmax = 0;
+    bool ok[8];
+#pragma unroll
     for (int k = 0; k < 8; k++) {
         const uint64_t r = T.rec(k);
-        if (r >= T.e) break;
-        if (!present_at(col, r)) continue;
+        ok[k] = r < T.e && present_at(col, r);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint64_t r = T.rec(k);
+        if (!ok[k]) continue;
         nn++;
         if (col.phys == 6) {
             raw += 4 + col.slen[r];   // min/max: k_str_minmax, after the dictionary phase
@@ -333,7 +339,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     if (threadIdx.x == 0) skip = __hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (skip) return;
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];   // by value: not reloaded after stores
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     const uint32_t cap = C.ht_cap;
     HtSlot *tab = ht + C.ht_off;
@@ -442,7 +448,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
     const bool active = C.is_dict && !C.fallback;
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];   // by value: not reloaded after stores
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     uint32_t cnt = 0;
     uint64_t sz = 0;
@@ -522,19 +528,33 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, con
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
     if (!C.is_dict || C.fallback) return;
-    const DevCol &col = cols[C.col];
+    // by value: the stores to ids[] below may not alias them, so their loads are not repeated
+    const DevCol col = cols[C.col];
+    const uint64_t ids_off = C.ids_off, ht_off = C.ht_off, ent_off = C.ent_off;
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
+    // three independent passes over the 8 records (positions, slots, ids) so each pass's
+    // loads are in flight together instead of one dependent chain per record
+    uint64_t o[8];
+    bool ok[8];
+#pragma unroll
     for (int k = 0; k < 8; k++) {
         const uint64_t r = T.rec(k);
-        if (r >= T.e) break;
-        if (!present_at(col, r)) continue;
-        const uint64_t o = C.ids_off + T.rank(col, r);
-        const uint32_t id = ht[C.ht_off + ids[o]].id;
-        ids[o] = id;
-        if (col.phys == 6) {  // verify the hash-keyed dictionary byte-for-byte
-            const uint64_t e = ent_rec[C.ent_off + id];
-            if (!str_eq(col, data, e, r, data_end)) atomicOr(collision, 1u);
-        }
+        ok[k] = r < T.e && present_at(col, r);
+        o[k] = ok[k] ? ids_off + T.rank(col, r) : 0;
+    }
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = ok[k] ? ids[o[k]] : 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = ok[k] ? ht[ht_off + v[k]].id : 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (ok[k]) ids[o[k]] = v[k];
+    if (col.phys == 6) {   // verify the hash-keyed dictionary byte-for-byte
+        bool bad = false;
+        for (int k = 0; k < 8; k++)
+            if (ok[k]) bad |= !str_eq(col, data, ent_rec[ent_off + v[k]], T.rec(k), data_end);
+        if (bad) atomicOr(collision, 1u);
     }
 }
 
