@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_str_minmax(const ChunkDesc *ch, c
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];   // by value: not reloaded after stores
     if (col.phys != 6) return;
     const uint64_t data_end = *data_end_p;
     // a page of a multi-page chunk is only part of what its dictionary covers: use its values
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_str_final(ChunkDesc *ch, const De
     __shared__ uint64_t li[KPW_BLOCK], la[KPW_BLOCK];
     const int ci = blockIdx.x;
     ChunkDesc &C = ch[ci];
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];   // by value: not reloaded after stores
     if (col.phys != 6 || !C.nn) return;
     const uint64_t data_end = *data_end_p;
     uint64_t a = ~0ull, b = ~0ull;
@@ -663,7 +663,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_headers(const ChunkDesc *ch
     const int ci = blockIdx.x * blockDim.x + threadIdx.x;
     if (ci >= nchunks) return;
     const ChunkDesc &C = ch[ci];
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];   // by value: not reloaded after stores
     if (col.optional && !v2) {   // v1: 4-byte length in front of the definition levels
         uint8_t *p = out + C.body_off + C.dictpage_len;
         const uint32_t l = (uint32_t)C.dl_len;
@@ -708,7 +708,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_page(const ChunkDesc *ch, co
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
     if (!C.is_dict || C.fallback) return;
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];   // by value: not reloaded after stores
     const uint64_t e0 = (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
     uint8_t *page = out + C.body_off;
     for (int k = 0; k < 8; k++) {
@@ -737,7 +737,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_plain(const ChunkDesc *ch, const 
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];   // by value: not reloaded after stores
     if ((C.is_dict && !C.fallback) || col.phys == 0 || C.dj0 >= 0) return;   // dj0: v2 DELTA fallback instead
     const uint64_t p0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P + threadIdx.x * 8;
     uint8_t *vout = out + C.val_off;
