@@ -780,23 +780,55 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_plain(const ChunkDesc *ch, const 
 }
 
 // BooleanPlainValuesWriter: compacted value bits, LSB first (output pre-zeroed)
+// position of the j-th (0-based) set bit of m (m has more than j set bits)
+__device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t j)
+{
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t w = 32; w >= 1; w >>= 1) {
+        const uint64_t low = m & ((1ull << w) - 1);
+        const uint32_t c = (uint32_t)__popcll(low);
+        if (j >= c) { j -= c; m >>= w; pos += w; }
+        else m = low;
+    }
+    return pos;
+}
+
+// PLAIN booleans (BooleanPlainValuesWriter: LSB-first bit packing).  Each wave packs its 64
+// records per step with ballots: the values of the present records, in rank order, become one
+// 64-bit word (lane j picks the j-th present lane), and lane 0 ORs it into the output at the
+// slice's first rank (at most three 32-bit atomics per 64 records instead of one per true value).
 __global__ void __launch_bounds__(KPW_BLOCK) k_plain_bool(const ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
                                                           const uint32_t *ctile_first, uint8_t *out)
 {
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
-    const DevCol &col = cols[C.col];
+    const DevCol col = cols[C.col];
     if (col.phys != 0 || C.bool_job >= 0) return;   // bool_job: v2 RLE booleans instead
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     const uint64_t base_bit = C.val_off * 8;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t *o32 = (uint32_t *)out;
     for (int k = 0; k < 8; k++) {
         const uint64_t r = T.rec(k);
-        if (r >= T.e) break;
-        if (!present_at(col, r)) continue;
-        if ((col.vbits[r >> 6] >> (r & 63)) & 1ull) {
-            const uint64_t bit = base_bit + T.rank(col, r);
-            atomicOr((uint32_t *)(out + ((bit >> 3) & ~3ull)), 1u << (((bit >> 3) & 3) * 8 + (bit & 7)));
+        const uint64_t r0 = r - lane;   // the wave's first record of this step
+        if (r0 >= T.e) break;           // wave-uniform
+        const bool pres = r < T.e && present_at(col, r);
+        const bool val = pres && ((col.vbits[r >> 6] >> (r & 63)) & 1ull);
+        const uint64_t pm = __ballot(pres), tm = __ballot(val);
+        const uint32_t cnt = (uint32_t)__popcll(pm);
+        const bool bit = lane < cnt && ((tm >> select_bit(pm, lane)) & 1ull);
+        const uint64_t P = __ballot(bit);
+        if (lane == 0 && P) {
+            const uint64_t B = base_bit + T.rank(col, r0);
+            const uint64_t w = B >> 5;
+            const uint32_t sh = (uint32_t)(B & 31);
+            const uint64_t lo = P << sh;
+            const uint32_t hi = sh ? (uint32_t)(P >> (64 - sh)) : 0u;
+            if ((uint32_t)lo) atomicOr(&o32[w], (uint32_t)lo);
+            if ((uint32_t)(lo >> 32)) atomicOr(&o32[w + 1], (uint32_t)(lo >> 32));
+            if (hi) atomicOr(&o32[w + 2], hi);
         }
     }
 }
