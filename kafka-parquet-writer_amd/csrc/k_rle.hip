@@ -48,6 +48,30 @@ __device__ __forceinline__ uint32_t run_map(uint32_t a, uint32_t b)
     return m;
 }
 
+// values p0 .. p0+7 of a stream (0 past len): one bitmask word pair or eight independent
+// loads, instead of a chain of guarded single loads
+__device__ __forceinline__ void src_get8(const ValSrc &s, int64_t p0, int64_t len, uint32_t v[8])
+{
+    if (p0 + 8 <= len) {
+        if (s.kind == 0) {
+            const uint64_t b = s.base + (uint64_t)p0;
+            const uint64_t *w = (const uint64_t *)s.ptr;
+            const uint32_t sh = (uint32_t)(b & 63);
+            uint64_t bits = w[b >> 6] >> sh;
+            if (sh > 56) bits |= w[(b >> 6) + 1] << (64 - sh);
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = (uint32_t)((bits >> k) & 1ull);
+        } else {
+            const uint32_t *q = (const uint32_t *)s.ptr + s.base + (uint64_t)p0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = q[k];
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = p0 + k < len ? src_get(s, (uint64_t)(p0 + k)) : 0u;
+}
+
 // ------------------------------------------------------------------ long runs
 
 __global__ void __launch_bounds__(KPW_BLOCK) k_rle_bounds(const RleJob *jobs, const uint32_t *ptile_job, int64_t *last_brk)
@@ -61,11 +85,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_bounds(const RleJob *jobs, co
     int64_t last = -1;
     if (p0 < len) {
         uint32_t prev = p0 > 0 ? src_get(src, p0 - 1) : 0;
+        uint32_t vv[8];
+        src_get8(src, p0, len, vv);
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             const int64_t i = p0 + k;
             if (i >= len) break;
-            const uint32_t v = src_get(src, i);
+            const uint32_t v = vv[k];
             if (i == 0 || v != prev) last = i;
             prev = v;
         }
@@ -89,11 +115,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(const RleJob *jobs, 
     int64_t local_last = -1;
     if (p0 < len) {
         uint32_t prev = p0 > 0 ? src_get(src, p0 - 1) : 0;
+        uint32_t vv[8];
+        src_get8(src, p0, len, vv);
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             const int64_t i = p0 + k;
             if (i >= len) break;
-            const uint32_t v = src_get(src, i);
+            const uint32_t v = vv[k];
             if (i == 0 || v != prev) { brk |= 1u << k; local_last = i; }
             prev = v;
         }
