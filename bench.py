@@ -52,6 +52,17 @@ import numpy as np  # noqa: E402
 MiB = 1024 * 1024
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 POLL_BATCH = 500_000    # records per write call (a poll() batch)
+# kernels inside the K7 HIP-event window (engine.cpp kev_[2]..kev_[3]); profiles/summarize.py K7
+K7_KERNELS = ["k_snappy_v x2", "k_snappy_s_rest x2", "k_snappy_seg", "k_snappy_page_sizes", "k_snappy_copy"]
+# what each HIP-event stage of kpw_encoder_stage_times covers (engine.cpp ev_[0..6])
+STAGE_KERNELS = {
+    "decode": "K1 k_decode",
+    "plan": "prefix scans (k_mj_*), def-level RLE structure (k_rle_*, k_phase_*, k_r_*), events, K8 k_plan",
+    "stats_dict": "K6 k_chunk_stats, k_str_minmax; K2 k_dict_insert, k_dict_firsts, k_dict_ids",
+    "rle": "K3 structure of the level / id streams (k_rle_*, k_phase_*, k_r_*)",
+    "layout_plain_write": "layout; K4 k_plain, k_plain_bool, k_dict_page; K3 k_rle_write_*",
+    "compress": "K7 window + page size D2H and the host's longest-first fragment order",
+}
 
 
 def log(msg):
@@ -126,18 +137,18 @@ def stage_bytes(schema, st):
     }
 
 
-def pmc_traffic(workload, kernels):
-    """HBM bytes per launch summed over `kernels` from the newest profiles/*_<workload>_pmc_traffic.json
-    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload; profiles/summarize.py
-    applies the gfx950 x2 FETCH correction to streaming kernels only).  Returns (bytes, file)."""
+def pmc_traffic(workload):
+    """K7 HBM bytes per encode job from the newest profiles/*_<workload>_pmc_traffic.json: separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py --no-resident` (every launch a
+    writer job), each K7 kernel's dispatches summed and divided by the pass's jobs (calls per job
+    weighted), the gfx950 x2 FETCH correction on 16 B/lane streaming kernels only
+    (profiles/summarize.py).  Returns (bytes, file) or (None, None)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_%s_pmc_traffic.json" % workload)))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    ks = [d.get("kernels", {}).get(k) for k in kernels]
-    if not all(ks):
-        return None, None
-    return int(sum(k["traffic_bytes"] for k in ks)), os.path.relpath(files[-1], ROOT)
+    for f in reversed(files):
+        d = json.load(open(f))
+        if "k7_traffic_bytes_per_job" in d:   # per-job format (r03 on)
+            return int(d["k7_traffic_bytes_per_job"]), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def dist_init(world, local_rank, backend="nccl"):
@@ -271,6 +282,65 @@ def cpu_baseline(kind, seed, sample_records, threads, runs=5):
                 records_per_s=round(per * threads / med, 1))
 
 
+def per_record_leg(kpw, schema, sschema, kind, seed, n, device, max_file_size, page_size):
+    """The reference's unchanged WorkerThread loop (KafkaProtoParquetWriter.java:268-285,306-308):
+    ONE kpw_writer_write + ONE kpw_writer_data_size per record through the C-ABI (the two
+    downcalls a JVM host makes, driven from C: synth/loop.c), rotating files when getDataSize()
+    >= maxFileSize, on a C2-shaped stream in ordinary (unpinned) host memory (a JVM byte[]).
+    The CPU oracle's same loop is timed in the cpu_baseline leg (cpu_baseline_per_record)."""
+    import synth
+    data, offs = synth.generate(kind, seed + 0x77, n)
+    nbytes = int(offs[-1])
+    L = kpw.load_library()
+    props = kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=kpw.SNAPPY, page_size=page_size)
+    pf = kpw.ParquetFile(None, schema, props, device=device)   # warm-up: library caches, first encode
+    synth.per_record_loop("kpw", L.kpw_writer_write, L.kpw_writer_data_size, pf._h, data, offs, 0, min(n, 20000),
+                          max_file_size)
+    pf.close()
+    pf.__del__()
+    t0 = time.perf_counter()
+    done = files = 0
+    while done < n:
+        pf = kpw.ParquetFile(None, schema, props, device=device)
+        got, full, st, _ = synth.per_record_loop("kpw", L.kpw_writer_write, L.kpw_writer_data_size, pf._h, data, offs,
+                                                 done, n - done, max_file_size)
+        if st:
+            pf._check(st, "per-record write")
+        pf.close()
+        pf.__del__()
+        files += 1
+        done += got
+    dt = time.perf_counter() - t0
+    return dict(records=n, bytes=nbytes, records_per_s=round(n / dt, 1), gbps=round(nbytes / dt / 1e9, 4),
+                wall_s=round(dt, 3), files=files, max_file_size=max_file_size, page_size=page_size,
+                calls_per_record="1 kpw_writer_write (n=1) + 1 kpw_writer_data_size, from C (synth/loop.c)",
+                reference_sizing_hint_records_per_s=300000)
+
+
+def cpu_baseline_per_record(sschema, kind, seed, n, max_file_size, page_size):
+    """CPU-baseline leg of the per-record loop: the oracle's kpwo_write + kpwo_data_size per
+    record on the same records as per_record_leg, one thread (one WorkerThread)."""
+    import synth
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    data, offs = synth.generate(kind, seed + 0x77, n)
+    OL = oracle.lib()
+    oprops = oracle.make_props(block_size=128 * MiB, page_size=page_size, codec=oracle.SNAPPY)
+    t1 = time.perf_counter()
+    done = files = 0
+    while done < n:
+        w = oracle.OracleWriter(sschema, oprops)
+        got, full, st, _ = synth.per_record_loop("oracle", OL.kpwo_write, OL.kpwo_data_size, w._h, data, offs, done,
+                                                 n - done, max_file_size)
+        if st:
+            raise RuntimeError("oracle per-record loop status %d" % st)
+        w.close()
+        files += 1
+        done += got
+    odt = time.perf_counter() - t1
+    return dict(records=n, records_per_s=round(n / odt, 1), wall_s=round(odt, 3), files=files, cores=1, kind="port")
+
+
 def bind_to_gpu_numa(device):
     """One process per GPU, bound to the CPUs of the GPU's NUMA node (the usual deployment of a
     GPU worker): pinned batches, stage/page buffers and the writer's threads then sit next to the
@@ -345,6 +415,12 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-resident", action="store_true")
+    ap.add_argument("--per-record-records", type=int, default=3_000_000,
+                    help="records of the per-record leg (the reference's write + getDataSize loop; 0 = skip)")
+    ap.add_argument("--per-record-max-file-mb", type=int, default=1024,
+                    help="maxFileSize of the per-record leg (reference default 1 GiB, KafkaProtoParquetWriter.java:462)")
+    ap.add_argument("--per-record-page-kb", type=int, default=128 * 1024,
+                    help="pageSize of the per-record leg (reference default = blockSize, KafkaProtoParquetWriter.java:474)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -422,30 +498,35 @@ def main():
     value = total_bytes / elapsed / 1e9
     rec_s = total_records / elapsed
     jobs = max(1.0, agg.get("jobs", 1.0))
-    # dominant kernel of the timed steps: HIP events around K1 / K7 on the encoder's stream,
-    # averaged per launch (one launch per encode job)
-    k1_bytes = (agg["record_bytes"] + 8 * (agg["records"] + jobs) + decode_out_bytes(sschema, agg["records"])) / jobs
+    # dominant kernel group of the timed steps: K7, timed with HIP events on the encoder's stream
+    # around its kernels (engine.cpp kev_[2]..kev_[3]), one window per encode job
     k7_bytes = (agg["page_bytes_uncompressed"] + agg["page_bytes_compressed"]) / jobs
-    kern = {"kpw::k_decode": (k1_bytes, agg["k_decode_ms"] / jobs, ("kpw::k_decode",)),
-            "K7 kpw::k_snappy_v + k_snappy_seg + k_snappy_s_rest": (
-                k7_bytes, agg["k7_snappy_ms"] / jobs, ("kpw::k_snappy_v", "kpw::k_snappy_seg", "kpw::k_snappy_s_rest"))}
-    dom = max(kern, key=lambda k: kern[k][1])
-    ab, ams, knames = kern[dom]
-    achieved = ab / (ams * 1e-3) / 1e9 if ams > 0 else 0.0
-    traffic, tsrc = pmc_traffic(args.workload, knames)
+    ams = agg["k7_snappy_ms"] / jobs
+    achieved = k7_bytes / (ams * 1e-3) / 1e9 if ams > 0 else 0.0
+    traffic, tsrc = pmc_traffic(args.workload)
     sb = stage_bytes(sschema, agg)
     stage_ms = {"decode": agg["decode_ms"], "plan": agg["plan_ms"], "stats_dict": agg["stats_dict_ms"],
                 "rle": agg["rle_ms"], "layout_plain_write": agg["layout_plain_write_ms"], "compress": agg["compress_ms"]}
     t_stages = sum(stage_ms.values())
     pipe = sum(sb.values()) / (t_stages * 1e-3) / 1e9 if t_stages > 0 else 0.0
-    roof = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBPS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBPS, 5),
-                traffic=(round(traffic / (ams * 1e-3) / 1e9, 2) if traffic else None),
-                traffic_bytes_per_launch=traffic, traffic_source=tsrc, algorithmic_bytes_per_launch=int(ab),
-                avg_launch_ms=round(ams, 4), launches=int(jobs),
+    roof = dict(bound="hbm", kernel="K7 Snappy: " + ", ".join(K7_KERNELS), achieved=round(achieved, 2),
+                peak=HBM_PEAK_GBPS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBPS, 5),
+                traffic=traffic, traffic_unit="HBM bytes per launch (FETCH_SIZE + WRITE_SIZE)",
+                traffic_source=tsrc, traffic_over_algorithmic=(round(traffic / k7_bytes, 3) if traffic else None),
+                algorithmic_bytes_per_launch=int(k7_bytes), avg_launch_ms=round(ams, 4), launches=int(jobs),
                 pipeline_achieved=round(pipe, 2), pipeline_frac=round(pipe / HBM_PEAK_GBPS, 5),
                 pipeline_stage_ms=round(t_stages / jobs, 3),
                 copy_ceiling=ceiling, frac_of_copy_ceiling=round(achieved / ceiling, 5) if ceiling else None)
+    stage_roof = {}
+    for k, ms in stage_ms.items():
+        b_job, ms_job = sb[k] / jobs, ms / jobs
+        g = b_job / (ms_job * 1e-3) / 1e9 if ms_job > 0 else 0.0
+        stage_roof[k] = dict(kernels=STAGE_KERNELS[k], alg_bytes_per_job=int(b_job), ms_per_job=round(ms_job, 4),
+                             gbps=round(g, 1), frac=round(g / HBM_PEAK_GBPS, 5))
+    per_record = None
+    if args.per_record_records and world == 1:
+        per_record = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_records, local_rank,
+                                    args.per_record_max_file_mb * MiB, args.per_record_page_kb * 1024)
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         threads = args.cpu_threads or host_threads()
@@ -453,6 +534,10 @@ def main():
         if args.workload not in ("c2", "c5"):   # the same ~1.5 GB of wire bytes as the C2 sample
             sample = max(threads, int(sample * 62 / max(1.0, set_bytes[0] / n)))
         cpu = cpu_baseline(kind, wseed, sample, threads)
+        if per_record:
+            cpu["per_record"] = cpu_baseline_per_record(sschema, kind, wseed, args.per_record_records,
+                                                        args.per_record_max_file_mb * MiB, args.per_record_page_kb * 1024)
+            per_record["oracle_records_per_s"] = cpu["per_record"]["records_per_s"]
     out = {
         "metric": "Parquet encode GB/s + records/sec (whole node) at 1/2/4/8 MI355X vs CPU writer",
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -472,6 +557,8 @@ def main():
         "stage_ms_per_step": {k: round(v / args.steps, 3) for k, v in stage_ms.items()},
         "resident_encode": resident,
         "roofline": roof,
+        "stage_roofline": stage_roof,
+        "per_record": per_record,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -60,6 +60,13 @@ int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64_t *offsets
 void *kpw_host_alloc(uint64_t bytes, int *status);
 void kpw_host_free(void *p);
 
+/* The library keeps freed HBM and pinned blocks for the next writer (a writer is one file and
+ * files rotate; hipFree synchronises the device): up to KPW_DEV_CACHE_GB per device (default 96)
+ * and KPW_PIN_CACHE_GB pinned (default 48), read once per process.  This releases every idle
+ * block now (e.g. before a co-located consumer or framework allocates).  Thread-safe.  No
+ * reference counterpart (the JVM writer allocates on the Java heap). */
+void kpw_trim_caches(void);
+
 /* The WorkerThread size-rotation loop (KafkaProtoParquetWriter.java:277-285,306-308):
  * writes records in order and stops right after the first one for which
  * getDataSize() >= max_file_size.  *n_accepted = records written, *full = 1 if the stop
@@ -166,7 +173,8 @@ int kpw_encoder_copy_pages(kpw_encoder *e, uint64_t off, uint64_t len, void *hos
 /* Timing of the last encode: device milliseconds measured with HIP events on the encoder's
  * stream.  Index order: [0] decode, [1] plan, [2] stats+dictionary, [3] rle,
  * [4] layout+plain+write, [5] compress, [6] metadata, [7] total, [8] k_decode kernel alone,
- * [9] K7 Snappy kernels alone (k_snappy_v, k_snappy_seg, k_snappy_s_rest; 0 when uncompressed).  Returns entries written (<= cap). */
+ * [9] K7 Snappy kernels alone (k_snappy_v x2, k_snappy_s_rest x2, k_snappy_seg, k_snappy_page_sizes,
+ * k_snappy_copy; 0 when uncompressed).  Returns entries written (<= cap). */
 int kpw_encoder_stage_times(const kpw_encoder *e, float *ms, int cap);
 
 #ifdef __cplusplus

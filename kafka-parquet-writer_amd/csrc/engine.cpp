@@ -30,13 +30,26 @@ void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, c
         if (e_ != hipSuccess) return fail(KPW_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+namespace {
+thread_local hipStream_t tl_order = nullptr;   // StreamOrder: the stream this thread's buffers are used on
+}
+StreamOrder::StreamOrder(hipStream_t s) : prev_(tl_order) { tl_order = s; }
+StreamOrder::~StreamOrder() { tl_order = prev_; }
+
 // Buffers come from the process-wide cache (memcache.h).  Growing one may replace a block
-// that queued work (e.g. a D2H of the previous job's pages) still reads, so the device is
-// synchronised before the old block goes back to the cache (what hipFree used to imply).
+// that queued work (e.g. a D2H of the previous job's pages) still reads: under a StreamOrder
+// the old block returns to the cache once that stream has passed this point (work queued
+// later on it may already use the new block); without one the device is synchronised first
+// (what hipFree used to imply).
 int DevBuf::ensure(size_t bytes)
 {
     if (bytes <= cap && p) return 0;
-    if (p) { (void)hipDeviceSynchronize(); dev_free(p); p = nullptr; cap = 0; }
+    if (p) {
+        if (tl_order) dev_free_after(p, tl_order);
+        else { (void)hipDeviceSynchronize(); dev_free(p); }
+        p = nullptr;
+        cap = 0;
+    }
     size_t c = bytes < 256 ? 256 : bytes + bytes / 8;
     p = dev_alloc(c);
     if (!p) return -1;
@@ -222,6 +235,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
 {
     out = BatchOut();
     CK(hipSetDevice(device));
+    StreamOrder order(stream);
     if (user_stream) {  // order our stream after the caller's work
         CK(hipEventRecord(ev_[8], user_stream));
         CK(hipStreamWaitEvent(stream, ev_[8], 0));
@@ -685,14 +699,17 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             }
         }
         if (seg_args(sa)) return KPW_ERR_NOMEM;
+        // K7 window (stage_ms[9]): every kernel from the first fragment kernel to the compressed
+        // pages in place (k_snappy_v, k_snappy_s_rest, k_snappy_seg, k_snappy_v, k_snappy_s_rest,
+        // k_snappy_page_sizes, k_snappy_copy; one 4-byte fill of the fragment counter)
         CK(hipEventRecord(kev_[2], s));
         launch_snappy(sa, s);
+        launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), s);
+        CK(hipEventRecord(kev_[3], s));
         if (nf) {
             sn_ft_.resize(2 * (size_t)nf);
             CK(hipMemcpyAsync(sn_ft_.data(), d_sprof.p, sn_ft_.size() * 8, hipMemcpyDeviceToHost, s));
         }
-        CK(hipEventRecord(kev_[3], s));
-        launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), s);
         CK(hipGetLastError());
         pcoff.resize(2 * nch);
         pclen.resize(2 * nch);

@@ -55,6 +55,20 @@ struct MpRun {
     std::vector<std::vector<PageOut>> cols;
 };
 
+// While alive, DevBuf::ensure on this thread orders the release of a replaced block after the
+// work already queued on `s` (every reader of the thread's buffers runs on s or waits on it)
+// instead of synchronising the whole device.
+class StreamOrder {
+public:
+    explicit StreamOrder(hipStream_t s);
+    ~StreamOrder();
+    StreamOrder(const StreamOrder &) = delete;
+    StreamOrder &operator=(const StreamOrder &) = delete;
+
+private:
+    hipStream_t prev_;
+};
+
 class DevBuf {
 public:
     void *p = nullptr;

@@ -1,23 +1,46 @@
 // memcache.cpp — see memcache.h.
 #include "memcache.h"
 
-#include <hip/hip_runtime.h>
-
 #include <cstdint>
+#include <cstdlib>
 #include <map>
 #include <mutex>
+#include <vector>
 
 namespace kpw {
 
 namespace {
 
-constexpr size_t kDevCacheCap = 96ull << 30;   // idle HBM kept per device (of 288 GB)
-constexpr size_t kPinCacheCap = 48ull << 30;   // idle pinned host memory kept
+size_t cap_gb(const char *env, size_t dflt)
+{
+    const char *e = getenv(env);
+    if (!e || !*e) return dflt << 30;
+    const long long v = atoll(e);
+    return v > 0 ? (size_t)v << 30 : 0;
+}
+// idle memory kept (KPW_DEV_CACHE_GB per device / KPW_PIN_CACHE_GB; 0 = keep nothing idle)
+size_t dev_cache_cap()
+{
+    static const size_t v = cap_gb("KPW_DEV_CACHE_GB", 96);
+    return v;
+}
+size_t pin_cache_cap()
+{
+    static const size_t v = cap_gb("KPW_PIN_CACHE_GB", 48);
+    return v;
+}
 
 struct Pool {
     std::multimap<size_t, void *> free_;   // size -> block
     std::map<void *, size_t> size_;        // every block this pool allocated (live or free)
     size_t free_bytes = 0;
+};
+
+// a block handed back with dev_free_after: it rejoins its pool once `ev` has completed
+struct Deferred {
+    void *p;
+    int dev;
+    hipEvent_t ev;
 };
 
 std::mutex g_mu;
@@ -26,6 +49,7 @@ Pool g_pin;
 std::map<uintptr_t, size_t> g_pin_live;     // live pinned blocks (pin_contains)
 std::map<void *, int> g_dev_of;             // device of every block dev_alloc handed out
                                             // (hipPointerGetAttributes per free cost ~0.3 ms)
+std::vector<Deferred> g_deferred;
 
 // best fit within 2x (and never more than 1 GiB of slack)
 void *take(Pool &p, size_t bytes)
@@ -53,6 +77,38 @@ void trim(Pool &p, size_t keep, FreeFn fn)
     }
 }
 
+void dev_release(void *b)
+{
+    g_dev_of.erase(b);
+    (void)hipFree(b);
+}
+
+// a block of ours back into its pool (under g_mu)
+void dev_return(void *q, int dev)
+{
+    Pool &p = g_dev[dev];
+    auto it = p.size_.find(q);
+    if (it == p.size_.end()) { (void)hipFree(q); return; }
+    p.free_.emplace(it->second, q);
+    p.free_bytes += it->second;
+    trim(p, dev_cache_cap(), dev_release);
+}
+
+// deferred blocks whose event completed rejoin their pools (under g_mu); wait: block on them
+void reap(bool wait)
+{
+    size_t k = 0;
+    for (size_t i = 0; i < g_deferred.size(); i++) {
+        Deferred &d = g_deferred[i];
+        const hipError_t e = wait ? hipEventSynchronize(d.ev) : hipEventQuery(d.ev);
+        if (e == hipErrorNotReady) { g_deferred[k++] = d; continue; }
+        (void)hipGetLastError();
+        (void)hipEventDestroy(d.ev);
+        dev_return(d.p, d.dev);
+    }
+    g_deferred.resize(k);
+}
+
 }  // namespace
 
 void *dev_alloc(size_t bytes)
@@ -61,12 +117,14 @@ void *dev_alloc(size_t bytes)
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
     if (bytes < 256) bytes = 256;
     std::lock_guard<std::mutex> g(g_mu);
+    if (!g_deferred.empty()) reap(false);
     Pool &p = g_dev[dev];
     if (void *q = take(p, bytes)) return q;
     void *q = nullptr;
     if (hipMalloc(&q, bytes) != hipSuccess) {
         (void)hipGetLastError();
-        trim(p, 0, [](void *b) { g_dev_of.erase(b); (void)hipFree(b); });   // give the idle blocks back and retry
+        reap(true);
+        trim(p, 0, dev_release);   // give the idle blocks back and retry
         if (hipMalloc(&q, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
     }
     p.size_[q] = bytes;
@@ -80,12 +138,29 @@ void dev_free(void *q)
     std::lock_guard<std::mutex> g(g_mu);
     auto d = g_dev_of.find(q);
     if (d == g_dev_of.end()) { (void)hipFree(q); return; }   // not ours
-    Pool &p = g_dev[d->second];
-    auto it = p.size_.find(q);
-    if (it == p.size_.end()) { (void)hipFree(q); return; }
-    p.free_.emplace(it->second, q);
-    p.free_bytes += it->second;
-    trim(p, kDevCacheCap, [](void *b) { g_dev_of.erase(b); (void)hipFree(b); });
+    dev_return(q, d->second);
+}
+
+void dev_free_after(void *q, hipStream_t s)
+{
+    if (!q) return;
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, s) != hipSuccess) {
+        (void)hipGetLastError();
+        if (ev) (void)hipEventDestroy(ev);
+        (void)hipStreamSynchronize(s);   // cannot defer: order the free after the stream the slow way
+        dev_free(q);
+        return;
+    }
+    std::lock_guard<std::mutex> g(g_mu);
+    auto d = g_dev_of.find(q);
+    if (d == g_dev_of.end()) {   // not ours: a plain free after the stream
+        (void)hipEventSynchronize(ev);
+        (void)hipEventDestroy(ev);
+        (void)hipFree(q);
+        return;
+    }
+    g_deferred.push_back(Deferred{q, d->second, ev});
 }
 
 void *pin_alloc(size_t bytes)
@@ -114,7 +189,7 @@ void pin_free(void *q)
     g_pin_live.erase((uintptr_t)q);
     g_pin.free_.emplace(it->second, q);
     g_pin.free_bytes += it->second;
-    trim(g_pin, kPinCacheCap, [](void *b) { (void)hipHostFree(b); });
+    trim(g_pin, pin_cache_cap(), [](void *b) { (void)hipHostFree(b); });
 }
 
 size_t pin_size(const void *q)
@@ -135,4 +210,14 @@ bool pin_contains(const void *q, size_t n)
     return (uintptr_t)q >= it->first && (uintptr_t)q + n <= it->first + it->second;
 }
 
+void trim_caches()
+{
+    std::lock_guard<std::mutex> g(g_mu);
+    reap(true);
+    for (auto &p : g_dev) trim(p, 0, dev_release);
+    trim(g_pin, 0, [](void *b) { (void)hipHostFree(b); });
+}
+
 }  // namespace kpw
+
+extern "C" void kpw_trim_caches(void) { kpw::trim_caches(); }

@@ -5,18 +5,27 @@
 // and page buffers cost more than encoding a row group (hipFree also synchronises the whole
 // device).  Freed blocks are kept per device (per size, best fit within 2x) and handed to the
 // next allocation.  A block goes back to the cache only when no queued work can still touch
-// it: the callers free after synchronising the stream that used it (Engine / writer teardown,
-// buffer growth after a sync).
+// it: the callers free after synchronising the stream that used it (Engine / writer teardown),
+// or hand it over with dev_free_after(stream) (buffer growth: the block returns once the
+// stream's queued work has passed an event, without a device-wide synchronisation).
+//
+// Idle memory kept: KPW_DEV_CACHE_GB per device (default 96 of 288 GB: C5 runs 8 writers per
+// GPU and re-opens them every file) and KPW_PIN_CACHE_GB of pinned host memory (default 48);
+// kpw_trim_caches() (kpw_gpu.h) releases every idle block, e.g. before a co-located consumer
+// allocates.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stddef.h>
 
 namespace kpw {
 
 void *dev_alloc(size_t bytes);     // on the current device; nullptr on failure
 void dev_free(void *p);            // nullptr ok
+void dev_free_after(void *p, hipStream_t s);   // back to the cache once s has run what it queued so far
 void *pin_alloc(size_t bytes);     // page-locked host memory; nullptr on failure
 void pin_free(void *p);            // nullptr ok
 size_t pin_size(const void *p);    // usable bytes of a pin_alloc block containing p (0 if none)
 bool pin_contains(const void *p, size_t n);   // [p, p+n) inside one live pin_alloc block
+void trim_caches();                // release every idle block (device pools and pinned)
 
 }  // namespace kpw

@@ -316,7 +316,12 @@ static int acquire_fill(kpw_writer *w)
     }
     StageBuf &b = w->buf[k];
     const size_t need = w->gap_ + stage_flush_bytes() + (64ull << 20);
-    if (b.cap < need && alloc_buf(w, b, need)) return wfail(w, KPW_ERR_NOMEM, "device stage buffer allocation failed");
+    if (b.cap < need && alloc_buf(w, b, need)) {
+        std::lock_guard<std::mutex> g(w->mu);
+        b.state = BUF_FREE;   // not taken: the caller has no fill buffer (w->fill stays -1)
+        w->cv.notify_all();
+        return wfail(w, KPW_ERR_NOMEM, "device stage buffer allocation failed");
+    }
     if (trace_on()) w->t_acquire += now_ms() - ta;
     b.gap = w->gap_;
     b.len = w->gap_;
@@ -878,6 +883,7 @@ static void worker_main(kpw_writer *w, int x)
 {
     (void)hipSetDevice(w->eng.device);
     Worker &W = w->wk[x];
+    StreamOrder order(W.eng->stream);   // this worker's buffers are used on its engine stream
     for (;;) {
         Job j;
         hipEvent_t prev_carry;
@@ -938,8 +944,13 @@ static int submit(kpw_writer *w, int kind, int64_t n_exact)
             F.state = BUF_QUEUED;
         }
         if (int st = acquire_fill(w)) {
-            std::lock_guard<std::mutex> g(w->mu);
-            F.state = BUF_FREE;
+            // F's records were accepted by earlier writes and cannot be encoded now: sticky,
+            // so every later write / getDataSize / close reports it instead of a short file
+            {
+                std::lock_guard<std::mutex> g(w->mu);
+                F.state = BUF_FREE;
+            }
+            set_fatal(w, st, "stage buffer for the next records unavailable: " + w->err);
             return st;
         }
         next = w->fill;
@@ -1309,6 +1320,7 @@ static int write_until_full_bulk(kpw_writer *w, const uint8_t *data, const uint6
         return wfail(w, KPW_ERR_UNSUPPORTED,
                      "write_until_full: batches over 65536 records with HDFS alignment: use write + getDataSize");
     if (int st = drain(w)) return st;
+    StreamOrder order(w->eng.stream);
     if (int st = flush_slot(w)) return st;
     if (hipEventRecord(w->buf[w->fill].copied, w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "event record failed");
     if (int st = materialize(w, w->buf[w->fill], w->eng.stream)) return wfail(w, st, "stage buffer rebuild failed");
@@ -1433,6 +1445,7 @@ static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offse
     if (full) *full = 0;
     if (w->closed) return KPW_ERR_STATE;
     if (int st = observe_failure(w)) return st;
+    if (w->fill < 0) return wfail(w, KPW_ERR_STATE, "no stage buffer (an earlier failure)");
     if (!n) return KPW_OK;
     if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
     if (w->model_on && n > model_max_batch()) w->model_on = false;   // bulk path: cuts planned on the GPU
@@ -1548,6 +1561,10 @@ extern "C" int kpw_writer_file_bytes(const kpw_writer *w, const uint8_t **bytes,
     if (!w->closed) return KPW_ERR_STATE;
     *bytes = w->fw->memory_data();
     *len = w->fw->memory_size();
+    if (!*bytes && *len) {   // the contiguous copy of a multi-chunk file could not be allocated
+        *len = 0;
+        return KPW_ERR_NOMEM;
+    }
     return KPW_OK;
 }
 

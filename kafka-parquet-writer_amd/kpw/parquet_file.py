@@ -39,17 +39,20 @@ class ParquetProperties:
     """ParquetFile.ParquetProperties (ParquetFile.java:105-122).
 
     The output stream itself is a local path or memory.  hadoop_conf (a dict of Hadoop
-    configuration keys) only selects parquet-mr's row-group alignment: when fs.defaultFS is on a
-    block file system (the reference writes under new Path(fs.defaultFS, targetDir),
-    KafkaProtoParquetWriter.java:137-141) ParquetFileWriter uses PaddingAlignment with the
-    file system's block size (dfs.blocksize, default 128 MiB) and ParquetWriter's
-    MAX_PADDING_SIZE_DEFAULT (8 MiB): row groups are sized to end at HDFS block boundaries and
-    zero padding fills a block's last <= 8 MiB.  dfs_block_size / max_padding_size set the
-    same explicitly (0 = NoAlignment, a local file system)."""
+    configuration keys) only selects parquet-mr's row-group alignment: when the file's path is
+    on a block file system ParquetFileWriter uses PaddingAlignment with the file system's block
+    size (dfs.blocksize, default 128 MiB) and ParquetWriter's MAX_PADDING_SIZE_DEFAULT (8 MiB):
+    row groups are sized to end at HDFS block boundaries and zero padding fills a block's last
+    <= 8 MiB.  The reference writes under targetDir = new Path(fs.defaultFS, builder.targetDir)
+    (KafkaProtoParquetWriter.java:137-141), so the file system is the resolved path's: a
+    target_dir with its own scheme ("file:///data") wins over fs.defaultFS, as in Hadoop's
+    Path(parent, child).  dfs_block_size / max_padding_size set the same explicitly (0 =
+    NoAlignment, a local file system).  Byte parity of padded files with parquet-mr is checked
+    against the oracle only (the reference holds no padded fixture): parity unpinned."""
 
     def __init__(self, hadoop_conf=None, block_size=128 * MiB, compression_codec_name=UNCOMPRESSED,
                  page_size=128 * MiB, enable_dictionary=True, writer_version=1, dfs_block_size=None,
-                 max_padding_size=8 * MiB):
+                 max_padding_size=8 * MiB, target_dir=None):
         self.hadoop_conf = hadoop_conf
         self.block_size = int(block_size)
         self.compression_codec_name = int(compression_codec_name)
@@ -61,8 +64,7 @@ class ParquetProperties:
         if dfs_block_size is None:
             dfs_block_size = 0
             conf = hadoop_conf if isinstance(hadoop_conf, dict) else {}
-            fs = str(conf.get("fs.defaultFS", ""))
-            scheme = fs.split("://", 1)[0].lower() if "://" in fs else ""
+            scheme = resolved_scheme(str(conf.get("fs.defaultFS", "")), target_dir)
             if scheme in HDFS_SCHEMES:
                 dfs_block_size = _hadoop_size(conf.get("dfs.blocksize", 128 * MiB))
         self.dfs_block_size = int(dfs_block_size)
@@ -75,6 +77,16 @@ class ParquetProperties:
         effective_dictionary = 1
         return _PropsC(self.block_size, self.page_size, MiB, effective_dictionary, self.compression_codec_name,
                        self.writer_version, 0, self.dfs_block_size, self.max_padding_size)
+
+
+def resolved_scheme(default_fs, target_dir=None):
+    """Scheme of new Path(default_fs, target_dir) (org.apache.hadoop.fs.Path(Path, Path)): the
+    child's scheme when it has one, otherwise the parent's."""
+    def scheme(u):
+        u = str(u or "")
+        head = u.split("/", 1)[0]
+        return head[:-1].lower() if head.endswith(":") and len(head) > 2 else ""
+    return scheme(target_dir) or scheme(default_fs)
 
 
 def _hadoop_size(v):

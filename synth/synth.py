@@ -102,6 +102,25 @@ def generate(kind, seed, n, start=0, param=0, alloc=None):
     return data, offsets
 
 
+def per_record_loop(kind, write_fn, data_size_fn, handle, data, offsets, start, n, max_file_size):
+    """The reference WorkerThread loop in C (synth/loop.c): records [start, start+n) written
+    ONE at a time, getDataSize() after each, stop after the first with getDataSize() >=
+    max_file_size.  kind "kpw": write_fn / data_size_fn are kpw_writer_write /
+    kpw_writer_data_size (ctypes functions); "oracle": kpwo_write / kpwo_data_size.
+    Returns (records written, full, status, last getDataSize())."""
+    L = lib()
+    fn = L.loop_kpw if kind == "kpw" else L.loop_oracle
+    fn.restype = ctypes.c_uint64
+    fn.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64,
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int64)]
+    full, st, last = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int64(0)
+    got = fn(ctypes.cast(write_fn, ctypes.c_void_p), ctypes.cast(data_size_fn, ctypes.c_void_p), handle,
+             data.ctypes.data, offsets.ctypes.data + 8 * start, n, max_file_size, ctypes.byref(full), ctypes.byref(st),
+             ctypes.byref(last))
+    return int(got), bool(full.value), st.value, last.value
+
+
 def records(data, offsets):
     return [bytes(data[int(offsets[i]):int(offsets[i + 1])]) for i in range(len(offsets) - 1)]
 

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_header_symbols():
     L = kpw.load_library()
     hdr = open(os.path.join(ROOT, "include", "kpw_gpu.h")).read()
-    declared = set(re.findall(r"\b(kpw_(?:writer|encoder|host)_[a-z_]+)\s*\(", hdr))
+    declared = set(re.findall(r"\b(kpw_[a-z_]+)\s*\(", hdr))
     assert declared == set(_lib.EXPORTED)
     for sym in declared:
         assert hasattr(L, sym), sym
@@ -91,3 +91,19 @@ def test_properties_hdfs_alignment():
     p = kpw.ParquetProperties(dfs_block_size=3 * MiB, max_padding_size=MiB)
     c = p.to_c()
     assert (c.dfs_block_size, c.max_padding_size) == (3 * MiB, MiB)
+
+
+def test_properties_alignment_follows_resolved_target_path():
+    """targetDir = new Path(fs.defaultFS, builder.targetDir) (KafkaProtoParquetWriter.java:137-141):
+    a target dir with its own scheme decides the file system, otherwise fs.defaultFS does."""
+    from kpw.parquet_file import resolved_scheme
+    MiB = 1 << 20
+    assert resolved_scheme("hdfs://nn:8020", "/data/out") == "hdfs"
+    assert resolved_scheme("hdfs://nn:8020", "file:///data/out") == "file"
+    assert resolved_scheme("file:///", "webhdfs://nn/x") == "webhdfs"
+    p = kpw.ParquetProperties(hadoop_conf={"fs.defaultFS": "hdfs://nn:8020"}, target_dir="file:///tmp/out")
+    assert p.dfs_block_size == 0
+    p = kpw.ParquetProperties(hadoop_conf={"fs.defaultFS": "file:///"}, target_dir="hdfs://nn/out")
+    assert p.dfs_block_size == 128 * MiB
+    p = kpw.ParquetProperties(hadoop_conf={"fs.defaultFS": "hdfs://nn:8020"}, target_dir="/rel/out")
+    assert p.dfs_block_size == 128 * MiB
