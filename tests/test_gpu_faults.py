@@ -78,7 +78,7 @@ def test_write_failure_mid_file(tmp_path, mode):
                 except Exception:  # noqa: BLE001
                     failed_at = a
                     break
-                if pf.get_data_size() < 0:
+                if pf._L.kpw_writer_data_size(pf._h) < 0:   # the failure surfaced at getDataSize
                     break
         else:
             L = pf._L
