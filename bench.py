@@ -421,6 +421,9 @@ def main():
                     help="maxFileSize of the per-record leg (reference default 1 GiB, KafkaProtoParquetWriter.java:462)")
     ap.add_argument("--per-record-page-kb", type=int, default=128 * 1024,
                     help="pageSize of the per-record leg (reference default = blockSize, KafkaProtoParquetWriter.java:474)")
+    ap.add_argument("--per-record-mp-page-kb", type=int, default=1024,
+                    help="pageSize of a second per-record leg with page cuts inside row groups (pageSize(...), "
+                         "KafkaProtoParquetWriter.java:656-659; 0 = skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -523,10 +526,13 @@ def main():
         g = b_job / (ms_job * 1e-3) / 1e9 if ms_job > 0 else 0.0
         stage_roof[k] = dict(kernels=STAGE_KERNELS[k], alg_bytes_per_job=int(b_job), ms_per_job=round(ms_job, 4),
                              gbps=round(g, 1), frac=round(g / HBM_PEAK_GBPS, 5))
-    per_record = None
+    per_record = per_record_mp = None
     if args.per_record_records and world == 1:
         per_record = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_records, local_rank,
                                     args.per_record_max_file_mb * MiB, args.per_record_page_kb * 1024)
+        if args.per_record_mp_page_kb:   # pageSize < blockSize: page cuts inside row groups (size probes)
+            per_record_mp = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_records, local_rank,
+                                           args.per_record_max_file_mb * MiB, args.per_record_mp_page_kb * 1024)
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         threads = args.cpu_threads or host_threads()
@@ -559,6 +565,7 @@ def main():
         "roofline": roof,
         "stage_roofline": stage_roof,
         "per_record": per_record,
+        "per_record_multipage": per_record_mp,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -87,6 +87,12 @@ public:
     int encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
                hipStream_t user_stream, BatchOut &out);
     int copy_pages(uint64_t off, uint64_t len, void *host);
+    // Multi-page regime: the records [0, n) are the open row group's prefix (no row-group cut
+    // inside it).  Per column: the pages ColumnWriterV1 cut within them (a cut after record
+    // n - 1 included) and those pages' header + compressed bytes, which is what
+    // ColumnChunkPageWriter.getMemSize() adds to getBufferedSize() (the writer's size model).
+    int probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, std::vector<int32_t> &npages,
+                    std::vector<int64_t> &flushed);
     const std::string &error() const { return err_; }
     // Alternate the page output buffers between encodes, so the previous encode's pages can
     // still be read (D2H on another stream) while this one runs.  The caller orders this
@@ -151,6 +157,9 @@ private:
     int run_rle(std::vector<RleJob> &jobs, uint32_t &nptiles, uint32_t &netiles, RleScratch &sc);
     // multi-page regime (engine_mp.cpp)
     bool mp_ = false;
+    bool probe_ = false;                 // encode() is a probe_pages call
+    std::vector<int32_t> probe_npages_;
+    std::vector<int64_t> probe_flushed_;
     int encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                   const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out);
     int mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vector<int64_t>> &cuts);

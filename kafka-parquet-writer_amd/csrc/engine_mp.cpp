@@ -431,6 +431,34 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     a.sp = mp_spp.as<const uint64_t *>(); a.next_rg_size = T;
     if (opt_idx_.empty()) { a.E = nullptr; a.gend = nullptr; }
 
+    if (probe_) {
+        // probe_pages: the open row group's prefix [0, ne) -> the pages every column cut inside it
+        // (cuts <= ne, a cut at ne included) and their header + compressed bytes, i.e.
+        // ColumnChunkPageWriter.getMemSize() after record ne - 1
+        std::vector<std::vector<int64_t>> pc;
+        MpRun pr;
+        int rs = mp_cuts(a, 0, (int64_t)ne, pc);
+        if (rs) return rs;
+        rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr);
+        if (rs) return rs;
+        probe_npages_.assign(nc, 0);
+        probe_flushed_.assign(nc, 0);
+        for (int c = 0; c < nc; c++) {
+            size_t i = 0;
+            for (const PageOut &p : pr.cols[c]) {
+                if (p.page_type == KPW_DICTIONARY_PAGE) continue;
+                if (i < pc[c].size()) {
+                    probe_flushed_[c] += (int64_t)page_header(p, cols[c].phys).size() + p.compressed_size;
+                    probe_npages_[c]++;
+                }
+                i++;
+            }
+        }
+        out.records_consumed = 0;
+        out.open_records = (int64_t)ne;
+        CK(hipStreamSynchronize(st));
+        return KPW_OK;
+    }
     uint64_t acc_len = 0;
     const uint64_t per_rec = std::max<uint64_t>(1, Ptot / ne);
     int64_t guess = std::max<int64_t>(1000, (int64_t)(2 * (uint64_t)T / per_rec));
@@ -519,6 +547,21 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     CK(hipEventSynchronize(ev_[7]));
     for (int i = 0; i < 10; i++) stage_ms[i] = 0;
     CK(hipEventElapsedTime(&stage_ms[7], ev_[0], ev_[7]));
+    return KPW_OK;
+}
+
+int Engine::probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, std::vector<int32_t> &npages,
+                        std::vector<int64_t> &flushed)
+{
+    if (!mp_) return fail(KPW_ERR_STATE, "probe_pages: single-page regime (no page cuts inside row groups)");
+    BatchOut out;
+    probe_ = true;
+    const int st = encode(d_data, d_off, n, false, props.block_size, nullptr, out);
+    probe_ = false;
+    if (st) return st;
+    if (out.invalid_record >= 0) return fail(KPW_ERR_INVALID_PROTO, "probe_pages: invalid record in a modelled row group");
+    npages = probe_npages_;
+    flushed = probe_flushed_;
     return KPW_OK;
 }
 

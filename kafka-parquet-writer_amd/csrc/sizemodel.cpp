@@ -130,7 +130,8 @@ int64_t SizeModel::Col::mem() const
 
 bool SizeModel::init(const std::vector<ColInfo> &cols, const kpw_props &p)
 {
-    if (p.writer_version != 1 || p.page_size < p.block_size) return false;
+    if (p.writer_version != 1) return false;
+    multi_ = p.page_size < p.block_size;
     page_size_ = p.page_size;
     block_size_ = p.block_size;
     next_rg_size_ = p.block_size;
@@ -158,10 +159,19 @@ void SizeModel::reset_store()
     for (Col &k : cols_) {
         k.dl = RleCount();
         k.data = 0;
+        k.flushed = 0;
+        k.pages = 0;
         k.value_count = 0;
         k.next_check = 100;   // props.getMinRowCountForPageSizeCheck()
     }
     record_count_ = 0;
+}
+
+void SizeModel::restart(int64_t next_rg_size)
+{
+    reset_store();
+    next_mem_check_ = 100;
+    next_rg_size_ = next_rg_size;
 }
 
 // parser.parseFrom(record.value()) validity + presence + raw sizes (K1's rules)
@@ -205,13 +215,14 @@ bool SizeModel::scan(const uint8_t *d, uint64_t len)
 int64_t SizeModel::buffered() const
 {
     int64_t s = 0;
-    for (const Col &k : cols_) s += k.mem();
+    for (const Col &k : cols_) s += k.mem() + k.flushed;
     return s;
 }
 
 int SizeModel::add(const uint8_t *rec, uint64_t len)
 {
     if (!scan(rec, len)) return INVALID;
+    bool cut = false;
     for (size_t c = 0; c < cols_.size(); c++) {
         Col &k = cols_[c];
         const bool present = seen_[c] != 0;
@@ -220,14 +231,39 @@ int SizeModel::add(const uint8_t *rec, uint64_t len)
         // ColumnWriterV1.accountForValueWritten
         if (++k.value_count > k.next_check) {
             const int64_t mem = k.mem();
-            if (mem > page_size_) return LEAVE;   // writePage inside the row group
+            if (mem > page_size_) {
+                // writePage inside the row group: the check restarts at half this page's
+                // values; the page's header + compressed bytes join pageWriter.getMemSize()
+                // (finish_pages, from the GPU)
+                k.next_check = k.value_count / 2;
+                k.value_count = 0;
+                k.dl = RleCount();
+                k.data = 0;
+                k.pages++;
+                cut = true;
+                continue;
+            }
             float t = (float)k.value_count * (float)page_size_;
             t = t / (float)mem;
             k.next_check = java_f2i((float)k.value_count + t) / 2 + 1;
         }
     }
-    // InternalParquetRecordWriter.write -> checkBlockSizeReached
     ++record_count_;
+    return cut ? PAGES : block_check();
+}
+
+int SizeModel::finish_pages(const std::vector<int32_t> &npages, const std::vector<int64_t> &flushed)
+{
+    if (npages.size() != cols_.size() || flushed.size() != cols_.size()) return MISMATCH;
+    for (size_t c = 0; c < cols_.size(); c++)
+        if (npages[c] != cols_[c].pages) return MISMATCH;
+    for (size_t c = 0; c < cols_.size(); c++) cols_[c].flushed = flushed[c];
+    return block_check();
+}
+
+// InternalParquetRecordWriter.write -> checkBlockSizeReached
+int SizeModel::block_check()
+{
     if (record_count_ >= next_mem_check_) {
         const int64_t mem = buffered();
         const int64_t rec_size = mem / record_count_;

@@ -11,16 +11,20 @@
 //     -> invalid) giving presence and the raw (plain-equivalent) size of every column;
 //   - per column ColumnWriterV1's buffered size: definition-level RunLengthBitPackingHybrid
 //     encoder bytes emitted so far (counted, no bytes kept) + FallbackValuesWriter
-//     rawDataByteSize / PlainValuesWriter size / BooleanPlainValuesWriter (count+7)/8;
-//   - ColumnWriterV1.accountForValueWritten's sampled page check (a page cut inside the row
-//     group leaves the model: the writer then asks the GPU);
+//     rawDataByteSize / PlainValuesWriter size / BooleanPlainValuesWriter (count+7)/8, plus
+//     ColumnChunkPageWriter.getMemSize(): the header + compressed bytes of the pages this
+//     column already cut in the open row group;
+//   - ColumnWriterV1.accountForValueWritten's sampled page check.  A page cut (pageSize <
+//     blockSize) resets the column's page state here, and the cut page's header + compressed
+//     size comes from the GPU (the writer encodes the open row group's prefix, Engine::
+//     probe_pages) before the record's row-group check: add() returns PAGES and finish_pages()
+//     completes the record with those sizes;
 //   - InternalParquetRecordWriter.checkBlockSizeReached's sampled row-group check with Java's
 //     float/long arithmetic.
 //
 // It decides row-group cuts on the host for this loop; the GPU encodes exactly those records
-// (the encoder's own planner plans the same cut, checked per row group).  Only PARQUET_1_0
-// with single-page chunks is modelled (the reference's configuration: pageSize defaults to
-// blockSize, KafkaProtoParquetWriter.java:473-474); other configurations keep the GPU path.
+// (the encoder's own planner plans the same cut, checked per row group).  PARQUET_1_0 only
+// (the reference's writer version, ParquetFile.java:42-50); PARQUET_2_0 keeps the GPU path.
 #pragma once
 #include <stdint.h>
 #include <vector>
@@ -44,32 +48,44 @@ struct RleCount {
 
 class SizeModel {
 public:
-    enum { OK = 0, CUT = 1, INVALID = -1, LEAVE = -2 };
-    // false if the configuration is outside the model (v2, multi-page)
+    enum { OK = 0, CUT = 1, PAGES = 2, INVALID = -1, MISMATCH = -3 };
+    // false if the configuration is outside the model (v2)
     bool init(const std::vector<ColInfo> &cols, const kpw_props &props);
     // One record: OK, CUT (a row group ends with this record), INVALID (parseFrom would
-    // throw; nothing changed), LEAVE (a page cut: the model stops tracking this file).
+    // throw; nothing changed), PAGES (at least one column cut a page with this record: call
+    // finish_pages with the flushed page bytes before anything else).
     int add(const uint8_t *rec, uint64_t len);
+    // Completes a PAGES record: per column the pages cut in the open row group so far and their
+    // header + compressed bytes (from the GPU).  OK, CUT, or MISMATCH (page counts differ from
+    // the model's: the two restatements disagree, a bug).
+    int finish_pages(const std::vector<int32_t> &npages, const std::vector<int64_t> &flushed);
     int64_t buffered() const;               // columnStore.getBufferedSize()
     int64_t record_count() const { return record_count_; }
+    bool multi_page() const { return multi_; }
     // nextRowGroupSize for the open row group (HDFS alignment: set after each cut from the
     // file position; blockSize otherwise)
     void set_next_rg_size(int64_t t) { next_rg_size_ = t; }
+    // a fresh row group (resynchronisation after the GPU planned the cuts)
+    void restart(int64_t next_rg_size);
 
 private:
     struct Col {
         int32_t field_number, wire_type, phys, optional, vsize;
         RleCount dl;
         int64_t data = 0;                   // raw bytes (non-boolean) or boolean values
+        int64_t flushed = 0;                // pageWriter.getMemSize(): cut pages, header + compressed
+        int32_t pages = 0;                  // pages cut in the open row group
         int32_t value_count = 0, next_check = 100;
-        int64_t mem() const;
+        int64_t mem() const;                // rl + dl + data buffered (the page check's memSize)
     };
     bool scan(const uint8_t *rec, uint64_t len);
+    int block_check();                      // checkBlockSizeReached after a record: OK / CUT
     void reset_store();
     std::vector<Col> cols_;
     std::vector<int16_t> fmap_;             // field number (< 1024) -> column
     std::vector<uint8_t> seen_;
     std::vector<uint32_t> raw_;
+    bool multi_ = false;
     int64_t page_size_ = 0, block_size_ = 0, next_rg_size_ = 0;
     int64_t record_count_ = 0, next_mem_check_ = 100;
 };

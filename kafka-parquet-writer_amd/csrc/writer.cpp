@@ -222,7 +222,15 @@ struct kpw_writer {
     bool closed = false;
     std::string err;
     SizeModel model;
-    bool model_on = false;
+    bool model_ok = false;             // the configuration has a size model (PARQUET_1_0)
+    bool model_on = false;             // the model tracks the open row group (per-record path)
+    // multi-page regime: probes of the open row group's cut pages (Engine::probe_pages) on their
+    // own engine (the workers' engines may be encoding row groups meanwhile)
+    Engine peng;
+    DevBuf pr_off;                     // device boundaries of the fill buffer's records
+    PinnedBuf pr_h;
+    uint64_t fill_gen = 0, pr_gen = ~0ull;   // fill buffer generation / the one pr_off describes
+    size_t pr_up = 0;                  // boundaries of that generation already on the device
     bool dirty = false;                // records appended since the last PLANNED job (model off)
     bool pending_cut = false;          // an EXACT job may not be in the file yet (lastRowGroupEndPos stale)
     DevBuf probe_off;                  // write_until_full on the bulk path: offsets of staged prefixes
@@ -331,6 +339,7 @@ static int acquire_fill(kpw_writer *w)
     b.ncarry_expected = 0;
     b.first_new_global = w->num_records;
     w->fill = k;
+    w->fill_gen++;
     return KPW_OK;
 }
 
@@ -1025,7 +1034,11 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
     // the open row group of a job lands in the next buffer's gap (its wire bytes are a small
     // multiple of its buffered size for every schema but pathological ones; see materialize)
     gap_ = std::max<uint64_t>(64ull << 20, 2 * (uint64_t)eng.props.block_size) + 4096;
-    model_on = model.init(eng.cols, eng.props);
+    model_ok = model.init(eng.cols, eng.props);
+    model_on = model_ok;
+    if (model_ok && model.multi_page()) {
+        if (int st = peng.init(eng.device, schema, props)) return st;
+    }
     for (int x = 0; x < nworkers; x++) wk[x].th = std::thread(worker_main, this, x);
     return acquire_fill(this);
 }
@@ -1170,10 +1183,68 @@ static int stage_record(kpw_writer *w, const uint8_t *src, uint64_t len)
     return KPW_OK;
 }
 
+// boundary i of a buffer's records (carried, then appended), as boundaries() lays them out
+static uint64_t boundary_at(const StageBuf &B, size_t i)
+{
+    if (B.carry.empty()) return i == 0 ? B.gap : B.ends.data()[i - 1];
+    return i < B.carry.size() ? B.carry[i] : B.ends.data()[i - B.carry.size()];
+}
+
+// Multi-page regime: the pages every column cut in the open row group up to its record m - 1,
+// and their header + compressed bytes (ColumnChunkPageWriter.getMemSize), from a GPU encode of
+// the open row group's first m records.  In the model path those are the fill buffer's first m
+// records (an EXACT job leaves the next buffer with no carried records; a resynchronisation
+// materialises its carried ones in place first).
+static int probe_flushed(kpw_writer *w, size_t m, std::vector<int32_t> &np, std::vector<int64_t> &fl)
+{
+    StageBuf &F = w->buf[w->fill];
+    Engine &P = w->peng;
+    StreamOrder order(P.stream);
+    if (int st = flush_slot(w)) return st;
+    if (hipEventRecord(F.copied, w->copy_stream) != hipSuccess || hipStreamWaitEvent(P.stream, F.copied, 0) != hipSuccess)
+        return wfail(w, KPW_ERR_DEVICE, "probe: staging order failed");
+    // boundaries [0, m] on the device, uploaded incrementally (records are only appended)
+    if (w->pr_gen != w->fill_gen) { w->pr_gen = w->fill_gen; w->pr_up = 0; }
+    const size_t nb = m + 1;
+    if (nb * 8 > w->pr_off.cap) {
+        if (w->pr_off.ensure(std::max<size_t>(nb * 16, 1u << 20))) return wfail(w, KPW_ERR_NOMEM, "probe offsets");
+        w->pr_up = 0;
+    }
+    if (nb > w->pr_up) {
+        const size_t k = nb - w->pr_up;
+        if (w->pr_h.ensure(k * 8)) return wfail(w, KPW_ERR_NOMEM, "probe offsets");
+        uint64_t *h = (uint64_t *)w->pr_h.p;
+        for (size_t i = 0; i < k; i++) h[i] = boundary_at(F, w->pr_up + i);
+        if (hipMemcpyAsync(w->pr_off.as<uint64_t>() + w->pr_up, h, k * 8, hipMemcpyHostToDevice, P.stream) != hipSuccess)
+            return wfail(w, KPW_ERR_DEVICE, "probe: H2D of offsets failed");
+        w->pr_up = nb;
+    }
+    if (int st = P.probe_pages(F.d, w->pr_off.as<uint64_t>(), m, np, fl)) return wfail(w, st, P.error());
+    return KPW_OK;
+}
+
+// A record the model reported PAGES for: its row-group check with the cut pages' sizes.
+static int model_pages(kpw_writer *w, size_t m, int &r)
+{
+    std::vector<int32_t> np;
+    std::vector<int64_t> fl;
+    if (int st = probe_flushed(w, m, np, fl)) {
+        set_fatal(w, st, "page-size probe failed: " + w->err);   // the record is staged: no retry
+        return st;
+    }
+    r = w->model.finish_pages(np, fl);
+    if (r == SizeModel::MISMATCH) {
+        set_fatal(w, KPW_ERR_DEVICE, "page cuts of the size model and the GPU differ");
+        return KPW_ERR_DEVICE;
+    }
+    return KPW_OK;
+}
+
 // write / write_until_full with the size model on: records go one by one through the model
-// (O(columns) each) and the slot; an invalid record stops the batch right there (the
-// reference throws at parseFrom, KafkaProtoParquetWriter.java:270-276); a row-group cut hands
-// the fill buffer, which then holds exactly that row group, to the worker.
+// (O(columns) each, plus a GPU probe of the open row group when a column cuts a page) and the
+// slot; an invalid record stops the batch right there (the reference throws at parseFrom,
+// KafkaProtoParquetWriter.java:270-276); a row-group cut hands the fill buffer, which then
+// holds exactly that row group, to the worker.
 static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n, int64_t max_file_size,
                           uint64_t *n_accepted, int *full)
 {
@@ -1182,7 +1253,7 @@ static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *of
     for (; i < n; i++) {
         const uint8_t *rec = data + offsets[i];
         const uint64_t len = offsets[i + 1] - offsets[i];
-        const int r = w->model.add(rec, len);
+        int r = w->model.add(rec, len);
         if (r == SizeModel::INVALID) {
             w->failed_record = w->num_records;
             w->err = "Invalid proto message received (record " + std::to_string(w->failed_record) + ")";
@@ -1194,25 +1265,8 @@ static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *of
         StageBuf &F = w->buf[w->fill];
         F.ends.push_back(F.len);
         w->num_records++;
-        if (r == SizeModel::LEAVE) {
-            // a page cut inside the row group (pageSize reached first): the GPU plans from here on
-            w->model_on = false;
-            w->dirty = true;
-            i++;
-            if (max_file_size < 0) {   // plain write: stage the rest on the bulk path
-                const uint64_t bytes = offsets[n] - offsets[i];
-                if (i < n) {
-                    if (int st = grow_fill(w, bytes)) return st;
-                    StageBuf &G = w->buf[w->fill];
-                    const uint64_t delta = G.len - offsets[i];
-                    if (int st = stage_bytes(w, data + offsets[i], bytes)) return st;
-                    if (int st = wait_direct(w)) return st;
-                    for (uint64_t k = i + 1; k <= n; k++) G.ends.push_back(offsets[k] + delta);
-                    w->num_records += (int64_t)(n - i);
-                    i = n;
-                }
-            }
-            break;
+        if (r == SizeModel::PAGES) {
+            if (int st = model_pages(w, nbounds(F) - 1, r)) return st;
         }
         if (r == SizeModel::CUT) {
             const int64_t nrec = F.ncarry_expected + (int64_t)F.ends.size();
@@ -1240,6 +1294,46 @@ static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *of
     }
     if (n_accepted) *n_accepted = i;
     return rc;
+}
+
+// Back to the per-record model after bulk writes (GPU-planned cuts): encode what is staged
+// (the row groups it completes reach the file; the open row group's records are carried to
+// the fill buffer), then replay the open row group's records through the model from its start
+// (page probes included).  The GPU planner left them open, so the replay cannot cut.
+static int model_resync(kpw_writer *w)
+{
+    if (w->dirty)
+        if (int st = submit(w, JOB_PLANNED, 0)) return st;
+    if (int st = drain(w)) return st;
+    if (int st = observe_failure(w)) return st;
+    StageBuf &F = w->buf[w->fill];
+    if (int st = flush_slot(w)) return st;
+    if (hipEventRecord(F.copied, w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "event record failed");
+    if (int st = materialize(w, F, w->eng.stream)) return wfail(w, st, "stage buffer rebuild failed");
+    std::vector<uint64_t> hb;
+    boundaries(F, hb);
+    const size_t nrec = hb.size() - 1;
+    w->model.restart(w->aligned ? w->fw->next_row_group_size() : w->eng.props.block_size);
+    w->fill_gen++;   // boundaries changed in place: re-upload probe offsets
+    F.ncarry_expected = (int64_t)(F.carry.empty() ? 0 : F.carry.size() - 1);
+    if (nrec) {
+        std::vector<uint8_t> bytes(hb[nrec] - hb[0]);
+        if (hipStreamSynchronize(w->copy_stream) != hipSuccess ||
+            hipMemcpy(bytes.data(), F.d + hb[0], bytes.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return wfail(w, KPW_ERR_DEVICE, "model resync: D2H of the open row group failed");
+        for (size_t i = 0; i < nrec; i++) {
+            int r = w->model.add(bytes.data() + (hb[i] - hb[0]), hb[i + 1] - hb[i]);
+            if (r == SizeModel::PAGES)
+                if (int st = model_pages(w, i + 1, r)) return st;
+            if (r != SizeModel::OK) {
+                set_fatal(w, KPW_ERR_DEVICE, "model resync: the open row group does not replay as open");
+                return KPW_ERR_DEVICE;
+            }
+        }
+    }
+    w->model_on = true;
+    w->dirty = false;
+    return KPW_OK;
 }
 
 // e[i] = offsets[i + 1] + delta for i < n, split over a few host threads for large batches
@@ -1314,11 +1408,8 @@ static int ds_prefix(kpw_writer *w, uint64_t m, int64_t &ds, BatchOut &out)
 static int write_until_full_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n,
                                  int64_t max_file_size, uint64_t *n_accepted, int *full)
 {
-    if (w->eng.props.writer_version == 1 && w->eng.props.page_size < w->eng.props.block_size)
-        return wfail(w, KPW_ERR_UNSUPPORTED, "write_until_full: pageSize < blockSize (multi-page chunks): use write + getDataSize");
-    if (w->aligned)
-        return wfail(w, KPW_ERR_UNSUPPORTED,
-                     "write_until_full: batches over 65536 records with HDFS alignment: use write + getDataSize");
+    if ((w->eng.props.writer_version == 1 && w->eng.props.page_size < w->eng.props.block_size) || w->aligned)
+        return wfail(w, KPW_ERR_UNSUPPORTED, "write_until_full: no bulk search in this regime");   // v2 only (v1 is modelled)
     if (int st = drain(w)) return st;
     StreamOrder order(w->eng.stream);
     if (int st = flush_slot(w)) return st;
@@ -1448,7 +1539,17 @@ static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offse
     if (w->fill < 0) return wfail(w, KPW_ERR_STATE, "no stage buffer (an earlier failure)");
     if (!n) return KPW_OK;
     if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
-    if (w->model_on && n > model_max_batch()) w->model_on = false;   // bulk path: cuts planned on the GPU
+    if (w->model_ok) {
+        // write_until_full is record-at-a-time where the bulk search is not exact (multi-page
+        // chunks: a page cut can shrink the buffered size inside a row group; HDFS alignment:
+        // each limit follows the previous row group's end); otherwise large writes take the
+        // bulk path (GPU-planned cuts) and small ones the per-record model
+        const bool bulk_search = !w->model.multi_page() && !w->aligned;
+        const bool modelled = (max_file_size >= 0 && !bulk_search) || n <= model_max_batch();
+        if (!modelled) w->model_on = false;
+        else if (!w->model_on)
+            if (int st = model_resync(w)) return st;
+    }
     int rc;
     if (w->model_on) {
         rc = write_modelled(w, data, offsets, n, max_file_size, n_accepted, full);

@@ -79,6 +79,7 @@ def test_write_failure_mid_file(tmp_path, mode):
                     failed_at = a
                     break
                 if pf._L.kpw_writer_data_size(pf._h) < 0:   # the failure surfaced at getDataSize
+                    failed_at = b
                     break
         else:
             L = pf._L
