@@ -119,10 +119,10 @@ typedef struct kpw_page_info {
     int64_t null_count;
     int32_t has_min_max;
     int32_t min_len, max_len;   /* stats bytes (Statistics.getMinBytes/getMaxBytes) */
-    int32_t dl_byte_length;     /* v2: definition-level bytes at the start of the body (never compressed) */
+    int32_t dl_byte_length;     /* v2: definition-level bytes after the repetition levels (never compressed) */
     uint64_t min_off, max_off;  /* offsets into kpw_batch_info.stats_bytes */
     int32_t num_rows;           /* v2 DataPageHeaderV2.num_rows (= num_values: no repeated fields) */
-    int32_t reserved;
+    int32_t rl_byte_length;     /* v2: repetition-level bytes at the start of the body (never compressed) */
 } kpw_page_info;
 
 typedef struct kpw_chunk_info {

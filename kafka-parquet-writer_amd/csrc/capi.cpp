@@ -68,7 +68,7 @@ static void fill_info(kpw_encoder *e, kpw_batch_info *info)
         q.rl_encoding = p.rl_encoding; q.has_stats = p.has_stats; q.uncompressed_size = p.uncompressed_size;
         q.compressed_size = p.compressed_size; q.offset = p.offset; q.null_count = p.null_count; q.has_min_max = p.has_min_max;
         q.min_len = (int32_t)p.min.size(); q.max_len = (int32_t)p.max.size();
-        q.dl_byte_length = p.dl_byte_length; q.num_rows = p.num_rows;
+        q.dl_byte_length = p.dl_byte_length; q.num_rows = p.num_rows; q.rl_byte_length = p.rl_byte_length;
         q.min_off = e->stats.size(); e->stats += p.min;
         q.max_off = e->stats.size(); e->stats += p.max;
         e->pages.push_back(q);

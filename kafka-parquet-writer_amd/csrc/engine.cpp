@@ -112,8 +112,12 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     if (pr->block_size <= 0 || pr->page_size <= 0 || pr->dictionary_page_size <= 0) return fail(KPW_ERR_INVALID_ARG, "sizes");
     props = *pr;
     v2_ = pr->writer_version == 2;
-    // pages cut inside row groups: ColumnWriterV1 page checks + compressed-size row-group checks
-    mp_ = !v2_ && pr->page_size < pr->block_size;
+    // pages cut inside row groups: ColumnWriterV1 page checks / ColumnWriteStoreV2 size checks
+    // + compressed-size row-group checks.  v2 cuts a page once a column's buffered size is within
+    // 10% of pageSize, which a column can reach before its row group flushes even when pageSize
+    // >= blockSize (the reference default pageSize = blockSize): v2 plans pages unless pageSize
+    // is at least twice blockSize (the single-page path keeps a guard for that case).
+    mp_ = pr->page_size < pr->block_size || (v2_ && pr->page_size / 2 < pr->block_size);
     message_name = schema->message_name;
     proto_class = schema->proto_class ? schema->proto_class : schema->message_name;
     for (int c = 0; c < schema->num_columns; c++) {
@@ -313,7 +317,8 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     uint32_t npt = 0, net = 0;
     std::vector<RleJob> pj;
     std::vector<PlanStream> hs(nstreams);
-    std::vector<uint64_t *> cbits(nbool, nullptr);
+    std::vector<uint64_t *> &cbits = cbits_;
+    cbits.assign(nbool, nullptr);
     if (v2_) {
         for (uint32_t i = 0; i < nbool; i++) {
             const uint32_t c = bool_idx_[i];
@@ -852,6 +857,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         p.compressed_size = (int64_t)pclen[2 * ci + 1];
         p.offset = pcoff[2 * ci + 1];
         p.dl_byte_length = v2_ ? (int32_t)C.dl_len : 0;
+        p.rl_byte_length = v2_ ? C.rl0_len : 0;
         p.num_rows = (int32_t)(C.e - C.s);
         p.null_count = (int64_t)C.null_count;
         p.has_min_max = C.has_minmax ? 1 : 0;
@@ -893,7 +899,8 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
                                                  "(pageSize smaller than a column chunk): multi-page chunks are the next round");
         } else {
             const int64_t tol = (int64_t)((float)props.page_size * 0.1f);
-            const int64_t colmem = (int64_t)C.dl_len + (int64_t)(col.phys == KPW_BOOLEAN ? C.val_len - 4 : C.raw_bytes);
+            // buffered sizes: a width-0 level encoder emits nothing before toBytes
+            const int64_t colmem = (col.optional ? (int64_t)C.dl_len : 0) + (int64_t)(col.phys == KPW_BOOLEAN ? C.val_len - 4 : C.raw_bytes);
             if ((int64_t)props.page_size - colmem <= tol)
                 return fail(KPW_ERR_UNSUPPORTED, "column '" + col.name + "' could be split into several v2 pages "
                                                  "(within 10% of pageSize): multi-page chunks are the next round");

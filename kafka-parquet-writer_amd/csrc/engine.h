@@ -25,7 +25,8 @@ struct PageOut {
     uint64_t offset;            // into the device page buffer
     int64_t null_count;
     int32_t has_min_max;
-    int32_t dl_byte_length = 0; // DataPageV2: uncompressed definition-level bytes at the body start
+    int32_t dl_byte_length = 0; // DataPageV2: uncompressed definition-level bytes after the repetition levels
+    int32_t rl_byte_length = 0; // DataPageV2: uncompressed repetition-level bytes at the body start
     int32_t num_rows = 0;       // DataPageV2
     std::string min, max;       // Statistics.getMinBytes / getMaxBytes
 };
@@ -149,6 +150,7 @@ private:
     // v2 (PARQUET_2_0): boolean value streams, planner streams, DELTA streams
     bool v2_ = false;
     std::vector<DevBuf> col_cbits;
+    std::vector<uint64_t *> cbits_;    // per BOOLEAN column (bool_idx_ order): its value stream bits (this encode)
     DevBuf d_cbits_ptr, d_streams, d_djobs, d_blk_job, d_blk_min, d_blk_w, d_blk_sz, d_blk_off, d_btot, d_dense, d_pre, d_sfx,
         d_tile_sfx, d_tile_sfx_off, d_chunk_sfx, d_page_pre;
     hipEvent_t ev_[9] = {};
@@ -168,7 +170,7 @@ private:
     int grow_keep(DevBuf &b, size_t bytes, size_t keep);
     std::vector<DevBuf> mp_sp;
     DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_flag, mp_dch, mp_dtile_chunk, mp_dtile_first, mp_dtile_count, mp_dtile_raw,
-        mp_dtile_smin, mp_dtile_smax, mp_dtile_cnt, mp_dtile_sz, mp_ssz, mp_spp, mp_cstream, mp_acc;
+        mp_dtile_smin, mp_dtile_smax, mp_dtile_cnt, mp_dtile_sz, mp_ssz, mp_spp, mp_cstream, mp_bstream, mp_acc;
     uint8_t *pages_dev_ = nullptr;
     uint64_t pages_len_ = 0;
 };

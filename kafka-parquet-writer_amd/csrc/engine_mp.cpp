@@ -1,7 +1,8 @@
-// engine_mp.cpp — the multi-page regime: PARQUET_1_0 with pageSize < blockSize.
+// engine_mp.cpp — the multi-page regime: PARQUET_1_0 with pageSize < blockSize, and PARQUET_2_0.
 //
 // parquet-mr 1.10.1 cuts a column's page inside a row group (ColumnWriterV1
-// .accountForValueWritten), and from then on the row-group size check
+// .accountForValueWritten per column; v2: ColumnWriteStoreV2.sizeCheck per store, once a
+// column's page is within 10% of pageSize), and from then on the row-group size check
 // (InternalParquetRecordWriter.checkBlockSizeReached) counts the flushed pages by their
 // header + compressed bytes (ColumnChunkPageWriter.getMemSize) instead of their raw size.  A
 // row-group boundary therefore depends on the encoded and compressed sizes of the pages
@@ -104,6 +105,10 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     run.cols.assign(nc, {});
     std::vector<ChunkDesc> dch(nc), pg;
     std::vector<RleJob> ej;
+    std::vector<DeltaJob> dj;          // v2: DELTA streams of the pages (INT32/INT64: 1, BYTE_ARRAY: 2)
+    std::vector<uint32_t> dblk_job;    // v2: job of each DELTA block tile
+    std::vector<int> bool_pos(nc, -1);
+    for (size_t i = 0; i < bool_idx_.size(); i++) bool_pos[bool_idx_[i]] = (int)i;
     uint64_t ht_off = 0, ids_off = 0;
     std::vector<uint32_t> dtj, dfirst(nc), dcount(nc), ptj, pfirst, pcount;
     for (int c = 0; c < nc; c++) {
@@ -154,6 +159,32 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
                 P.id_job = (int32_t)ej.size();
                 ej.push_back(J);
             }
+            if (v2_ && cols[c].phys == KPW_BOOLEAN) {   // RunLengthBitPackingHybridValuesWriter(1)
+                RleJob J;
+                memset(&J, 0, sizeof(J));
+                J.src.kind = 0; J.src.ptr = cbits_[bool_pos[c]];
+                J.src.base = cols[c].optional ? 0 : (uint64_t)P.s;   // optional: rank of P.s, set on the device
+                J.len = (uint32_t)(pe - q); J.bw = 1;
+                P.bool_job = (int32_t)ej.size();
+                ej.push_back(J);
+            }
+            if (v2_ && P.is_dict && (cols[c].phys == KPW_INT32 || cols[c].phys == KPW_INT64 || cols[c].phys == KPW_BYTE_ARRAY)) {
+                // DefaultV2ValuesWriterFactory fallback writers, one DELTA stream per page
+                // (reset with the page); base = the page's rank offset, set on the device
+                P.dj0 = (int32_t)dj.size();
+                const bool ba = cols[c].phys == KPW_BYTE_ARRAY;
+                const uint64_t plen = (uint64_t)(pe - q);
+                const uint32_t nblk = (uint32_t)std::max<uint64_t>(1, plen > 1 ? (plen - 1 + 127) / 128 : 1);
+                for (int k = 0; k < (ba ? 2 : 1); k++) {
+                    DeltaJob Dj;
+                    memset(&Dj, 0, sizeof(Dj));
+                    Dj.flags = DJ_INACTIVE | (cols[c].phys == KPW_INT64 ? DJ_LONG : 0u) | (ba ? DJ_U32_SRC : 0u);
+                    Dj.blk0 = (uint32_t)dblk_job.size();
+                    Dj.nblk = nblk;
+                    dblk_job.insert(dblk_job.end(), nblk, (uint32_t)dj.size());
+                    dj.push_back(Dj);
+                }
+            }
             const uint32_t pt = (uint32_t)std::max<uint64_t>(1, ((uint64_t)(pe - q) + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
             pfirst.push_back((uint32_t)ptj.size());
             pcount.push_back(pt);
@@ -185,6 +216,26 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_page_off, 2 * npg * 8); ENS(d_page_len, 2 * npg * 8); ENS(d_page_pre, 2 * npg * 8); ENS(d_tot, 64); ENS(d_collision, 64);
     for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
+    DeltaArgs dla{};
+    if (v2_) {
+        ENS(d_dense, std::max<uint64_t>(1, ids_off) * 8); ENS(d_pre, std::max<uint64_t>(1, ids_off) * 4);
+        ENS(d_sfx, std::max<uint64_t>(1, ids_off) * 4);
+        ENS(d_tile_sfx, npt * 8); ENS(d_tile_sfx_off, npt * 8); ENS(d_chunk_sfx, npg * 8);
+        CK(hipMemsetAsync(d_chunk_sfx.p, 0, npg * 8, st));
+        for (const ChunkDesc &P : pg) {
+            if (P.dj0 < 0) continue;
+            if (cols[P.col].phys == KPW_BYTE_ARRAY) { dj[P.dj0].vals = d_pre.p; dj[P.dj0 + 1].vals = d_sfx.p; }
+            else dj[P.dj0].vals = d_dense.p;
+        }
+        const size_t nb = std::max<size_t>(1, dblk_job.size());
+        ENS(d_djobs, std::max<size_t>(1, dj.size()) * sizeof(DeltaJob)); ENS(d_blk_job, nb * 4); ENS(d_blk_min, nb * 8);
+        ENS(d_blk_w, nb * 4); ENS(d_blk_sz, nb * 8); ENS(d_blk_off, nb * 8); ENS(d_btot, std::max<size_t>(1, dj.size()) * 8);
+        if (!dblk_job.empty()) CK(hipMemcpyAsync(d_blk_job.p, dblk_job.data(), dblk_job.size() * 4, hipMemcpyHostToDevice, st));
+        dla.jobs = d_djobs.as<DeltaJob>(); dla.njobs = (uint32_t)dj.size(); dla.nblk = (uint32_t)dblk_job.size();
+        dla.blk_job = d_blk_job.as<uint32_t>(); dla.blk_min = d_blk_min.as<uint64_t>(); dla.blk_w = d_blk_w.as<uint32_t>();
+        dla.blk_sz = d_blk_sz.as<uint64_t>(); dla.blk_off = d_blk_off.as<uint64_t>(); dla.btot = d_btot.as<uint64_t>();
+        dla.seg = &seg_;
+    }
     CK(hipMemcpyAsync(d_ctile_chunk.p, ptj.data(), npt * 4, hipMemcpyHostToDevice, st));
     CK(hipMemcpyAsync(d_ctile_first.p, pfirst.data(), npg * 4, hipMemcpyHostToDevice, st));
     CK(hipMemcpyAsync(d_ctile_count.p, pcount.data(), npg * 4, hipMemcpyHostToDevice, st));
@@ -206,6 +257,8 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ap.page_pre = d_page_pre.as<uint64_t>();
     ap.mp = 1;
     ap.seg = &seg_;
+    ap.v2 = v2_ ? 1 : 0;
+    if (v2_) { ap.djobs = dla.jobs; ap.djobs_w = dla.jobs; ap.chunk_sfx = d_chunk_sfx.as<uint64_t>(); }
     ChunkArgs ad = ap;
     ad.ch = mp_dch.as<ChunkDesc>(); ad.nchunks = nc; ad.nctiles = ndt;
     ad.ctile_chunk = mp_dtile_chunk.as<uint32_t>(); ad.ctile_first = mp_dtile_first.as<uint32_t>();
@@ -224,10 +277,12 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         CK(hipMemcpyAsync(mp_dch.p, dch.data(), nc * sizeof(ChunkDesc), hipMemcpyHostToDevice, st));
         CK(hipMemsetAsync(d_collision.p, 0, 4, st));
         if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), st));
+        if (v2_ && !dj.empty()) CK(hipMemcpyAsync(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), hipMemcpyHostToDevice, st));
         launch_chunk_stats(ap, st);                          // K6 per page (+ nn, raw bytes)
         if (!ej.empty()) {
             int rs = run_rle(ej, enpt, enet, esc);
             if (rs) return rs;
+            if (v2_) launch_v2_bool_jobs(ap, d_jobs.as<RleJob>(), st);   // optional booleans: page rank base + length
         }
         launch_mp_pages_init(ap.ch, npg, ad.ch, ap.cols, d_jobs.as<RleJob>(), st);
         launch_dict(ad, d_jobs.as<RleJob>(), st);            // K2 per column chunk
@@ -237,6 +292,12 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         CK(hipGetLastError());
         if (!ej.empty()) launch_rle_structure(d_jobs.as<RleJob>(), (int)ej.size(), enpt, enet, esc, st);
         launch_mp_satisfy(ap.ch, ad.ch, nc, ap.cols, ap.ent_rec, ap.ent_boff, d_jobs.as<RleJob>(), st);
+        if (v2_) {   // the fallback pages' DELTA streams
+            launch_v2_delta_jobs(ap, dla.jobs, st);
+            launch_v2_dense(ap, d_dense.as<uint64_t>(), d_pre.as<uint32_t>(), d_sfx.as<uint32_t>(), d_tile_sfx.as<uint64_t>(),
+                            d_tile_sfx_off.as<uint64_t>(), d_chunk_sfx.as<uint64_t>(), st);
+            launch_delta_structure(dla, st);
+        }
         launch_layout(ap, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), st);
         CK(hipGetLastError());
         uint32_t coll = 0;
@@ -259,10 +320,15 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     launch_dict_page(ad, d_body.as<uint8_t>(), st);
     launch_chunk_write(ap, d_jobs.as<RleJob>(), d_body.as<uint8_t>(), st);
     if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), st);
+    if (v2_) {
+        launch_delta_write(dla, d_body.as<uint8_t>(), st);
+        launch_dba_suffixes(ap, d_pre.as<uint32_t>(), dla.jobs, d_tile_sfx_off.as<uint64_t>(), d_body.as<uint8_t>(), st);
+    }
     CK(hipGetLastError());
-    std::vector<uint64_t> poff(2 * npg), plen(2 * npg), pcoff(2 * npg), pclen(2 * npg);
+    std::vector<uint64_t> poff(2 * npg), plen(2 * npg), pcoff(2 * npg), pclen(2 * npg), ppre(2 * npg, 0);
     CK(hipMemcpyAsync(poff.data(), d_page_off.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(plen.data(), d_page_len.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
+    if (v2_) CK(hipMemcpyAsync(ppre.data(), d_page_pre.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
     // ---------------------------------------------------------------- K7
     if (props.codec == KPW_SNAPPY) {
@@ -289,7 +355,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         sa.frag_out = d_frag_out.as<uint8_t>(); sa.frag_len = d_frag_len.as<uint32_t>();
         sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
         sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
-        sa.page_pre = nullptr;
+        sa.page_pre = v2_ ? d_page_pre.as<uint64_t>() : nullptr;   // v2: levels in front, uncompressed
         if (seg_args(sa)) return KPW_ERR_NOMEM;
         launch_snappy(sa, st);
         launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), st);
@@ -301,9 +367,8 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         CK(hipStreamSynchronize(st));
         pages_dev_ = d_comp.as<uint8_t>();
         pages_len_ = ctot;
-    } else {
-        pcoff = poff;
-        pclen = plen;
+    } else {   // uncompressed: a (v2) page body starts at its level prefix
+        for (int p = 0; p < 2 * npg; p++) { pcoff[p] = poff[p] - ppre[p]; pclen[p] = plen[p] + ppre[p]; }
         pages_dev_ = d_body.as<uint8_t>();
         pages_len_ = body_tot;
     }
@@ -347,7 +412,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             PageOut d;
             d.page_type = KPW_DICTIONARY_PAGE;
             d.num_values = (int32_t)dch[C.col].dict_n;
-            d.encoding = KPW_ENC_PLAIN_DICTIONARY;
+            d.encoding = v2_ ? KPW_ENC_PLAIN : KPW_ENC_PLAIN_DICTIONARY;   // DictionaryValuesWriter v1 / v2 page encoding
             d.dl_encoding = d.rl_encoding = 0;
             d.has_stats = 0;
             d.uncompressed_size = (int64_t)plen[2 * p];
@@ -358,13 +423,24 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             out.push_back(d);
         }
         PageOut q;
-        q.page_type = KPW_DATA_PAGE;
+        q.page_type = v2_ ? KPW_DATA_PAGE_V2 : KPW_DATA_PAGE;
         q.num_values = (int32_t)(C.e - C.s);
-        q.encoding = (C.is_dict && !C.fallback) ? KPW_ENC_PLAIN_DICTIONARY : KPW_ENC_PLAIN;
+        if (!v2_) {
+            q.encoding = (C.is_dict && !C.fallback) ? KPW_ENC_PLAIN_DICTIONARY : KPW_ENC_PLAIN;
+        } else if (col.phys == KPW_BOOLEAN) {
+            q.encoding = KPW_ENC_RLE;
+        } else if (C.is_dict && !C.fallback) {
+            q.encoding = KPW_ENC_RLE_DICTIONARY;
+        } else {   // DefaultV2ValuesWriterFactory fallback writers
+            q.encoding = col.phys == KPW_BYTE_ARRAY ? KPW_ENC_DELTA_BYTE_ARRAY
+                       : (col.phys == KPW_INT32 || col.phys == KPW_INT64) ? KPW_ENC_DELTA_BINARY_PACKED : KPW_ENC_PLAIN;
+        }
         q.dl_encoding = col.optional ? KPW_ENC_RLE : KPW_ENC_BIT_PACKED;
         q.rl_encoding = KPW_ENC_BIT_PACKED;
         q.has_stats = 1;
-        q.uncompressed_size = (int64_t)plen[2 * p + 1];
+        q.dl_byte_length = v2_ ? (int32_t)C.dl_len : 0;
+        q.rl_byte_length = v2_ ? C.rl0_len : 0;
+        q.uncompressed_size = (int64_t)(plen[2 * p + 1] + ppre[2 * p + 1]);
         q.compressed_size = (int64_t)pclen[2 * p + 1];
         q.offset = pcoff[2 * p + 1];
         q.num_rows = (int32_t)(C.e - C.s);
@@ -416,9 +492,13 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         launch_prefix_raw(mp_ssz.as<uint32_t>(), ne, mp_sp[c].as<uint64_t>(), d_scan_tmp.as<uint64_t>(), st);
         sp[c] = mp_sp[c].as<uint64_t>();
     }
-    ENS(mp_spp, nc * sizeof(uint64_t *)); ENS(mp_cstream, nc * 4);
+    std::vector<int32_t> bstream(nc, -1);   // v2: planner stream of each BOOLEAN column's values
+    if (v2_)
+        for (size_t k = 0; k < bool_idx_.size(); k++) bstream[bool_idx_[k]] = (int32_t)(opt_idx_.size() + k);
+    ENS(mp_spp, nc * sizeof(uint64_t *)); ENS(mp_cstream, nc * 4); ENS(mp_bstream, nc * 4);
     CK(hipMemcpyAsync(mp_spp.p, sp.data(), nc * sizeof(uint64_t *), hipMemcpyHostToDevice, st));
     CK(hipMemcpyAsync(mp_cstream.p, cstream.data(), nc * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(mp_bstream.p, bstream.data(), nc * 4, hipMemcpyHostToDevice, st));
     uint64_t Ptot = 0;
     CK(hipMemcpyAsync(&Ptot, d_P.as<uint64_t>() + ne, 8, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
@@ -429,7 +509,8 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     a.col_stream = mp_cstream.as<int32_t>(); a.E = d_E.as<uint32_t>(); a.gend = d_gend.as<uint64_t>();
     a.gend_stride = gend_stride;
     a.sp = mp_spp.as<const uint64_t *>(); a.next_rg_size = T;
-    if (opt_idx_.empty()) { a.E = nullptr; a.gend = nullptr; }
+    a.col_bstream = mp_bstream.as<int32_t>(); a.streams = d_streams.as<PlanStream>(); a.v2 = v2_ ? 1 : 0;
+    if (opt_idx_.empty() && !(v2_ && !bool_idx_.empty())) { a.E = nullptr; a.gend = nullptr; }   // no planner streams
 
     if (probe_) {
         // probe_pages: the open row group's prefix [0, ne) -> the pages every column cut inside it

@@ -166,7 +166,7 @@ std::string page_header(const PageOut &pg, int phys)
             t.i32(3, pg.num_rows);
             t.i32(4, pg.encoding);
             t.i32(5, pg.dl_byte_length);
-            t.i32(6, 0);
+            t.i32(6, pg.rl_byte_length);
             if (!stats_empty(st)) write_stats(t, 8, st);
             t.end();
         } else {

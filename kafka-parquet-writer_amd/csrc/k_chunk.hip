@@ -578,6 +578,20 @@ __global__ void k_dict_jobs(ChunkDesc *ch, int nchunks, RleJob *jobs, uint32_t m
 
 // ------------------------------------------------------------------ layout (one block, all chunks)
 
+// v2 level streams of max level 0: ColumnWriterV2's RunLengthBitPackingHybridEncoder of width 0
+// after n writeInt(0) (parquet-mr 1.10.1 ParquetProperties.newLevelEncoder; v1 uses
+// DevNullValuesWriter instead): nothing for n = 0, one bit-packed run header for n < 8 (0x03),
+// else one RLE run header varint(n << 1) (the width-0 value takes no bytes).
+__device__ __forceinline__ uint32_t rle0_len(uint64_t n) { return n == 0 ? 0u : n < 8 ? 1u : varint_len32((uint32_t)(n << 1)); }
+__device__ __forceinline__ void rle0_put(uint8_t *p, uint64_t n)
+{
+    if (n == 0) return;
+    if (n < 8) { p[0] = 3; return; }
+    uint32_t v = (uint32_t)(n << 1);
+    while (v >= 0x80u) { *p++ = (uint8_t)(v | 0x80u); v >>= 7; }
+    *p = (uint8_t)v;
+}
+
 // Page bodies of every chunk, back to back: [dictionary page][data page].
 //   v1 data page (ColumnWriterV1.writePage): dl = 4-byte length + RLE (optional) | values
 //   v2 data page (ColumnWriterV2.writePage / writePageV2): dl = RLE without length (optional,
@@ -597,6 +611,11 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
             ChunkDesc &C = ch[ci];
             const DevCol &col = cols[C.col];
             C.dl_len = col.optional ? jobs[C.dl_job].total_bytes : 0;
+            C.rl0_len = 0;
+            if (v2) {   // every page: width-0 repetition levels; REQUIRED columns: width-0 definition levels
+                C.rl0_len = (int32_t)rle0_len((uint64_t)(C.e - C.s));
+                if (!col.optional) C.dl_len = C.rl0_len;
+            }
             uint64_t val = 0, dictp = 0;
             if (C.is_dict && !C.fallback) {
                 val = 1 + jobs[C.id_job].total_bytes;
@@ -619,7 +638,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
             }
             C.val_len = val;
             C.dictpage_len = dictp;
-            const uint64_t lv = col.optional ? (v2 ? 0 : 4) + C.dl_len : 0;
+            const uint64_t lv = v2 ? (uint64_t)C.rl0_len + C.dl_len : col.optional ? 4 + C.dl_len : 0;
             body = dictp + lv + val;
         }
         uint64_t t2;
@@ -629,9 +648,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
             const DevCol &col = cols[C.col];
             C.body_off = ex;
             const uint64_t dpage = ex + C.dictpage_len;
-            const uint64_t lv = col.optional ? (v2 ? 0 : 4) + C.dl_len : 0;
+            const uint64_t lv = v2 ? (uint64_t)C.rl0_len + C.dl_len : col.optional ? 4 + C.dl_len : 0;
             C.val_off = dpage + lv;
-            if (col.optional) jobs[C.dl_job].out_off = dpage + (v2 ? 0 : 4);
+            if (col.optional) jobs[C.dl_job].out_off = dpage + (v2 ? (uint64_t)C.rl0_len : 4);
             if (C.is_dict) jobs[C.id_job].out_off = C.val_off + 1;
             if (v2 && C.bool_job >= 0) jobs[C.bool_job].out_off = C.val_off + 4;
             if (v2 && C.dj0 >= 0 && C.fallback) {
@@ -668,6 +687,12 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_headers(const ChunkDesc *ch
         uint8_t *p = out + C.body_off + C.dictpage_len;
         const uint32_t l = (uint32_t)C.dl_len;
         p[0] = (uint8_t)l; p[1] = (uint8_t)(l >> 8); p[2] = (uint8_t)(l >> 16); p[3] = (uint8_t)(l >> 24);
+    }
+    if (v2) {   // width-0 repetition levels (+ definition levels of a REQUIRED column)
+        uint8_t *p = out + C.body_off + C.dictpage_len;
+        const uint64_t n = (uint64_t)(C.e - C.s);
+        rle0_put(p, n);
+        if (!col.optional) rle0_put(p + C.rl0_len, n);
     }
     uint8_t *p = out + C.val_off;
     if (C.is_dict && !C.fallback) p[0] = (uint8_t)C.bw;

@@ -343,6 +343,7 @@ __global__ void k_v2_delta_jobs(const ChunkDesc *ch, int nchunks, const DevCol *
     const int nj = cols[C.col].phys == 6 ? 2 : 1;
     for (int k = 0; k < nj; k++) {
         DeltaJob &J = dj[C.dj0 + k];
+        J.base = C.ids_off;   // multi-page: a page's rank offset inside its chunk (device-set)
         if (C.fallback) { J.n = C.nn; J.flags &= ~DJ_INACTIVE; }
         else { J.n = 0; J.flags |= DJ_INACTIVE; }
     }
@@ -413,6 +414,13 @@ void launch_v2_decide(const ChunkArgs &a, const RleJob *jobs, DeltaJob *djobs, h
     const dim3 g((a.nchunks + 255) / 256);
     hipLaunchKernelGGL(k_v2_decide, g, dim3(256), 0, s, a.ch, a.nchunks, jobs);
     hipLaunchKernelGGL(k_v2_delta_jobs, g, dim3(256), 0, s, (const ChunkDesc *)a.ch, a.nchunks, a.cols, djobs);
+}
+
+// multi-page: fallback decided per page (k_mp_dict_decide / k_mp_satisfy)
+void launch_v2_delta_jobs(const ChunkArgs &a, DeltaJob *djobs, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_v2_delta_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, (const ChunkDesc *)a.ch, a.nchunks, a.cols,
+                       djobs);
 }
 
 void launch_v2_dense(const ChunkArgs &a, uint64_t *dense, uint32_t *pre, uint32_t *sfx, uint64_t *tile_sfx, uint64_t *tile_sfx_off,

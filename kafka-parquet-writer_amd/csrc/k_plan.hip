@@ -330,21 +330,39 @@ __global__ void __launch_bounds__(256) k_str_sizes(const DevCol *cols, int c, ui
     sz[r] = pres ? 4u + col.slen[r] : 0u;
 }
 
-// rl(0) + dl + data buffered sizes of column c over the page [q, r):
-// dl = RunLengthBitPackingHybridEncoder bytes emitted since q (walker), data =
-// FallbackValuesWriter.rawDataByteSize / PlainValuesWriter size / boolean bit count.
-__device__ __forceinline__ uint64_t col_data_bytes(const PageCutArgs &a, int c, int64_t q, int64_t r)
-{
-    const DevCol &col = a.cols[c];
-    const uint64_t cnt = col.optional ? pc_at(col, (uint64_t)r) - pc_at(col, (uint64_t)q) : (uint64_t)(r - q);
-    if (col.phys == 0) return (cnt + 7) / 8;
-    if (col.phys == 6) return a.sp[c][r] - a.sp[c][q];
-    return cnt * (uint64_t)col.vsize;
-}
 __device__ __forceinline__ void walker_init(Walker &w, int64_t p)
 {
     w.p = p; w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
     w.pend_bytes = 0; w.pend_rle = 0; w.grp = 0; w.state = 0;
+}
+// v2 BOOLEAN column c: RLE bytes its value stream emitted since the page start (walker wb,
+// started by bool_walker_init at the page's first record); stream position = value rank for an
+// optional column
+__device__ __forceinline__ void bool_walker_init(const PageCutArgs &a, int c, Walker &wb, int64_t q)
+{
+    const DevCol &col = a.cols[c];
+    walker_init(wb, col.optional ? (int64_t)pc_at(col, (uint64_t)q) : q);
+}
+__device__ __forceinline__ uint64_t col_bool_rle(const PageCutArgs &a, int c, Walker &wb, int64_t r)
+{
+    const int k = a.col_bstream[c];
+    const DevCol &col = a.cols[c];
+    const PlanStream &S = a.streams[k];
+    const int64_t pos = col.optional ? (int64_t)pc_at(col, (uint64_t)r) : r;
+    return walker_query(wb, pos, S.bits, S.len, a.E + (uint64_t)k * (a.n + 1), a.gend + (uint64_t)k * a.gend_stride);
+}
+// rl(0) + dl + data buffered sizes of column c over the page [q, r):
+// dl = RunLengthBitPackingHybridEncoder bytes emitted since q (walker), data =
+// FallbackValuesWriter.rawDataByteSize / PlainValuesWriter size / boolean bit count (v1) or
+// boolean RLE bytes (v2, walker wb).
+__device__ __forceinline__ uint64_t col_data_bytes(const PageCutArgs &a, int c, Walker &wb, int64_t q, int64_t r)
+{
+    const DevCol &col = a.cols[c];
+    if (col.phys == 0 && a.v2) return col_bool_rle(a, c, wb, r);
+    const uint64_t cnt = col.optional ? pc_at(col, (uint64_t)r) - pc_at(col, (uint64_t)q) : (uint64_t)(r - q);
+    if (col.phys == 0) return (cnt + 7) / 8;
+    if (col.phys == 6) return a.sp[c][r] - a.sp[c][q];
+    return cnt * (uint64_t)col.vsize;
 }
 __device__ __forceinline__ uint64_t col_dl_bytes(const PageCutArgs &a, int c, Walker &w, int64_t r)
 {
@@ -363,7 +381,7 @@ __global__ void __launch_bounds__(64) k_page_cuts(PageCutArgs a)
 {
     const int c = blockIdx.x * 64 + threadIdx.x;
     if (c >= a.ncols) return;
-    Walker w;
+    Walker w, wb;
     int64_t q = a.s;
     walker_init(w, q);
     int32_t next = 100;
@@ -372,7 +390,7 @@ __global__ void __launch_bounds__(64) k_page_cuts(PageCutArgs a)
         const int64_t x = q + (int64_t)next;
         if (x >= a.h) break;
         const int32_t vc = next + 1;
-        const uint64_t mem = col_dl_bytes(a, c, w, x + 1) + col_data_bytes(a, c, q, x + 1);
+        const uint64_t mem = col_dl_bytes(a, c, w, x + 1) + col_data_bytes(a, c, wb, q, x + 1);
         if (mem > (uint64_t)a.page_size) {
             if (nc < a.cap) a.cuts[(uint64_t)c * a.cap + nc] = x + 1;
             else atomicOr(a.overflow, 1);
@@ -390,12 +408,66 @@ __global__ void __launch_bounds__(64) k_page_cuts(PageCutArgs a)
     a.ncuts[c] = nc < a.cap ? nc : a.cap;
 }
 
+// ColumnWriteStoreV2.sizeCheck (PARQUET_2_0), one wave for the whole store, lanes own columns:
+// the check runs after rowCount records once rowCount >= rowCountForNextSizeCheck (100 at a
+// row-group start).  Per column usedMem = rl + dl + data buffered since its page start (the
+// width-0 repetition / REQUIRED definition encoders emit nothing before toBytes); a column with
+// pageSize - usedMem <= (long)(pageSize * 0.1f) writes its page at rowCount; rowsToFillPage =
+// usedMem == 0 ? 10000 : (long)((float)rows) / usedMem * remainingMem (remainingMem = pageSize
+// after a write); the next check at rowCount + min(max(min over columns / 2, 100), 10000).
+__global__ void __launch_bounds__(64) k_page_cuts_v2(PageCutArgs a)
+{
+    __shared__ Walker Wd[MAX_COLS], Wb[MAX_COLS];
+    __shared__ int64_t Q[MAX_COLS];
+    __shared__ uint32_t NC[MAX_COLS];
+    const int lane = threadIdx.x;
+    for (int c = lane; c < a.ncols; c += 64) {
+        Q[c] = a.s;
+        NC[c] = 0;
+        walker_init(Wd[c], a.s);
+        if (a.col_bstream[c] >= 0) bool_walker_init(a, c, Wb[c], a.s);
+    }
+    const int64_t ps = a.page_size;
+    const int64_t tol = (int64_t)__fmul_rn((float)ps, 0.1f);
+    int64_t rc = 100;
+    while (a.s + rc <= a.h) {
+        const int64_t x1 = a.s + rc;   // rowCount = rc: records [s, x1) written
+        int64_t mn = INT64_MAX;
+        for (int c = lane; c < a.ncols; c += 64) {
+            const int64_t q = Q[c];
+            const int64_t used = (int64_t)(col_dl_bytes(a, c, Wd[c], x1) + col_data_bytes(a, c, Wb[c], q, x1));
+            const int64_t rows = x1 - q;
+            int64_t rem = ps - used;
+            if (rem <= tol) {   // ColumnWriterV2.writePage(rowCount)
+                if (NC[c] < a.cap) a.cuts[(uint64_t)c * a.cap + NC[c]] = x1;
+                else atomicOr(a.overflow, 1);
+                NC[c]++;
+                Q[c] = x1;
+                walker_init(Wd[c], x1);
+                if (a.col_bstream[c] >= 0) bool_walker_init(a, c, Wb[c], x1);
+                rem = ps;
+            }
+            const int64_t fill = used == 0 ? 10000 : ((int64_t)(float)rows / used) * rem;
+            mn = fill < mn ? fill : mn;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int64_t v = __shfl_xor(mn, o, 64);
+            mn = v < mn ? v : mn;
+        }
+        int64_t half = mn / 2;
+        half = half < 100 ? 100 : (half > 10000 ? 10000 : half);
+        rc += half;
+    }
+    for (int c = lane; c < a.ncols; c += 64) a.ncuts[c] = NC[c] < a.cap ? NC[c] : a.cap;
+}
+
 // checkBlockSizeReached over one row group from s with the page cuts above: memSize at
 // record count rc = sum over columns of (open page rl+dl+data) + (header + compressed
 // bytes of the pages already flushed to the ColumnChunkPageWriter).  One wave; lanes own
 // columns; r only grows, so each column's page cursor and walker advance monotonically.
 struct MpCol {
-    Walker w;
+    Walker w, wb;       // definition levels; v2 boolean values
     int64_t q;
     uint64_t pb;
     uint32_t ci, pad;
@@ -412,8 +484,9 @@ __device__ uint64_t mp_mem(const PageCutArgs &a, MpCol *S, int64_t r)
             m.q = a.cuts[(uint64_t)c * a.cap + m.ci];
             m.ci++;
             walker_init(m.w, m.q);
+            if (a.v2 && a.col_bstream[c] >= 0) bool_walker_init(a, c, m.wb, m.q);
         }
-        part += m.pb + col_dl_bytes(a, c, m.w, r) + col_data_bytes(a, c, m.q, r);
+        part += m.pb + col_dl_bytes(a, c, m.w, r) + col_data_bytes(a, c, m.wb, m.q, r);
     }
     return wave_sum(part);
 }
@@ -423,6 +496,7 @@ __global__ void __launch_bounds__(64) k_plan_mp(PageCutArgs a)
     __shared__ MpCol S[MAX_COLS];
     for (int c = threadIdx.x; c < a.ncols; c += 64) {
         walker_init(S[c].w, a.s);
+        if (a.v2 && a.col_bstream[c] >= 0) bool_walker_init(a, c, S[c].wb, a.s);
         S[c].q = a.s; S[c].pb = 0; S[c].ci = 0;
     }
     __syncthreads();
@@ -452,7 +526,8 @@ void launch_str_sizes(const DevCol *cols, int c, uint64_t n, uint32_t *sz, hipSt
 }
 void launch_page_cuts(const PageCutArgs &a, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_page_cuts, dim3((a.ncols + 63) / 64), dim3(64), 0, s, a);
+    if (a.v2) hipLaunchKernelGGL(k_page_cuts_v2, dim3(1), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_page_cuts, dim3((a.ncols + 63) / 64), dim3(64), 0, s, a);
 }
 void launch_plan_mp(const PageCutArgs &a, hipStream_t s)
 {

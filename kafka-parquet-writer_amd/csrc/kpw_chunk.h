@@ -71,6 +71,7 @@ struct DeltaArgs {
 void launch_delta_structure(const DeltaArgs &d, hipStream_t s);
 void launch_delta_write(const DeltaArgs &d, uint8_t *out, hipStream_t s);
 void launch_v2_decide(const ChunkArgs &a, const RleJob *jobs, DeltaJob *djobs, hipStream_t s);
+void launch_v2_delta_jobs(const ChunkArgs &a, DeltaJob *djobs, hipStream_t s);
 void launch_v2_dense(const ChunkArgs &a, uint64_t *dense, uint32_t *pre, uint32_t *sfx, uint64_t *tile_sfx, uint64_t *tile_sfx_off,
                      uint64_t *chunk_sfx, hipStream_t s);
 void launch_dba_suffixes(const ChunkArgs &a, const uint32_t *pre, const DeltaJob *djobs, const uint64_t *tile_sfx_off, uint8_t *out,

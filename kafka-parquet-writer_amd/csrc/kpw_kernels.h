@@ -154,9 +154,15 @@ struct PageCutArgs {
     const uint64_t *pbytes;        // k_plan_mp: [ncols * cap] header + compressed bytes of each cut page
     int64_t next_rg_size;
     int64_t *out;                  // k_plan_mp: [0] row-group end or -1, [1] memSize at n (open buffered)
+    // PARQUET_2_0: BOOLEAN values are a RunLengthBitPackingHybridValuesWriter stream (buffered
+    // size = RLE bytes emitted, walked like the level streams); pages are cut by the store
+    const int32_t *col_bstream;    // per column: its boolean value stream (E/gend index) or -1
+    const PlanStream *streams;     // the planner streams (bits / length of the boolean ones)
+    int32_t v2;
+    int32_t pad2;
 };
 void launch_str_sizes(const DevCol *cols, int c, uint64_t n, uint32_t *sz, hipStream_t s);
-void launch_page_cuts(const PageCutArgs &a, hipStream_t s);
+void launch_page_cuts(const PageCutArgs &a, hipStream_t s);   // v1 per column, v2 per store
 void launch_plan_mp(const PageCutArgs &a, hipStream_t s);
 
 struct ChunkDesc {
@@ -195,7 +201,7 @@ struct ChunkDesc {
     // a dictionary descriptor lists its pages [first_page, first_page + npages)
     int32_t owner;                 // page: dictionary descriptor index (-1 single-page regime)
     int32_t first_page, npages;    // dictionary descriptor: its pages
-    int32_t pad5;
+    int32_t rl0_len;               // v2: bytes of the width-0 repetition-level stream (layout)
 };
 
 // One DELTA_BINARY_PACKED stream (k_delta.hip).

@@ -122,16 +122,21 @@ void RleCount::write(uint32_t v)
     }
 }
 
-int64_t SizeModel::Col::mem() const
+int64_t SizeModel::Col::mem(bool v2) const
 {
-    // ColumnWriterV1: rl (DevNull) + dl + data buffered sizes
-    return (optional ? dl.out : 0) + (phys == KPW_BOOLEAN ? (data + 7) / 8 : data);
+    // ColumnWriterV1: rl (DevNull) + dl + data buffered sizes; ColumnWriterV2: width-0 level
+    // encoders emit nothing before toBytes, BOOLEAN values are RLE
+    const int64_t d = phys != KPW_BOOLEAN ? data : v2 ? bv.out : (data + 7) / 8;
+    return (optional ? dl.out : 0) + d;
 }
 
 bool SizeModel::init(const std::vector<ColInfo> &cols, const kpw_props &p)
 {
-    if (p.writer_version != 1) return false;
-    multi_ = p.page_size < p.block_size;
+    if (p.writer_version != 1 && p.writer_version != 2) return false;
+    v2_ = p.writer_version == 2;
+    // v2 cuts a page once a column is within 10% of pageSize, possible with pageSize >= blockSize
+    // (the engine plans v2 pages below 2 x blockSize alike, Engine::init)
+    multi_ = p.page_size < p.block_size || (v2_ && p.page_size / 2 < p.block_size);
     page_size_ = p.page_size;
     block_size_ = p.block_size;
     next_rg_size_ = p.block_size;
@@ -149,6 +154,7 @@ bool SizeModel::init(const std::vector<ColInfo> &cols, const kpw_props &p)
     }
     seen_.assign(cols_.size(), 0);
     raw_.assign(cols_.size(), 0);
+    bval_.assign(cols_.size(), 0);
     reset_store();
     next_mem_check_ = 100;
     return true;
@@ -163,8 +169,11 @@ void SizeModel::reset_store()
         k.pages = 0;
         k.value_count = 0;
         k.next_check = 100;   // props.getMinRowCountForPageSizeCheck()
+        k.bv = RleCount();
+        k.rows_written = 0;
     }
     record_count_ = 0;
+    v2_next_check_ = 100;
 }
 
 void SizeModel::restart(int64_t next_rg_size)
@@ -196,7 +205,11 @@ bool SizeModel::scan(const uint8_t *d, uint64_t len)
         }
         uint64_t v;
         switch (wt) {
-        case 0: if (!varint64(d, pos, end, v)) return false; raw_[c] = (uint32_t)cols_[c].vsize; break;
+        case 0:
+            if (!varint64(d, pos, end, v)) return false;
+            raw_[c] = (uint32_t)cols_[c].vsize;
+            bval_[c] = v != 0;   // CodedInputStream.readBool
+            break;
         case 1: if (end - pos < 8) return false; pos += 8; raw_[c] = 8; break;
         case 5: if (end - pos < 4) return false; pos += 4; raw_[c] = 4; break;
         default:   // 2: length-delimited (BYTE_ARRAY: 4-byte length + bytes)
@@ -215,7 +228,7 @@ bool SizeModel::scan(const uint8_t *d, uint64_t len)
 int64_t SizeModel::buffered() const
 {
     int64_t s = 0;
-    for (const Col &k : cols_) s += k.mem() + k.flushed;
+    for (const Col &k : cols_) s += k.mem(v2_) + k.flushed;
     return s;
 }
 
@@ -227,10 +240,16 @@ int SizeModel::add(const uint8_t *rec, uint64_t len)
         Col &k = cols_[c];
         const bool present = seen_[c] != 0;
         if (k.optional) k.dl.write(present ? 1u : 0u);
-        if (present) k.data += k.phys == KPW_BOOLEAN ? 1 : raw_[c];
+        if (present) {
+            if (k.phys != KPW_BOOLEAN) k.data += raw_[c];
+            else if (v2_) k.bv.write(bval_[c]);
+            else k.data += 1;
+        }
+        ++k.value_count;
+        if (v2_) continue;   // ColumnWriteStoreV2 checks the store after the record
         // ColumnWriterV1.accountForValueWritten
-        if (++k.value_count > k.next_check) {
-            const int64_t mem = k.mem();
+        if (k.value_count > k.next_check) {
+            const int64_t mem = k.mem(false);
             if (mem > page_size_) {
                 // writePage inside the row group: the check restarts at half this page's
                 // values; the page's header + compressed bytes join pageWriter.getMemSize()
@@ -248,7 +267,33 @@ int SizeModel::add(const uint8_t *rec, uint64_t len)
             k.next_check = java_f2i((float)k.value_count + t) / 2 + 1;
         }
     }
-    ++record_count_;
+    ++record_count_;   // InternalParquetRecordWriter.recordCount = ColumnWriteStoreV2.rowCount
+    if (v2_ && record_count_ >= v2_next_check_) {
+        // ColumnWriteStoreV2.sizeCheck: thresholdTolerance = (long)(pageSize * 0.1f);
+        // rowsToFillPage = (long)((float)rows) / usedMem * remainingMem
+        const int64_t tol = (int64_t)((float)page_size_ * 0.1f);
+        int64_t mn = INT64_MAX;
+        for (Col &k : cols_) {
+            const int64_t used = k.mem(true);
+            const int64_t rows = record_count_ - k.rows_written;
+            int64_t rem = page_size_ - used;
+            if (rem <= tol) {   // ColumnWriterV2.writePage(rowCount)
+                k.rows_written = record_count_;
+                k.value_count = 0;
+                k.dl = RleCount();
+                k.bv = RleCount();
+                k.data = 0;
+                k.pages++;
+                cut = true;
+                rem = page_size_;
+            }
+            const int64_t fill = used == 0 ? 10000 : ((int64_t)(float)rows / used) * rem;
+            if (fill < mn) mn = fill;
+        }
+        int64_t half = mn / 2;
+        half = half < 100 ? 100 : (half > 10000 ? 10000 : half);
+        v2_next_check_ = record_count_ + half;
+    }
     return cut ? PAGES : block_check();
 }
 

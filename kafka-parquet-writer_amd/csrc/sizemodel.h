@@ -22,9 +22,13 @@
 //   - InternalParquetRecordWriter.checkBlockSizeReached's sampled row-group check with Java's
 //     float/long arithmetic.
 //
+// PARQUET_2_0 (an explicit opt-in; the reference never selects it, ParquetFile.java:42-50):
+// ColumnWriteStoreV2.sizeCheck instead of the per-column page check (after the record, once
+// rowCount reaches rowCountForNextSizeCheck: a column within 10% of pageSize writes its page),
+// and BOOLEAN values counted as the RLE bytes of their RunLengthBitPackingHybridValuesWriter.
+//
 // It decides row-group cuts on the host for this loop; the GPU encodes exactly those records
-// (the encoder's own planner plans the same cut, checked per row group).  PARQUET_1_0 only
-// (the reference's writer version, ParquetFile.java:42-50); PARQUET_2_0 keeps the GPU path.
+// (the encoder's own planner plans the same cut, checked per row group).
 #pragma once
 #include <stdint.h>
 #include <vector>
@@ -49,7 +53,7 @@ struct RleCount {
 class SizeModel {
 public:
     enum { OK = 0, CUT = 1, PAGES = 2, INVALID = -1, MISMATCH = -3 };
-    // false if the configuration is outside the model (v2)
+    // false if the configuration is outside the model
     bool init(const std::vector<ColInfo> &cols, const kpw_props &props);
     // One record: OK, CUT (a row group ends with this record), INVALID (parseFrom would
     // throw; nothing changed), PAGES (at least one column cut a page with this record: call
@@ -76,7 +80,9 @@ private:
         int64_t flushed = 0;                // pageWriter.getMemSize(): cut pages, header + compressed
         int32_t pages = 0;                  // pages cut in the open row group
         int32_t value_count = 0, next_check = 100;
-        int64_t mem() const;                // rl + dl + data buffered (the page check's memSize)
+        RleCount bv;                        // v2 BOOLEAN: RunLengthBitPackingHybridValuesWriter of the values
+        int64_t rows_written = 0;           // v2: rowCount at this column's last page
+        int64_t mem(bool v2) const;         // rl + dl + data buffered (the page check's memSize)
     };
     bool scan(const uint8_t *rec, uint64_t len);
     int block_check();                      // checkBlockSizeReached after a record: OK / CUT
@@ -85,7 +91,9 @@ private:
     std::vector<int16_t> fmap_;             // field number (< 1024) -> column
     std::vector<uint8_t> seen_;
     std::vector<uint32_t> raw_;
-    bool multi_ = false;
+    std::vector<uint8_t> bval_;             // BOOLEAN columns: the record's value (last occurrence)
+    bool multi_ = false, v2_ = false;
+    int64_t v2_next_check_ = 100;           // ColumnWriteStoreV2.rowCountForNextSizeCheck
     int64_t page_size_ = 0, block_size_ = 0, next_rg_size_ = 0;
     int64_t record_count_ = 0, next_mem_check_ = 100;
 };

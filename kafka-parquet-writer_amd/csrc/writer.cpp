@@ -1408,8 +1408,10 @@ static int ds_prefix(kpw_writer *w, uint64_t m, int64_t &ds, BatchOut &out)
 static int write_until_full_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n,
                                  int64_t max_file_size, uint64_t *n_accepted, int *full)
 {
-    if ((w->eng.props.writer_version == 1 && w->eng.props.page_size < w->eng.props.block_size) || w->aligned)
-        return wfail(w, KPW_ERR_UNSUPPORTED, "write_until_full: no bulk search in this regime");   // v2 only (v1 is modelled)
+    // a page cut can shrink the buffered size inside a row group, and alignment moves each limit:
+    // those regimes are record-at-a-time through the size model (write_entry), never here
+    if (w->eng.multi_page() || w->aligned)
+        return wfail(w, KPW_ERR_UNSUPPORTED, "write_until_full: no bulk search with page cuts or HDFS alignment");
     if (int st = drain(w)) return st;
     StreamOrder order(w->eng.stream);
     if (int st = flush_slot(w)) return st;

@@ -69,7 +69,7 @@ class PageInfo(ctypes.Structure):
                 ("offset", ctypes.c_uint64), ("null_count", ctypes.c_int64), ("has_min_max", ctypes.c_int32),
                 ("min_len", ctypes.c_int32), ("max_len", ctypes.c_int32), ("dl_byte_length", ctypes.c_int32),
                 ("min_off", ctypes.c_uint64), ("max_off", ctypes.c_uint64), ("num_rows", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("rl_byte_length", ctypes.c_int32)]
 
 
 class ChunkInfo(ctypes.Structure):

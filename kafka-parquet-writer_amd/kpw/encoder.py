@@ -63,7 +63,7 @@ class Encoder:
                             dl_encoding=p.dl_encoding, uncompressed_size=p.uncompressed_size,
                             compressed_size=p.compressed_size, offset=p.offset, null_count=p.null_count,
                             has_min_max=p.has_min_max, min=stats[p.min_off:p.min_off + p.min_len],
-                            max=stats[p.max_off:p.max_off + p.max_len], dl_byte_length=p.dl_byte_length,
+                            max=stats[p.max_off:p.max_off + p.max_len], dl_byte_length=p.dl_byte_length, rl_byte_length=p.rl_byte_length,
                             num_rows=p.num_rows))
         return out
 

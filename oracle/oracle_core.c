@@ -1105,11 +1105,12 @@ static void pagestore_write_page(kpwo_writer *w, colw_t *c, const buf_t *body, i
  * compressed values; ParquetMetadataConverter.writeDataPageV2Header (is_compressed is
  * never set, so it is not serialised). */
 static void pagestore_write_page_v2(kpwo_writer *w, colw_t *c, int32_t rows, int32_t nulls, int32_t nvalues,
-                                    const buf_t *dl, int data_enc, const buf_t *data)
+                                    const buf_t *rl, const buf_t *dl, int data_enc, const buf_t *data)
 {
     buf_t comp = {0};
     page_compress(w, data, &comp);
-    const int32_t uncomp = (int32_t)(data->n + dl->n), compsz = (int32_t)(comp.n + dl->n);
+    const int32_t lv = (int32_t)(rl->n + dl->n);
+    const int32_t uncomp = (int32_t)data->n + lv, compsz = (int32_t)comp.n + lv;
     buf_t hdr = {0};
     tc_t t = {&hdr, {0}, 0};
     tc_i32(&t, 1, KPW_DATA_PAGE_V2);
@@ -1121,7 +1122,7 @@ static void pagestore_write_page_v2(kpwo_writer *w, colw_t *c, int32_t rows, int
     tc_i32(&t, 3, rows);
     tc_i32(&t, 4, data_enc);
     tc_i32(&t, 5, (int32_t)dl->n);
-    tc_i32(&t, 6, 0);
+    tc_i32(&t, 6, (int32_t)rl->n);
     if (!stats_empty(&c->pstats)) tc_statistics(&t, 8, &c->pstats);
     tc_struct_end(&t);
     buf_u8(&hdr, 0);
@@ -1131,6 +1132,7 @@ static void pagestore_write_page_v2(kpwo_writer *w, colw_t *c, int32_t rows, int
     if (!c->tstats_init) { stats_copy(&c->tstats, &c->pstats); c->tstats_init = 1; }
     else stats_merge(&c->tstats, &c->pstats);
     buf_put(&c->pages, hdr.p, hdr.n);
+    buf_put(&c->pages, rl->p, rl->n);
     buf_put(&c->pages, dl->p, dl->n);
     buf_put(&c->pages, comp.p, comp.n);
     if (c->ndata_encs == c->data_encs_cap) { c->data_encs_cap = c->data_encs_cap ? c->data_encs_cap * 2 : 16; c->data_encs = (int *)xrealloc(c->data_encs, (size_t)c->data_encs_cap * sizeof(int)); }
@@ -1139,21 +1141,41 @@ static void pagestore_write_page_v2(kpwo_writer *w, colw_t *c, int32_t rows, int
     buf_free(&comp);
 }
 
+/* RunLengthBitPackingHybridEncoder(bitWidth 0).toBytes() after n writeInt(0): the level encoder
+ * parquet-mr 1.10.1's ColumnWriterV2 builds for a max level of 0 (ParquetProperties
+ * .newLevelEncoder: always an RLE encoder in v2, unlike v1's DevNullValuesWriter): nothing
+ * for n = 0, one bit-packed run header (0x03) for n < 8, else varint(n << 1) of one RLE run. */
+static void rle0_bytes(int32_t n, buf_t *out)
+{
+    rle_t r;
+    rle_init(&r, 0);
+    for (int32_t i = 0; i < n; i++) rle_write(&r, 0);
+    rle_finish(&r);
+    buf_put(out, r.out.p, r.out.n);
+    buf_free(&r.out);
+}
+
 /* ColumnWriterV2.writePage(rowCount): dataColumn.getBytes()/getEncoding() first, then the
- * levels (max level 0 -> empty); RLE levels carry no length prefix in a v2 page. */
+ * levels; RLE levels carry no length prefix in a v2 page.  Every column is top-level and not
+ * repeated: the repetition levels are a width-0 stream, and so are the definition levels of
+ * REQUIRED columns (rle0_bytes). */
 static void colw_write_page_v2(kpwo_writer *w, colw_t *c, int64_t row_count)
 {
     const int32_t page_rows = (int32_t)(row_count - c->rows_written);
     c->rows_written = row_count;
-    buf_t data = {0}, dl = {0};
+    buf_t data = {0}, dl = {0}, rl = {0};
     const int enc = dataw_page(&c->data, &data);
+    rle0_bytes(c->value_count, &rl);
     if (c->ci->optional) {
         rle_finish(&c->dl);
         buf_put(&dl, c->dl.out.p, c->dl.out.n);
+    } else {
+        rle0_bytes(c->value_count, &dl);
     }
-    pagestore_write_page_v2(w, c, page_rows, (int32_t)c->pstats.nulls, c->value_count, &dl, enc, &data);
+    pagestore_write_page_v2(w, c, page_rows, (int32_t)c->pstats.nulls, c->value_count, &rl, &dl, enc, &data);
     buf_free(&data);
     buf_free(&dl);
+    buf_free(&rl);
     if (c->ci->optional) rle_reset(&c->dl);
     dataw_reset(&c->data);
     c->value_count = 0;

@@ -107,7 +107,8 @@ def compare_to_file(schema, data, offsets, fb, **kw):
                     st = dh.get(5, {})
                 else:   # DataPageHeaderV2
                     dh = h[8]
-                    got = (g["num_values"], g["null_count"], g["num_rows"], g["encoding"], g["dl_byte_length"], 0)
+                    got = (g["num_values"], g["null_count"], g["num_rows"], g["encoding"], g["dl_byte_length"],
+                           g["rl_byte_length"])
                     want = (dh[1], dh[2], dh[3], dh[4], dh[5], dh[6])
                     st = dh.get(8, {})
                 if got != want:

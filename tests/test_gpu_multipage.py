@@ -90,3 +90,50 @@ def test_multipage_writer_file_identical():
     assert fb == ob, pqwalk.first_difference(fb, ob)
     tbl = pq.read_table(io.BytesIO(fb))
     assert protoutil.table_columns(tbl, schema) == protoutil.decode_columns(schema, synth.records(data, offs))
+
+
+# ------------------------------------------------------------------ PARQUET_2_0 (A10 / f4)
+# ColumnWriteStoreV2.sizeCheck cuts pages for the whole store (a column within 10% of pageSize
+# writes its page; next check at rowCount + min(max(min rowsToFillPage / 2, 100), 10000)),
+# pages are DataPageV2 (width-0 repetition levels on every page, REQUIRED columns' width-0
+# definition levels, RLE booleans counted by their RLE bytes), DELTA fallback streams restart
+# on every page, and the row-group check counts flushed pages by header + levels + compressed
+# values.  Unreachable from the reference (ParquetFile.java:42-50 never selects v2): parity
+# against the oracle's restatement.
+
+@pytest.mark.parametrize("name,kind,param,n", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("codec", [0, 1], ids=["uncompressed", "snappy"])
+@pytest.mark.parametrize("block_size,page_size", [(256 * KiB, 8 * KiB), (128 * MiB, 16 * KiB), (64 * KiB, 1024)],
+                         ids=["rg256K_p8K", "rg128M_p16K", "rg64K_p1K"])
+def test_v2_multipage_matches_oracle(name, kind, param, n, codec, block_size, page_size):
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, 0xC0FFEE51 + kind, n, param=param)
+    errs = gh.compare_pages(schema, data, offs, codec=codec, block_size=block_size, page_size=page_size, writer_version=2)
+    assert not errs, "\n".join(errs[:12])
+
+
+def test_v2_multipage_fallback_mid_chunk():
+    # the page where the dictionary crosses dictPageSize and every later page fall back to
+    # DELTA_BYTE_ARRAY (query) with a fresh stream per page
+    import pqwalk
+    data, offs = _pairs_records(80000)
+    for codec in (0, 1):
+        errs = gh.compare_pages(synth.SAMPLE, data, offs, codec=codec, page_size=64 * KiB, writer_version=2)
+        assert not errs, "\n".join(errs[:12])
+    fb = oracle.encode_file(synth.SAMPLE, data, offs, oracle.make_props(codec=1, page_size=64 * KiB, writer_version=2))
+    encs = [p["header"][8][4] for p in pqwalk.pages(fb) if p["col"] == 0 and p["header"][1] == 3]
+    assert encs[0] == 8 and encs[-1] == 7, encs   # RLE_DICTIONARY first, DELTA_BYTE_ARRAY after the fallback
+
+
+def test_v2_multipage_writer_file_identical():
+    import kpw
+    import pqwalk
+    schema = synth.REC8
+    data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE53, 30000, param=0)
+    props = kpw.ParquetProperties(block_size=256 * 1024, page_size=16 * 1024, compression_codec_name=1, writer_version=2)
+    fb = gh.gpu_file(schema, data, offs, props, batches=3)
+    ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=256 * 1024, page_size=16 * 1024, codec=1,
+                                                                  writer_version=2))
+    assert fb == ob, pqwalk.first_difference(fb, ob)
+    tbl = pq.read_table(io.BytesIO(fb))
+    assert protoutil.table_columns(tbl, schema) == protoutil.decode_columns(schema, synth.records(data, offs))

@@ -228,7 +228,7 @@ def test_rotation_bulk_path(codec):
     assert sum(1 for _, f in files if f) >= 2
 
 
-def _per_record_against_oracle(schema, kind, seed, n, block_size, page_size, codec=1, bulk_first=0):
+def _per_record_against_oracle(schema, kind, seed, n, block_size, page_size, codec=1, bulk_first=0, writer_version=1):
     """The unchanged WorkerThread loop: one kpw_writer_write + one kpw_writer_data_size per record
     (after an optional bulk write of `bulk_first` records), every getDataSize() value compared
     with the oracle's, then the files.  Returns the per-record loop's wall time."""
@@ -236,9 +236,11 @@ def _per_record_against_oracle(schema, kind, seed, n, block_size, page_size, cod
     import kpw
     import pqwalk
     data, offs = synth.generate(kind, seed, n)
-    props = kpw.ParquetProperties(block_size=block_size, compression_codec_name=codec, page_size=page_size)
+    props = kpw.ParquetProperties(block_size=block_size, compression_codec_name=codec, page_size=page_size,
+                                  writer_version=writer_version)
     pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class), props)
-    ow = oracle.OracleWriter(schema, oracle.make_props(block_size=block_size, codec=codec, page_size=page_size))
+    ow = oracle.OracleWriter(schema, oracle.make_props(block_size=block_size, codec=codec, page_size=page_size,
+                                                       writer_version=writer_version))
     if bulk_first:
         pf.write_batch((data[:int(offs[bulk_first])], offs[:bulk_first + 1]))
         st, _ = ow.write_batch(data, offs[:bulk_first + 1])
@@ -304,3 +306,23 @@ def test_bulk_then_per_record_resync(page_kb):
     dt, nrg = _per_record_against_oracle(synth.REC8, synth.KIND_REC8, 56, 110_000, 1 * MiB, page_kb * 1024,
                                          bulk_first=80_000)
     assert nrg >= 2
+
+
+@pytest.mark.parametrize("page_kb", [16, 256], ids=["p16K", "p_eq_block"])
+def test_data_size_every_record_v2(page_kb):
+    """PARQUET_2_0 per-record loop: the size model runs ColumnWriteStoreV2.sizeCheck (store-level
+    page cuts, RLE boolean sizes) with page sizes from GPU probes; every getDataSize() equals the
+    oracle's and the file is byte-identical (pageSize = blockSize included: v2 cuts a page within
+    10% of pageSize)."""
+    dt, nrg = _per_record_against_oracle(synth.REC8, synth.KIND_REC8, 57, 60_000, 256 * 1024, page_kb * 1024,
+                                         writer_version=2)
+    assert nrg >= 2
+
+
+def test_rotation_v2_multipage():
+    """write_until_full under PARQUET_2_0 with pageSize = blockSize and poll()-sized batches:
+    record-at-a-time through the v2 size model."""
+    data, offs = synth.generate(synth.KIND_REC8, 58, 200000)
+    files = _rotate(synth.REC8, data, offs, 1536 * 1024, 256 * 1024, 1, chunk=70000, writer_version=2,
+                    page_size=256 * 1024, max_files=3)
+    assert sum(1 for _, f in files if f) >= 2

@@ -173,7 +173,10 @@ def test_delta_byte_array_matches_pyarrow(n):
     data, offs = synth.pack(recs)
     fb = oracle.encode_file(synth.SAMPLE, data, offs, oracle.make_props(writer_version=2, enable_dictionary=False))
     page = [p for p in pqwalk.pages(fb) if p["col"] == 0][0]
-    assert page["body"] == _arrow_v2_values(pa.array(words, type=pa.binary()), "DELTA_BYTE_ARRAY")
+    h = page["header"][8]
+    # the width-0 level streams of this REQUIRED column (ColumnWriterV2 level encoders) come first
+    assert (h[5], h[6]) == ((1, 1) if n < 8 else (len(_varint(n << 1)),) * 2)
+    assert page["body"][h[5] + h[6]:] == _arrow_v2_values(pa.array(words, type=pa.binary()), "DELTA_BYTE_ARRAY")
 
 
 def _sample_msg(**kw):
