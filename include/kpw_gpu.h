@@ -70,10 +70,12 @@ void kpw_trim_caches(void);
 /* The WorkerThread size-rotation loop (KafkaProtoParquetWriter.java:277-285,306-308):
  * writes records in order and stops right after the first one for which
  * getDataSize() >= max_file_size.  *n_accepted = records written, *full = 1 if the stop
- * condition fired (the caller then closes this file and opens the next).  The stop point is
- * found by encoding staged prefixes (segment checks + bisection), identical to the per-record
- * loop.  pageSize < blockSize (v1 multi-page chunks) returns KPW_ERR_UNSUPPORTED there: use
- * write + data_size per record.  An invalid record ends the batch as in kpw_writer_write. */
+ * condition fired (the caller then closes this file and opens the next).  Single-page chunks
+ * without HDFS alignment: the stop point is found by encoding staged prefixes (segment checks +
+ * bisection).  Multi-page chunks (page cuts shrink the buffered size inside a row group) and
+ * HDFS alignment: record at a time through the host getDataSize model, page sizes from GPU
+ * probes of the open row group.  Both are identical to the per-record loop.  An invalid record
+ * ends the batch as in kpw_writer_write. */
 int kpw_writer_write_until_full(kpw_writer *w, const uint8_t *data, const uint64_t *offsets,
                                 uint64_t n, int64_t max_file_size, uint64_t *n_accepted, int *full);
 

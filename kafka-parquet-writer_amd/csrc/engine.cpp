@@ -473,6 +473,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
                     D.flags = DJ_INACTIVE | (cols[c].phys == KPW_INT64 ? DJ_LONG : 0u) | (ba ? DJ_U32_SRC : 0u);
                     D.blk0 = (uint32_t)dblk_job.size();
                     D.nblk = nblk;
+                    D.prev = -1;   // one page per chunk: a fresh fallback writer
                     dblk_job.insert(dblk_job.end(), nblk, (uint32_t)dj.size());
                     dj.push_back(D);
                 }

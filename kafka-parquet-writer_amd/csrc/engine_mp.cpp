@@ -171,6 +171,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             if (v2_ && P.is_dict && (cols[c].phys == KPW_INT32 || cols[c].phys == KPW_INT64 || cols[c].phys == KPW_BYTE_ARRAY)) {
                 // DefaultV2ValuesWriterFactory fallback writers, one DELTA stream per page
                 // (reset with the page); base = the page's rank offset, set on the device
+                const int32_t prev0 = pg.size() > (size_t)D.first_page ? pg.back().dj0 : -1;   // this chunk's previous page
                 P.dj0 = (int32_t)dj.size();
                 const bool ba = cols[c].phys == KPW_BYTE_ARRAY;
                 const uint64_t plen = (uint64_t)(pe - q);
@@ -181,6 +182,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
                     Dj.flags = DJ_INACTIVE | (cols[c].phys == KPW_INT64 ? DJ_LONG : 0u) | (ba ? DJ_U32_SRC : 0u);
                     Dj.blk0 = (uint32_t)dblk_job.size();
                     Dj.nblk = nblk;
+                    Dj.prev = prev0 >= 0 ? prev0 + k : -1;
                     dblk_job.insert(dblk_job.end(), nblk, (uint32_t)dj.size());
                     dj.push_back(Dj);
                 }

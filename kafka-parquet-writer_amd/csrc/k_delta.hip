@@ -138,6 +138,44 @@ __global__ void k_delta_totals(DeltaJob *jobs, int njobs, const uint64_t *btot)
     J.total = J.hdr + btot[j];
 }
 
+// DeltaBinaryPackingValuesWriter.reset() clears neither deltaBlockBuffer nor bitWidths, and the
+// fallback writer lives on across a column chunk's pages (multi-page regime): a page whose first
+// block is partial writes the widths / padding slots the streams of the previous pages left.
+// Slot p (min-reduced delta) / width q as left before the stream whose predecessor is pj (an
+// inactive predecessor is a page that kept its dictionary: the fallback writer was fresh).
+__device__ uint64_t dj_stale_slot(const DeltaJob *jobs, int32_t pj, uint32_t p, const uint64_t *blk_min, uint64_t wmask)
+{
+    while (pj >= 0) {
+        const DeltaJob &P = jobs[pj];
+        if (P.flags & DJ_INACTIVE) return 0;
+        const uint64_t nd = P.n > 1 ? (uint64_t)P.n - 1 : 0;
+        if (nd) {
+            const uint32_t kl = (uint32_t)((nd - 1) / 128);
+            const DBlock L = dj_block(P, kl);
+            if (p < L.nd) return (dj_delta(P, L.d0 + p) - blk_min[P.blk0 + kl]) & wmask;
+            if (kl) return (dj_delta(P, L.d0 - 128 + p) - blk_min[P.blk0 + kl - 1]) & wmask;   // a full block
+        }
+        pj = P.prev;
+    }
+    return 0;
+}
+__device__ uint32_t dj_stale_width(const DeltaJob *jobs, int32_t pj, uint32_t q, const uint32_t *blk_w)
+{
+    while (pj >= 0) {
+        const DeltaJob &P = jobs[pj];
+        if (P.flags & DJ_INACTIVE) return 0;
+        const uint64_t nd = P.n > 1 ? (uint64_t)P.n - 1 : 0;
+        if (nd) {
+            const uint32_t kl = (uint32_t)((nd - 1) / 128);
+            const uint32_t nmb = (dj_block(P, kl).nd + 31) / 32;
+            if (q < nmb) return (blk_w[P.blk0 + kl] >> (8 * q)) & 0xffu;
+            if (kl) return (blk_w[P.blk0 + kl - 1] >> (8 * q)) & 0xffu;
+        }
+        pj = P.prev;
+    }
+    return 0;
+}
+
 __global__ void __launch_bounds__(64) k_delta_write(const DeltaJob *jobs, const uint32_t *blk_job, const uint64_t *blk_min,
                                                     const uint32_t *blk_w, const uint64_t *blk_off, uint8_t *out)
 {
@@ -162,7 +200,9 @@ __global__ void __launch_bounds__(64) k_delta_write(const DeltaJob *jobs, const 
     const uint32_t wc = blk_w[b], wp = k ? blk_w[b - 1] : 0u;
     uint32_t w[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) w[q] = (((uint32_t)q < nmb) ? (wc >> (8 * q)) : (wp >> (8 * q))) & 0xffu;
+    for (int q = 0; q < 4; q++)
+        w[q] = (uint32_t)q < nmb ? (wc >> (8 * q)) & 0xffu
+             : k ? (wp >> (8 * q)) & 0xffu : dj_stale_width(jobs, J.prev, (uint32_t)q, blk_w);
     uint8_t *o = base + J.hdr + blk_off[b];
     const uint64_t zm = dj_zigzag(J, m);
     const uint32_t mlen = varint_len64(zm);
@@ -182,7 +222,8 @@ __global__ void __launch_bounds__(64) k_delta_write(const DeltaJob *jobs, const 
         if (!wq) continue;
         uint64_t x;
         if (p < B.nd) x = (dj_delta(J, B.d0 + p) - m) & wmask;
-        else x = k ? ((dj_delta(J, B.d0 - 128 + p) - mprev) & wmask) : 0;   // stale deltaBlockBuffer slot
+        else x = k ? ((dj_delta(J, B.d0 - 128 + p) - mprev) & wmask)   // stale deltaBlockBuffer slot
+                   : dj_stale_slot(jobs, J.prev, p, blk_min, wmask);
         if (wq < 64) x &= (1ull << wq) - 1;
         const uint32_t bit = (p & 31) * wq;
         const uint32_t wi = bit >> 5, sh = bit & 31;

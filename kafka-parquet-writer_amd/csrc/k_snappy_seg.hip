@@ -180,27 +180,22 @@ __device__ __forceinline__ uint32_t put_lit_tag(sgg_u8 *o, uint32_t op, uint32_t
 }
 
 // per-workgroup global scratch
-struct SgScratch_ {
+struct SgScratch {
     uint16_t sig[65536];          // positions sorted by (hash, position)
     uint64_t bflag[SG_T];         // bit j of word t: sorted entry 64t+j starts a hash bucket
     uint64_t rec[SG_T * SG_RECS]; // copies found by the last parse, per segment
     uint32_t job[2 * SG_T][4];    // long literals: src, dst, len
 };
-typedef __attribute__((address_space(1))) SgScratch_ SgScratch;
 
-// setup: 16384 bucket counters (two uint16 per word), and the window of
-// sorted entries built in LDS before it is copied out with 16-byte stores
-constexpr uint32_t SG_CNTW = 8192;
-constexpr uint32_t SG_WIN = (65536 * 2 - SG_CNTW * 4) / 2 / 64 * 64;   // entries per window (48960)
+constexpr uint32_t SG_DATA = 65536 + 64;   // setup: the fragment's bytes (+ read padding)
 struct SgShared {
     union {
         uint16_t cand[65536];     // rounds: candidate (table entry) per position
         struct {
-            uint32_t cnt[SG_CNTW];        // setup: bucket counters
-            uint16_t win[SG_WIN];         // setup: the fragment (histogram), then sorted entries [base, base + SG_WIN)
+            uint32_t data[SG_DATA / 4];   // setup: the fragment, staged for the sort
+            uint32_t cnt[8192 + 2];       // setup: bucket counters, two uint16 per word; + a dummy
         } su;
     };
-    uint16_t ring[2][SG_W][64];   // setup: hashes of the next 16 position groups (all waves -> the scatter wave)
     uint64_t ibits[SG_T];         // inserted positions (bit q of word q/64)
     uint64_t entry[SG_T];
     uint64_t exitst[SG_T];
@@ -208,10 +203,16 @@ struct SgShared {
     uint32_t lfl[SG_T / 32];      // thread k inserted 64k-1
     uint32_t wf[SG_W], wv[SG_W];  // block scan
     uint32_t njobs;
-    uint32_t hwin;                // setup: end hash of the current window
     int frag;
     uint64_t prof[16];            // microbench phase counters (thread 0)
 };
+
+// 4 bytes at position p of the LDS-staged fragment
+__device__ __forceinline__ uint32_t lds_ld32(const SgShared &S, uint32_t p)
+{
+    const uint32_t d = p >> 2;
+    return __builtin_amdgcn_alignbyte(S.su.data[d + 1], S.su.data[d], p & 3);
+}
 
 __device__ __forceinline__ uint32_t cnt_add(SgShared &S, uint32_t h)
 {
@@ -336,7 +337,7 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
 
 }  // namespace
 
-constexpr size_t SEG_SCRATCH_BYTES = sizeof(SgScratch_);
+constexpr size_t SEG_SCRATCH_BYTES = sizeof(SgScratch);
 
 template <bool PROF>
 __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
@@ -393,37 +394,33 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         const uint64_t c_setup = pf ? clock64() : 0;
 
         // ------------------------------------------------ setup: sort positions by (hash, position)
-        // Counting sort with uint16 counters; positions are hashed from the fragment in global
-        // memory (L1/L2).  A histogram wave instruction covers 64 consecutive positions (periodic
-        // data spreads over several counters).  The scatter is one wave walking the positions in
-        // order (LDS atomics of one instruction on the same counter return in lane order:
-        // checked below, a violation hands the fragment on) into an LDS window of SG_WIN sorted
-        // entries; the window (whole buckets, hash range [h0, h1)) is checked and copied to the
-        // global permutation with 16-byte stores.  Two windows cover a typical fragment.
-        uint32_t *const dat = (uint32_t *)S.su.win;   // the fragment, staged for the histogram
+        // The fragment is staged in LDS; counting sort with uint16 counters.  A histogram wave
+        // instruction covers 64 consecutive positions (periodic data spreads over several
+        // counters).  The scatter is one wave walking the positions in order: LDS atomics of one
+        // instruction on the same counter return in lane order (checked below; a violation
+        // hands the fragment on).
         {
             const uintptr_t fb = (uintptr_t)in.base;
-            sgg_cu32 *src = (sgg_cu32 *)(fb & ~(uintptr_t)3);
+            const uint32_t *src = (const uint32_t *)(fb & ~(uintptr_t)3);
             const uint32_t sh = (uint32_t)(fb & 3);
             // only the dwords that cover [0, n) (+ the 16 bytes of read padding the page buffer
             // has) are loaded: a short fragment may end near the end of the buffer
-            const uint32_t nw = (n + sh + 3) / 4 + 1;
+            const uint32_t nw = (n + sh + 3) / 4 + 1;    // source dwords covering the fragment (+1)
             uint32_t v[17];
 #pragma unroll
             for (int i = 0; i < 17; i++) v[i] = (t * 16 + i < nw) ? src[t * 16 + i] : 0u;
 #pragma unroll
-            for (int i = 0; i < 16; i++) dat[t * 16 + i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
-            if (t < 16) dat[SG_T * 16 + t] = 0;
+            for (int i = 0; i < 16; i++) S.su.data[t * 16 + i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+            if (t < 16) S.su.data[SG_T * 16 + t] = 0;
+            for (uint32_t i = t; i <= tsize / 2; i += SG_T) S.su.cnt[i] = 0;
+            S.ibits[t] = 0;   // bucket-start bits during the sort
         }
-        for (uint32_t i = t; i < SG_CNTW; i += SG_T) S.su.cnt[i] = 0;
-        S.ibits[t] = 0;   // bucket-start bits during the sort
         __syncthreads();
         PMARK(8);
 #pragma unroll 8
         for (uint32_t j = 0; j < SG_SEG; j++) {
             const uint32_t p = j * SG_T + t;
-            if (p >= 1 && p <= ip_limit)
-                (void)cnt_add(S, sg_hash(__builtin_amdgcn_alignbyte(dat[(p >> 2) + 1], dat[p >> 2], p & 3), shift));
+            if (p >= 1 && p <= ip_limit) (void)cnt_add(S, sg_hash(lds_ld32(S, p), shift));
         }
         __syncthreads();
         PMARK(9);
@@ -446,95 +443,50 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         }
         __syncthreads();
         PMARK(10);
-        int bad = 0;
-        uint32_t base = 0, h0 = 0;   // window: sorted entries from `base`, hashes from h0
-        while (base < npos) {
-            // h1 = the last hash boundary whose start is within SG_WIN entries of base (a bucket
-            // start never moves before its own window's scatter)
-            if (t == 0) S.hwin = h0;
-            __syncthreads();
-            {
-                const uint32_t words = tsize / 2, wpt = (words + SG_T - 1) / SG_T, w0 = t * wpt;
-                uint32_t best = h0;
-                for (uint32_t i = 0; i < wpt; i++) {
-                    const uint32_t wi = w0 + i;
-                    if (wi >= words) break;
-                    const uint32_t x = S.su.cnt[wi];
-                    if (2 * wi > h0 && (x & 0xffffu) - base <= SG_WIN) best = 2 * wi;
-                    if (2 * wi + 1 > h0 && (x >> 16) - base <= SG_WIN) best = 2 * wi + 1;
+        if (w == 0) {   // branch-free (a dummy counter takes the lanes past the end) so a batch's atomics issue back to back
+            const uint32_t ngr = ip_limit / 64 + 1;
+            for (uint32_t g0 = 0; g0 < ngr; g0 += 16) {
+                uint32_t h[16], idx[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const uint32_t p = (g0 + u) * 64 + lane;
+                    const uint32_t hv = sg_hash(lds_ld32(S, p & 0xffffu), shift);
+                    h[u] = (p >= 1 && p <= ip_limit) ? hv : tsize;
                 }
-                if (t == SG_T - 1 && npos - base <= SG_WIN) best = tsize;
-                if (best > h0) atomicMax(&S.hwin, best);
+#pragma unroll
+                for (int u = 0; u < 16; u++) idx[u] = atomicAdd(&S.su.cnt[h[u] >> 1], 1u << ((h[u] & 1) * 16));
+#pragma unroll
+                for (int u = 0; u < 16; u++) asm volatile("" : "+v"(idx[u]));   // one wait for the batch
+#pragma unroll
+                for (int u = 0; u < 16; u++)
+                    if (h[u] < tsize) G.sig[(idx[u] >> ((h[u] & 1) * 16)) & 0xffffu] = (uint16_t)((g0 + u) * 64 + lane);
             }
-            __syncthreads();
-            const uint32_t h1 = S.hwin;
-            if (h1 == h0) { bad = 1; break; }   // one bucket alone exceeds the window: sequential kernels
-            const uint32_t wend = h1 >= tsize ? npos : (h1 & 1 ? S.su.cnt[h1 >> 1] >> 16 : S.su.cnt[h1 >> 1] & 0xffffu);
-            __syncthreads();
-            {   // scatter: all waves hash the next 16 position groups into the ring (one global
-                // load pair per lane: L1/L2 hits), the scatter wave places the previous 16 in
-                // order
-                const uint32_t nbat = (ip_limit / 64 + 1 + SG_W - 1) / SG_W;
-                auto fill = [&](uint32_t b) {
-                    const uint32_t p = (b * SG_W + w) * 64 + lane;
-                    const uint32_t hv = sg_hash(in.ld32(p < 1 ? 1 : (p > ip_limit ? ip_limit : p)), shift);
-                    S.ring[b & 1][w][lane] = (p >= 1 && p <= ip_limit && hv >= h0 && hv < h1) ? (uint16_t)hv : (uint16_t)0xffffu;
-                };
-                fill(0);
-                __syncthreads();
-                for (uint32_t b = 0; b < nbat; b++) {
-                    if (b + 1 < nbat) fill(b + 1);
-                    if (w == 0) {
-                        // lanes outside the window issue no atomic (LDS returning atomics cost per
-                        // active lane: a dummy counter for them doubled the pass)
-                        uint32_t h[SG_W], idx[SG_W];
-#pragma unroll
-                        for (int u = 0; u < (int)SG_W; u++) h[u] = S.ring[b & 1][u][lane];
-#pragma unroll
-                        for (int u = 0; u < (int)SG_W; u++) {
-                            idx[u] = 0;
-                            if (h[u] != 0xffffu) idx[u] = atomicAdd(&S.su.cnt[h[u] >> 1], 1u << ((h[u] & 1) * 16));
-                        }
-#pragma unroll
-                        for (int u = 0; u < (int)SG_W; u++) asm volatile("" : "+v"(idx[u]));   // one wait for the batch
-#pragma unroll
-                        for (int u = 0; u < (int)SG_W; u++)
-                            if (h[u] != 0xffffu)
-                                S.su.win[((idx[u] >> ((h[u] & 1) * 16)) & 0xffffu) - base] = (uint16_t)((b * SG_W + u) * 64 + lane);
-                    }
-                    __syncthreads();
-                }
-            }
-            {   // order check (positions increase within a bucket), then the window out: 16-byte
-                // stores for the aligned 8-entry chunks inside it, 2-byte stores at its two ends
-                const uint32_t cnt = wend - base;
-                for (uint32_t i = t; i < cnt; i += SG_T) {
-                    const uint32_t gi = base + i;
-                    if (i && !((S.ibits[gi >> 6] >> (gi & 63)) & 1) && S.su.win[i] <= S.su.win[i - 1]) bad = 1;
-                }
-                const uint32_t c0 = (base + 7) & ~7u, c1 = wend & ~7u;   // aligned chunk range [c0, c1)
-                for (uint32_t i = base + t; i < min(c0, wend); i += SG_T) G.sig[i] = S.su.win[i - base];
-                for (uint32_t i = max(c1, c0) + t; i < wend; i += SG_T) G.sig[i] = S.su.win[i - base];
-                if (c1 > c0) {
-                    for (uint32_t k = c0 / 8 + t; k < c1 / 8; k += SG_T) {
-                        const uint32_t o = 8 * k - base;
-                        uint32_t q[4];
-#pragma unroll
-                        for (int e = 0; e < 4; e++) q[e] = (uint32_t)S.su.win[o + 2 * e] | ((uint32_t)S.su.win[o + 2 * e + 1] << 16);
-                        ((uint4 *)G.sig)[k] = uint4{q[0], q[1], q[2], q[3]};
-                    }
-                }
-            }
-            base = wend;
-            h0 = h1;
-            bad = __syncthreads_or(bad);
-            if (bad) break;
         }
-        bf = S.ibits[t];
-        G.bflag[t] = bf;
         __threadfence_block();
         __syncthreads();
         PMARK(11);
+        // order check, bucket-start bits -> global (every round reads its 64 entries and bits)
+        int bad = 0;
+        {
+            const uint32_t i0 = t * SG_SEG;
+            bf = S.ibits[t];
+            const uint4 *gs = (const uint4 *)&G.sig[i0];
+            uint32_t prevp = (i0 > 0 && i0 <= npos) ? G.sig[i0 - 1] : 0;
+#pragma unroll 1
+            for (int q = 0; q < 8; q++) {
+                const uint4 vq = gs[q];
+                const uint32_t vv[4] = {vq.x, vq.y, vq.z, vq.w};
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    const uint32_t j = q * 8 + e;
+                    const uint32_t p = (vv[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+                    if (i0 + j < npos && !((bf >> j) & 1) && p <= prevp) bad = 1;
+                    prevp = p;
+                }
+            }
+            G.bflag[t] = bf;
+        }
+        __syncthreads();
         // round 0: every position inserted; entries advanced from the start over match-free segments
         const PS init{MS, 1, 32, 0};
         S.ibits[t] = t < nseg ? ~0ull : 0ull;

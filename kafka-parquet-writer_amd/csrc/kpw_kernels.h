@@ -217,6 +217,9 @@ struct DeltaJob {
     uint64_t out_off;              // absolute output offset (device-set by the layout)
     uint64_t hdr;                  // header bytes (device)
     uint64_t total;                // header + blocks (device)
+    int32_t prev;                  // multi-page: the same stream of the chunk's previous page (the
+                                   // fallback writer is reset, not rebuilt, between pages), or -1
+    int32_t pad;
 };
 
 // ---------------------------------------------------------------- launch wrappers
