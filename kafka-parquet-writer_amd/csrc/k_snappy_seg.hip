@@ -27,9 +27,9 @@
 // (long repeats: cheap for the sequential kernels) or whose sort check fails is marked
 // SEG_ABORTED and compressed by k_snappy_v / k_snappy_s_rest instead (same bytes).
 //
-// LDS: cand u16[65536] (128 KiB; the bucket counters during setup), the inserted-position
-// bitmask (8 KiB), entry and exit states (8 KiB each): one workgroup per CU; the grid is one
-// workgroup per CU and pulls fragments from a counter.
+// LDS: cand u16[65536] (128 KiB; the staged fragment and the bucket counters during setup),
+// the inserted-position bitmask (8 KiB), entry and exit states (8 KiB each): one workgroup per
+// CU; the grid is one workgroup per CU and pulls fragments from a counter.
 #include "kpw_device.h"
 #include "kpw_chunk.h"
 
@@ -45,6 +45,10 @@ constexpr uint32_t SG_MAXLEN = 512;
 constexpr uint32_t SG_RECS = 16;         // copies per segment (each >= 4 bytes, starting inside it)
 constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the whole workgroup
 constexpr uint32_t SG_PB = 4;            // search probes in flight per parse step
+#ifndef SG_SW
+#define SG_SW 4u                 // sort scatter: waves (each owns the hashes h % SG_SW)
+#endif
+constexpr uint32_t SG_NOMATCH = 0xffff;  // cand[]: the table entry's 4 bytes differ (positions < 65521)
 
 enum : uint32_t { MS = 0, MP = 1, MT = 2 };
 struct PS {
@@ -93,6 +97,10 @@ __device__ PS sg_ff(PS x, uint32_t s, uint32_t ip_limit)
 // global-memory views (explicit address space: global_load, not flat_load, whose waits also
 // cover the LDS counter)
 typedef const __attribute__((address_space(1))) uint32_t sgg_cu32;
+typedef const __attribute__((address_space(1))) uint16_t sgg_cu16;
+typedef unsigned int sg_u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) sg_u32x4 sgg_cu4;
+typedef __attribute__((address_space(1))) uint16_t sgg_u16;
 typedef const __attribute__((address_space(1))) uint8_t sgg_cu8;
 typedef __attribute__((address_space(1))) uint8_t sgg_u8;
 
@@ -179,13 +187,19 @@ __device__ __forceinline__ uint32_t put_lit_tag(sgg_u8 *o, uint32_t op, uint32_t
     return op;
 }
 
-// per-workgroup global scratch
+// per-workgroup global scratch.  Lane-major layouts where a thread owns a row: the c-th 4 keys
+// of thread t's 64 sorted entries sit at key4[c * SG_T + t], the r-th copy record of segment t
+// at rec[r * SG_T + t], so a wave's loads and stores cover contiguous 1 KiB / 512 B spans.
 struct SgScratch {
-    uint16_t sig[65536];          // positions sorted by (hash, position)
+    uint4 sig4[8 * SG_T];         // positions sorted by (hash, position), 8 entries per piece
+    uint4 key4[16 * SG_T];        // the 4 bytes at each sorted entry's position
     uint64_t bflag[SG_T];         // bit j of word t: sorted entry 64t+j starts a hash bucket
     uint64_t rec[SG_T * SG_RECS]; // copies found by the last parse, per segment
     uint32_t job[2 * SG_T][4];    // long literals: src, dst, len
 };
+
+// uint16 slot of sorted entry i
+__device__ __forceinline__ uint32_t sig_slot(uint32_t i) { return i; }
 
 constexpr uint32_t SG_DATA = 65536 + 64;   // setup: the fragment's bytes (+ read padding)
 struct SgShared {
@@ -195,10 +209,12 @@ struct SgShared {
             uint32_t data[SG_DATA / 4];   // setup: the fragment, staged for the sort
             uint32_t cnt[8192 + 2];       // setup: bucket counters, two uint16 per word; + a dummy
         } su;
-    };
-    uint64_t ibits[SG_T];         // inserted positions (bit q of word q/64)
-    uint64_t entry[SG_T];
-    uint64_t exitst[SG_T];
+    } a;
+    struct {
+        uint64_t entry[SG_T];
+        uint64_t exitst[SG_T];
+    } b;
+    uint64_t ibits[SG_T];         // inserted positions (bit q of word q/64); bucket starts during setup
     uint64_t found[SG_W];
     uint32_t lfl[SG_T / 32];      // thread k inserted 64k-1
     uint32_t wf[SG_W], wv[SG_W];  // block scan
@@ -211,13 +227,13 @@ struct SgShared {
 __device__ __forceinline__ uint32_t lds_ld32(const SgShared &S, uint32_t p)
 {
     const uint32_t d = p >> 2;
-    return __builtin_amdgcn_alignbyte(S.su.data[d + 1], S.su.data[d], p & 3);
+    return __builtin_amdgcn_alignbyte(S.a.su.data[d + 1], S.a.su.data[d], p & 3);
 }
 
 __device__ __forceinline__ uint32_t cnt_add(SgShared &S, uint32_t h)
 {
     const uint32_t sh = (h & 1) * 16;
-    return (atomicAdd(&S.su.cnt[h >> 1], 1u << sh) >> sh) & 0xffffu;
+    return (atomicAdd(&S.a.su.cnt[h >> 1], 1u << sh) >> sh) & 0xffffu;
 }
 
 // exclusive scan of u32 over the workgroup; *total = sum
@@ -280,16 +296,16 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
         if (st.mode == MP) {
             const uint32_t ipe = st.ip;
             if (ipe - 1 >= sk) o.own |= 1ull << (ipe - 1 - sk); else o.lfl = true;
-            c = S.cand[ipe];
+            c = S.a.cand[ipe];
             o.own |= 1ull << (ipe - sk);
-            if (in.ld32(ipe) != in.ld32(c)) { st = PS{MS, ipe + 1, 32, ipe}; continue; }
+            if (c == SG_NOMATCH) { st = PS{MS, ipe + 1, 32, ipe}; continue; }
             base = ipe; lit = false;
         } else {
             // SG_PB probes of the search at once: their positions (ip += skip++ >> 5) do not
             // depend on the data, so the cand -> data load chains of the next SG_PB decisions
             // overlap; the first probe that matches is the one the sequential loop takes, and
             // every probe up to it is inserted (the same state as SG_PB sequential steps)
-            uint32_t q[SG_PB], cc[SG_PB], d[SG_PB], e[SG_PB];
+            uint32_t q[SG_PB], cc[SG_PB];
             bool v[SG_PB];
             uint32_t ipk = st.ip, skk = st.skip;
             bool alive = true, term = false;
@@ -304,13 +320,11 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
                 if (v[k]) { ipk = nx; skk++; }
             }
 #pragma unroll
-            for (int k = 0; k < (int)SG_PB; k++) cc[k] = S.cand[q[k]];
-#pragma unroll
-            for (int k = 0; k < (int)SG_PB; k++) { d[k] = in.ld32(q[k]); e[k] = in.ld32(cc[k]); }
+            for (int k = 0; k < (int)SG_PB; k++) cc[k] = S.a.cand[q[k]];
             int hit = -1;
 #pragma unroll
             for (int k = (int)SG_PB - 1; k >= 0; k--)
-                if (v[k] && d[k] == e[k]) hit = k;
+                if (v[k] && cc[k] != SG_NOMATCH) hit = k;
 #pragma unroll
             for (int k = 0; k < (int)SG_PB; k++)
                 if (v[k] && (hit < 0 || k <= hit)) o.own |= 1ull << (q[k] - sk);
@@ -327,7 +341,7 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
         const uint32_t len = 4 + sg_fml(in, c + 4, base + 4, n, SG_MAXLEN);
         if (len > SG_MAXLEN) { o.lng = true; break; }
         o.fnd = true;
-        G.rec[t * SG_RECS + o.nrec++] = (uint64_t)base | ((uint64_t)(base - c) << 16) | ((uint64_t)len << 32) | ((uint64_t)lit << 48);
+        G.rec[(o.nrec++) * SG_T + t] = (uint64_t)base | ((uint64_t)(base - c) << 16) | ((uint64_t)len << 32) | ((uint64_t)lit << 48);
         const uint32_t ipe = base + len;
         st = ipe >= ip_limit ? st_T(ipe) : st_P(ipe);
     }
@@ -398,10 +412,10 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         // instruction covers 64 consecutive positions (periodic data spreads over several
         // counters).  The scatter is one wave walking the positions in order: LDS atomics of one
         // instruction on the same counter return in lane order (checked below; a violation
-        // hands the fragment on).
+        // hands the fragment on).  Sorted entries go to the lane-major global layout.
         {
             const uintptr_t fb = (uintptr_t)in.base;
-            const uint32_t *src = (const uint32_t *)(fb & ~(uintptr_t)3);
+            sgg_cu32 *src = (sgg_cu32 *)(fb & ~(uintptr_t)3);
             const uint32_t sh = (uint32_t)(fb & 3);
             // only the dwords that cover [0, n) (+ the 16 bytes of read padding the page buffer
             // has) are loaded: a short fragment may end near the end of the buffer
@@ -410,9 +424,9 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
 #pragma unroll
             for (int i = 0; i < 17; i++) v[i] = (t * 16 + i < nw) ? src[t * 16 + i] : 0u;
 #pragma unroll
-            for (int i = 0; i < 16; i++) S.su.data[t * 16 + i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
-            if (t < 16) S.su.data[SG_T * 16 + t] = 0;
-            for (uint32_t i = t; i <= tsize / 2; i += SG_T) S.su.cnt[i] = 0;
+            for (int i = 0; i < 16; i++) S.a.su.data[t * 16 + i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+            if (t < 16) S.a.su.data[SG_T * 16 + t] = 0;
+            for (uint32_t i = t; i <= tsize / 2; i += SG_T) S.a.su.cnt[i] = 0;
             S.ibits[t] = 0;   // bucket-start bits during the sort
         }
         __syncthreads();
@@ -429,13 +443,13 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             const uint32_t words = tsize / 2, wpt = (words + SG_T - 1) / SG_T, w0 = t * wpt;
             uint32_t loc = 0;
             for (uint32_t i = 0; i < wpt; i++)
-                if (w0 + i < words) { const uint32_t x = S.su.cnt[w0 + i]; loc += (x & 0xffffu) + (x >> 16); }
+                if (w0 + i < words) { const uint32_t x = S.a.su.cnt[w0 + i]; loc += (x & 0xffffu) + (x >> 16); }
             uint32_t tot;
             uint32_t run = sg_scan_excl(loc, S, &tot);
             for (uint32_t i = 0; i < wpt; i++)
                 if (w0 + i < words) {
-                    const uint32_t x = S.su.cnt[w0 + i], lo = x & 0xffffu, hi = x >> 16;
-                    S.su.cnt[w0 + i] = run | ((run + lo) << 16);
+                    const uint32_t x = S.a.su.cnt[w0 + i], lo = x & 0xffffu, hi = x >> 16;
+                    S.a.su.cnt[w0 + i] = run | ((run + lo) << 16);
                     if (lo) atomicOr((unsigned long long *)&S.ibits[run >> 6], 1ull << (run & 63));   // bucket starts
                     if (hi) atomicOr((unsigned long long *)&S.ibits[(run + lo) >> 6], 1ull << ((run + lo) & 63));
                     run += lo + hi;
@@ -443,7 +457,11 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         }
         __syncthreads();
         PMARK(10);
-        if (w == 0) {   // branch-free (a dummy counter takes the lanes past the end) so a batch's atomics issue back to back
+        if (w < SG_SW) {
+            // SG_SW waves walk the positions in order, wave w placing the hashes h with
+            // h % SG_SW == w: a bucket belongs to one wave, so its entries stay in position
+            // order; the other lanes issue no atomic (a returning LDS atomic costs per active lane)
+            sgg_u16 *sig = (sgg_u16 *)G.sig4;
             const uint32_t ngr = ip_limit / 64 + 1;
             for (uint32_t g0 = 0; g0 < ngr; g0 += 16) {
                 uint32_t h[16], idx[16];
@@ -451,15 +469,22 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 for (int u = 0; u < 16; u++) {
                     const uint32_t p = (g0 + u) * 64 + lane;
                     const uint32_t hv = sg_hash(lds_ld32(S, p & 0xffffu), shift);
-                    h[u] = (p >= 1 && p <= ip_limit) ? hv : tsize;
+                    h[u] = (p >= 1 && p <= ip_limit && (hv % SG_SW) == w) ? hv : 0xffffffffu;
                 }
 #pragma unroll
-                for (int u = 0; u < 16; u++) idx[u] = atomicAdd(&S.su.cnt[h[u] >> 1], 1u << ((h[u] & 1) * 16));
+                for (int u = 0; u < 16; u++) {
+                    idx[u] = 0;
+                    if (h[u] != 0xffffffffu) idx[u] = atomicAdd(&S.a.su.cnt[h[u] >> 1], 1u << ((h[u] & 1) * 16));
+                }
 #pragma unroll
                 for (int u = 0; u < 16; u++) asm volatile("" : "+v"(idx[u]));   // one wait for the batch
 #pragma unroll
                 for (int u = 0; u < 16; u++)
-                    if (h[u] < tsize) G.sig[(idx[u] >> ((h[u] & 1) * 16)) & 0xffffu] = (uint16_t)((g0 + u) * 64 + lane);
+#ifdef SG_NOSTORE
+                    if (h[u] != 0xffffffffu && idx[u] == 0x12345678u) sig[sig_slot((idx[u] >> ((h[u] & 1) * 16)) & 0xffffu)] = (uint16_t)((g0 + u) * 64 + lane);
+#else
+                    if (h[u] != 0xffffffffu) sig[sig_slot((idx[u] >> ((h[u] & 1) * 16)) & 0xffffu)] = (uint16_t)((g0 + u) * 64 + lane);
+#endif
             }
         }
         __threadfence_block();
@@ -470,11 +495,10 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         {
             const uint32_t i0 = t * SG_SEG;
             bf = S.ibits[t];
-            const uint4 *gs = (const uint4 *)&G.sig[i0];
-            uint32_t prevp = (i0 > 0 && i0 <= npos) ? G.sig[i0 - 1] : 0;
-#pragma unroll 1
+            uint32_t prevp = (i0 > 0 && i0 <= npos) ? ((sgg_cu16 *)G.sig4)[sig_slot(i0 - 1)] : 0;
+#pragma unroll 2
             for (int q = 0; q < 8; q++) {
-                const uint4 vq = gs[q];
+                const uint4 vq = G.sig4[t * 8 + q];
                 const uint32_t vv[4] = {vq.x, vq.y, vq.z, vq.w};
 #pragma unroll
                 for (int e = 0; e < 8; e++) {
@@ -485,12 +509,23 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 }
             }
             G.bflag[t] = bf;
+            // the 4 bytes at every sorted entry's position, from the staged fragment: the rounds
+            // compare a position with its candidate there, so the parse's probes are LDS reads
+#pragma unroll 1
+            for (int c = 0; c < 16; c++) {
+                const uint2 sp = ((const uint2 *)G.sig4)[t * 16 + c];
+                uint4 k;
+                k.x = lds_ld32(S, sp.x & 0xffffu); k.y = lds_ld32(S, sp.x >> 16);
+                k.z = lds_ld32(S, sp.y & 0xffffu); k.w = lds_ld32(S, sp.y >> 16);
+                G.key4[c * SG_T + t] = k;
+            }
         }
+        const uint32_t key0 = lds_ld32(S, 0);   // the empty table's candidate is position 0
         __syncthreads();
         // round 0: every position inserted; entries advanced from the start over match-free segments
         const PS init{MS, 1, 32, 0};
         S.ibits[t] = t < nseg ? ~0ull : 0ull;
-        S.entry[t] = pk(t == 0 ? init : sg_ff(init, t * SG_SEG, ip_limit));
+        S.b.entry[t] = pk(t == 0 ? init : sg_ff(init, t * SG_SEG, ip_limit));
         if (t < SG_T / 32) S.lfl[t] = 0;
         if (t < SG_W) S.found[t] = 0;
         __threadfence_block();
@@ -498,6 +533,8 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         PMARK(12);
         bool converged = false;
         uint32_t rounds = 0;
+        uint64_t sc_ins = 0;      // the scan's inserted bits and carry-in of the previous round
+        uint32_t sc_carry = 0;
         const uint32_t sk = t * SG_SEG;
         if (pf) prof[0] += clock64() - c_setup;
         ParseOut po{};
@@ -510,10 +547,9 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 const uint32_t i0 = t * SG_SEG;
                 uint32_t sg2[SG_SEG / 2];
                 {
-                    const uint4 *gs = (const uint4 *)&G.sig[i0];
 #pragma unroll
                     for (int q = 0; q < 8; q++) {
-                        const uint4 v = gs[q];
+                        const uint4 v = G.sig4[t * 8 + q];
                         sg2[4 * q] = v.x; sg2[4 * q + 1] = v.y; sg2[4 * q + 2] = v.z; sg2[4 * q + 3] = v.w;
                     }
                 }
@@ -542,22 +578,54 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                         if (ins) m = p;
                     }
                 }
+                PMARK(13);
                 m = sg_segmax_carry(i0 < npos && bf != 0, i0 < npos ? m : 0, S);
+                PMARK(14);
+                // cand[p] = the candidate when its 4 bytes equal p's, else SG_NOMATCH.  The
+                // thread's cand[] values are a function of its inserted bits and its carry-in
+                // alone: when neither changed since the last round they are already in LDS
+                const bool same = rounds > 1 && insm == sc_ins && m == sc_carry;
+                sc_ins = insm;
+                sc_carry = m;
+                uint32_t km = (!same && m) ? in.ld32(m) : key0;
 #pragma unroll
                 for (int q = 0; q < (int)SG_SEG / 2; q++) asm volatile("" : "+v"(sg2[q]));   // re-extract, do not keep 64 values live
+                if (!same) {
+                    // keys in 4 chunks of 4 pieces, the next chunk's loads in flight while one is
+                    // used (the base is re-derived every round: hoisted per-piece addresses spill)
+                    sgg_cu4 *kp = (sgg_cu4 *)(G.key4 + t);
+                    asm volatile("" : "+v"(kp));
+                    sg_u32x4 kb[2][4];
 #pragma unroll
-                for (int j = 0; j < (int)SG_SEG; j++) {
-                    const uint32_t p = (sg2[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-                    if ((bf >> j) & 1) m = 0;
-                    if (i0 + j < npos) S.cand[p] = (uint16_t)m;
-                    if ((insm >> j) & 1) m = p;
+                    for (int i = 0; i < 4; i++) kb[0][i] = kp[i * SG_T];
+#pragma unroll
+                    for (int c4 = 0; c4 < 4; c4++) {
+                        if (c4 < 3) {
+#pragma unroll
+                            for (int i = 0; i < 4; i++) kb[(c4 + 1) & 1][i] = kp[((c4 + 1) * 4 + i) * SG_T];
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const sg_u32x4 k4 = kb[c4 & 1][i];
+                            const uint32_t kk[4] = {k4.x, k4.y, k4.z, k4.w};
+#pragma unroll
+                            for (int e = 0; e < 4; e++) {
+                                const int j = (c4 * 4 + i) * 4 + e;
+                                const uint32_t p = (sg2[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+                                if ((bf >> j) & 1) { m = 0; km = key0; }
+                                if (i0 + j < npos) S.a.cand[p] = (uint16_t)(km == kk[e] ? m : SG_NOMATCH);
+                                if ((insm >> j) & 1) { m = p; km = kk[e]; }
+                            }
+                        }
+                    }
                 }
             }
+            PMARK(15);
             __syncthreads();
             PMARK(1);
             // ---------------------------------------------- parse my segment
-            po = t < nseg ? sg_parse(S, G, in, upk(S.entry[t]), t, n, ip_limit) : ParseOut{upk(S.entry[t]), 0, false, false, false, 0};
-            S.exitst[t] = pk(po.st);
+            po = t < nseg ? sg_parse(S, G, in, upk(S.b.entry[t]), t, n, ip_limit) : ParseOut{upk(S.b.entry[t]), 0, false, false, false, 0};
+            S.b.exitst[t] = pk(po.st);
             if (po.lfl) atomicOr(&S.lfl[t >> 5], 1u << (t & 31));
             {
                 const uint64_t fm = __ballot(po.fnd);
@@ -572,7 +640,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 const uint32_t k1 = t + 1;
                 nb = po.own | ((k1 < SG_T && ((S.lfl[k1 >> 5] >> (k1 & 31)) & 1)) ? (1ull << 63) : 0ull);
                 diff = nb != S.ibits[t];
-                if (t + 1 < nseg && S.exitst[t] != S.entry[t + 1]) diff = true;
+                if (t + 1 < nseg && S.b.exitst[t] != S.b.entry[t + 1]) diff = true;
             }
             __syncthreads();
             if (t < nseg) S.ibits[t] = nb;
@@ -588,8 +656,8 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                         for (int ww = (int)w - 1; ww >= 0; ww--)
                             if (S.found[ww]) { j = ww * 64 + 63 - __builtin_clzll(S.found[ww]); break; }
                 }
-                const PS e = t == 0 ? init : sg_ff(j >= 0 ? upk(S.exitst[j]) : init, sk, ip_limit);
-                S.entry[t] = pk(e);
+                const PS e = t == 0 ? init : sg_ff(j >= 0 ? upk(S.b.exitst[j]) : init, sk, ip_limit);
+                S.b.entry[t] = pk(e);
             }
             __syncthreads();
             if (t < SG_T / 32) S.lfl[t] = 0;
@@ -604,11 +672,11 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             continue;
         }
         // ---------------------------------------------- emit the converged parse's copies
-        const PS e0 = upk(S.entry[t]);
+        const PS e0 = upk(S.b.entry[t]);
         uint32_t osz = 0;
         uint32_t ne = e0.ne;
         for (uint32_t r = 0; r < po.nrec; r++) {
-            const uint64_t rc = G.rec[t * SG_RECS + r];
+            const uint64_t rc = G.rec[r * SG_T + t];
             const uint32_t base = (uint32_t)(rc & 0xffff), off = (uint32_t)((rc >> 16) & 0xffff);
             const uint32_t len = (uint32_t)((rc >> 32) & 0xffff), lit = (uint32_t)(rc >> 48) & 1;
             if (lit) osz += lit_size(base - ne);
@@ -635,7 +703,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 op += len;
             };
             for (uint32_t r = 0; r < po.nrec; r++) {
-                const uint64_t rc = G.rec[t * SG_RECS + r];
+                const uint64_t rc = G.rec[r * SG_T + t];
                 const uint32_t base = (uint32_t)(rc & 0xffff), off = (uint32_t)((rc >> 16) & 0xffff);
                 const uint32_t len = (uint32_t)((rc >> 32) & 0xffff), lit = (uint32_t)(rc >> 48) & 1;
                 if (lit) lit_out(ne, base - ne);

@@ -135,8 +135,8 @@ int main(int argc, char **argv)
                 printf("per fragment (kcycles): setup %.1f scan %.1f parse %.1f check %.1f emit %.1f | rounds %.2f | frags %llu handed on %llu\n",
                        pr[0] / fr / 1e3, pr[1] / fr / 1e3, pr[2] / fr / 1e3, pr[3] / fr / 1e3, pr[4] / fr / 1e3, pr[5] / fr,
                        (unsigned long long)pr[6], (unsigned long long)pr[7]);
-                printf("  setup: stage %.1f hist %.1f cscan %.1f scatter %.1f check %.1f | scan carry %.1f\n", pr[8] / fr / 1e3,
-                       pr[9] / fr / 1e3, pr[10] / fr / 1e3, pr[11] / fr / 1e3, pr[12] / fr / 1e3, pr[13] / fr / 1e3);
+                printf("  setup: stage %.1f hist %.1f cscan %.1f scatter %.1f check %.1f | scan: pass1 %.1f carry %.1f pass2 %.1f (rest = final barrier)\n", pr[8] / fr / 1e3,
+                       pr[9] / fr / 1e3, pr[10] / fr / 1e3, pr[11] / fr / 1e3, pr[12] / fr / 1e3, pr[13] / fr / 1e3, pr[14] / fr / 1e3, pr[15] / fr / 1e3);
                 hipFree(d_prof);
             }
             launch_snappy(a, 0);
