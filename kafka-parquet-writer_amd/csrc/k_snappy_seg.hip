@@ -44,7 +44,9 @@ constexpr uint32_t SG_MAXR = 64;
 constexpr uint32_t SG_MAXLEN = 512;
 constexpr uint32_t SG_RECS = 16;         // copies per segment (each >= 4 bytes, starting inside it)
 constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the whole workgroup
-constexpr uint32_t SG_PB = 4;            // search probes in flight per parse step
+#ifndef SG_PB
+#define SG_PB 4u                 // search probes in flight per parse step
+#endif
 #ifndef SG_SW
 #define SG_SW 4u                 // sort scatter: waves (each owns the hashes h % SG_SW)
 #endif
@@ -100,6 +102,7 @@ typedef const __attribute__((address_space(1))) uint32_t sgg_cu32;
 typedef const __attribute__((address_space(1))) uint16_t sgg_cu16;
 typedef unsigned int sg_u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) sg_u32x4 sgg_cu4;
+typedef __attribute__((address_space(1))) sg_u32x4 sgg_u4;
 typedef __attribute__((address_space(1))) uint16_t sgg_u16;
 typedef const __attribute__((address_space(1))) uint8_t sgg_cu8;
 typedef __attribute__((address_space(1))) uint8_t sgg_u8;
@@ -302,9 +305,10 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
             base = ipe; lit = false;
         } else {
             // SG_PB probes of the search at once: their positions (ip += skip++ >> 5) do not
-            // depend on the data, so the cand -> data load chains of the next SG_PB decisions
-            // overlap; the first probe that matches is the one the sequential loop takes, and
-            // every probe up to it is inserted (the same state as SG_PB sequential steps)
+            // depend on the data, so the cand[] reads of the next SG_PB decisions overlap (a
+            // cand[] entry already says whether the candidate's 4 bytes match); the first probe
+            // that matches is the one the sequential loop takes, and every probe up to it is
+            // inserted (the same state as SG_PB sequential steps)
             uint32_t q[SG_PB], cc[SG_PB];
             bool v[SG_PB];
             uint32_t ipk = st.ip, skk = st.skip;
@@ -496,29 +500,34 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             const uint32_t i0 = t * SG_SEG;
             bf = S.ibits[t];
             uint32_t prevp = (i0 > 0 && i0 <= npos) ? ((sgg_cu16 *)G.sig4)[sig_slot(i0 - 1)] : 0;
-#pragma unroll 2
-            for (int q = 0; q < 8; q++) {
-                const uint4 vq = G.sig4[t * 8 + q];
-                const uint32_t vv[4] = {vq.x, vq.y, vq.z, vq.w};
+            // with the check, the 4 bytes at every sorted entry's position, from the staged
+            // fragment: the rounds compare a position with its candidate there, so the parse's
+            // probes are LDS reads
+            sgg_cu4 *sp4 = (sgg_cu4 *)(G.sig4 + t * 8);
+            sgg_u4 *kp = (sgg_u4 *)(G.key4 + t);
+#pragma unroll
+            for (int q0 = 0; q0 < 8; q0 += 4) {
+            sg_u32x4 vq[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) vq[q] = sp4[q0 + q];
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const int q = q0 + qq;
+                uint32_t pp[8], kk[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) pp[e] = (vq[qq][e >> 1] >> ((e & 1) * 16)) & 0xffffu;
 #pragma unroll
                 for (int e = 0; e < 8; e++) {
                     const uint32_t j = q * 8 + e;
-                    const uint32_t p = (vv[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-                    if (i0 + j < npos && !((bf >> j) & 1) && p <= prevp) bad = 1;
-                    prevp = p;
+                    if (i0 + j < npos && !((bf >> j) & 1) && pp[e] <= prevp) bad = 1;
+                    prevp = pp[e];
+                    kk[e] = lds_ld32(S, pp[e]);
                 }
+                kp[(2 * q) * SG_T] = sg_u32x4{kk[0], kk[1], kk[2], kk[3]};
+                kp[(2 * q + 1) * SG_T] = sg_u32x4{kk[4], kk[5], kk[6], kk[7]};
+            }
             }
             G.bflag[t] = bf;
-            // the 4 bytes at every sorted entry's position, from the staged fragment: the rounds
-            // compare a position with its candidate there, so the parse's probes are LDS reads
-#pragma unroll 1
-            for (int c = 0; c < 16; c++) {
-                const uint2 sp = ((const uint2 *)G.sig4)[t * 16 + c];
-                uint4 k;
-                k.x = lds_ld32(S, sp.x & 0xffffu); k.y = lds_ld32(S, sp.x >> 16);
-                k.z = lds_ld32(S, sp.y & 0xffffu); k.w = lds_ld32(S, sp.y >> 16);
-                G.key4[c * SG_T + t] = k;
-            }
         }
         const uint32_t key0 = lds_ld32(S, 0);   // the empty table's candidate is position 0
         __syncthreads();
