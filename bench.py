@@ -146,8 +146,10 @@ def pmc_traffic(workload):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_%s_pmc_traffic.json" % workload)))
     for f in reversed(files):
         d = json.load(open(f))
-        if "k7_traffic_bytes_per_job" in d:   # per-job format (r03 on)
-            return int(d["k7_traffic_bytes_per_job"]), os.path.relpath(f, ROOT)
+        if d.get("k7_traffic_over_algorithmic"):   # r03c on: traffic relative to the same jobs' bytes
+            return ("ratio", float(d["k7_traffic_over_algorithmic"])), os.path.relpath(f, ROOT)
+        if "k7_traffic_bytes_per_job" in d:   # per-job format (r03a/b)
+            return ("bytes", int(d["k7_traffic_bytes_per_job"])), os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -506,7 +508,14 @@ def main():
     k7_bytes = (agg["page_bytes_uncompressed"] + agg["page_bytes_compressed"]) / jobs
     ams = agg["k7_snappy_ms"] / jobs
     achieved = k7_bytes / (ams * 1e-3) / 1e9 if ams > 0 else 0.0
-    traffic, tsrc = pmc_traffic(args.workload)
+    tk, tsrc = pmc_traffic(args.workload)
+    traffic, tunit = None, "HBM bytes per launch (FETCH_SIZE + WRITE_SIZE)"
+    if tk and tk[0] == "ratio":   # job sizes vary (eager jobs): scale the profile's traffic/algorithmic ratio
+        traffic = int(round(tk[1] * k7_bytes))
+        tunit += ": the PMC passes' K7 counter bytes / K7 algorithmic bytes (%.3f, same jobs) x this line's " \
+                 "algorithmic bytes per launch" % tk[1]
+    elif tk:
+        traffic = tk[1]
     sb = stage_bytes(sschema, agg)
     stage_ms = {"decode": agg["decode_ms"], "plan": agg["plan_ms"], "stats_dict": agg["stats_dict_ms"],
                 "rle": agg["rle_ms"], "layout_plain_write": agg["layout_plain_write_ms"], "compress": agg["compress_ms"]}
@@ -514,7 +523,7 @@ def main():
     pipe = sum(sb.values()) / (t_stages * 1e-3) / 1e9 if t_stages > 0 else 0.0
     roof = dict(bound="hbm", kernel="K7 Snappy: " + ", ".join(K7_KERNELS), achieved=round(achieved, 2),
                 peak=HBM_PEAK_GBPS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBPS, 5),
-                traffic=traffic, traffic_unit="HBM bytes per launch (FETCH_SIZE + WRITE_SIZE)",
+                traffic=traffic, traffic_unit=tunit,
                 traffic_source=tsrc, traffic_over_algorithmic=(round(traffic / k7_bytes, 3) if traffic else None),
                 algorithmic_bytes_per_launch=int(k7_bytes), avg_launch_ms=round(ams, 4), launches=int(jobs),
                 pipeline_achieved=round(pipe, 2), pipeline_frac=round(pipe / HBM_PEAK_GBPS, 5),

@@ -930,7 +930,12 @@ int Engine::seg_args(SnappyArgs &sa)
     ENS(d_seg_counter, 64);
     sa.seg_scratch = d_seg_scratch.as<uint8_t>();
     sa.seg_counter = d_seg_counter.as<uint32_t>();
-    sa.seg_grid = (uint32_t)cus;
+    {   // KPW_SEG_RESERVE_CUS: CUs kept out of the persistent segment kernel's grid (its workgroup
+        // holds a CU's whole VGPR file, so nothing else runs beside it: the other encode worker's
+        // kernels wait for it unless CUs are left over)
+        static const int reserve = [] { const char *e = getenv("KPW_SEG_RESERVE_CUS"); return e ? atoi(e) : 0; }();
+        sa.seg_grid = (uint32_t)std::max(1, cus - std::max(0, reserve));
+    }
     return 0;
 }
 

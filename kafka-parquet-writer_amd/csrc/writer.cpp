@@ -76,6 +76,22 @@ uint64_t stage_flush_bytes()
     static const uint64_t v = env_mb("KPW_STAGE_FLUSH_MB", 1024);
     return v;
 }
+// Eager jobs: a fill buffer holding at least this many appended bytes is submitted early when
+// an encode worker is idle and nothing is queued (KPW_EAGER_MB, default 512; a negative value
+// turns it off).  The GPU then starts on the data already in HBM instead of waiting for a full
+// job, and close() finds less left to encode; jobs stay at the full size while the workers are
+// busy.  C2 writer path 33.5 -> 35.8 GB/s, C5 28.4 -> 31.6 (384 / 640 / 768 MiB measured lower;
+// DESIGN.md §6).
+uint64_t eager_job_bytes()
+{
+    static const uint64_t b = [] {
+        const char *e = getenv("KPW_EAGER_MB");
+        const long long v = e ? atoll(e) : 512;
+        return v > 0 ? (uint64_t)v << 20 : 0ull;
+    }();
+    return b;
+}
+
 // Writes of more records than this leave the per-record size model (bulk path).
 uint64_t model_max_batch()
 {
@@ -1563,7 +1579,18 @@ static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offse
     }
     if (rc) return rc;
     StageBuf &F = w->buf[w->fill];
-    if (!w->model_on && F.len - F.gap >= stage_flush_bytes()) return submit(w, JOB_PLANNED, 0);
+    if (!w->model_on) {
+        const uint64_t used = F.len - F.gap;
+        if (used >= stage_flush_bytes()) return submit(w, JOB_PLANNED, 0);
+        if (eager_job_bytes() && used >= eager_job_bytes()) {
+            bool idle;
+            {
+                std::lock_guard<std::mutex> g(w->mu);
+                idle = w->q.empty() && w->inflight < w->nworkers;
+            }
+            if (idle) return submit(w, JOB_PLANNED, 0);
+        }
+    }
     return KPW_OK;
 }
 

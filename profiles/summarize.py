@@ -67,11 +67,27 @@ def pmc(tag, workload):
         traffic[k] = {"calls_per_job": round(len(fetch.get(k, [])) / jf, 3), "fetch_bytes_raw_per_job": round(f_raw),
                       "fetch_correction": corr, "fetch_bytes_per_job": round(corr * f_raw),
                       "write_bytes_per_job": round(w), "traffic_bytes_per_job": round(corr * f_raw + w)}
+    # traffic relative to the algorithmic bytes of the same jobs: every pass runs --warmup 0, so
+    # its bench line's launches are exactly the pass's jobs (eager jobs vary in size with timing)
+    ratio = None
+    bf = bench_line(os.path.join(src, "fetch.log"))
+    bw = bench_line(os.path.join(src, "write.log"))
+    if bf and bw and bf.get("roofline") and bw.get("roofline"):
+        af = bf["roofline"]["algorithmic_bytes_per_launch"] * bf["roofline"]["launches"]
+        aw = bw["roofline"]["algorithmic_bytes_per_launch"] * bw["roofline"]["launches"]
+        if bf["roofline"]["launches"] == jf and bw["roofline"]["launches"] == jw and af > 0 and aw > 0:
+            kf = sum((2.0 if k in STREAMING_16B else 1.0) * sum(fetch.get(k, [])) for k in K7)
+            kw = sum(sum(write.get(k, [])) for k in K7)
+            ratio = round(kf / af + kw / aw, 4)
     out = {"tag": tag, "workload": workload, "unit": "bytes per encode job (= per launch of the bench line's "
            "dominant kernel group); every dispatch of a kernel in the pass summed, divided by the pass's %s "
            "dispatches" % JOB_KERNEL, "jobs": {"fetch_pass": jf, "write_pass": jw},
            "streaming_16b_x2": sorted(STREAMING_16B), "k7_kernels": K7,
            "k7_traffic_bytes_per_job": sum(traffic[k]["traffic_bytes_per_job"] for k in K7 if k in traffic),
+           "k7_traffic_over_algorithmic": ratio,
+           "k7_ratio_note": "K7 FETCH (x2 on 16 B/lane streams) / K7 algorithmic bytes of the fetch pass + K7 WRITE / "
+                            "K7 algorithmic bytes of the write pass (algorithmic = page bytes in + compressed bytes out, "
+                            "from each pass's bench line; launches == jobs)",
            "kernels": traffic}
     path = os.path.join(ROOT, "profiles", "%s_%s_pmc_traffic.json" % (tag, workload))
     json.dump(out, open(path, "w"), indent=1)
@@ -99,8 +115,8 @@ def full(tag, workload):
     bl = bench_line(os.path.join(src, "trace.log"))
     with open(os.path.join(dst, name + "_summary.md"), "w") as fo:
         fo.write("# Profile %s — bench.py --workload %s --no-resident, rocprofv3\n\n" % (tag, workload))
-        fo.write("Commands: `profiles/profile_round.sh %s %s`: two PMC passes (FETCH_SIZE, WRITE_SIZE; bench --steps 2 "
-                 "--warmup 1) then the kernel-trace pass (bench --steps 3 --warmup 1), all `--no-resident "
+        fo.write("Commands: `profiles/profile_round.sh %s %s`: two PMC passes (FETCH_SIZE, WRITE_SIZE; bench --steps 3 "
+                 "--warmup 0) then the kernel-trace pass (bench --steps 3 --warmup 0), all `--no-resident "
                  "--no-cpu-baseline`, so every launch is a writer encode job.  Jobs: trace pass %d, fetch pass %d, "
                  "write pass %d (`%s` dispatches).  Per-job figures = every dispatch of the kernel in the pass / the "
                  "pass's jobs.  FETCH is raw except for the 16 B/lane streaming kernels %s (x2, MI355X_MICROARCH.md "
@@ -133,8 +149,14 @@ def full(tag, workload):
             fo.write("- achieved = %d B / %.3f ms = **%.1f GB/s**, frac = %.1f / 8000 = **%.5f**\n"
                      % (ab, ro["avg_launch_ms"], ab / (ro["avg_launch_ms"] * 1e-3) / 1e9,
                         ab / (ro["avg_launch_ms"] * 1e-3) / 1e9, ab / (ro["avg_launch_ms"] * 1e-3) / HBM_PEAK))
-            fo.write("- counter traffic / algorithmic bytes = %.1f MB / %.1f MB = **%.2fx**\n"
-                     % (k7_tr / 1e6, ab / 1e6, k7_tr / max(1, ab)))
+            if pm.get("k7_traffic_over_algorithmic"):
+                rr = pm["k7_traffic_over_algorithmic"]
+                fo.write("- counter traffic / algorithmic bytes (PMC passes, same jobs: %s) = **%.2fx**; for this pass's "
+                         "launches: %.2f x %d B = **%.1f MB per launch** (the bench line's `traffic`)\n"
+                         % (pm.get("k7_ratio_note", ""), rr, rr, ab, rr * ab / 1e6))
+            else:
+                fo.write("- counter traffic / algorithmic bytes = %.1f MB / %.1f MB = **%.2fx**\n"
+                         % (k7_tr / 1e6, ab / 1e6, k7_tr / max(1, ab)))
             st = bl.get("stage_roofline")
             if st:
                 fo.write("\n## Encode stages per job (HIP events on the encoder stream, algorithmic bytes of "

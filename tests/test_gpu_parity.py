@@ -416,3 +416,40 @@ def test_writer_batches_split_at_job_size():
     env = dict(os.environ, KPW_STAGE_FLUSH_MB="2")
     r = subprocess.run([sys.executable, "-c", _SPLIT_CHILD, paths], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "split ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+_EAGER_CHILD = r"""
+import sys
+sys.path[:0] = sys.argv[1].split(":")
+import kpw, oracle, pqwalk, synth
+schema = synth.REC8
+n = 1_500_000
+data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE0B, n)
+for block in (1 << 20, 8 << 20):
+    props = kpw.ParquetProperties(block_size=block, compression_codec_name=1)
+    pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class), props)
+    for i in range(0, n, 100_000):
+        j = min(n, i + 100_000)
+        pf.write_batch((data[int(offs[i]):int(offs[j])], offs[i:j + 1] - offs[i]))
+    pf.close()
+    fb = pf.file_bytes()
+    ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=block, codec=1))
+    assert fb == ob, pqwalk.first_difference(fb, ob)
+print("eager ok")
+"""
+
+
+def test_writer_eager_jobs():
+    """Eager jobs (writer.cpp eager_job_bytes): a fill buffer past KPW_EAGER_MB is submitted as
+    soon as an encode worker idles, so job boundaries depend on timing.  With 1 MiB eager jobs
+    and 6 MB batches nearly every batch becomes a job whose open row group is carried into the
+    next; the file must stay byte-identical to the oracle's at either row-group size.  Runs in a
+    child process (the job size is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = ":".join(os.path.join(root, d) for d in ("synth", "oracle", "tests", "kafka-parquet-writer_amd", ""))
+    env = dict(os.environ, KPW_EAGER_MB="1", KPW_STAGE_FLUSH_MB="64")
+    r = subprocess.run([sys.executable, "-c", _EAGER_CHILD, paths], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "eager ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
