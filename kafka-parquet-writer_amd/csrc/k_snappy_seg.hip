@@ -40,7 +40,9 @@ namespace {
 constexpr uint32_t SG_SEG = 64;          // bytes per thread segment
 constexpr uint32_t SG_T = 1024;          // threads per workgroup (segments per 64 KiB fragment)
 constexpr uint32_t SG_W = SG_T / 64;     // waves
-constexpr uint32_t SG_MAXR = 64;
+#ifndef SG_MAXR
+#define SG_MAXR 128u             // rounds before a fragment is handed to the sequential kernels
+#endif
 constexpr uint32_t SG_MAXLEN = 512;
 constexpr uint32_t SG_RECS = 16;         // copies per segment (each >= 4 bytes, starting inside it)
 constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the whole workgroup

@@ -10,3 +10,10 @@ for b in tests/microbench/build/seg_bench_*; do
     timeout -k 10 120 $b /tmp/p2.bin 3 > gpurun_out/${v}_c2.log 2>&1
     timeout -k 10 120 $b /tmp/p4.bin 3 > gpurun_out/${v}_c4.log 2>&1
 done
+if [ -n "$SEG_C3" ]; then
+    python tests/microbench/dump_any.py 3 400000 /tmp/p3.bin
+    for b in tests/microbench/build/seg_bench_*; do
+        v=$(basename $b)
+        timeout -k 10 120 $b /tmp/p3.bin 3 > gpurun_out/${v}_c3.log 2>&1
+    done
+fi
