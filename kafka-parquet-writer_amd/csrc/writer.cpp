@@ -204,6 +204,8 @@ struct Worker {
     hipEvent_t d2h_ev[2] = {};         // D2H done, per page buffer set of the engine
     bool d2h_used[2] = {false, false};
     PinnedBuf h_asm;                   // device assembly: header blob + pieces (H2D source)
+    hipEvent_t asm_ev = nullptr;       // after a job's assembly H2D, gather and D2H into the file
+    bool asm_pending = false;          // asm_ev recorded and not yet waited for
     DevBuf d_asm_in, d_asm_out;        // device assembly: blob + pieces, the job's file bytes
     uint64_t njobs = 0;
     bool busy = false;
@@ -609,6 +611,12 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
             for (uint32_t o = 0; o < g.len; o += 65536)
                 pcs.push_back({g.dst + o, g.src + o, std::min<uint32_t>(65536u, g.len - o), g.dev});
         const size_t bb = (blob.size() + 15) & ~(size_t)15, pb = pcs.size() * sizeof(AsmPiece);
+        // this worker's previous assembly may still read h_asm (H2D) and write d_asm_out's
+        // D2H; the device side is stream-ordered, the host buffer is not
+        if (W.asm_pending) {
+            if (hipEventSynchronize(W.asm_ev) != hipSuccess) return KPW_ERR_DEVICE;
+            W.asm_pending = false;
+        }
         if (W.h_asm.ensure(bb + pb) || W.d_asm_in.ensure(bb + pb + 16) || W.d_asm_out.ensure(total + 64)) return KPW_ERR_NOMEM;
         memcpy(W.h_asm.p, blob.data(), blob.size());
         memcpy(W.h_asm.p + bb, pcs.data(), pb);
@@ -622,9 +630,10 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
                 return KPW_ERR_DEVICE;
             at += sp.second;
         }
-        const int slot = w->page_slot;
-        if (hipEventRecord(w->fd2h_ev[slot], s) != hipSuccess) return KPW_ERR_DEVICE;
-        if (hipEventSynchronize(w->fd2h_ev[slot]) != hipSuccess) return KPW_ERR_DEVICE;   // page buffers are reused next
+        // not waited for here: the engine's next encode reuses the page buffers after the gather
+        // in stream order, and drain() (close, getDataSize after a cut) waits for the file bytes
+        if (hipEventRecord(W.asm_ev, s) != hipSuccess) return KPW_ERR_DEVICE;
+        W.asm_pending = true;
         w->last_rg_end = w->fw->pos();
         if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
         return KPW_OK;
@@ -641,8 +650,10 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
         if (hipMemcpyAsync(w->host_pages[slot].p, out.d_pages, out.pages_len, hipMemcpyDeviceToHost, s) != hipSuccess)
             return KPW_ERR_DEVICE;
     }
+    // the assembly thread waits for this D2H; the engine's next encode reuses the device page
+    // buffers after it in stream order, and this slot's host pages again two jobs later, after
+    // this job's assembly thread was joined
     if (hipEventRecord(w->fd2h_ev[slot], s) != hipSuccess) return KPW_ERR_DEVICE;
-    if (hipEventSynchronize(w->fd2h_ev[slot]) != hipSuccess) return KPW_ERR_DEVICE;   // the engine reuses its buffers next
     if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
     start_assembly(w, std::move(out), slot);
     // HDFS alignment: the next row group's size limit depends on where this one ends in the file
@@ -1003,6 +1014,13 @@ static int drain(kpw_writer *w)
     }
     // no job runs now: the file-mode assembly thread and the D2H stream are the caller's
     (void)join_assembly(w);
+    for (int x = 0; x < w->nworkers; x++) {   // in-memory files: the last jobs' bytes have landed
+        Worker &W = w->wk[x];
+        if (W.asm_pending) {
+            if (hipEventSynchronize(W.asm_ev) != hipSuccess) set_fatal(w, KPW_ERR_DEVICE, "D2H of pages failed");
+            W.asm_pending = false;
+        }
+    }
     if (w->d2h_stream && hipStreamSynchronize(w->d2h_stream) != hipSuccess) set_fatal(w, KPW_ERR_DEVICE, "D2H of pages failed");
     std::lock_guard<std::mutex> g(w->mu);
     if (w->fatal_st) {
@@ -1044,7 +1062,8 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
         if (hipEventCreateWithFlags(&W.carry_ev, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&W.enc_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&W.d2h_ev[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&W.d2h_ev[1], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&W.d2h_ev[1], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&W.asm_ev, hipEventDisableTiming) != hipSuccess)
             return KPW_ERR_DEVICE;
     }
     // the open row group of a job lands in the next buffer's gap (its wire bytes are a small
@@ -1085,7 +1104,7 @@ kpw_writer::~kpw_writer()
     for (auto &e : slot_ev) if (e) (void)hipEventDestroy(e);
     for (auto &e : fd2h_ev) if (e) (void)hipEventDestroy(e);
     for (auto &W : wk) {
-        for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1]}) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1], W.asm_ev}) if (e) (void)hipEventDestroy(e);
     }
     if (direct_ev) (void)hipEventDestroy(direct_ev);
     if (trace_on()) tf[2] = now_ms();
