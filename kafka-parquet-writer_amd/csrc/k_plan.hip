@@ -23,7 +23,7 @@
 // started at s re-synchronises with it (both end an RLE run at the same position; from
 // there on the encoders are in identical states), and from a short local walk before.
 //
-// One block walks the row groups sequentially; its 256 threads split the streams / boolean
+// One block walks the row groups sequentially; its 1024 threads split the streams / boolean
 // columns (every thread takes the same decisions from block-wide sums).
 #include "kpw_device.h"
 #include "kpw_kernels.h"
@@ -147,7 +147,8 @@ __device__ __forceinline__ int64_t stream_pos(const PlanArgs &a, const PlanStrea
     return S.rank_col < 0 ? r : (int64_t)pc_at(a.cols[S.rank_col], (uint64_t)r);
 }
 
-constexpr int PLAN_T = 256;   // k_plan block: four waves, each thread owns streams tid, tid + 256, ...
+constexpr int PLAN_T = 1024;  // k_plan block: 16 waves, each thread owns streams tid, tid + 1024, ... (C3: 199 streams;
+                               // the clamp-point evaluation splits them over the waves: 13 per lane, not 50)
 
 __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 {
@@ -177,7 +178,7 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 // memSize at the 64 clamp-step check points s + rc + 10000*j, valid only when every walker is
 // past its convergence point (or has no further events): E_s(q) is then one lookup per stream.
 // The block splits (point, stream) pairs: lane j of every wave owns point j, wave g the streams
-// g, g + 4, ... (independent loads, no walking), and the four partial sums meet in LDS; every
+// g, g + 16, ... (independent loads, no walking), and the 16 partial sums meet in LDS; every
 // lane j returns the memSize of point j.
 __device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, int64_t s, int64_t rc)
 {
