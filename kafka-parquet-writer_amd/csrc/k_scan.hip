@@ -18,6 +18,13 @@ struct RawF {
     __device__ uint64_t get(uint32_t, uint64_t i) const { return raw[i]; }
     __device__ void put(uint32_t, uint64_t i, uint64_t v) const { P[i] = v; }
 };
+// record lengths narrowed to T (u8 / u16) on the host; element 0 is `base` (the first boundary)
+template <typename T>
+struct NarrowF {
+    const T *raw; uint64_t base; uint64_t *P;
+    __device__ uint64_t get(uint32_t, uint64_t i) const { return i ? (uint64_t)raw[i] : base; }
+    __device__ void put(uint32_t, uint64_t i, uint64_t v) const { P[i] = v; }
+};
 struct PcntF {
     const DevCol *cols; const uint32_t *opt;
     __device__ uint64_t get(uint32_t j, uint64_t w) const { return __popcll(cols[opt[j]].pres[w]); }
@@ -100,6 +107,12 @@ void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, uint64_t *t
 {
     RawF f{raw, P};
     mj_scan(f, n, 1, tmp, s);
+}
+
+void launch_prefix_narrow(const void *raw, int width, uint64_t base, uint64_t n, uint64_t *P, uint64_t *tmp, hipStream_t s)
+{
+    if (width == 1) mj_scan(NarrowF<uint8_t>{(const uint8_t *)raw, base, P}, n, 1, tmp, s);
+    else mj_scan(NarrowF<uint16_t>{(const uint16_t *)raw, base, P}, n, 1, tmp, s);
 }
 
 void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, uint64_t *tmp, hipStream_t s)

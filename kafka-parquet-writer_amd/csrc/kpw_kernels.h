@@ -225,6 +225,8 @@ struct DeltaJob {
 // ---------------------------------------------------------------- launch wrappers
 void launch_decode(const DecodeArgs &a, hipStream_t s);
 void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, uint64_t *tile_tmp, hipStream_t s);
+// P[0] = 0, P[k] = base + raw[1] + ... + raw[k-1] (k >= 1) for u8 (width 1) / u16 (width 2) raw
+void launch_prefix_narrow(const void *raw, int width, uint64_t base, uint64_t n, uint64_t *P, uint64_t *tile_tmp, hipStream_t s);
 
 void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t n_etiles,
                           const RleScratch &sc, hipStream_t s);

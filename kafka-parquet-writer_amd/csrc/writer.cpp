@@ -196,7 +196,8 @@ struct Worker {
     Engine *eng = nullptr;
     DevBuf d_off;                      // device record offsets of the running job ([0] = 0, then offs)
     PinnedBuf h_off;                   // host record boundaries of the running job
-    PinnedBuf h_len;                   // u32 record lengths (H2D source: half the bytes of offsets)
+    PinnedBuf h_len;                   // record lengths, u8 / u16 / u32 (H2D source: 1/8 .. 1/2 the bytes of offsets)
+    int len_width = 1;                 // bytes per length of the previous job
     DevBuf d_len, d_tmp;               // device lengths, prefix-scan scratch
     const uint64_t *offs = nullptr;    // device record offsets handed to the engine
     hipEvent_t carry_ev = nullptr;     // recorded after this worker placed a job's carried records
@@ -665,6 +666,9 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
 // before the encode.  PCIe is the writer's ceiling, so they cross as u32 lengths
 // (lens[0] = the first boundary) and a prefix scan rebuilds the u64 offsets in HBM.  (A per-worker
 // copy stream measured 3-5 % slower end to end: profiles/r02d_copy_paths.md.)
+// Lengths cross in the narrowest of u8 / u16 / u32 that holds every record of the job (C2's
+// ~62-byte records: 1 byte each, a quarter of the u32 bytes): the width of the worker's previous
+// job is tried first, and a record that does not fit sends this job through the next width.
 static int upload_offsets(Worker &W, size_t count, hipStream_t s)
 {
     const uint64_t *hb = (const uint64_t *)W.h_off.p;
@@ -676,14 +680,36 @@ static int upload_offsets(Worker &W, size_t count, hipStream_t s)
     if (W.h_len.ensure(count * 4) || W.d_len.ensure(count * 4) || W.d_off.ensure((count + 1) * 8) ||
         W.d_tmp.ensure(mj_scan_tmp_words(count, 1) * 8 + 64))
         return KPW_ERR_NOMEM;
-    uint32_t *len = (uint32_t *)W.h_len.p;
-    len[0] = (uint32_t)hb[0];
-    par_for(count - 1, [=](uint64_t a, uint64_t b) { for (uint64_t i = a; i < b; i++) len[i + 1] = (uint32_t)(hb[i + 1] - hb[i]); });
-    if (hipMemcpyAsync(W.d_len.p, len, count * 4, hipMemcpyHostToDevice, s) != hipSuccess) return KPW_ERR_DEVICE;
-    launch_prefix_raw(W.d_len.as<uint32_t>(), count, W.d_off.as<uint64_t>(), W.d_tmp.as<uint64_t>(), s);
-    if (hipGetLastError() != hipSuccess) return KPW_ERR_DEVICE;
-    W.offs = W.d_off.as<uint64_t>() + 1;   // P[k + 1] = boundary k
-    return KPW_OK;
+    for (int width = W.len_width;; width *= 2) {
+        std::atomic<bool> over{false};
+        if (width == 4) {
+            uint32_t *len = (uint32_t *)W.h_len.p;
+            len[0] = (uint32_t)hb[0];
+            par_for(count - 1, [=](uint64_t a, uint64_t b) { for (uint64_t i = a; i < b; i++) len[i + 1] = (uint32_t)(hb[i + 1] - hb[i]); });
+        } else {
+            auto narrow = [&](auto *len, uint64_t lim) {
+                len[0] = 0;
+                par_for(count - 1, [=, &over](uint64_t a, uint64_t b) {
+                    uint64_t m = 0;
+                    for (uint64_t i = a; i < b; i++) {
+                        const uint64_t d = hb[i + 1] - hb[i];
+                        m |= d;
+                        len[i + 1] = (decltype(+len[0]))d;
+                    }
+                    if (m > lim) over = true;
+                });
+            };
+            if (width == 1) narrow((uint8_t *)W.h_len.p, 0xff); else narrow((uint16_t *)W.h_len.p, 0xffff);
+            if (over) continue;   // (m is an OR of lengths: > lim iff some length has a bit above lim)
+        }
+        W.len_width = width;
+        if (hipMemcpyAsync(W.d_len.p, W.h_len.p, count * width, hipMemcpyHostToDevice, s) != hipSuccess) return KPW_ERR_DEVICE;
+        if (width == 4) launch_prefix_raw(W.d_len.as<uint32_t>(), count, W.d_off.as<uint64_t>(), W.d_tmp.as<uint64_t>(), s);
+        else launch_prefix_narrow(W.d_len.p, width, hb[0], count, W.d_off.as<uint64_t>(), W.d_tmp.as<uint64_t>(), s);
+        if (hipGetLastError() != hipSuccess) return KPW_ERR_DEVICE;
+        W.offs = W.d_off.as<uint64_t>() + 1;   // P[k + 1] = boundary k
+        return KPW_OK;
+    }
 }
 
 static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
@@ -1073,6 +1099,11 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
     model_on = model_ok;
     if (model_ok && model.multi_page()) {
         if (int st = peng.init(eng.device, schema, props)) return st;
+    }
+    {   // KPW_LEN_BYTES=4: record lengths always cross as u32 (A/B of the narrow lengths)
+        const char *e = getenv("KPW_LEN_BYTES");
+        const int lw = e && (atoi(e) == 2 || atoi(e) == 4) ? atoi(e) : 1;
+        for (int x = 0; x < nworkers; x++) wk[x].len_width = lw;
     }
     for (int x = 0; x < nworkers; x++) wk[x].th = std::thread(worker_main, this, x);
     return acquire_fill(this);
