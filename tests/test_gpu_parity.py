@@ -453,3 +453,55 @@ def test_writer_eager_jobs():
     env = dict(os.environ, KPW_EAGER_MB="1", KPW_STAGE_FLUSH_MB="64")
     r = subprocess.run([sys.executable, "-c", _EAGER_CHILD, paths], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "eager ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+_LEN_CHILD = r"""
+import sys
+import numpy as np
+sys.path[:0] = sys.argv[1].split(":")
+import kpw, oracle, pqwalk, synth
+
+def varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+def rec(i, qlen):
+    q = bytes((65 + (i + k) % 26) for k in range(qlen))
+    return b"\x0a" + varint(len(q)) + q + b"\x10" + varint(1700000000000 + i)
+
+schema = synth.SAMPLE
+for name, big in (("u8", 0), ("u16", 300), ("u32", 70000)):
+    recs = [rec(i, big if big and i % 97 == 5 else 3 + i % 40) for i in range(3000)]
+    offs = np.zeros(len(recs) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(r) for r in recs])
+    data = np.frombuffer(b"".join(recs), dtype=np.uint8)
+    props = kpw.ParquetProperties(block_size=64 << 10, compression_codec_name=1)
+    pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class), props)
+    for i in range(0, len(recs), 500):
+        j = min(len(recs), i + 500)
+        pf.write_batch((data[int(offs[i]):int(offs[j])], offs[i:j + 1] - offs[i]))
+    pf.close()
+    fb = pf.file_bytes()
+    ob = oracle.encode_file(schema, data, offs, oracle.make_props(block_size=64 << 10, codec=1))
+    assert fb == ob, name + ": " + str(pqwalk.first_difference(fb, ob))
+print("lengths ok")
+"""
+
+
+def test_writer_record_length_widths():
+    """Record offsets cross PCIe as u8 / u16 / u32 lengths (writer.cpp upload_offsets): a job
+    whose records all fit a byte goes as u8, a 300-byte or 70 KB record sends the job through
+    u16 / u32.  Bulk writes of 500 records (KPW_MODEL_MAX_BATCH=8, so they skip the per-record
+    model) with such records every 97th; each file byte-identical to the oracle's."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = ":".join(os.path.join(root, d) for d in ("synth", "oracle", "tests", "kafka-parquet-writer_amd", ""))
+    env = dict(os.environ, KPW_MODEL_MAX_BATCH="8", KPW_STAGE_FLUSH_MB="1", KPW_EAGER_MB="-1")
+    r = subprocess.run([sys.executable, "-c", _LEN_CHILD, paths], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "lengths ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
