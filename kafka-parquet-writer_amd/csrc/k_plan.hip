@@ -147,9 +147,12 @@ __device__ __forceinline__ int64_t stream_pos(const PlanArgs &a, const PlanStrea
     return S.rank_col < 0 ? r : (int64_t)pc_at(a.cols[S.rank_col], (uint64_t)r);
 }
 
-constexpr int PLAN_T = 1024;  // k_plan block: 16 waves, each thread owns streams tid, tid + 1024, ... (C3: 199 streams;
-                               // the clamp-point evaluation splits them over the waves: 13 per lane, not 50)
+// k_plan block: PLAN_T threads, each owning streams tid, tid + PLAN_T, ...; 1024 (16 waves) for
+// many streams (C3: 199, so the clamp-point evaluation takes 13 per lane instead of 50 with 4
+// waves; 1.72 -> 1.46 ms per job), 256 for few (C2: 4 streams, where 16 waves only add barrier
+// cost: resident plan stage 13.1 -> 17.2 ms per 100 M records with 1024)
 
+template <int PLAN_T>
 __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 {
     __shared__ uint64_t red[PLAN_T / 64];
@@ -180,6 +183,7 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 // The block splits (point, stream) pairs: lane j of every wave owns point j, wave g the streams
 // g, g + 16, ... (independent loads, no walking), and the 16 partial sums meet in LDS; every
 // lane j returns the memSize of point j.
+template <int PLAN_T>
 __device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, int64_t s, int64_t rc)
 {
     __shared__ uint64_t red[PLAN_T];
@@ -210,6 +214,7 @@ __device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, int64_t 
     return tot;
 }
 
+template <int PLAN_T>
 __device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walker *W, int64_t r)
 {
     bool ok = true;
@@ -218,6 +223,7 @@ __device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walke
     return __syncthreads_and(ok ? 1 : 0) != 0;
 }
 
+template <int PLAN_T>
 __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
 {
     __shared__ Walker W[MAX_STREAMS];
@@ -246,8 +252,8 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
             // check points and the scalar replay below takes parquet-mr's decisions over them,
             // stopping where a decision leaves the clamp path (or cuts).  Near the cut (the
             // estimate halves the distance each check) one point at a time is cheaper.
-            if (clamp && walkers_converged(a, W, s + rc)) {
-                const uint64_t Mj = eval_mem_points(a, W, s, rc);
+            if (clamp && walkers_converged<PLAN_T>(a, W, s + rc)) {
+                const uint64_t Mj = eval_mem_points<PLAN_T>(a, W, s, rc);
                 bool left = false;
                 for (int j = 0; j < 64; j++) {
                     const int64_t rcv = rc + 10000 * (int64_t)j;
@@ -270,7 +276,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
                 continue;
             }
             r = s + rc;
-            const int64_t M = (int64_t)eval_mem(a, W, s, r);
+            const int64_t M = (int64_t)eval_mem<PLAN_T>(a, W, s, r);
             const int64_t rs = M / rc;
             if (M > T - 2 * rs) { cut = true; break; }
             const float q = __fdiv_rn((float)T, (float)rs);
@@ -296,7 +302,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
         }
         // the open row group [s, n)
         int64_t open_buf = 0;
-        if (s < n) open_buf = (int64_t)eval_mem(a, W, s, n);
+        if (s < n) open_buf = (int64_t)eval_mem<PLAN_T>(a, W, s, n);
         if (a.final_flush && s < n) {
             if (nrg < a.max_rgs) { if (tid == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = n; } }
             else overflow = 1;
@@ -316,7 +322,8 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
 
 void launch_plan(const PlanArgs &a, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(PLAN_T), 0, s, a);
+    if (a.nstreams > 64) hipLaunchKernelGGL(k_plan<1024>, dim3(1), dim3(1024), 0, s, a);
+    else hipLaunchKernelGGL(k_plan<256>, dim3(1), dim3(256), 0, s, a);
 }
 
 // ------------------------------------------------------------------ multi-page (v1)
