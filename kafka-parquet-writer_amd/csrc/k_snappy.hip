@@ -652,8 +652,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_copy(SnappyArgs a)
     }
     const uint8_t *s = a.frag_out + (uint64_t)f * SNAPPY_FRAG_CAP;
     uint8_t *d = a.out + a.page_coff[pg] + a.frag_coff[f];
-    const uint32_t n = a.frag_len[f];
-    for (uint32_t i = threadIdx.x; i < n; i += KPW_BLOCK) d[i] = s[i];
+    block_copy(d, s, a.frag_len[f], threadIdx.x, KPW_BLOCK);
 }
 
 // v2: the level bytes that sit in front of a page's values, copied verbatim ahead of its

@@ -148,4 +148,36 @@ __device__ __forceinline__ uint64_t bits_window(const uint64_t *w, uint64_t bit)
     return (lo >> sh) | (w[(bit >> 6) + 1] << (64 - sh));
 }
 
+// A workgroup copies n bytes between arbitrary byte addresses: 16-byte aligned stores for the
+// body (each built from aligned dword loads of the source shifted with alignbyte), single bytes
+// for the unaligned head and the tail.  Reads stay inside [src, src + n): a chunk whose last
+// source dword would end past it is copied bytewise.
+__device__ __forceinline__ void block_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t tid, uint32_t nth)
+{
+    uint32_t head = (uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u);
+    if (head > n) head = n;
+    const uint32_t chunks = (n - head) / 16u;
+    const uint32_t tail0 = head + chunks * 16u;
+    if (tid < head) dst[tid] = src[tid];
+    for (uint32_t i = tail0 + tid; i < n; i += nth) dst[i] = src[i];
+    const uintptr_t sa = (uintptr_t)(src + head);
+    const uint32_t sh = (uint32_t)(sa & 3u);
+    const uint32_t *sw = (const uint32_t *)(sa & ~(uintptr_t)3);
+    uint4 *dw = (uint4 *)(dst + head);
+    for (uint32_t k = tid; k < chunks; k += nth) {
+        const uint32_t *w = sw + 4u * k;
+        if (sh && head + 16u * k + 20u - sh > n) {   // the fifth dword would read past the source
+            for (uint32_t i = 0; i < 16u; i++) dst[head + 16u * k + i] = src[head + 16u * k + i];
+            continue;
+        }
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = sh ? w[4] : 0u;
+        uint4 v;
+        v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        v.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        dw[k] = v;
+    }
+}
+
 }  // namespace kpw
