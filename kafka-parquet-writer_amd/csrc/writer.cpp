@@ -226,7 +226,7 @@ struct kpw_writer {
     hipStream_t copy_stream = nullptr;
     StageBuf buf[kBufs];
     int fill = -1;                     // buffer the caller appends to
-    uint64_t gap_ = 0;
+    std::atomic<uint64_t> gap_{0};   // raised by the workers when a carry does not fit (place_carry)
     // pinned slots for non-pinned sources
     PinnedBuf slot[kSlots];
     hipEvent_t slot_ev[kSlots] = {};
@@ -281,6 +281,7 @@ struct kpw_writer {
     BatchOut asm_out;
     int64_t last_rg_end = 0;           // InternalParquetRecordWriter.lastRowGroupEndPos
     int64_t open_buffered = 0;         // open row group's buffered size after the last PLANNED job
+    std::atomic<int> n_materialize{0};
     double t_open = 0, t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0;
     double stats[16] = {0};            // kpw_writer_stats (job order; read after drain)
 
@@ -474,6 +475,7 @@ static void par_for(uint64_t n, Fn fn)
 static int materialize(kpw_writer *w, StageBuf &B, hipStream_t s)
 {
     if (!B.carry_in_store) return KPW_OK;
+    w->n_materialize++;
     const uint64_t cs = B.carry.back();                 // carried bytes (store offsets start at 0)
     const uint64_t app = B.len - B.gap;
     const size_t cap = std::max<size_t>(B.cap, cs + app + w->gap_ + (64ull << 20));
@@ -496,6 +498,12 @@ static int materialize(kpw_writer *w, StageBuf &B, hipStream_t s)
     return KPW_OK;
 }
 
+static bool gap_adapt()
+{
+    static const bool on = [] { const char *e = getenv("KPW_GAP_ADAPT"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
 // Place records [hb[i0], hb[i1]) of buffer `src` in front of buffer `dst`'s appended records
 // (on stream s).
 static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, size_t i0, size_t i1, StageBuf &dst,
@@ -504,6 +512,15 @@ static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, s
     const uint64_t b0 = hb[i0], c = hb[i1] - b0;
     uint64_t at;
     uint8_t *base;
+    // A carry larger than the gap goes through carry_store and a rebuild of the whole buffer
+    // (materialize: two device copies of up to a job's bytes and a stream sync).  Open row
+    // groups of wide records (C3) carry more wire bytes than 2 x blockSize, so the gap of the
+    // buffers acquired from now on grows to 1.25 x the largest carry seen.
+    if (c > dst.gap && gap_adapt()) {
+        const uint64_t want = (c + c / 4 + (1ull << 20) - 1) & ~((1ull << 20) - 1);
+        uint64_t cur = w->gap_.load();
+        while (cur < want && !w->gap_.compare_exchange_weak(cur, want)) {}
+    }
     if (c <= dst.gap) {
         at = dst.gap - c;
         base = dst.d;
@@ -1726,8 +1743,10 @@ extern "C" int kpw_writer_close(kpw_writer *w)
             fprintf(stderr, "[kpw] close: entered at %.1f, footer done at %.1f ms\n", t_close - w->t_open, now_ms() - w->t_open);
         if (trace_on())
             fprintf(stderr, "[kpw] close: worker encode %.1f ms; caller: pinned DMA waits %.1f ms, buffer acquire %.1f ms; "
-                            "worker: page buffer alloc + D2H issue %.1f ms; assembly %.1f ms\n",
-                    w->t_encode, w->t_dma, w->t_acquire, w->t_d2h_alloc, w->t_asm);
+                            "worker: page buffer alloc + D2H issue %.1f ms; assembly %.1f ms; buffers rebuilt for "
+                            "a carry %d, gap %.0f MiB\n",
+                    w->t_encode, w->t_dma, w->t_acquire, w->t_d2h_alloc, w->t_asm, w->n_materialize.load(),
+                    w->gap_.load() / 1048576.0);
         return KPW_OK;
     } catch (...) {
         set_fatal(w, KPW_ERR_DEVICE, "close failed");
