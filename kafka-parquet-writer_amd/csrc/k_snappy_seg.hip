@@ -49,6 +49,9 @@ constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the wh
 #ifndef SG_PB
 #define SG_PB 4u                 // search probes in flight per parse step
 #endif
+#ifndef SG_LITW
+#define SG_LITW 1                // emit: short literals stored as dwords
+#endif
 #ifndef SG_SW
 #define SG_SW 4u                 // sort scatter: waves (each owns the hashes h % SG_SW)
 #endif
@@ -706,7 +709,15 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             auto lit_out = [&](uint32_t src, uint32_t len) {
                 op = put_lit_tag(out, op, len);
                 if (len <= SG_LITCOPY) {
+#if SG_LITW
+                    // dword stores once the output is aligned (the thread owns [op, op + len))
+                    uint32_t i = 0;
+                    for (; i < len && ((op + i) & 3); i++) out[op + i] = in.ld8(src + i);
+                    for (; i + 4 <= len; i += 4) *(__attribute__((address_space(1))) uint32_t *)(out + op + i) = in.ld32(src + i);
+                    for (; i < len; i++) out[op + i] = in.ld8(src + i);
+#else
                     for (uint32_t i = 0; i < len; i++) out[op + i] = in.ld8(src + i);
+#endif
                 } else {
                     const uint32_t jx = atomicAdd(&S.njobs, 1u);
                     G.job[jx][0] = src; G.job[jx][1] = op; G.job[jx][2] = len;
