@@ -633,7 +633,11 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     }
     // +512: K7 reads its input through 256-byte register windows that may run past the last page
     ENS(d_body, body_tot + 512 + 4096);   // + 4 KiB: the writer D2Hs whole 4 KiB units
-    CK(hipMemsetAsync(d_body.p, 0, body_tot + 512, s));
+    // only the tail K7's windows may read is cleared here; the PLAIN boolean values are zeroed
+    // by k_zero_bool (launch_chunk_write) and every other body byte is written by its kernel
+    // (KPW_BODY_POISON=1 fills the body with 0xAB first: the GPU parity suite checks that)
+    if (body_poison()) CK(hipMemsetAsync(d_body.p, 0xAB, body_tot, s));
+    CK(hipMemsetAsync(d_body.as<uint8_t>() + body_tot, 0, 512, s));
     launch_chunk_write(a, d_jobs.as<RleJob>(), d_body.as<uint8_t>(), s);
     if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), s);
     if (v2_) {

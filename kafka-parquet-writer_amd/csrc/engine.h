@@ -11,6 +11,14 @@
 #include "kpw_kernels.h"
 
 namespace kpw {
+
+// KPW_BODY_POISON=1: fill each job's page-body buffer with 0xAB before the writers run (test
+// infrastructure: shows that no output byte depends on the buffer's previous contents)
+inline bool body_poison()
+{
+    static const bool on = [] { const char *e = getenv("KPW_BODY_POISON"); return e && e[0] == '1'; }();
+    return on;
+}
 struct SnappyArgs;
 
 struct ColInfo {

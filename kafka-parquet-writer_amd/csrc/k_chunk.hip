@@ -858,6 +858,27 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_plain_bool(const ChunkDesc *ch, c
     }
 }
 
+// Zero the values part of the PLAIN boolean pages before k_plain_bool ORs its words in (the rest
+// of the page body is written in full by its kernels, so the body is not cleared as a whole).
+// Grid (chunks, 16): the dwords inside the range with dword stores, the edge bytes with byte stores.
+__global__ void __launch_bounds__(KPW_BLOCK) k_zero_bool(const ChunkDesc *ch, const DevCol *cols, uint8_t *out)
+{
+    const ChunkDesc &C = ch[blockIdx.x];
+    const DevCol col = cols[C.col];
+    if (col.phys != 0 || C.bool_job >= 0 || C.val_len == 0) return;
+    const uint64_t b = C.val_off, e = C.val_off + C.val_len;
+    const uint64_t wb = (b + 3) & ~3ull, we = e & ~3ull;
+    const uint64_t tid = (uint64_t)blockIdx.y * KPW_BLOCK + threadIdx.x, nth = (uint64_t)gridDim.y * KPW_BLOCK;
+    if (wb >= we) {
+        for (uint64_t i = b + tid; i < e; i += nth) out[i] = 0;
+        return;
+    }
+    uint32_t *o32 = (uint32_t *)out;
+    for (uint64_t w = (wb >> 2) + tid; w < (we >> 2); w += nth) o32[w] = 0u;
+    if (tid < wb - b) out[b + tid] = 0;
+    if (tid < e - we) out[we + tid] = 0;
+}
+
 // Binary statistics: meta[4c..4c+3] = (min offset, min len, max offset, max len) of chunk c
 // (pass 1, blob == nullptr); pass 2 copies the bytes into blob at the running offset.
 __global__ void __launch_bounds__(KPW_BLOCK) k_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols,
@@ -958,6 +979,7 @@ void launch_chunk_write(const ChunkArgs &a, const RleJob *jobs, uint8_t *out, hi
     seg_tile_scan_u64(a.tile_raw, a.tile_raw_off, a.ctile_chunk, a.nctiles, a.seg, s);
     hipLaunchKernelGGL(k_plain, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
                        a.tile_raw_off, out);
+    if (a.nchunks) hipLaunchKernelGGL(k_zero_bool, dim3(a.nchunks, 16), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, out);
     hipLaunchKernelGGL(k_plain_bool, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, out);
 }
 
