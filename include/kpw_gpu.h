@@ -179,6 +179,16 @@ int kpw_encoder_copy_pages(kpw_encoder *e, uint64_t off, uint64_t len, void *hos
  * k_snappy_copy; 0 when uncompressed).  Returns entries written (<= cap). */
 int kpw_encoder_stage_times(const kpw_encoder *e, float *ms, int cap);
 
+/* Device memory for kpw_encoder_encode's batches, from this library's own HIP runtime (a JVM
+ * host that binds the flush path directly has no other; tests and bench.py use it too, so one
+ * runtime owns every device pointer the encoder sees).  No reference counterpart: parquet-mr
+ * keeps its buffers on the Java heap.  kpw_device_alloc returns NULL with *status set on
+ * failure; the copies are synchronous and return a status. */
+void *kpw_device_alloc(int device, uint64_t bytes, int *status);
+void kpw_device_free(void *d_ptr);
+int kpw_copy_h2d(int device, void *d_dst, const void *src, uint64_t bytes);
+int kpw_copy_d2h(int device, void *dst, const void *d_src, uint64_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -123,3 +123,36 @@ extern "C" int kpw_encoder_stage_times(const kpw_encoder *e, float *ms, int cap)
 }
 
 // The ParquetFile drop-in (kpw_writer_*) and kpw_host_alloc live in writer.cpp.
+
+// ---------------------------------------------------------------- device memory (flush-path batches)
+
+extern "C" void *kpw_device_alloc(int device, uint64_t bytes, int *status)
+{
+    void *p = nullptr;
+    int st = KPW_OK;
+    if (hipSetDevice(device) != hipSuccess) st = KPW_ERR_DEVICE;
+    else if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) { st = KPW_ERR_NOMEM; p = nullptr; }
+    if (status) *status = st;
+    return p;
+}
+
+extern "C" void kpw_device_free(void *d_ptr)
+{
+    if (d_ptr) (void)hipFree(d_ptr);
+}
+
+extern "C" int kpw_copy_h2d(int device, void *d_dst, const void *src, uint64_t bytes)
+{
+    if (!bytes) return KPW_OK;
+    if (!d_dst || !src) return KPW_ERR_INVALID_ARG;
+    if (hipSetDevice(device) != hipSuccess) return KPW_ERR_DEVICE;
+    return hipMemcpy(d_dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
+}
+
+extern "C" int kpw_copy_d2h(int device, void *dst, const void *d_src, uint64_t bytes)
+{
+    if (!bytes) return KPW_OK;
+    if (!dst || !d_src) return KPW_ERR_INVALID_ARG;
+    if (hipSetDevice(device) != hipSuccess) return KPW_ERR_DEVICE;
+    return hipMemcpy(dst, d_src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
+}

@@ -150,8 +150,9 @@ __device__ __forceinline__ uint64_t bits_window(const uint64_t *w, uint64_t bit)
 
 // A workgroup copies n bytes between arbitrary byte addresses: 16-byte aligned stores for the
 // body (each built from aligned dword loads of the source shifted with alignbyte), single bytes
-// for the unaligned head and the tail.  Reads stay inside [src, src + n): a chunk whose last
-// source dword would end past it is copied bytewise.
+// for the unaligned head and the tail.  Reads never end past src + n (a chunk whose last source
+// dword would is copied bytewise); they may start up to 3 bytes before src + head, inside the
+// same aligned dword, so they never touch another page.
 __device__ __forceinline__ void block_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t tid, uint32_t nth)
 {
     uint32_t head = (uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u);

@@ -197,7 +197,7 @@ struct Worker {
     DevBuf d_off;                      // device record offsets of the running job ([0] = 0, then offs)
     PinnedBuf h_off;                   // host record boundaries of the running job
     PinnedBuf h_len;                   // record lengths, u8 / u16 / u32 (H2D source: 1/8 .. 1/2 the bytes of offsets)
-    int len_width = 1;                 // bytes per length of the previous job
+    int len_width = 1;                 // narrowest length width a job tries (KPW_LEN_BYTES)
     DevBuf d_len, d_tmp;               // device lengths, prefix-scan scratch
     const uint64_t *offs = nullptr;    // device record offsets handed to the engine
     hipEvent_t carry_ev = nullptr;     // recorded after this worker placed a job's carried records
@@ -343,7 +343,10 @@ static int acquire_fill(kpw_writer *w)
         w->buf[k].state = BUF_FILLING;
     }
     StageBuf &b = w->buf[k];
-    const size_t need = w->gap_ + stage_flush_bytes() + (64ull << 20);
+    // one read of gap_: a worker may raise it (place_carry) while this runs, and the buffer's
+    // gap must be the one its capacity was sized for
+    const uint64_t gap = w->gap_.load();
+    const size_t need = gap + stage_flush_bytes() + (64ull << 20);
     if (b.cap < need && alloc_buf(w, b, need)) {
         std::lock_guard<std::mutex> g(w->mu);
         b.state = BUF_FREE;   // not taken: the caller has no fill buffer (w->fill stays -1)
@@ -351,8 +354,8 @@ static int acquire_fill(kpw_writer *w)
         return wfail(w, KPW_ERR_NOMEM, "device stage buffer allocation failed");
     }
     if (trace_on()) w->t_acquire += now_ms() - ta;
-    b.gap = w->gap_;
-    b.len = w->gap_;
+    b.gap = gap;
+    b.len = gap;
     b.carry.clear();
     b.carry_in_store = false;
     b.ends.clear();
@@ -697,8 +700,13 @@ static int upload_offsets(Worker &W, size_t count, hipStream_t s)
     if (W.h_len.ensure(count * 4) || W.d_len.ensure(count * 4) || W.d_off.ensure((count + 1) * 8) ||
         W.d_tmp.ensure(mj_scan_tmp_words(count, 1) * 8 + 64))
         return KPW_ERR_NOMEM;
-    for (int width = W.len_width;; width *= 2) {
-        std::atomic<bool> over{false};
+    // Every job starts at u8 (no ratchet: one long record must not keep the worker on wide
+    // lengths for the rest of the file); the u8 pass ORs the lengths, so a job that
+    // does not fit goes straight to the width that holds it (at most two host passes).
+    int width = W.len_width;   // 1 unless KPW_LEN_BYTES forces wider lengths (A/B)
+    for (;;) {
+        std::atomic<uint64_t> all_or{0};
+        bool over = false;
         if (width == 4) {
             uint32_t *len = (uint32_t *)W.h_len.p;
             len[0] = (uint32_t)hb[0];
@@ -706,20 +714,20 @@ static int upload_offsets(Worker &W, size_t count, hipStream_t s)
         } else {
             auto narrow = [&](auto *len, uint64_t lim) {
                 len[0] = 0;
-                par_for(count - 1, [=, &over](uint64_t a, uint64_t b) {
+                par_for(count - 1, [=, &all_or](uint64_t a, uint64_t b) {
                     uint64_t m = 0;
                     for (uint64_t i = a; i < b; i++) {
                         const uint64_t d = hb[i + 1] - hb[i];
                         m |= d;
                         len[i + 1] = (decltype(+len[0]))d;
                     }
-                    if (m > lim) over = true;
+                    all_or.fetch_or(m, std::memory_order_relaxed);
                 });
+                over = all_or.load() > lim;   // an OR of lengths is > lim iff some length is
             };
             if (width == 1) narrow((uint8_t *)W.h_len.p, 0xff); else narrow((uint16_t *)W.h_len.p, 0xffff);
-            if (over) continue;   // (m is an OR of lengths: > lim iff some length has a bit above lim)
+            if (over) { width = all_or.load() <= 0xffff ? 2 : 4; continue; }
         }
-        W.len_width = width;
         if (hipMemcpyAsync(W.d_len.p, W.h_len.p, count * width, hipMemcpyHostToDevice, s) != hipSuccess) return KPW_ERR_DEVICE;
         if (width == 4) launch_prefix_raw(W.d_len.as<uint32_t>(), count, W.d_off.as<uint64_t>(), W.d_tmp.as<uint64_t>(), s);
         else launch_prefix_narrow(W.d_len.p, width, hb[0], count, W.d_off.as<uint64_t>(), W.d_tmp.as<uint64_t>(), s);

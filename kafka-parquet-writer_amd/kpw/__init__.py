@@ -8,7 +8,7 @@ is no CPU fallback: constructing a ParquetFile without the library raises.
 from ._lib import (KpwError, InvalidProtoError, load_library, library_path, Schema, Column,
                    UNCOMPRESSED, SNAPPY)
 from .parquet_file import ParquetFile, ParquetProperties, pinned_empty
-from .encoder import Encoder
+from .encoder import Encoder, DeviceBuffer
 
-__all__ = ["ParquetFile", "ParquetProperties", "Encoder", "Schema", "Column", "KpwError", "InvalidProtoError",
+__all__ = ["ParquetFile", "ParquetProperties", "Encoder", "DeviceBuffer", "Schema", "Column", "KpwError", "InvalidProtoError",
            "load_library", "library_path", "UNCOMPRESSED", "SNAPPY", "pinned_empty"]

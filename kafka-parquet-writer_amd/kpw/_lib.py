@@ -154,6 +154,12 @@ def load_library():
     L.kpw_host_free.argtypes = [vp]
     L.kpw_trim_caches.argtypes = []
     L.kpw_trim_caches.restype = None
+    L.kpw_device_alloc.restype = vp
+    L.kpw_device_alloc.argtypes = [i32, u64, ctypes.POINTER(i32)]
+    L.kpw_device_free.argtypes = [vp]
+    L.kpw_device_free.restype = None
+    L.kpw_copy_h2d.argtypes = [i32, vp, vp, u64]
+    L.kpw_copy_d2h.argtypes = [i32, vp, vp, u64]
     _lib = L
     return L
 
@@ -162,4 +168,5 @@ EXPORTED = ["kpw_writer_open", "kpw_writer_write", "kpw_writer_write_until_full"
             "kpw_writer_num_records", "kpw_writer_creation_time_ms", "kpw_writer_close", "kpw_writer_file_bytes",
             "kpw_writer_failed_record", "kpw_writer_last_error", "kpw_writer_free", "kpw_encoder_create",
             "kpw_encoder_destroy", "kpw_encoder_last_error", "kpw_encoder_encode", "kpw_encoder_copy_pages",
-            "kpw_encoder_stage_times", "kpw_host_alloc", "kpw_host_free", "kpw_writer_stats", "kpw_trim_caches"]
+            "kpw_encoder_stage_times", "kpw_host_alloc", "kpw_host_free", "kpw_writer_stats", "kpw_trim_caches",
+            "kpw_device_alloc", "kpw_device_free", "kpw_copy_h2d", "kpw_copy_d2h"]

@@ -1,6 +1,7 @@
 """Encoder — the flush-path primitive (kpw_encoder_*): device-resident record batch ->
 encoded pages + metadata for every row group parquet-mr would cut.  Used by bench.py and
-the GPU parity tests; takes torch CUDA(HIP) tensors for device memory."""
+the GPU parity tests; batches live in DeviceBuffer memory (kpw_device_alloc: the library's own
+HIP runtime, so no second runtime is involved)."""
 import ctypes
 
 import numpy as np
@@ -14,6 +15,48 @@ def props_c(block_size=128 * MiB, page_size=128 * MiB, codec=0, enable_dictionar
             writer_version=1):
     return _PropsC(block_size, page_size, dictionary_page_size, 1 if enable_dictionary else 0, codec, writer_version, 0, 0,
                    8 * MiB)
+
+
+class DeviceBuffer:
+    """HBM owned by libkpw_gpu.so (kpw_device_alloc); `ptr` is the device address.
+    DeviceBuffer(nbytes) or DeviceBuffer.from_array(numpy array) (a synchronous H2D copy)."""
+
+    def __init__(self, nbytes, device=0):
+        self._L = load_library()
+        self.device = device
+        self.nbytes = int(nbytes)
+        st = ctypes.c_int(0)
+        self.ptr = self._L.kpw_device_alloc(device, max(1, self.nbytes), ctypes.byref(st))
+        if not self.ptr:
+            raise KpwError(st.value, "device allocation of %d bytes" % self.nbytes)
+
+    @classmethod
+    def from_array(cls, arr, device=0):
+        a = np.ascontiguousarray(arr)
+        b = cls(a.nbytes, device)
+        if a.nbytes:
+            st = b._L.kpw_copy_h2d(device, b.ptr, a.ctypes.data, a.nbytes)
+            if st:
+                raise KpwError(st, "H2D copy")
+        return b
+
+    def to_array(self, dtype=np.uint8, count=None):
+        dt = np.dtype(dtype)
+        n = self.nbytes // dt.itemsize if count is None else count
+        out = np.empty(max(1, n), dtype=dt)
+        if n:
+            st = self._L.kpw_copy_d2h(self.device, out.ctypes.data, self.ptr, n * dt.itemsize)
+            if st:
+                raise KpwError(st, "D2H copy")
+        return out[:n]
+
+    def free(self):
+        if getattr(self, "ptr", None):
+            self._L.kpw_device_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
 
 
 class Encoder:

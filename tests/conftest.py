@@ -19,21 +19,3 @@ def pytest_configure(config):
         lib = {"oracle": "build/libkpw_oracle.so", "synth": "build/libkpw_synth.so"}[d]
         if not os.path.exists(os.path.join(ROOT, d, lib)):
             subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, d)])
-
-
-_torch_hip_ready = False
-
-
-@pytest.fixture(autouse=True)
-def _torch_hip_first(request):
-    """PyTorch-ROCm bundles its own libamdhip64 next to /opt/rocm's, which libkpw_gpu.so
-    links.  Whichever initialises first owns the device for the process: when the kpw library
-    goes first, torch's later lazy init reports "No HIP GPUs are available".  GPU tests use
-    torch (device buffers for the encoder API), so torch's runtime is initialised before the
-    first GPU test, whatever the test order."""
-    global _torch_hip_ready
-    if not _torch_hip_ready and request.node.get_closest_marker("gpu"):
-        import torch
-        torch.cuda.init()
-        _torch_hip_ready = True
-    yield

@@ -1,6 +1,8 @@
 """Helpers for the GPU parity tests: run the HIP encoder on device-resident batches and
 compare, page by page, with the CPU oracle's file for the same records and properties."""
 import io
+import os
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -11,9 +13,11 @@ MiB = 1024 * 1024
 
 
 def to_device(data, offsets):
-    import torch
-    d = torch.from_numpy(np.ascontiguousarray(data) if len(data) else np.zeros(1, np.uint8)).to("cuda")
-    o = torch.from_numpy(offsets.astype(np.int64)).to("cuda")
+    """Record bytes and u64 offsets in HBM allocated by the library itself (kpw.DeviceBuffer):
+    one HIP runtime owns every device pointer the encoder sees."""
+    import kpw
+    d = kpw.DeviceBuffer.from_array(np.ascontiguousarray(data) if len(data) else np.zeros(1, np.uint8))
+    o = kpw.DeviceBuffer.from_array(np.ascontiguousarray(offsets, dtype=np.uint64))
     return d, o
 
 
@@ -22,14 +26,12 @@ def gpu_encoder_pages(schema, data, offsets, codec=0, block_size=128 * MiB, page
     """Returns (row_groups, [(rg, col, [page dicts with 'body'])]) from the HIP encoder
     (a fresh one, or `enc` to reuse an encoder across batches)."""
     import kpw
-    import torch
     if enc is None:
         enc = kpw.Encoder(kpw.Schema(schema.message_name, schema.columns, schema.proto_class), codec=codec,
                           block_size=block_size, page_size=page_size, enable_dictionary=dictionary,
                           writer_version=writer_version)
     d, o = to_device(data, offsets)
-    torch.cuda.synchronize()
-    info = enc.encode(d.data_ptr(), o.data_ptr(), len(offsets) - 1, final=True)
+    info = enc.encode(d.ptr, o.ptr, len(offsets) - 1, final=True)
     blob = enc.pages_bytes()
     pages = enc.pages()
     chunks = enc.chunks()
@@ -142,3 +144,78 @@ def gpu_file(schema, data, offsets, props=None, batches=1):
         pf.write_batch((data[int(offsets[i]):int(offsets[j])], sub))
     pf.close()
     return pf.file_bytes()
+
+
+# ---------------------------------------------------------------- full-size parity, row group by row group
+
+AHEAD = 10_001   # MAXIMUM_RECORD_COUNT_FOR_CHECK + 1: the next size check is at most this far
+
+
+def _workers():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 8
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+
+
+def chunk_table(fb):
+    """Per row group: (num_rows, [(chunk bytes, ColumnMetaData without file offsets)])."""
+    fm = pqwalk.footer(fb)
+    out = []
+    for rg in fm[4]:
+        cols = []
+        for cc in rg[1]:
+            md = dict(cc[3])
+            start = min(md[9], md[11]) if md.get(11) else md[9]
+            body = fb[start:start + md[7]]
+            for k in (9, 10, 11):
+                md.pop(k, None)
+            cols.append((body, md))
+        out.append((rg[3], cols))
+    return out
+
+
+def check_row_groups(schema, data, offs, fb, props):
+    """Every row group of file `fb` (records data/offs) against the oracle, in parallel:
+    parquet-mr's row groups are independent (after a flush InternalParquetRecordWriter resets
+    recordCount and checks again at 100 records; column chunks depend only on their row
+    group's records), so row group r is checked against the oracle run on records
+    [start_r, end_r + AHEAD): its first row group must end at end_r (the cut is re-derived)
+    and every column chunk must be byte-identical, with equal ColumnMetaData apart from file
+    offsets.  Returns a list of mismatch descriptions (empty = identical)."""
+    n = len(offs) - 1
+    got = chunk_table(fb)
+    starts = np.cumsum([0] + [r[0] for r in got])
+    errs = []
+    if starts[-1] != n:
+        return ["row groups cover %d of %d records" % (starts[-1], n)]
+
+    def one(r):
+        s, cnt = int(starts[r]), got[r][0]
+        e = min(n, s + cnt + AHEAD)
+        w = oracle.OracleWriter(schema, props)
+        st, nw = w.write_batch(data, offs[s:e + 1])
+        if st:
+            return ["rg %d: oracle write failed (%d at %d)" % (r, st, nw)]
+        w.close()
+        want = chunk_table(w.file_bytes())
+        del w
+        if want[0][0] != cnt:
+            return ["rg %d (records %d..): GPU cut after %d records, oracle after %d" % (r, s, cnt, want[0][0])]
+        bad = []
+        for c, ((gb, gm), (ob, om)) in enumerate(zip(got[r][1], want[0][1])):
+            if gm != om:
+                bad.append("rg %d col %s: column metadata differs" % (r, schema.columns[c][0]))
+            if gb != ob:
+                i = next((j for j in range(min(len(gb), len(ob))) if gb[j] != ob[j]), min(len(gb), len(ob)))
+                bad.append("rg %d col %s: chunk bytes differ at %d (len %d vs %d)" % (r, schema.columns[c][0], i,
+                                                                                     len(gb), len(ob)))
+        return bad
+
+    with ThreadPoolExecutor(_workers()) as ex:   # ctypes releases the GIL inside the oracle
+        for b in ex.map(one, range(len(got))):
+            errs += b
+    return errs
+
+

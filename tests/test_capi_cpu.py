@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_header_symbols():
     L = kpw.load_library()
     hdr = open(os.path.join(ROOT, "include", "kpw_gpu.h")).read()
-    declared = set(re.findall(r"\b(kpw_[a-z_]+)\s*\(", hdr))
+    declared = set(re.findall(r"\b(kpw_[a-z0-9_]+)\s*\(", hdr))
     assert declared == set(_lib.EXPORTED)
     for sym in declared:
         assert hasattr(L, sym), sym

@@ -1,0 +1,60 @@
+"""Full-size parity of the bench workloads through the ParquetFile drop-in (kpw_writer_*):
+C2 (100 M Rec8), C3 (10 M Wide), C4 (20 M HighCard), SNAPPY, 128 MiB row groups, the bench's
+seeds (VERDICT r03 "missing 2").  The single-threaded oracle would take minutes
+for a whole file, but every row group is independent in parquet-mr: after a flush
+InternalParquetRecordWriter resets recordCount and checks again at 100 records, and column
+chunks depend only on the row group's records.  So each row group of the GPU file is checked
+against the oracle run on records [start, end + 10001) (the next size check is at most 10 000
+records ahead), in parallel on the host's cores:
+  - the oracle's first row group ends where the GPU's does (the cut is re-derived);
+  - every column chunk is byte-identical (page headers, dictionary and data pages, Snappy
+    bytes), and its ColumnMetaData (encodings, sizes, statistics) equal apart from file offsets.
+KPW_FULL_SCALE (default 1.0) scales the record counts down for a quick run."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import synth
+from gpu_helpers import check_row_groups
+
+pytestmark = pytest.mark.gpu
+MiB = 1024 * 1024
+SCALE = float(os.environ.get("KPW_FULL_SCALE", "1.0"))
+
+
+def _writer_file(schema, data, offs, batch):
+    import kpw
+    pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class),
+                         kpw.ParquetProperties(compression_codec_name=kpw.SNAPPY))
+    n = len(offs) - 1
+    for a in range(0, n, batch):
+        b = min(n, a + batch)
+        pf.write_batch((data[int(offs[a]):int(offs[b])], (offs[a:b + 1] - offs[a]).astype(np.uint64)))
+    pf.close()
+    fb = pf.file_bytes()
+    assert pf.get_num_written_records() == n
+    return fb
+
+
+@pytest.mark.parametrize("kind,n,seed", [
+    (synth.KIND_REC8, 100_000_000, 0xC0FFEE02),    # C2
+    (synth.KIND_WIDE, 10_000_000, 0xC0FFEE03),     # C3
+    (synth.KIND_HIGHCARD, 20_000_000, 0xC0FFEE04),  # C4
+], ids=["c2", "c3", "c4"])
+def test_full_size_writer_matches_oracle_per_row_group(kind, n, seed):
+    n = max(1000, int(n * SCALE))
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, seed, n)
+    fb = _writer_file(schema, data, offs, 500_000)   # the bench's poll() batch size
+    assert fb[:4] == b"PAR1" and fb[-4:] == b"PAR1"
+    props = oracle.make_props(block_size=128 * MiB, page_size=128 * MiB, codec=1, enable_dictionary=True)
+    errs = check_row_groups(schema, data, offs, fb, props)
+    assert not errs, errs[:10]
+    # the file also reads back in an independent reader with the right shape
+    import io
+
+    import pyarrow.parquet as pq
+    md = pq.ParquetFile(io.BytesIO(fb)).metadata
+    assert md.num_rows == n and md.num_columns == len(schema.columns)

@@ -23,21 +23,20 @@ SEED = 0xC0FFEE02   # bench.py's C2 seed
 
 @pytest.fixture(scope="module")
 def c2():
-    import torch
+    import kpw
     data, offs = synth.generate(synth.KIND_REC8, SEED, N)
-    d = torch.from_numpy(data).to("cuda")
-    o = torch.from_numpy(offs.astype(np.int64)).to("cuda")
-    torch.cuda.synchronize()
-    return data, offs, d, o
+    d = kpw.DeviceBuffer.from_array(data)   # HBM from the library's own HIP runtime
+    o = kpw.DeviceBuffer.from_array(offs.astype(np.uint64))
+    yield data, offs, d, o
+    d.free()
+    o.free()
 
 
 def _encode(d, o, codec):
     import kpw
-    import torch
     s = synth.REC8
     enc = kpw.Encoder(kpw.Schema(s.message_name, s.columns, s.proto_class), codec=codec)
-    torch.cuda.synchronize()
-    enc.encode(d.data_ptr(), o.data_ptr(), N, final=True)
+    enc.encode(d.ptr, o.ptr, N, final=True)
     return enc
 
 
