@@ -21,7 +21,10 @@ opens fresh writers, so nothing an encoder learns (K7's longest-first fragment o
 between steps.
 
 Secondary keys: `resident_encode` (kpw_encoder_encode on a batch already in HBM, the r01
-headline), `roofline` (the dominant kernel, timed with HIP events on the encoder's stream inside
+headline), `c4` (the C4 writer line, 2 steps) and `bulk_multipage` (C2 bulk writes with 1 MiB
+pages inside 128 MiB row groups, 2 steps), `per_record` / `per_record_multipage` (the
+reference's write + getDataSize loop at 128 MiB / 1 MiB pages, the oracle's same loops in
+`cpu_baseline`), `roofline` (the dominant kernel, timed with HIP events on the encoder's stream inside
 the timed writer steps; algorithmic bytes per launch), `roofline.pipeline_frac` (sum of
 algorithmic bytes over sum of device time of every encode stage, §8d), a measured device copy
 ceiling, and `cpu_baseline` (the CPU oracle — a C restatement of parquet-mr 1.10.1 — doing the
@@ -319,6 +322,33 @@ def per_record_leg(kpw, schema, sschema, kind, seed, n, device, max_file_size, p
                 reference_sizing_hint_records_per_s=300000)
 
 
+def writer_leg(kpw, kind, seed, n, device, steps, warmup, page_size=128 * MiB, sets=None):
+    """Secondary writer-path line (same drop-in and timing as the headline, fewer steps): another
+    workload (C4) or another page size (pageSize(...) < blockSize, KafkaProtoParquetWriter.java:656-659
+    -> ParquetFile.java:47: bulk writes with page cuts inside row groups)."""
+    import synth
+    sschema = synth.SCHEMAS[kind]
+    schema = kpw.Schema(sschema.message_name, sschema.columns, sschema.proto_class)
+    if sets is None:
+        sets = [synth.generate(kind, seed + 0x1000 * k, n, alloc=kpw.pinned_empty) for k in range(2)]
+    props = kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=kpw.SNAPPY, page_size=page_size)
+    for i in range(warmup):
+        write_file(kpw, schema, props, sets[i % 2][0], sets[i % 2][1], device)
+    t0 = time.perf_counter()
+    nb = 0
+    file_bytes = 0
+    for i in range(steps):
+        d, o = sets[(warmup + i) % 2]
+        size, _ = write_file(kpw, schema, props, d, o, device)
+        nb += int(o[-1])
+        file_bytes += size
+    dt = time.perf_counter() - t0
+    return dict(value=round(nb / dt / 1e9, 4), unit="GB/s", records_per_s=round(steps * (len(sets[0][1]) - 1) / dt, 1),
+                ms_per_step=round(dt / steps * 1e3, 3), steps=steps, warmup=warmup, records_per_step=len(sets[0][1]) - 1,
+                bytes_per_step=int(nb / steps), file_bytes_per_step=int(file_bytes / steps), page_size=page_size,
+                workload=sschema.message_name.split(".")[-1] + ", SNAPPY, 128 MiB row groups, pageSize %d" % page_size)
+
+
 def cpu_baseline_per_record(sschema, kind, seed, n, max_file_size, page_size):
     """CPU-baseline leg of the per-record loop: the oracle's kpwo_write + kpwo_data_size per
     record on the same records as per_record_leg, one thread (one WorkerThread)."""
@@ -378,28 +408,27 @@ def host_threads():
 def resident_encode(kpw, schema, batches, device, steps=3):
     """Secondary: kpw_encoder_encode on batches already in HBM (pages stay in HBM), cycling
     over the distinct batches; returns GB/s and the mean per-stage device ms."""
-    import torch
     enc = kpw.Encoder(schema, device=device, codec=1, block_size=128 * MiB, page_size=128 * MiB)
     dev = []
-    for data, offs in batches:
-        dev.append((torch.from_numpy(data).to("cuda"), torch.from_numpy(offs.view(np.int64)).to("cuda"), len(offs) - 1,
+    for data, offs in batches:   # HBM from the library's own runtime (kpw_device_alloc)
+        dev.append((kpw.DeviceBuffer.from_array(data, device), kpw.DeviceBuffer.from_array(offs, device), len(offs) - 1,
                     int(offs[-1])))
-    torch.cuda.synchronize()
-    enc.encode(dev[0][0].data_ptr(), dev[0][1].data_ptr(), dev[0][2], final=True)   # warm-up
+    enc.encode(dev[0][0].ptr, dev[0][1].ptr, dev[0][2], final=True)   # warm-up
     acc = np.zeros(10)
     tot_bytes = 0
     k7_bytes = 0
     t0 = time.perf_counter()
     for i in range(steps):
         d, o, n, nb = dev[(i + 1) % len(dev)]
-        enc.encode(d.data_ptr(), o.data_ptr(), n, final=True)
+        enc.encode(d.ptr, o.ptr, n, final=True)
         acc += np.array(enc.stage_times()[:10], dtype=np.float64)
         tot_bytes += nb
         k7_bytes += sum(p["uncompressed_size"] + p["compressed_size"] for p in enc.pages())
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt = time.perf_counter() - t0   # kpw_encoder_encode is blocking
+    for d, o, _, _ in dev:
+        d.free()
+        o.free()
     del dev
-    torch.cuda.empty_cache()
     names = ["decode", "plan", "stats+dict", "rle", "layout+plain+write", "compress", "metadata", "total", "k_decode",
              "k7_snappy"]
     k7_ms = acc[9] / steps
@@ -432,6 +461,8 @@ def main():
                     help="maxFileSize of the per-record leg (reference default 1 GiB, KafkaProtoParquetWriter.java:462)")
     ap.add_argument("--per-record-page-kb", type=int, default=128 * 1024,
                     help="pageSize of the per-record leg (reference default = blockSize, KafkaProtoParquetWriter.java:474)")
+    ap.add_argument("--secondary-steps", type=int, default=2,
+                    help="timed steps of the secondary writer legs at N=1 (c4 and bulk_multipage; 0 = skip)")
     ap.add_argument("--per-record-mp-page-kb", type=int, default=1024,
                     help="pageSize of a second per-record leg with page cuts inside row groups (pageSize(...), "
                          "KafkaProtoParquetWriter.java:656-659; 0 = skip)")
@@ -441,7 +472,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    torch.cuda.set_device(local_rank)   # torch's HIP runtime first (tests/conftest.py: _torch_hip_first)
+    # torch (RCCL bookkeeping, the copy-ceiling probe) bundles its own HIP runtime; it must
+    # initialise before libkpw_gpu.so's, or it reports no GPU.  The data path never uses it.
+    torch.cuda.set_device(local_rank)
     torch.cuda.init()
     numa = None if os.environ.get("KPW_BENCH_NO_NUMA") == "1" else bind_to_gpu_numa(local_rank)
     dist = dist_init(world, local_rank)
@@ -551,6 +584,13 @@ def main():
         if args.per_record_mp_page_kb:   # pageSize < blockSize: page cuts inside row groups (size probes)
             per_record_mp = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_records, local_rank,
                                            args.per_record_max_file_mb * MiB, args.per_record_mp_page_kb * 1024)
+    c4_leg = bulk_mp = None
+    if args.secondary_steps and world == 1 and args.workload == "c2":
+        # the config where encode, not PCIe, sets the pace (C4), and bulk writes with 1 MiB pages
+        c4k, c4n, c4seed, _ = WORKLOADS["c4"]
+        c4_leg = writer_leg(kpw, c4k, c4seed, c4n, local_rank, args.secondary_steps, 1)
+        bulk_mp = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, page_size=MiB,
+                             sets=[s[0] for s in sets])
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         threads = args.cpu_threads or host_threads()
@@ -562,6 +602,11 @@ def main():
             cpu["per_record"] = cpu_baseline_per_record(sschema, kind, wseed, args.per_record_records,
                                                         args.per_record_max_file_mb * MiB, args.per_record_page_kb * 1024)
             per_record["oracle_records_per_s"] = cpu["per_record"]["records_per_s"]
+        if per_record_mp:   # the oracle's same loop at the same page size
+            cpu["per_record_multipage"] = cpu_baseline_per_record(sschema, kind, wseed, args.per_record_records,
+                                                                  args.per_record_max_file_mb * MiB,
+                                                                  args.per_record_mp_page_kb * 1024)
+            per_record_mp["oracle_records_per_s"] = cpu["per_record_multipage"]["records_per_s"]
     out = {
         "metric": "Parquet encode GB/s + records/sec (whole node) at 1/2/4/8 MI355X vs CPU writer",
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -584,6 +629,8 @@ def main():
         "stage_roofline": stage_roof,
         "per_record": per_record,
         "per_record_multipage": per_record_mp,
+        "c4": c4_leg,
+        "bulk_multipage": bulk_mp,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

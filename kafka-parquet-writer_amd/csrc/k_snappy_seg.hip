@@ -112,22 +112,6 @@ typedef __attribute__((address_space(1))) uint16_t sgg_u16;
 typedef const __attribute__((address_space(1))) uint8_t sgg_cu8;
 typedef __attribute__((address_space(1))) uint8_t sgg_u8;
 
-// Scratch traffic (sorted entries, keys, bucket flags, copy records) is streamed: every round
-// re-reads a workgroup's ~400 KiB, which no L2 holds for 32 workgroups per XCD, so it is loaded
-// and stored non-temporally and the L2 keeps the fragment bytes the parse's compares read.
-#ifndef SG_NT
-#define SG_NT 1
-#endif
-#if SG_NT
-#define SG_LD(p) __builtin_nontemporal_load(p)
-#define SG_ST(v, p) __builtin_nontemporal_store(v, p)
-#else
-#define SG_LD(p) (*(p))
-#define SG_ST(v, p) (*(p) = (v))
-#endif
-typedef __attribute__((address_space(1))) uint64_t sgg_u64;
-typedef const __attribute__((address_space(1))) uint64_t sgg_cu64;
-
 // fragment bytes through aligned dword loads (the page buffer is padded past its last page)
 struct FIn {
     const uint8_t *base;
@@ -366,8 +350,7 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
         const uint32_t len = 4 + sg_fml(in, c + 4, base + 4, n, SG_MAXLEN);
         if (len > SG_MAXLEN) { o.lng = true; break; }
         o.fnd = true;
-        SG_ST((uint64_t)base | ((uint64_t)(base - c) << 16) | ((uint64_t)len << 32) | ((uint64_t)lit << 48),
-              (sgg_u64 *)&G.rec[(o.nrec++) * SG_T + t]);
+        G.rec[(o.nrec++) * SG_T + t] = (uint64_t)base | ((uint64_t)(base - c) << 16) | ((uint64_t)len << 32) | ((uint64_t)lit << 48);
         const uint32_t ipe = base + len;
         st = ipe >= ip_limit ? st_T(ipe) : st_P(ipe);
     }
@@ -531,7 +514,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             for (int q0 = 0; q0 < 8; q0 += 4) {
             sg_u32x4 vq[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) vq[q] = SG_LD(&sp4[q0 + q]);
+            for (int q = 0; q < 4; q++) vq[q] = sp4[q0 + q];
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
                 const int q = q0 + qq;
@@ -545,11 +528,11 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                     prevp = pp[e];
                     kk[e] = lds_ld32(S, pp[e]);
                 }
-                SG_ST((sg_u32x4{kk[0], kk[1], kk[2], kk[3]}), &kp[(2 * q) * SG_T]);
-                SG_ST((sg_u32x4{kk[4], kk[5], kk[6], kk[7]}), &kp[(2 * q + 1) * SG_T]);
+                kp[(2 * q) * SG_T] = sg_u32x4{kk[0], kk[1], kk[2], kk[3]};
+                kp[(2 * q + 1) * SG_T] = sg_u32x4{kk[4], kk[5], kk[6], kk[7]};
             }
             }
-            SG_ST(bf, (sgg_u64 *)&G.bflag[t]);
+            G.bflag[t] = bf;
         }
         const uint32_t key0 = lds_ld32(S, 0);   // the empty table's candidate is position 0
         __syncthreads();
@@ -580,11 +563,11 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 {
 #pragma unroll
                     for (int q = 0; q < 8; q++) {
-                        const sg_u32x4 v = SG_LD((sgg_cu4 *)&G.sig4[t * 8 + q]);
+                        const uint4 v = G.sig4[t * 8 + q];
                         sg2[4 * q] = v.x; sg2[4 * q + 1] = v.y; sg2[4 * q + 2] = v.z; sg2[4 * q + 3] = v.w;
                     }
                 }
-                const uint64_t bf = SG_LD((sgg_cu64 *)&G.bflag[t]);
+                const uint64_t bf = G.bflag[t];
                 uint32_t m = 0;
                 uint64_t insm = 0;   // bit j: sorted entry i0+j is an inserted position
                 const uint32_t *ib32 = (const uint32_t *)S.ibits;
@@ -628,12 +611,12 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                     asm volatile("" : "+v"(kp));
                     sg_u32x4 kb[2][4];
 #pragma unroll
-                    for (int i = 0; i < 4; i++) kb[0][i] = SG_LD(&kp[i * SG_T]);
+                    for (int i = 0; i < 4; i++) kb[0][i] = kp[i * SG_T];
 #pragma unroll
                     for (int c4 = 0; c4 < 4; c4++) {
                         if (c4 < 3) {
 #pragma unroll
-                            for (int i = 0; i < 4; i++) kb[(c4 + 1) & 1][i] = SG_LD(&kp[((c4 + 1) * 4 + i) * SG_T]);
+                            for (int i = 0; i < 4; i++) kb[(c4 + 1) & 1][i] = kp[((c4 + 1) * 4 + i) * SG_T];
                         }
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
@@ -707,7 +690,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         uint32_t osz = 0;
         uint32_t ne = e0.ne;
         for (uint32_t r = 0; r < po.nrec; r++) {
-            const uint64_t rc = SG_LD((sgg_cu64 *)&G.rec[r * SG_T + t]);
+            const uint64_t rc = G.rec[r * SG_T + t];
             const uint32_t base = (uint32_t)(rc & 0xffff), off = (uint32_t)((rc >> 16) & 0xffff);
             const uint32_t len = (uint32_t)((rc >> 32) & 0xffff), lit = (uint32_t)(rc >> 48) & 1;
             if (lit) osz += lit_size(base - ne);
@@ -742,7 +725,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 op += len;
             };
             for (uint32_t r = 0; r < po.nrec; r++) {
-                const uint64_t rc = SG_LD((sgg_cu64 *)&G.rec[r * SG_T + t]);
+                const uint64_t rc = G.rec[r * SG_T + t];
                 const uint32_t base = (uint32_t)(rc & 0xffff), off = (uint32_t)((rc >> 16) & 0xffff);
                 const uint32_t len = (uint32_t)((rc >> 32) & 0xffff), lit = (uint32_t)(rc >> 48) & 1;
                 if (lit) lit_out(ne, base - ne);

@@ -201,7 +201,8 @@ class ParquetFile:
         p = ctypes.c_void_p()
         n = ctypes.c_uint64()
         self._check(self._L.kpw_writer_file_bytes(self._h, ctypes.byref(p), ctypes.byref(n)), "file_bytes")
-        return ctypes.string_at(p.value, n.value)
+        # (ctypes.string_at takes a C int size: files of >= 2 GiB need the array view)
+        return (ctypes.c_char * n.value).from_address(p.value).raw if n.value else b""
 
     # AutoCloseable
     def __enter__(self):

@@ -151,7 +151,7 @@ class OracleWriter:
         st = lib().kpwo_file_bytes(self._h, ctypes.byref(p), ctypes.byref(n))
         if st:
             raise OracleError(st, "file_bytes")
-        return ctypes.string_at(p.value, n.value)
+        return (ctypes.c_char * n.value).from_address(p.value).raw if n.value else b""   # >= 2 GiB too
 
     def __del__(self):
         h = getattr(self, "_h", None)
