@@ -209,9 +209,11 @@ def write_file(kpw, schema, props, data, offs, device, batch=POLL_BATCH):
     optr = offs.ctypes.data
     n = len(offs) - 1
     t1 = time.perf_counter()
+    # kpw_writer_write_async: each poll batch's DMA is queued behind the previous one (the
+    # batches are never modified, so the "until the next call returns" reuse rule holds)
     for a in range(0, n, batch):
         b = min(n, a + batch)
-        st = L.kpw_writer_write(h, base, optr + 8 * a, b - a)   # absolute offsets into `data`
+        st = L.kpw_writer_write_async(h, base, optr + 8 * a, b - a)   # absolute offsets into `data`
         if st:
             pf._check(st, "write")
     t2 = time.perf_counter()

@@ -54,6 +54,15 @@ kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, const kpw_prop
  * close() writes the ones before it. */
 int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n);
 
+/* kpw_writer_write for a consumer that polls into a ring of >= 2 kpw_host_alloc batches
+ * (north_star: polled batches in pinned staging, moved to HBM by hipMemcpyAsync on a side
+ * stream): the call returns once the batch's DMA is queued, and the DMA may still read `data`
+ * until the NEXT kpw_writer_* call on this handle returns (the next async write waits for it
+ * then, with its own DMA already queued behind it, so the copy stream never idles between
+ * poll batches).  `offsets` may be reused at once.  Same records, file and errors as
+ * kpw_writer_write; memory outside kpw_host_alloc is copied before the call returns. */
+int kpw_writer_write_async(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n);
+
 /* Pinned (page-locked) host memory for record batches: where polled Kafka batches are meant
  * to land (north_star: "pinned host staging buffers"), so kpw_writer_write can DMA them to
  * HBM without a host copy.  Thread-safe; any writer handle on any device may read them. */

@@ -256,7 +256,10 @@ void par_copy(uint8_t *dst, const uint8_t *src, size_t n)
     if (t <= 1) { memcpy(dst, src, n); return; }
     std::vector<std::thread> th;
     th.reserve(t - 1);
-    const size_t per = (n / t + 4095) & ~(size_t)4095;
+    // ceil(n / t) rounded up to 4 KiB: the t chunks cover all n bytes (floor(n / t) lost the
+    // last n % t bytes whenever it was already a multiple of 4 KiB: a C4 slot at 192 MiB kept 6
+    // stale bytes, found by tests/test_gpu_fullsize.py)
+    const size_t per = ((n + t - 1) / t + 4095) & ~(size_t)4095;
     for (unsigned i = 1; i < t; i++) {
         const size_t a = std::min(n, per * i), b = std::min(n, per * (i + 1));
         if (b > a) th.emplace_back([=] { memcpy(dst + a, src + a, b - a); });

@@ -234,6 +234,12 @@ struct kpw_writer {
     uint64_t slot_used = 0, slot_dev = 0;   // pending bytes in the current slot and their device offset
     hipEvent_t direct_ev = nullptr;
     bool direct_pending = false;       // a DMA from the caller's pinned batch is in flight
+    // kpw_writer_write_async: the DMAs of call k may still read the caller's batch until call
+    // k+1 returns (call_ev[k & 1] follows them on the copy stream)
+    bool async_call = false;
+    hipEvent_t call_ev[2] = {nullptr, nullptr};
+    bool call_pending[2] = {false, false};
+    int call_k = 0;
     // caller-side state
     int64_t num_records = 0;           // ParquetFile.numWrittenRecords
     int64_t created_ms = 0;
@@ -1106,6 +1112,8 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
     for (auto &e : fd2h_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     if (hipEventCreateWithFlags(&direct_ev, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    for (auto &e : call_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &b : buf)
         if (hipEventCreateWithFlags(&b.copied, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     for (int x = 0; x < nworkers; x++) {
@@ -1163,6 +1171,7 @@ kpw_writer::~kpw_writer()
         for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1], W.asm_ev}) if (e) (void)hipEventDestroy(e);
     }
     if (direct_ev) (void)hipEventDestroy(direct_ev);
+    for (auto &e : call_ev) if (e) (void)hipEventDestroy(e);
     if (trace_on()) tf[2] = now_ms();
     if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
@@ -1250,6 +1259,41 @@ static int wait_direct(kpw_writer *w)
     w->direct_pending = false;
     if (hipEventSynchronize(w->direct_ev) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
     if (trace_on()) w->t_dma += now_ms() - ta;
+    return KPW_OK;
+}
+
+// Every batch an earlier kpw_writer_write_async may still be reading is released (its DMAs are
+// done): called by every entry point except the async write itself.
+static int release_batches(kpw_writer *w)
+{
+    for (int k = 0; k < 2; k++) {
+        if (!w->call_pending[k]) continue;
+        const double ta = trace_on() ? now_ms() : 0.0;
+        w->call_pending[k] = false;
+        if (hipEventSynchronize(w->call_ev[k]) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
+        if (trace_on()) w->t_dma += now_ms() - ta;
+    }
+    return KPW_OK;
+}
+
+// End of an async write: the DMAs this call issued are marked by call_ev[call_k]; the previous
+// call's batch is released (waited for) now, so the copy stream always has the next batch
+// queued behind the current one.
+static int finish_async_call(kpw_writer *w)
+{
+    const int k = w->call_k;
+    if (w->direct_pending) {
+        w->direct_pending = false;
+        if (hipEventRecord(w->call_ev[k], w->copy_stream) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "event record failed");
+        w->call_pending[k] = true;
+    }
+    w->call_k ^= 1;
+    if (w->call_pending[k ^ 1]) {
+        const double ta = trace_on() ? now_ms() : 0.0;
+        w->call_pending[k ^ 1] = false;
+        if (hipEventSynchronize(w->call_ev[k ^ 1]) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
+        if (trace_on()) w->t_dma += now_ms() - ta;
+    }
     return KPW_OK;
 }
 
@@ -1447,7 +1491,7 @@ static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offset
     rebase_ends(F.ends.grow(n), offsets, n, delta);
     w->num_records += (int64_t)n;
     w->dirty = true;
-    return wait_direct(w);
+    return w->async_call ? KPW_OK : wait_direct(w);   // async: finish_async_call waits a call later
 }
 
 // Plain bulk write: a batch that does not fit the fill buffer's capacity (gap + job size +
@@ -1628,6 +1672,8 @@ static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offse
     if (n_accepted) *n_accepted = 0;
     if (full) *full = 0;
     if (w->closed) return KPW_ERR_STATE;
+    if (!w->async_call)
+        if (int st = release_batches(w)) return st;
     if (int st = observe_failure(w)) return st;
     if (w->fill < 0) return wfail(w, KPW_ERR_STATE, "no stage buffer (an earlier failure)");
     if (!n) return KPW_OK;
@@ -1683,6 +1729,28 @@ extern "C" int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64
     }
 }
 
+extern "C" int kpw_writer_write_async(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n)
+{
+    if (!w || (n && (!data || !offsets))) return KPW_ERR_INVALID_ARG;
+    try {
+        // the modelled path (small writes) stages through the library's own pinned slots, so it
+        // never reads the batch after returning; only the bulk path's direct DMA is deferred
+        w->async_call = true;
+        int st = write_entry(w, data, offsets, n, -1, nullptr, nullptr);
+        w->async_call = false;
+        const int st2 = finish_async_call(w);
+        return st ? st : st2;
+    } catch (const std::bad_alloc &) {
+        w->async_call = false;
+        set_fatal(w, KPW_ERR_NOMEM, "host staging allocation failed");
+        return KPW_ERR_NOMEM;
+    } catch (...) {
+        w->async_call = false;
+        set_fatal(w, KPW_ERR_DEVICE, "unexpected failure");
+        return KPW_ERR_DEVICE;
+    }
+}
+
 extern "C" int kpw_writer_write_until_full(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n,
                                            int64_t max_file_size, uint64_t *n_accepted, int *full)
 {
@@ -1704,6 +1772,7 @@ extern "C" int64_t kpw_writer_data_size(kpw_writer *w)
     if (!w) return -1;
     try {
         if (w->closed) return w->fw->pos();
+        if (release_batches(w)) return -1;
         if (observe_failure(w)) return -1;
         if (w->model_on) {
             if (w->pending_cut) {
@@ -1735,6 +1804,7 @@ extern "C" int kpw_writer_close(kpw_writer *w)
     const double t_close = now_ms();
     try {
         if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
+        if (int st = release_batches(w)) return st;
         {
             std::lock_guard<std::mutex> g(w->mu);
             if (w->fatal_st) { w->err = w->fatal_err; return w->fatal_st; }
@@ -1780,7 +1850,7 @@ extern "C" void kpw_writer_free(kpw_writer *w) { delete w; }
 extern "C" int kpw_writer_stats(kpw_writer *w, double *out, int cap)
 {
     if (!w || !out || cap <= 0) return 0;
-    if (drain(w)) return 0;
+    if (release_batches(w) || drain(w)) return 0;
     const int n = cap < 16 ? cap : 16;
     for (int i = 0; i < n; i++) out[i] = w->stats[i];
     return n;

@@ -126,6 +126,7 @@ def load_library():
     L.kpw_writer_open.argtypes = [i32, ctypes.POINTER(_SchemaC), ctypes.POINTER(_PropsC), ctypes.c_char_p,
                                   ctypes.POINTER(i32)]
     L.kpw_writer_write.argtypes = [vp, vp, vp, u64]
+    L.kpw_writer_write_async.argtypes = [vp, vp, vp, u64]
     L.kpw_writer_write_until_full.argtypes = [vp, vp, vp, u64, i64, ctypes.POINTER(u64), ctypes.POINTER(i32)]
     L.kpw_writer_data_size.restype = i64
     L.kpw_writer_data_size.argtypes = [vp]
@@ -164,7 +165,7 @@ def load_library():
     return L
 
 
-EXPORTED = ["kpw_writer_open", "kpw_writer_write", "kpw_writer_write_until_full", "kpw_writer_data_size",
+EXPORTED = ["kpw_writer_open", "kpw_writer_write", "kpw_writer_write_async", "kpw_writer_write_until_full", "kpw_writer_data_size",
             "kpw_writer_num_records", "kpw_writer_creation_time_ms", "kpw_writer_close", "kpw_writer_file_bytes",
             "kpw_writer_failed_record", "kpw_writer_last_error", "kpw_writer_free", "kpw_encoder_create",
             "kpw_encoder_destroy", "kpw_encoder_last_error", "kpw_encoder_encode", "kpw_encoder_copy_pages",

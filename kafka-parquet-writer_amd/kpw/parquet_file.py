@@ -163,6 +163,13 @@ class ParquetFile:
         n = len(offsets) - 1
         self._check(self._L.kpw_writer_write(self._h, data.ctypes.data, offsets.ctypes.data, n), "write")
 
+    def write_batch_async(self, data, offsets):
+        """kpw_writer_write_async: `data` (a pinned_empty batch) may still be read by the DMA
+        until the next call on this file returns; `offsets` may be reused at once."""
+        n = len(offsets) - 1
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self._check(self._L.kpw_writer_write_async(self._h, data.ctypes.data, offsets.ctypes.data, n), "write")
+
     def write_until_full(self, values, max_file_size):
         data, offsets = _as_batch(values)
         n = len(offsets) - 1

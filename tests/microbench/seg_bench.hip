@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 #include <unistd.h>
 
 using namespace kpw;
@@ -72,6 +73,47 @@ int main(int argc, char **argv)
         int64_t w = kpwo_snappy_compress(host.data() + off[p], len[p], want[p].data(), want[p].size());
         want[p].resize((size_t)w);
     }
+    // per fragment: the oracle's output for the fragment alone (a fragment is compressed with
+    // a fresh table: strip the varint length prefix), to name a mismatching fragment
+    std::vector<std::vector<uint8_t>> wantf(nf);
+    for (uint32_t f = 0; f < nf; f++) {
+        if (fpage[f] >= np0) continue;
+        const uint64_t o0 = (uint64_t)fidx[f] * SNAPPY_FRAG;
+        const uint32_t fn = (uint32_t)std::min<uint64_t>(SNAPPY_FRAG, len[fpage[f]] - o0);
+        std::vector<uint8_t> w(64 + fn + fn / 6);
+        const int64_t wl = kpwo_snappy_compress(host.data() + off[fpage[f]] + o0, fn, w.data(), w.size());
+        uint32_t pre = 1, v = fn;
+        while (v >= 0x80) { v >>= 7; pre++; }
+        wantf[f].assign(w.begin() + pre, w.begin() + wl);
+    }
+    auto check_frags = [&](const char *what) -> int {
+        std::vector<uint32_t> fl(nf);
+        CK(hipMemcpy(fl.data(), d_flen, nf * 4, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> fo((size_t)nf * SNAPPY_FRAG_CAP);
+        CK(hipMemcpy(fo.data(), d_fout, fo.size(), hipMemcpyDeviceToHost));
+        int nbad = 0;
+        for (uint32_t f = 0; f < nf; f++) {
+            if (fpage[f] >= np0) continue;
+            const uint8_t *g = fo.data() + (size_t)f * SNAPPY_FRAG_CAP;
+            const auto &w = wantf[f];
+            if (fl[f] == w.size() && !memcmp(g, w.data(), w.size())) continue;
+            uint32_t d = 0;
+            while (d < fl[f] && d < w.size() && g[d] == w[d]) d++;
+            if (nbad < 8)
+                printf("FRAG MISMATCH [%s] frag %u (page %u idx %u): len %u want %zu, first diff at %u (got %02x want %02x)\n", what, f,
+                       fpage[f], fidx[f], fl[f], w.size(), d, d < fl[f] ? g[d] : 0, d < w.size() ? w[d] : 0);
+            if (nbad == 0 && getenv("SEG_DUMP_BAD")) {   // the fragment's input bytes, for the CPU model
+                FILE *fp = fopen(getenv("SEG_DUMP_BAD"), "wb");
+                const uint64_t o0 = (uint64_t)fidx[f] * SNAPPY_FRAG;
+                const uint64_t fn = std::min<uint64_t>(SNAPPY_FRAG, len[fpage[f]] - o0);
+                if (fp) { fwrite(&fn, 8, 1, fp); fwrite(host.data() + off[fpage[f]] + o0, 1, fn, fp); fclose(fp); }
+            }
+            nbad++;
+        }
+        if (nbad) printf("[%s] %d mismatching fragments\n", what, nbad);
+        fflush(stdout);
+        return nbad;
+    };
     int bad = 0;
     for (int mode = 0; mode < 2; mode++) {
         SnappyArgs a{};
@@ -82,6 +124,7 @@ int main(int argc, char **argv)
         if (!(mode && getenv("SEG_DEBUG"))) {
             launch_snappy(a, 0);
             CK(hipDeviceSynchronize());
+            bad += check_frags(mode ? "seg+v+s" : "v+s");
         }
         if (mode && getenv("SEG_DEBUG")) {   // watch k_snappy_seg alone through host-visible progress words
             uint32_t *dbg; CK(hipHostMalloc((void **)&dbg, (size_t)cus * 16, hipHostMallocCoherent | hipHostMallocMapped));
@@ -124,6 +167,20 @@ int main(int argc, char **argv)
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             printf("k_snappy_seg alone: %.3f ms, handed on %u of %u fragments\n", ms / reps, ho, nf);
+            {   // fragments k_snappy_seg finished itself must be exact
+                std::vector<uint32_t> fl3(nf);
+                CK(hipMemcpy(fl3.data(), d_flen, nf * 4, hipMemcpyDeviceToHost));
+                std::vector<uint8_t> fo((size_t)nf * SNAPPY_FRAG_CAP);
+                CK(hipMemcpy(fo.data(), d_fout, fo.size(), hipMemcpyDeviceToHost));
+                int nb = 0;
+                for (uint32_t f = 0; f < nf; f++) {
+                    if (fpage[f] >= np0 || fl3[f] == SEG_ABORTED) continue;
+                    const auto &w = wantf[f];
+                    if (fl3[f] == w.size() && !memcmp(fo.data() + (size_t)f * SNAPPY_FRAG_CAP, w.data(), w.size())) continue;
+                    if (nb++ < 8) printf("SEG-ALONE MISMATCH frag %u (page %u idx %u): len %u want %zu\n", f, fpage[f], fidx[f], fl3[f], w.size());
+                }
+                if (nb) { printf("[seg alone] %d mismatching fragments\n", nb); bad += nb; }
+            }
             {   // phase profile of one launch (thread 0 of every workgroup, summed)
                 uint64_t *d_prof; CK(hipMalloc(&d_prof, 128)); CK(hipMemset(d_prof, 0, 128));
                 SnappyArgs c = b; c.seg_prof = d_prof;

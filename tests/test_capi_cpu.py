@@ -107,3 +107,21 @@ def test_properties_alignment_follows_resolved_target_path():
     assert p.dfs_block_size == 128 * MiB
     p = kpw.ParquetProperties(hadoop_conf={"fs.defaultFS": "hdfs://nn:8020"}, target_dir="/rel/out")
     assert p.dfs_block_size == 128 * MiB
+
+
+def test_par_copy_covers_every_byte():
+    """The host staging copy (kpw::par_copy, writer slots and file assembly) splits large copies
+    over threads; every byte must arrive whatever n % threads is (a chunk size of floor(n/t)
+    rounded to 4 KiB once dropped the last n % t bytes: 6 stale bytes in a C4 slot)."""
+    import numpy as np
+    L = kpw.load_library()
+    fn = getattr(L, "_ZN3kpw8par_copyEPhPKhm")
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    fn.restype = None
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, 256, 40 << 20, dtype=np.uint8)
+    for n in (32600070, 7 * 4657152 + 1, 8 * (4 << 20) + 3, 5 * 4096 * 1024 + 4, (4 << 20) * 3 - 1, 12345, 40 << 20):
+        dst = np.zeros(n + 16, dtype=np.uint8)
+        fn(dst.ctypes.data, src.ctypes.data, n)
+        assert np.array_equal(dst[:n], src[:n]), n
+        assert not dst[n:].any(), n
