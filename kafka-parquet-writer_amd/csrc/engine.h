@@ -177,7 +177,7 @@ private:
                     const std::vector<std::vector<int64_t>> &cuts, MpRun &run);
     int grow_keep(DevBuf &b, size_t bytes, size_t keep);
     std::vector<DevBuf> mp_sp;
-    DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_flag, mp_dch, mp_dtile_chunk, mp_dtile_first, mp_dtile_count, mp_dtile_raw,
+    DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_pboff, mp_flag, mp_dch, mp_dtile_chunk, mp_dtile_first, mp_dtile_count, mp_dtile_raw,
         mp_dtile_smin, mp_dtile_smax, mp_dtile_cnt, mp_dtile_sz, mp_ssz, mp_spp, mp_cstream, mp_bstream, mp_acc;
     uint8_t *pages_dev_ = nullptr;
     uint64_t pages_len_ = 0;

@@ -70,10 +70,9 @@ int Engine::mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vecto
     a.s = s;
     a.h = h;
     a.cap = (uint32_t)std::min<uint64_t>((uint64_t)(h - s) / 2 + 2, 0xFFFFFFF0ull);
-    ENS(mp_ncuts, nc * 4); ENS(mp_cutpos, (uint64_t)nc * a.cap * 8); ENS(mp_pbytes, (uint64_t)nc * a.cap * 8); ENS(mp_flag, 64);
+    ENS(mp_ncuts, nc * 4); ENS(mp_cutpos, (uint64_t)nc * a.cap * 8); ENS(mp_flag, 64);
     a.ncuts = mp_ncuts.as<uint32_t>();
     a.cuts = mp_cutpos.as<int64_t>();
-    a.pbytes = mp_pbytes.as<uint64_t>();
     a.overflow = mp_flag.as<int32_t>();
     a.out = mp_flag.as<int64_t>() + 1;
     CK(hipMemsetAsync(mp_flag.p, 0, 64, stream));
@@ -581,17 +580,26 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
             if (rs) return rs;
             rs = mp_pipeline(d_data, d_off, n, hc, s0, h, cuts, run);
             if (rs) return rs;
-            // header + compressed bytes of every cut page (the open page per column is last)
-            std::vector<uint64_t> pb((size_t)nc * a.cap, 0);
+            // header + compressed bytes of every cut page (the open page per column is last),
+            // column c's at pb_off[c] (compact: the cut capacity per column is (h - s) / 2 + 2,
+            // and a strided table of that size cost a 100+ MB host fill and H2D per row group)
+            std::vector<uint64_t> pb, pboff(nc);
             for (int c = 0; c < nc; c++) {
+                pboff[c] = pb.size();
                 size_t i = 0;
                 for (const PageOut &p : run.cols[c]) {
                     if (p.page_type == KPW_DICTIONARY_PAGE) continue;
-                    if (i < cuts[c].size()) pb[(size_t)c * a.cap + i] = page_header(p, cols[c].phys).size() + (uint64_t)p.compressed_size;
+                    if (i < cuts[c].size()) pb.push_back(page_header(p, cols[c].phys).size() + (uint64_t)p.compressed_size);
                     i++;
                 }
             }
+            pb.push_back(0);
+            ENS(mp_pbytes, pb.size() * 8); ENS(mp_pboff, nc * 8);
+            // (pb / pboff outlive the copies: the stream is synchronised below)
             CK(hipMemcpyAsync(mp_pbytes.p, pb.data(), pb.size() * 8, hipMemcpyHostToDevice, st));
+            CK(hipMemcpyAsync(mp_pboff.p, pboff.data(), nc * 8, hipMemcpyHostToDevice, st));
+            a.pbytes = mp_pbytes.as<uint64_t>();
+            a.pb_off = mp_pboff.as<uint64_t>();
             a.s = s0; a.h = h;
             launch_plan_mp(a, st);
             CK(hipGetLastError());

@@ -488,7 +488,7 @@ __device__ uint64_t mp_mem(const PageCutArgs &a, MpCol *S, int64_t r)
         MpCol &m = S[c];
         const uint32_t nc = a.ncuts[c];
         while (m.ci < nc && a.cuts[(uint64_t)c * a.cap + m.ci] <= r) {
-            m.pb += a.pbytes[(uint64_t)c * a.cap + m.ci];
+            m.pb += a.pbytes[a.pb_off[c] + m.ci];
             m.q = a.cuts[(uint64_t)c * a.cap + m.ci];
             m.ci++;
             walker_init(m.w, m.q);

@@ -151,7 +151,8 @@ struct PageCutArgs {
     uint32_t *ncuts;               // [ncols]
     int64_t *cuts;                 // [ncols * cap] page ends (exclusive record index), increasing
     int32_t *overflow;
-    const uint64_t *pbytes;        // k_plan_mp: [ncols * cap] header + compressed bytes of each cut page
+    const uint64_t *pbytes;        // k_plan_mp: header + compressed bytes of each cut page, column c's
+    const uint64_t *pb_off;        // at pbytes[pb_off[c] + i] (compact: sum of ncuts entries)
     int64_t next_rg_size;
     int64_t *out;                  // k_plan_mp: [0] row-group end or -1, [1] memSize at n (open buffered)
     // PARQUET_2_0: BOOLEAN values are a RunLengthBitPackingHybridValuesWriter stream (buffered
