@@ -100,8 +100,10 @@ public:
     // inside it).  Per column: the pages ColumnWriterV1 cut within them (a cut after record
     // n - 1 included) and those pages' header + compressed bytes, which is what
     // ColumnChunkPageWriter.getMemSize() adds to getBufferedSize() (the writer's size model).
+    // `cols_mask` (optional): only those columns are encoded (the ones that cut a page since the
+    // last probe; the others' pages are unchanged, so their npages / flushed come back as -1).
     int probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, std::vector<int32_t> &npages,
-                    std::vector<int64_t> &flushed);
+                    std::vector<int64_t> &flushed, const std::vector<char> *cols_mask = nullptr);
     const std::string &error() const { return err_; }
     // Alternate the page output buffers between encodes, so the previous encode's pages can
     // still be read (D2H on another stream) while this one runs.  The caller orders this
@@ -169,12 +171,13 @@ private:
     bool mp_ = false;
     bool probe_ = false;                 // encode() is a probe_pages call
     std::vector<int32_t> probe_npages_;
+    const std::vector<char> *probe_mask_ = nullptr;
     std::vector<int64_t> probe_flushed_;
     int encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                   const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out);
     int mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vector<int64_t>> &cuts);
     int mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s, int64_t e,
-                    const std::vector<std::vector<int64_t>> &cuts, MpRun &run);
+                    const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask = nullptr);
     int grow_keep(DevBuf &b, size_t bytes, size_t keep);
     std::vector<DevBuf> mp_sp;
     DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_pboff, mp_flag, mp_dch, mp_dtile_chunk, mp_dtile_first, mp_dtile_count, mp_dtile_raw,

@@ -41,6 +41,9 @@ void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, c
     } while (0)
 #define ENS(buf, bytes) do { if ((buf).ensure(bytes)) return fail(KPW_ERR_NOMEM, "device allocation failed: " #buf); } while (0)
 
+// multi-page dictionary insertion round: tiles (of KPW_TILE_P_H records) per chunk and round
+constexpr uint32_t kMpRoundTiles = 64;
+
 static inline uint64_t next_pow2_mp(uint64_t x)
 {
     uint64_t p = 1;
@@ -97,7 +100,7 @@ int Engine::mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vecto
 // Encode the column chunks [s, e) split at `cuts` (page ends <= e).  Result pages are in
 // pages_dev_ (PageOut offsets), grouped per column: optional dictionary page, data pages.
 int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s,
-                        int64_t e, const std::vector<std::vector<int64_t>> &cuts, MpRun &run)
+                        int64_t e, const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask)
 {
     hipStream_t st = stream;
     const int nc = (int)cols.size();
@@ -115,22 +118,30 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         memset(&D, 0, sizeof(D));
         const uint64_t len = (uint64_t)(e - s);
         D.s = s; D.e = e; D.col = c; D.rg = 0;
-        D.is_dict = cols[c].dict ? 1 : 0;
+        const bool on = !mask || (*mask)[c];   // a probe of a column subset: the others get no pages
+        D.is_dict = cols[c].dict && on ? 1 : 0;
         D.smin = ~0ull; D.smax = 0;
         D.ids_off = ids_off; D.ent_off = ids_off;
-        ids_off += len;
-        if (D.is_dict) {   // no 1 MiB early stop: pages before the fallback page keep their ids
-            D.ht_cap = (uint32_t)next_pow2_mp(std::max<uint64_t>(16, 2 * len));
+        if (on) ids_off += len;
+        if (D.is_dict) {
+            // Insertion runs in rounds of kMpRoundTiles tiles per chunk and a chunk stops after
+            // the round in which its dictionary passed dictPageSize (pages before the fallback
+            // page keep their ids: every value before the crossing is inserted).  So a table
+            // holds at most dictPageSize / (smallest entry) + 1 entries plus one round's values.
+            const uint64_t esz = (cols[c].phys == KPW_INT64 || cols[c].phys == KPW_DOUBLE) ? 8 : 4;
+            const uint64_t maxent = (uint64_t)props.dictionary_page_size / esz + 1 + (uint64_t)kMpRoundTiles * KPW_TILE_P_H;
+            D.ht_cap = (uint32_t)next_pow2_mp(std::max<uint64_t>(16, 2 * std::min<uint64_t>(len, maxent)));
             D.ht_off = ht_off;
             ht_off += D.ht_cap + 1;
         }
         D.dl_job = D.id_job = D.bool_job = D.dj0 = -1;
         D.owner = -1;
         D.first_page = (int32_t)pg.size();
-        const uint32_t nt = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
+        const uint32_t nt = on ? (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H) : 0u;
         dfirst[c] = (uint32_t)dtj.size();
         dcount[c] = nt;
         dtj.insert(dtj.end(), nt, (uint32_t)c);
+        if (!on) { D.npages = 0; continue; }
         int64_t q = s;
         for (size_t i = 0; i <= cuts[c].size(); i++) {
             const int64_t pe = i < cuts[c].size() ? std::min<int64_t>(cuts[c][i], e) : e;
@@ -197,13 +208,15 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     const int npg = (int)pg.size();
     const uint32_t npt = (uint32_t)ptj.size(), ndt = (uint32_t)dtj.size();
-    std::vector<uint32_t> dorder;
+    std::vector<uint32_t> dorder, rlen;   // tile k of every chunk before tile k + 1; per round its slice
     {
         uint32_t maxnt = 0;
         for (int c = 0; c < nc; c++) if (dch[c].is_dict) maxnt = std::max(maxnt, dcount[c]);
-        for (uint32_t k = 0; k < maxnt; k++)
+        for (uint32_t k = 0; k < maxnt; k++) {
+            if (k % kMpRoundTiles == 0) rlen.push_back(0);
             for (int c = 0; c < nc; c++)
-                if (dch[c].is_dict && k < dcount[c]) dorder.push_back(dfirst[c] + k);
+                if (dch[c].is_dict && k < dcount[c]) { dorder.push_back(dfirst[c] + k); rlen.back()++; }
+        }
     }
     // page descriptors use the engine's chunk buffers; dictionary descriptors their own
     ENS(d_chunks, npg * sizeof(ChunkDesc)); ENS(d_ctile_chunk, npt * 4); ENS(d_ctile_first, npg * 4); ENS(d_ctile_count, npg * 4);
@@ -268,6 +281,8 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ad.tile_cnt = mp_dtile_cnt.as<uint32_t>(); ad.tile_sz = mp_dtile_sz.as<uint64_t>();
     ad.max_dict_bytes = 0xFFFFFFFFu;   // the dictPageSize limit is applied per page (k_mp_dict_decide)
     ad.dict_order = d_dict_order.as<uint32_t>(); ad.ndict_tiles = (uint32_t)dorder.size();
+    ad.mp_round_tiles = kMpRoundTiles; ad.mp_nrounds = (uint32_t)rlen.size(); ad.mp_round_len = rlen.data();
+    ad.mp_dict_limit = (uint32_t)props.dictionary_page_size;
 
     uint32_t enpt = 0, enet = 0;
     RleScratch esc{};
@@ -313,6 +328,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
         for (int c = 0; c < nc; c++) {   // restore the host descriptors for the exact re-run
             dch[c].nn = 0; dch[c].dict_bytes = 0; dch[c].dict_n = 0; dch[c].fallback = 0; dch[c].overflow = 0;
+            dch[c].stop_tile = 0;
         }
     }
     ENS(d_body, body_tot + 512 + 4096);   // + 4 KiB: the writer D2Hs whole 4 KiB units
@@ -525,11 +541,12 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         MpRun pr;
         int rs = mp_cuts(a, 0, (int64_t)ne, pc);
         if (rs) return rs;
-        rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr);
+        rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_);
         if (rs) return rs;
         probe_npages_.assign(nc, 0);
         probe_flushed_.assign(nc, 0);
         for (int c = 0; c < nc; c++) {
+            if (probe_mask_ && !(*probe_mask_)[c]) { probe_npages_[c] = -1; probe_flushed_[c] = -1; continue; }
             size_t i = 0;
             for (const PageOut &p : pr.cols[c]) {
                 if (p.page_type == KPW_DICTIONARY_PAGE) continue;
@@ -646,13 +663,15 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
 }
 
 int Engine::probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, std::vector<int32_t> &npages,
-                        std::vector<int64_t> &flushed)
+                        std::vector<int64_t> &flushed, const std::vector<char> *cols_mask)
 {
     if (!mp_) return fail(KPW_ERR_STATE, "probe_pages: single-page regime (no page cuts inside row groups)");
     BatchOut out;
     probe_ = true;
+    probe_mask_ = cols_mask;
     const int st = encode(d_data, d_off, n, false, props.block_size, nullptr, out);
     probe_ = false;
+    probe_mask_ = nullptr;
     if (st) return st;
     if (out.invalid_record >= 0) return fail(KPW_ERR_INVALID_PROTO, "probe_pages: invalid record in a modelled row group");
     npages = probe_npages_;

@@ -339,6 +339,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     if (threadIdx.x == 0) skip = __hip_atomic_load(&C.fallback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (skip) return;
+    if (C.stop_tile && t - ctile_first[ci] >= C.stop_tile) return;   // multi-page: past dictPageSize
     const DevCol col = cols[C.col];   // by value: not reloaded after stores
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     const uint32_t cap = C.ht_cap;
@@ -447,7 +448,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
-    const bool active = C.is_dict && !C.fallback;
+    const bool active = C.is_dict && !C.fallback && !(C.stop_tile && t - ctile_first[ci] >= C.stop_tile);
     const DevCol col = cols[C.col];   // by value: not reloaded after stores
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     uint32_t cnt = 0;
@@ -528,6 +529,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, con
     const uint32_t ci = ctile_chunk[t];
     const ChunkDesc &C = ch[ci];
     if (!C.is_dict || C.fallback) return;
+    if (C.stop_tile && t - ctile_first[ci] >= C.stop_tile) return;   // multi-page: those pages are PLAIN
     // by value: the stores to ids[] below may not alias them, so their loads are not repeated
     const DevCol col = cols[C.col];
     const uint64_t ids_off = C.ids_off, ht_off = C.ht_off, ent_off = C.ent_off;
@@ -932,11 +934,36 @@ void launch_chunk_stats(const ChunkArgs &a, hipStream_t s)
     hipLaunchKernelGGL(k_chunk_stats_final, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks);
 }
 
+// multi-page dictionary rounds: a chunk whose dictionary passed dictPageSize with the tiles of
+// the rounds so far skips its later tiles (their values fall in the fallback page or after it,
+// so they need no ids); stop is decided between rounds, so no earlier tile is ever skipped
+__global__ void k_mp_dict_stop(ChunkDesc *ch, int nchunks, uint32_t round_end, uint32_t limit)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    ChunkDesc &C = ch[c];
+    if (C.is_dict && !C.stop_tile && C.dict_bytes > limit) C.stop_tile = round_end;
+}
+
 void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
 {
-    if (a.ndict_tiles)
+    if (a.ndict_tiles && a.mp_nrounds) {
+        // dict_order is round-major (tile k of every chunk before tile k + 1): a round is a slice
+        uint32_t o = 0;
+        for (uint32_t j = 0; j < a.mp_nrounds; j++) {
+            const uint32_t cnt = a.mp_round_len[j];
+            if (j)
+                hipLaunchKernelGGL(k_mp_dict_stop, dim3((a.nchunks + 63) / 64), dim3(64), 0, s, a.ch, a.nchunks,
+                                   j * a.mp_round_tiles, a.mp_dict_limit);
+            if (cnt)
+                hipLaunchKernelGGL(k_dict_insert, dim3(cnt), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order + o,
+                                   a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
+            o += cnt;
+        }
+    } else if (a.ndict_tiles) {
         hipLaunchKernelGGL(k_dict_insert, dim3(a.ndict_tiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order,
                            a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
+    }
     hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes,
                        a.collision + 1);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
@@ -1082,7 +1109,7 @@ __global__ void k_mp_satisfy(ChunkDesc *pg, ChunkDesc *dch, int ndch, const DevC
 __global__ void k_mp_dictpage_off(const ChunkDesc *pg, ChunkDesc *dch, int ndch)
 {
     const int d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= ndch) return;
+    if (d >= ndch || dch[d].npages <= 0) return;   // (a probe's columns outside its subset have no pages)
     dch[d].body_off = pg[dch[d].first_page].body_off;
 }
 

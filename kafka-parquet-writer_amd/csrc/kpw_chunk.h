@@ -43,7 +43,14 @@ struct ChunkArgs {
     const uint64_t *chunk_sfx;     // v2: DELTA_BYTE_ARRAY suffix bytes per chunk
     uint64_t *page_pre;            // v2: uncompressed level bytes in front of each page's values
     int32_t mp;                    // multi-page regime: descriptors are pages (dictionary decided per chunk)
-    int32_t pad_mp;
+    // multi-page dictionary insertion in rounds (host-side, read by launch_dict): round j is
+    // dict_order[sum(len[0..j)), +len[j]) = tiles [j * round_tiles, (j + 1) * round_tiles) of
+    // every chunk; between rounds a chunk past dict_limit bytes stops (ChunkDesc::stop_tile)
+    uint32_t mp_round_tiles;
+    uint32_t mp_nrounds;
+    const uint32_t *mp_round_len;
+    uint32_t mp_dict_limit;
+    uint32_t pad_mp;
     SegScratch *seg;               // the handle's segmented-scan scratch
 };
 

@@ -185,7 +185,10 @@ struct ChunkDesc {
     uint64_t ent_off;              // dictionary entries array offset (first-occurrence value index)
     // stats
     uint64_t smin, smax;           // fixed: canonical bits; binary: value index of min/max
-    uint32_t has_minmax, pad3;
+    uint32_t has_minmax;
+    uint32_t stop_tile;            // multi-page dictionary descriptor: tiles >= this one (within
+                                   // the chunk) are skipped, the dictionary having passed
+                                   // dictPageSize before them (0: none)
     uint64_t null_count;
     // layout
     uint64_t dl_len;               // RLE def-level bytes (without the 4-byte prefix)

@@ -167,6 +167,7 @@ void SizeModel::reset_store()
         k.data = 0;
         k.flushed = 0;
         k.pages = 0;
+        k.pages_known = 0;
         k.value_count = 0;
         k.next_check = 100;   // props.getMinRowCountForPageSizeCheck()
         k.bv = RleCount();
@@ -300,10 +301,20 @@ int SizeModel::add(const uint8_t *rec, uint64_t len)
 int SizeModel::finish_pages(const std::vector<int32_t> &npages, const std::vector<int64_t> &flushed)
 {
     if (npages.size() != cols_.size() || flushed.size() != cols_.size()) return MISMATCH;
-    for (size_t c = 0; c < cols_.size(); c++)
-        if (npages[c] != cols_[c].pages) return MISMATCH;
-    for (size_t c = 0; c < cols_.size(); c++) cols_[c].flushed = flushed[c];
+    for (size_t c = 0; c < cols_.size(); c++) {
+        if (npages[c] < 0 ? cols_[c].pages != cols_[c].pages_known : npages[c] != cols_[c].pages) return MISMATCH;
+    }
+    for (size_t c = 0; c < cols_.size(); c++) {
+        if (npages[c] >= 0) cols_[c].flushed = flushed[c];
+        cols_[c].pages_known = cols_[c].pages;
+    }
     return block_check();
+}
+
+void SizeModel::cut_columns(std::vector<char> &mask) const
+{
+    mask.assign(cols_.size(), 0);
+    for (size_t c = 0; c < cols_.size(); c++) mask[c] = cols_[c].pages != cols_[c].pages_known;
 }
 
 // InternalParquetRecordWriter.write -> checkBlockSizeReached

@@ -62,7 +62,11 @@ public:
     // Completes a PAGES record: per column the pages cut in the open row group so far and their
     // header + compressed bytes (from the GPU).  OK, CUT, or MISMATCH (page counts differ from
     // the model's: the two restatements disagree, a bug).
+    // npages[c] < 0: column c was not probed (it cut no page since the last finish_pages, so
+    // its flushed bytes are unchanged).
     int finish_pages(const std::vector<int32_t> &npages, const std::vector<int64_t> &flushed);
+    // the columns that cut a page since the last finish_pages (the ones a probe must encode)
+    void cut_columns(std::vector<char> &mask) const;
     int64_t buffered() const;               // columnStore.getBufferedSize()
     int64_t record_count() const { return record_count_; }
     bool multi_page() const { return multi_; }
@@ -79,6 +83,7 @@ private:
         int64_t data = 0;                   // raw bytes (non-boolean) or boolean values
         int64_t flushed = 0;                // pageWriter.getMemSize(): cut pages, header + compressed
         int32_t pages = 0;                  // pages cut in the open row group
+        int32_t pages_known = 0;            // pages whose flushed bytes `flushed` holds
         int32_t value_count = 0, next_check = 100;
         RleCount bv;                        // v2 BOOLEAN: RunLengthBitPackingHybridValuesWriter of the values
         int64_t rows_written = 0;           // v2: rowCount at this column's last page

@@ -1354,7 +1354,11 @@ static int probe_flushed(kpw_writer *w, size_t m, std::vector<int32_t> &np, std:
             return wfail(w, KPW_ERR_DEVICE, "probe: H2D of offsets failed");
         w->pr_up = nb;
     }
-    if (int st = P.probe_pages(F.d, w->pr_off.as<uint64_t>(), m, np, fl)) return wfail(w, st, P.error());
+    // only the columns that cut a page since the last probe are encoded (the others' cut pages,
+    // hence their flushed bytes, are unchanged)
+    std::vector<char> mask;
+    w->model.cut_columns(mask);
+    if (int st = P.probe_pages(F.d, w->pr_off.as<uint64_t>(), m, np, fl, &mask)) return wfail(w, st, P.error());
     return KPW_OK;
 }
 

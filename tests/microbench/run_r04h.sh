@@ -1,0 +1,8 @@
+#!/bin/bash
+OUT=gpurun_out/r04h
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -k "multipage or rotation or v2 or fullsize or async" > $OUT/pytest_mp.log 2>&1 || exit $?
+KPW_TRACE=1 timeout -k 10 300 python tests/microbench/mp_leg.py 10000000 1048576 3 > $OUT/mp_trace.log 2>&1 || exit $?
+timeout -k 10 600 python bench.py --steps 1 --warmup 0 --no-resident --no-cpu-baseline --secondary-steps 0 --per-record-records 3000000 > $OUT/per_record.log 2>&1 || exit $?
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/mp_prof -o run -- python tests/microbench/mp_leg.py 10000000 1048576 2 > $OUT/mp_prof.log 2>&1
