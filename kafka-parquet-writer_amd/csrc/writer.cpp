@@ -651,15 +651,24 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
         launch_asm_gather((const AsmPiece *)(W.d_asm_in.as<uint8_t>() + bb), (uint32_t)pcs.size(), W.d_asm_in.as<uint8_t>(),
                           W.d_asm_out.as<uint8_t>(), s);
         if (hipGetLastError() != hipSuccess) return KPW_ERR_DEVICE;
+        // KPW_ASM_D2H_STREAM=1: the file bytes' D2H on the writer's D2H stream (after the gather)
+        // instead of the engine stream (A/B; d_asm_out is rewritten only after asm_ev, above)
+        static const bool sep = [] { const char *e = getenv("KPW_ASM_D2H_STREAM"); return e && e[0] == '1'; }();
+        hipStream_t ds = s;
+        if (sep) {
+            if (hipEventRecord(W.enc_done, s) != hipSuccess || hipStreamWaitEvent(w->d2h_stream, W.enc_done, 0) != hipSuccess)
+                return KPW_ERR_DEVICE;
+            ds = w->d2h_stream;
+        }
         uint64_t at = 0;
         for (const auto &sp : spans) {
-            if (hipMemcpyAsync(sp.first, W.d_asm_out.as<uint8_t>() + at, sp.second, hipMemcpyDeviceToHost, s) != hipSuccess)
+            if (hipMemcpyAsync(sp.first, W.d_asm_out.as<uint8_t>() + at, sp.second, hipMemcpyDeviceToHost, ds) != hipSuccess)
                 return KPW_ERR_DEVICE;
             at += sp.second;
         }
         // not waited for here: the engine's next encode reuses the page buffers after the gather
         // in stream order, and drain() (close, getDataSize after a cut) waits for the file bytes
-        if (hipEventRecord(W.asm_ev, s) != hipSuccess) return KPW_ERR_DEVICE;
+        if (hipEventRecord(W.asm_ev, ds) != hipSuccess) return KPW_ERR_DEVICE;
         W.asm_pending = true;
         w->last_rg_end = w->fw->pos();
         if (trace_on()) w->t_d2h_alloc += now_ms() - ta;
@@ -693,8 +702,8 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
 // (lens[0] = the first boundary) and a prefix scan rebuilds the u64 offsets in HBM.  (A per-worker
 // copy stream measured 3-5 % slower end to end: profiles/r02d_copy_paths.md.)
 // Lengths cross in the narrowest of u8 / u16 / u32 that holds every record of the job (C2's
-// ~62-byte records: 1 byte each, a quarter of the u32 bytes): the width of the worker's previous
-// job is tried first, and a record that does not fit sends this job through the next width.
+// ~62-byte records: 1 byte each, a quarter of the u32 bytes): u8 is tried first, and the OR of
+// the lengths that pass computes picks the width when it does not fit.
 static int upload_offsets(Worker &W, size_t count, hipStream_t s)
 {
     const uint64_t *hb = (const uint64_t *)W.h_off.p;

@@ -6,3 +6,7 @@ KPW_TRACE=1 timeout -k 10 300 python tests/microbench/mp_leg.py 10000000 1048576
 timeout -k 10 600 python bench.py --steps 1 --warmup 0 --no-resident --no-cpu-baseline --secondary-steps 0 --per-record-records 3000000 > $OUT/per_record.log 2>&1 || exit $?
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/mp_prof -o run -- python tests/microbench/mp_leg.py 10000000 1048576 2 > $OUT/mp_prof.log 2>&1
+for v in 0 1 0 1; do
+  KPW_ASM_D2H_STREAM=$v KPW_TRACE=1 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-resident --per-record-records 0 --secondary-steps 0 > $OUT/d2hab_$v.log 2>&1 || exit $?
+  grep -h '"value"' $OUT/d2hab_$v.log | python -c "import sys,json; d=json.loads(sys.stdin.read()); print('d2h_stream=$v', d['value'], d['ms_per_step'])" >> $OUT/d2hab.txt
+done
