@@ -18,8 +18,6 @@
 
 namespace kpw {
 
-void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, uint64_t *tmp, hipStream_t s);
-void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, uint64_t *tmp, hipStream_t s);
 void launch_snappy_finish(const SnappyArgs &a, const uint32_t *page_frag0, hipStream_t s);
 void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, const uint8_t *data, uint64_t *meta,
                          uint8_t *blob, hipStream_t s);
@@ -67,6 +65,7 @@ Engine::~Engine()
     for (auto &e : kev_) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamSynchronize(stream);
     seg_scratch_free(seg_);
+    pin_free(xfer_);
     if (stream) (void)hipStreamDestroy(stream);
     if (tr)
         fprintf(stderr, "[kpw] engine free: events+stream %.1f ms\n",
@@ -163,6 +162,61 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
 
 #define ENS(buf, bytes) do { if ((buf).ensure(bytes)) return fail(KPW_ERR_NOMEM, "device allocation failed: " #buf); } while (0)
 
+hipError_t Engine::xreserve(size_t bytes, hipStream_t s, size_t *off)
+{
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (xfer_off_ + need > xfer_cap_) {
+        // queued copies may still read the arena (and readbacks land in it): drain, then grow
+        if (hipError_t e = xsync(s)) return e;
+        if (need > xfer_cap_) {
+            pin_free(xfer_);
+            xfer_cap_ = std::max<size_t>(need * 2, xfer_cap_ * 2 + (1u << 20));
+            xfer_ = (uint8_t *)pin_alloc(xfer_cap_);
+            if (!xfer_) { xfer_cap_ = 0; return hipErrorOutOfMemory; }
+        }
+    }
+    *off = xfer_off_;
+    xfer_off_ += need;
+    return hipSuccess;
+}
+
+// KPW_XFER=0: plain pageable copies (A/B)
+static bool xfer_pinned()
+{
+    static const bool on = [] { const char *e = getenv("KPW_XFER"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
+hipError_t Engine::xh2d(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    if (!bytes) return hipSuccess;
+    if (!xfer_pinned()) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+    size_t off;
+    if (hipError_t e = xreserve(bytes, s, &off)) return e;
+    memcpy(xfer_ + off, src, bytes);
+    return hipMemcpyAsync(dst, xfer_ + off, bytes, hipMemcpyHostToDevice, s);
+}
+
+hipError_t Engine::xd2h(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    if (!bytes) return hipSuccess;
+    if (!xfer_pinned()) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+    size_t off;
+    if (hipError_t e = xreserve(bytes, s, &off)) return e;
+    xpend_.push_back(XPend{dst, off, bytes});
+    return hipMemcpyAsync(xfer_ + off, src, bytes, hipMemcpyDeviceToHost, s);
+}
+
+hipError_t Engine::xsync(hipStream_t s)
+{
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e == hipSuccess)
+        for (const XPend &p : xpend_) memcpy(p.host, xfer_ + p.off, p.bytes);
+    xpend_.clear();
+    xfer_off_ = 0;   // every queued copy has run
+    return e;
+}
+
 // Lays out tiles for the given jobs, uploads them and runs the structure pass.
 int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, RleScratch &sc)
 {
@@ -190,39 +244,19 @@ int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, Rle
         etj.insert(etj.end(), J.netiles, (uint32_t)j);
     }
     const size_t nj = jobs.size();
-    ENS(r_ptile_job, npt * 4); ENS(r_last, npt * 8); ENS(r_prev, npt * 8); ENS(r_lrcnt, npt * 4); ENS(r_lroff, npt * 4);
-    ENS(r_etile_job, net * 4); ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_emap, net * 4); ENS(r_emappre, net * 4);
-    ENS(r_rcnt, net * 4); ENS(r_roff, net * 4); ENS(r_rg, e0 * 4); ENS(r_rb, e0 * 4); ENS(r_rbytes, e0 * 8);
-    ENS(r_rgroups, e0 * 8); ENS(r_etbytes, net * 8); ENS(r_etgroups, net * 8); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8);
-    ENS(r_jnlong, nj * 4); ENS(r_jnrle, nj * 4); ENS(r_jbtot, nj * 8); ENS(r_jgtot, nj * 8); ENS(d_jobs, nj * sizeof(RleJob));
-    CK(hipMemcpyAsync(r_ptile_job.p, ptj.data(), npt * 4, hipMemcpyHostToDevice, s));
-    CK(hipMemcpyAsync(r_etile_job.p, etj.data(), net * 4, hipMemcpyHostToDevice, s));
-    CK(hipMemcpyAsync(d_jobs.p, jobs.data(), nj * sizeof(RleJob), hipMemcpyHostToDevice, s));
+    ENS(r_ptile_job, npt * 4); ENS(r_etile_job, net * 4); ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_rg, e0 * 4);
+    ENS(r_rb, e0 * 4); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8); ENS(d_jobs, nj * sizeof(RleJob));
+    CK(xh2d(r_ptile_job.p, ptj.data(), npt * 4, s));
+    CK(xh2d(r_etile_job.p, etj.data(), net * 4, s));
+    CK(xh2d(d_jobs.p, jobs.data(), nj * sizeof(RleJob), s));
     sc.ptile_job = r_ptile_job.as<uint32_t>();
-    sc.first_brk = nullptr;
-    sc.last_brk = r_last.as<int64_t>();
-    sc.prev_brk = r_prev.as<int64_t>();
-    sc.lr_cnt = r_lrcnt.as<uint32_t>();
-    sc.lr_off = r_lroff.as<uint32_t>();
     sc.etile_job = r_etile_job.as<uint32_t>();
     sc.lr_a = r_lra.as<uint32_t>();
     sc.lr_b = r_lrb.as<uint32_t>();
-    sc.emap = r_emap.as<uint32_t>();
-    sc.emap_pre = r_emappre.as<uint32_t>();
-    sc.r_cnt = r_rcnt.as<uint32_t>();
-    sc.r_off = r_roff.as<uint32_t>();
     sc.r_g = r_rg.as<uint32_t>();
     sc.r_b = r_rb.as<uint32_t>();
-    sc.r_bytes = r_rbytes.as<uint64_t>();
-    sc.r_groups = r_rgroups.as<uint64_t>();
-    sc.et_bytes = r_etbytes.as<uint64_t>();
-    sc.et_groups = r_etgroups.as<uint64_t>();
     sc.r_boff = r_rboff.as<uint64_t>();
     sc.r_goff = r_rgoff.as<uint64_t>();
-    sc.job_nlong = r_jnlong.as<uint32_t>();
-    sc.job_nrle = r_jnrle.as<uint32_t>();
-    sc.job_btot = r_jbtot.as<uint64_t>();
-    sc.job_gtot = r_jgtot.as<uint64_t>();
     sc.seg = &seg_;
     return KPW_OK;
 }
@@ -279,7 +313,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         }
     }
     ENS(d_cols, nc * sizeof(DevCol));
-    CK(hipMemcpyAsync(d_cols.p, hc.data(), nc * sizeof(DevCol), hipMemcpyHostToDevice, s));
+    CK(xh2d(d_cols.p, hc.data(), nc * sizeof(DevCol), s));
     ENS(d_raw, n * 4); ENS(d_err, 64);
     CK(hipMemsetAsync(d_err.p, 0xFF, 8, s));
     DecodeArgs da;
@@ -292,21 +326,21 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     CK(hipGetLastError());
     CK(hipEventRecord(ev_[1], s));
     uint64_t err_idx = ~0ull;
-    CK(hipMemcpyAsync(&err_idx, d_err.p, 8, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
+    CK(xd2h(&err_idx, d_err.p, 8, s));
+    CK(xsync(s));
     const uint64_t ne = std::min<uint64_t>(n, err_idx);
     out.invalid_record = err_idx < n ? (int64_t)err_idx : -1;
 
     // ---------------------------------------------------------------- planning inputs
-    ENS(d_scan_tmp, mj_scan_tmp_words(std::max<uint64_t>(ne + 1, nwords + 1), std::max<uint32_t>(1, nopt)) * 8 + 64);
     ENS(d_P, (ne + 1) * 8);
-    if (nopt) launch_pcnt_scan(d_cols.as<DevCol>(), d_opt.as<uint32_t>(), nopt, nwords, d_scan_tmp.as<uint64_t>(), s);
-    launch_prefix_raw(d_raw.as<uint32_t>(), ne, d_P.as<uint64_t>(), d_scan_tmp.as<uint64_t>(), s);
+    if (nopt) launch_pcnt_scan(d_cols.as<DevCol>(), d_opt.as<uint32_t>(), nopt, nwords, &seg_, s);
+    launch_prefix_raw(d_raw.as<uint32_t>(), ne, d_P.as<uint64_t>(), &seg_, s);
+    if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     if (ne == 0) {
         out.records_consumed = 0;
         out.open_records = 0;
         if (on_plan) on_plan(out);
-        CK(hipStreamSynchronize(s));
+        CK(xsync(s));
         return KPW_OK;
     }
     // RLE streams whose emitted bytes count in checkBlockSizeReached: definition levels of
@@ -343,7 +377,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         }
     }
     ENS(d_streams, std::max<size_t>(1, nstreams) * sizeof(PlanStream));
-    if (nstreams) CK(hipMemcpyAsync(d_streams.p, hs.data(), nstreams * sizeof(PlanStream), hipMemcpyHostToDevice, s));
+    if (nstreams) CK(xh2d(d_streams.p, hs.data(), nstreams * sizeof(PlanStream), s));
     if (nstreams) {
         pj.resize(nstreams);
         for (uint32_t k = 0; k < nstreams; k++) {
@@ -360,7 +394,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         if (st) return st;
         if (v2_ && nbool) {
             ENS(d_cbits_ptr, nbool * sizeof(uint64_t *));
-            CK(hipMemcpyAsync(d_cbits_ptr.p, cbits.data(), nbool * sizeof(uint64_t *), hipMemcpyHostToDevice, s));
+            CK(xh2d(d_cbits_ptr.p, cbits.data(), nbool * sizeof(uint64_t *), s));
             launch_bool_streams(d_cols.as<DevCol>(), d_bool.as<uint32_t>(), nbool, ne, d_cbits_ptr.as<uint64_t *>(),
                                 d_jobs.as<RleJob>(), nopt, d_streams.as<PlanStream>(), nopt, s);
         }
@@ -371,7 +405,8 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         CK(hipMemsetAsync(d_gend.p, 0, (uint64_t)nstreams * nwords * 8, s));
         launch_rle_structure(d_jobs.as<RleJob>(), (int)nstreams, npt, net, sc, s);
         launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), d_gend.as<uint64_t>(), nwords, s);
-        launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ne, nstreams, d_scan_tmp.as<uint64_t>(), s);
+        launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ne, nstreams, &seg_, s);
+        if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     }
     if (mp_) return encode_mp(d_data, d_off, n, ne, final_flush, next_rg_size, hc, nwords, out);
     // ---------------------------------------------------------------- A9 plan
@@ -389,16 +424,16 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     launch_plan(pa, s);
     CK(hipGetLastError());
     int64_t po[4];
-    CK(hipMemcpyAsync(po, d_plan_out.p, 32, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
+    CK(xd2h(po, d_plan_out.p, 32, s));
+    CK(xsync(s));
     CK(hipEventRecord(ev_[2], s));
     const int nrg = (int)po[0];
     if (po[3]) return fail(KPW_ERR_DEVICE, "planner row-group table overflow");
     std::vector<int64_t> rs(nrg), re(nrg);
     if (nrg) {
-        CK(hipMemcpyAsync(rs.data(), d_rg_start.p, nrg * 8, hipMemcpyDeviceToHost, s));
-        CK(hipMemcpyAsync(re.data(), d_rg_end.p, nrg * 8, hipMemcpyDeviceToHost, s));
-        CK(hipStreamSynchronize(s));
+        CK(xd2h(rs.data(), d_rg_start.p, nrg * 8, s));
+        CK(xd2h(re.data(), d_rg_end.p, nrg * 8, s));
+        CK(xsync(s));
     }
     out.records_consumed = po[1];
     out.open_records = (int64_t)ne - po[1];
@@ -407,7 +442,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     if (on_plan) on_plan(out);
     if (nrg == 0 || plan_only) {   // plan_only: cuts + open buffered size, no pages (out.rgs carry no chunks)
         for (int i = 3; i < 8; i++) CK(hipEventRecord(ev_[i], s));
-        CK(hipStreamSynchronize(s));
+        CK(xsync(s));
         return KPW_OK;
     }
 
@@ -527,7 +562,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
                 if (ch[ci].is_dict && k < ccount[ci]) dorder.push_back(cfirst[ci] + k);
     }
     ENS(d_dict_order, std::max<size_t>(1, dorder.size()) * 4);
-    if (!dorder.empty()) CK(hipMemcpyAsync(d_dict_order.p, dorder.data(), dorder.size() * 4, hipMemcpyHostToDevice, s));
+    if (!dorder.empty()) CK(xh2d(d_dict_order.p, dorder.data(), dorder.size() * 4, s));
     ENS(d_chunks, nch * sizeof(ChunkDesc)); ENS(d_ctile_chunk, nct * 4); ENS(d_ctile_first, nch * 4); ENS(d_ctile_count, nch * 4);
     ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
     ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8);
@@ -536,9 +571,9 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_page_off, 2 * nch * 8); ENS(d_page_len, 2 * nch * 8); ENS(d_tot, 64);
     for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
-    CK(hipMemcpyAsync(d_ctile_chunk.p, ctj.data(), nct * 4, hipMemcpyHostToDevice, s));
-    CK(hipMemcpyAsync(d_ctile_first.p, cfirst.data(), nch * 4, hipMemcpyHostToDevice, s));
-    CK(hipMemcpyAsync(d_ctile_count.p, ccount.data(), nch * 4, hipMemcpyHostToDevice, s));
+    CK(xh2d(d_ctile_chunk.p, ctj.data(), nct * 4, s));
+    CK(xh2d(d_ctile_first.p, cfirst.data(), nch * 4, s));
+    CK(xh2d(d_ctile_count.p, ccount.data(), nch * 4, s));
     ENS(d_collision, 64);
     ChunkArgs a{};
     a.ch = d_chunks.as<ChunkDesc>(); a.nchunks = nch; a.nctiles = nct; a.cols = d_cols.as<DevCol>(); a.data = d_data;
@@ -572,7 +607,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         const size_t nb = std::max<size_t>(1, dblk_job.size());
         ENS(d_djobs, std::max<size_t>(1, dj.size()) * sizeof(DeltaJob)); ENS(d_blk_job, nb * 4); ENS(d_blk_min, nb * 8);
         ENS(d_blk_w, nb * 4); ENS(d_blk_sz, nb * 8); ENS(d_blk_off, nb * 8); ENS(d_btot, std::max<size_t>(1, dj.size()) * 8);
-        if (!dblk_job.empty()) CK(hipMemcpyAsync(d_blk_job.p, dblk_job.data(), dblk_job.size() * 4, hipMemcpyHostToDevice, s));
+        if (!dblk_job.empty()) CK(xh2d(d_blk_job.p, dblk_job.data(), dblk_job.size() * 4, s));
         dla.jobs = d_djobs.as<DeltaJob>(); dla.njobs = (uint32_t)dj.size(); dla.nblk = (uint32_t)dblk_job.size();
         dla.blk_job = d_blk_job.as<uint32_t>(); dla.blk_min = d_blk_min.as<uint64_t>(); dla.blk_w = d_blk_w.as<uint32_t>();
         dla.blk_sz = d_blk_sz.as<uint64_t>(); dla.blk_off = d_blk_off.as<uint64_t>(); dla.btot = d_btot.as<uint64_t>();
@@ -587,10 +622,10 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     // A hint-sized table that overflowed (flag word 1) re-runs the phase at full size.
     for (bool exact = false;;) {
         a.exact_strings = exact ? 1 : 0;
-        CK(hipMemcpyAsync(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
+        CK(xh2d(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), s));
         CK(hipMemsetAsync(d_collision.p, 0, 8, s));
         if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), s));
-        if (v2_ && !dj.empty()) CK(hipMemcpyAsync(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), hipMemcpyHostToDevice, s));
+        if (v2_ && !dj.empty()) CK(xh2d(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), s));
         // ------------------------------------------------------------ K6 + K2
         launch_chunk_stats(a, s);
         CK(hipGetLastError());
@@ -617,9 +652,9 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         // ------------------------------------------------------------ layout
         launch_layout(a, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), s);
         uint32_t flags[2] = {0, 0};
-        CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, s));
-        CK(hipMemcpyAsync(flags, d_collision.p, 8, hipMemcpyDeviceToHost, s));
-        CK(hipStreamSynchronize(s));
+        CK(xd2h(&body_tot, d_tot.p, 8, s));
+        CK(xd2h(flags, d_collision.p, 8, s));
+        CK(xsync(s));
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
         if (flags[1]) {
             assign_tables(false);
@@ -647,10 +682,10 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     CK(hipGetLastError());
     CK(hipEventRecord(ev_[5], s));
     std::vector<uint64_t> poff(2 * nch), plen(2 * nch), ppre(2 * nch, 0), pcoff, pclen;
-    CK(hipMemcpyAsync(poff.data(), d_page_off.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
-    CK(hipMemcpyAsync(plen.data(), d_page_len.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
-    if (v2_) CK(hipMemcpyAsync(ppre.data(), d_page_pre.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
+    CK(xd2h(poff.data(), d_page_off.p, 2 * nch * 8, s));
+    CK(xd2h(plen.data(), d_page_len.p, 2 * nch * 8, s));
+    if (v2_) CK(xd2h(ppre.data(), d_page_pre.p, 2 * nch * 8, s));
+    CK(xsync(s));
     // ---------------------------------------------------------------- K7
     if (props.codec == KPW_SNAPPY) {
         std::vector<uint32_t> fpage, fidx, pfrag0(2 * nch);
@@ -666,10 +701,10 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         ENS(d_page_frag0, 2 * nch * 4);
         ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * nch * 8 + 64 + 4096);
         if (nf) {
-            CK(hipMemcpyAsync(d_frag_page.p, fpage.data(), nf * 4, hipMemcpyHostToDevice, s));
-            CK(hipMemcpyAsync(d_frag_idx.p, fidx.data(), nf * 4, hipMemcpyHostToDevice, s));
+            CK(xh2d(d_frag_page.p, fpage.data(), nf * 4, s));
+            CK(xh2d(d_frag_idx.p, fidx.data(), nf * 4, s));
         }
-        CK(hipMemcpyAsync(d_page_frag0.p, pfrag0.data(), 2 * nch * 4, hipMemcpyHostToDevice, s));
+        CK(xh2d(d_page_frag0.p, pfrag0.data(), 2 * nch * 4, s));
         SnappyArgs sa{};
         sa.in = d_body.as<uint8_t>(); sa.page_off = d_page_off.as<uint64_t>(); sa.page_len = d_page_len.as<uint64_t>();
         sa.npages = 2 * nch; sa.nfrags = nf; sa.frag_page = d_frag_page.as<uint32_t>(); sa.frag_idx = d_frag_idx.as<uint32_t>();
@@ -704,7 +739,7 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
                 std::sort(ranked.begin(), ranked.end());
                 for (uint32_t f = 0; f < nf; f++) sn_order_[f] = ranked[f].second;
                 ENS(d_sorder, (uint64_t)nf * 4);
-                CK(hipMemcpyAsync(d_sorder.p, sn_order_.data(), (size_t)nf * 4, hipMemcpyHostToDevice, s));
+                CK(xh2d(d_sorder.p, sn_order_.data(), (size_t)nf * 4, s));
                 sa.order = d_sorder.as<uint32_t>();
             }
         }
@@ -718,16 +753,16 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
         CK(hipEventRecord(kev_[3], s));
         if (nf) {
             sn_ft_.resize(2 * (size_t)nf);
-            CK(hipMemcpyAsync(sn_ft_.data(), d_sprof.p, sn_ft_.size() * 8, hipMemcpyDeviceToHost, s));
+            CK(xd2h(sn_ft_.data(), d_sprof.p, sn_ft_.size() * 8, s));
         }
         CK(hipGetLastError());
         pcoff.resize(2 * nch);
         pclen.resize(2 * nch);
         uint64_t ctot = 0;
-        CK(hipMemcpyAsync(pcoff.data(), d_page_coff.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
-        CK(hipMemcpyAsync(pclen.data(), d_page_clen.p, 2 * nch * 8, hipMemcpyDeviceToHost, s));
-        CK(hipMemcpyAsync(&ctot, d_tot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
-        CK(hipStreamSynchronize(s));
+        CK(xd2h(pcoff.data(), d_page_coff.p, 2 * nch * 8, s));
+        CK(xd2h(pclen.data(), d_page_clen.p, 2 * nch * 8, s));
+        CK(xd2h(&ctot, d_tot.as<uint64_t>() + 1, 8, s));
+        CK(xsync(s));
         if (nf) {
             // per-kind mean duration (fragments handed to k_snappy_s_rest count their short
             // k_snappy_v attempt); KPW_SNAPPY_PROFILE=<file> also dumps the raw records
@@ -768,13 +803,13 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     CK(hipEventRecord(ev_[6], s));
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
     // ---------------------------------------------------------------- metadata
-    CK(hipMemcpyAsync(ch.data(), d_chunks.p, nch * sizeof(ChunkDesc), hipMemcpyDeviceToHost, s));
+    CK(xd2h(ch.data(), d_chunks.p, nch * sizeof(ChunkDesc), s));
     // binary min/max bytes: gather (offset, len) pairs, then the bytes into one blob
     std::vector<uint64_t> smeta(4 * nch, 0);
     ENS(d_smeta, 4 * nch * 8);
     launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(), nullptr, s);
-    CK(hipMemcpyAsync(smeta.data(), d_smeta.p, 4 * nch * 8, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
+    CK(xd2h(smeta.data(), d_smeta.p, 4 * nch * 8, s));
+    CK(xsync(s));
     {   // next encode's table hints: the most entries of each column's chunks, none after a fallback
         std::vector<uint32_t> most(nc, 0);
         std::vector<char> seen(nc, 0), fell(nc, 0);
@@ -801,8 +836,8 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
             ENS(d_sblob, blob_len);
             launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(),
                                 d_sblob.as<uint8_t>(), s);
-            CK(hipMemcpyAsync(blob.data(), d_sblob.p, blob_len, hipMemcpyDeviceToHost, s));
-            CK(hipStreamSynchronize(s));
+            CK(xd2h(blob.data(), d_sblob.p, blob_len, s));
+            CK(xsync(s));
             for (int ci = 0; ci < nch; ci++) {
                 if (cols[ch[ci].col].phys != KPW_BYTE_ARRAY || !ch[ci].has_minmax) continue;
                 const uint64_t l1 = smeta[4 * ci + 1], l2 = smeta[4 * ci + 3];

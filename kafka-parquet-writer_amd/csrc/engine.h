@@ -136,13 +136,11 @@ private:
     // decode buffers
     std::vector<DevBuf> col_vals, col_shash, col_spfx, col_soff, col_slen, col_pres, col_vbits, col_pcnt;
     std::vector<uint32_t> dict_hint_;  // per column: most dictionary entries in the previous encode (0: none)
-    DevBuf d_cols, d_fmap, d_raw, d_P, d_err, d_scan_tmp, d_opt, d_bool;
+    DevBuf d_cols, d_fmap, d_raw, d_P, d_err, d_opt, d_bool;
     // planning
     DevBuf d_ev, d_E, d_gend, d_rg_start, d_rg_end, d_plan_out;
     // rle scratch (shared by planning and encoding)
-    DevBuf r_ptile_job, r_last, r_prev, r_lrcnt, r_lroff, r_etile_job, r_lra, r_lrb, r_emap, r_emappre, r_rcnt, r_roff,
-        r_rg, r_rb, r_rbytes, r_rgroups, r_etbytes, r_etgroups, r_rboff, r_rgoff, r_jnlong, r_jnrle, r_jbtot, r_jgtot,
-        d_jobs;
+    DevBuf r_ptile_job, r_etile_job, r_lra, r_lrb, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;
     // chunks
     DevBuf d_chunks, d_ctile_chunk, d_ctile_first, d_ctile_count, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
         d_tile_cnt, d_tile_sz, d_ht, d_ids, d_ent_rec, d_ent_boff, d_page_off, d_page_len, d_tot,
@@ -179,6 +177,18 @@ private:
     int mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s, int64_t e,
                     const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask = nullptr);
     int grow_keep(DevBuf &b, size_t bytes, size_t keep);
+    // Small host tables and readbacks cross through one pinned arena (SDMA copies: a pageable
+    // hipMemcpyAsync runs as a blit kernel, which on a busy GPU also queues for CUs behind K7).
+    // xd2h copies land in `dst` at the next xsync (a stream synchronisation), which also frees
+    // the arena for reuse.
+    hipError_t xh2d(void *dst, const void *src, size_t bytes, hipStream_t s);
+    hipError_t xd2h(void *dst, const void *src, size_t bytes, hipStream_t s);
+    hipError_t xsync(hipStream_t s);
+    hipError_t xreserve(size_t bytes, hipStream_t s, size_t *off);
+    struct XPend { void *host; size_t off, bytes; };
+    uint8_t *xfer_ = nullptr;
+    size_t xfer_cap_ = 0, xfer_off_ = 0;
+    std::vector<XPend> xpend_;
     std::vector<DevBuf> mp_sp;
     DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_pboff, mp_flag, mp_dch, mp_dtile_chunk, mp_dtile_first, mp_dtile_count, mp_dtile_raw,
         mp_dtile_smin, mp_dtile_smax, mp_dtile_cnt, mp_dtile_sz, mp_ssz, mp_spp, mp_cstream, mp_bstream, mp_acc;

@@ -59,7 +59,7 @@ int Engine::grow_keep(DevBuf &b, size_t bytes, size_t keep)
     void *np = dev_alloc(c);
     if (!np) return fail(KPW_ERR_NOMEM, "device allocation failed: multi-page output");
     if (keep && b.p) CK(hipMemcpyAsync(np, b.p, keep, hipMemcpyDeviceToDevice, stream));
-    CK(hipStreamSynchronize(stream));
+    CK(xsync(stream));
     dev_free(b.p);
     b.p = np;
     b.cap = c;
@@ -83,9 +83,9 @@ int Engine::mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vecto
     CK(hipGetLastError());
     std::vector<uint32_t> nct(nc);
     int32_t ovf = 0;
-    CK(hipMemcpyAsync(nct.data(), mp_ncuts.p, nc * 4, hipMemcpyDeviceToHost, stream));
-    CK(hipMemcpyAsync(&ovf, mp_flag.p, 4, hipMemcpyDeviceToHost, stream));
-    CK(hipStreamSynchronize(stream));
+    CK(xd2h(nct.data(), mp_ncuts.p, nc * 4, stream));
+    CK(xd2h(&ovf, mp_flag.p, 4, stream));
+    CK(xsync(stream));
     if (ovf) return fail(KPW_ERR_DEVICE, "page cut table overflow");
     cuts.assign(nc, {});
     for (int c = 0; c < nc; c++) {
@@ -93,7 +93,7 @@ int Engine::mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vecto
         if (nct[c]) CK(hipMemcpyAsync(cuts[c].data(), mp_cutpos.as<int64_t>() + (uint64_t)c * a.cap, nct[c] * 8ull,
                                       hipMemcpyDeviceToHost, stream));
     }
-    CK(hipStreamSynchronize(stream));
+    CK(xsync(stream));
     return KPW_OK;
 }
 
@@ -244,19 +244,19 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         const size_t nb = std::max<size_t>(1, dblk_job.size());
         ENS(d_djobs, std::max<size_t>(1, dj.size()) * sizeof(DeltaJob)); ENS(d_blk_job, nb * 4); ENS(d_blk_min, nb * 8);
         ENS(d_blk_w, nb * 4); ENS(d_blk_sz, nb * 8); ENS(d_blk_off, nb * 8); ENS(d_btot, std::max<size_t>(1, dj.size()) * 8);
-        if (!dblk_job.empty()) CK(hipMemcpyAsync(d_blk_job.p, dblk_job.data(), dblk_job.size() * 4, hipMemcpyHostToDevice, st));
+        if (!dblk_job.empty()) CK(xh2d(d_blk_job.p, dblk_job.data(), dblk_job.size() * 4, st));
         dla.jobs = d_djobs.as<DeltaJob>(); dla.njobs = (uint32_t)dj.size(); dla.nblk = (uint32_t)dblk_job.size();
         dla.blk_job = d_blk_job.as<uint32_t>(); dla.blk_min = d_blk_min.as<uint64_t>(); dla.blk_w = d_blk_w.as<uint32_t>();
         dla.blk_sz = d_blk_sz.as<uint64_t>(); dla.blk_off = d_blk_off.as<uint64_t>(); dla.btot = d_btot.as<uint64_t>();
         dla.seg = &seg_;
     }
-    CK(hipMemcpyAsync(d_ctile_chunk.p, ptj.data(), npt * 4, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(d_ctile_first.p, pfirst.data(), npg * 4, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(d_ctile_count.p, pcount.data(), npg * 4, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(mp_dtile_chunk.p, dtj.data(), ndt * 4, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(mp_dtile_first.p, dfirst.data(), nc * 4, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(mp_dtile_count.p, dcount.data(), nc * 4, hipMemcpyHostToDevice, st));
-    if (!dorder.empty()) CK(hipMemcpyAsync(d_dict_order.p, dorder.data(), dorder.size() * 4, hipMemcpyHostToDevice, st));
+    CK(xh2d(d_ctile_chunk.p, ptj.data(), npt * 4, st));
+    CK(xh2d(d_ctile_first.p, pfirst.data(), npg * 4, st));
+    CK(xh2d(d_ctile_count.p, pcount.data(), npg * 4, st));
+    CK(xh2d(mp_dtile_chunk.p, dtj.data(), ndt * 4, st));
+    CK(xh2d(mp_dtile_first.p, dfirst.data(), nc * 4, st));
+    CK(xh2d(mp_dtile_count.p, dcount.data(), nc * 4, st));
+    if (!dorder.empty()) CK(xh2d(d_dict_order.p, dorder.data(), dorder.size() * 4, st));
 
     ChunkArgs ap{};
     ap.ch = d_chunks.as<ChunkDesc>(); ap.nchunks = npg; ap.nctiles = npt; ap.cols = d_cols.as<DevCol>(); ap.data = d_data;
@@ -289,11 +289,11 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     uint64_t body_tot = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
         ap.exact_strings = ad.exact_strings = attempt;
-        CK(hipMemcpyAsync(d_chunks.p, pg.data(), npg * sizeof(ChunkDesc), hipMemcpyHostToDevice, st));
-        CK(hipMemcpyAsync(mp_dch.p, dch.data(), nc * sizeof(ChunkDesc), hipMemcpyHostToDevice, st));
+        CK(xh2d(d_chunks.p, pg.data(), npg * sizeof(ChunkDesc), st));
+        CK(xh2d(mp_dch.p, dch.data(), nc * sizeof(ChunkDesc), st));
         CK(hipMemsetAsync(d_collision.p, 0, 4, st));
         if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), st));
-        if (v2_ && !dj.empty()) CK(hipMemcpyAsync(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), hipMemcpyHostToDevice, st));
+        if (v2_ && !dj.empty()) CK(xh2d(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), st));
         launch_chunk_stats(ap, st);                          // K6 per page (+ nn, raw bytes)
         if (!ej.empty()) {
             int rs = run_rle(ej, enpt, enet, esc);
@@ -317,10 +317,10 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         launch_layout(ap, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), st);
         CK(hipGetLastError());
         uint32_t coll = 0;
-        CK(hipMemcpyAsync(&body_tot, d_tot.p, 8, hipMemcpyDeviceToHost, st));
-        CK(hipMemcpyAsync(&coll, d_collision.p, 4, hipMemcpyDeviceToHost, st));
-        CK(hipMemcpyAsync(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
-        CK(hipStreamSynchronize(st));
+        CK(xd2h(&body_tot, d_tot.p, 8, st));
+        CK(xd2h(&coll, d_collision.p, 4, st));
+        CK(xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st));
+        CK(xsync(st));
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
         for (int c = 0; c < nc; c++)
             if (dch[c].is_dict && dch[c].overflow) return fail(KPW_ERR_DEVICE, "multi-page dictionary table overflow");
@@ -347,10 +347,10 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     CK(hipGetLastError());
     std::vector<uint64_t> poff(2 * npg), plen(2 * npg), pcoff(2 * npg), pclen(2 * npg), ppre(2 * npg, 0);
-    CK(hipMemcpyAsync(poff.data(), d_page_off.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(plen.data(), d_page_len.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
-    if (v2_) CK(hipMemcpyAsync(ppre.data(), d_page_pre.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
-    CK(hipStreamSynchronize(st));
+    CK(xd2h(poff.data(), d_page_off.p, 2 * npg * 8, st));
+    CK(xd2h(plen.data(), d_page_len.p, 2 * npg * 8, st));
+    if (v2_) CK(xd2h(ppre.data(), d_page_pre.p, 2 * npg * 8, st));
+    CK(xsync(st));
     // ---------------------------------------------------------------- K7
     if (props.codec == KPW_SNAPPY) {
         std::vector<uint32_t> fpage, fidx, pfrag0(2 * npg);
@@ -366,10 +366,10 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         ENS(d_page_frag0, 2 * npg * 4);
         ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * npg * 8 + 64 + 4096);
         if (nf) {
-            CK(hipMemcpyAsync(d_frag_page.p, fpage.data(), nf * 4, hipMemcpyHostToDevice, st));
-            CK(hipMemcpyAsync(d_frag_idx.p, fidx.data(), nf * 4, hipMemcpyHostToDevice, st));
+            CK(xh2d(d_frag_page.p, fpage.data(), nf * 4, st));
+            CK(xh2d(d_frag_idx.p, fidx.data(), nf * 4, st));
         }
-        CK(hipMemcpyAsync(d_page_frag0.p, pfrag0.data(), 2 * npg * 4, hipMemcpyHostToDevice, st));
+        CK(xh2d(d_page_frag0.p, pfrag0.data(), 2 * npg * 4, st));
         SnappyArgs sa{};
         sa.in = d_body.as<uint8_t>(); sa.page_off = d_page_off.as<uint64_t>(); sa.page_len = d_page_len.as<uint64_t>();
         sa.npages = 2 * npg; sa.nfrags = nf; sa.frag_page = d_frag_page.as<uint32_t>(); sa.frag_idx = d_frag_idx.as<uint32_t>();
@@ -382,10 +382,10 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), st);
         CK(hipGetLastError());
         uint64_t ctot = 0;
-        CK(hipMemcpyAsync(pcoff.data(), d_page_coff.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
-        CK(hipMemcpyAsync(pclen.data(), d_page_clen.p, 2 * npg * 8, hipMemcpyDeviceToHost, st));
-        CK(hipMemcpyAsync(&ctot, d_tot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, st));
-        CK(hipStreamSynchronize(st));
+        CK(xd2h(pcoff.data(), d_page_coff.p, 2 * npg * 8, st));
+        CK(xd2h(pclen.data(), d_page_clen.p, 2 * npg * 8, st));
+        CK(xd2h(&ctot, d_tot.as<uint64_t>() + 1, 8, st));
+        CK(xsync(st));
         pages_dev_ = d_comp.as<uint8_t>();
         pages_len_ = ctot;
     } else {   // uncompressed: a (v2) page body starts at its level prefix
@@ -395,13 +395,13 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
     // ---------------------------------------------------------------- page metadata
-    CK(hipMemcpyAsync(pg.data(), d_chunks.p, npg * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), hipMemcpyDeviceToHost, st));
+    CK(xd2h(pg.data(), d_chunks.p, npg * sizeof(ChunkDesc), st));
+    CK(xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st));
     std::vector<uint64_t> smeta(4 * npg, 0);
     ENS(d_smeta, 4 * npg * 8);
     launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(), nullptr, st);
-    CK(hipMemcpyAsync(smeta.data(), d_smeta.p, 4 * npg * 8, hipMemcpyDeviceToHost, st));
-    CK(hipStreamSynchronize(st));
+    CK(xd2h(smeta.data(), d_smeta.p, 4 * npg * 8, st));
+    CK(xsync(st));
     std::vector<std::string> bmin(npg), bmax(npg);
     {
         uint64_t blob_len = 0;
@@ -415,8 +415,8 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             ENS(d_sblob, blob_len);
             launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(),
                                 d_sblob.as<uint8_t>(), st);
-            CK(hipMemcpyAsync(blob.data(), d_sblob.p, blob_len, hipMemcpyDeviceToHost, st));
-            CK(hipStreamSynchronize(st));
+            CK(xd2h(blob.data(), d_sblob.p, blob_len, st));
+            CK(xsync(st));
             for (int p = 0; p < npg; p++) {
                 if (cols[pg[p].col].phys != KPW_BYTE_ARRAY || !pg[p].has_minmax) continue;
                 const uint64_t l1 = smeta[4 * p + 1], l2 = smeta[4 * p + 3];
@@ -510,19 +510,20 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         if (cols[c].phys != KPW_BYTE_ARRAY) continue;
         ENS(mp_sp[c], (ne + 1) * 8); ENS(mp_ssz, ne * 4 + 4);
         launch_str_sizes(d_cols.as<DevCol>(), c, ne, mp_ssz.as<uint32_t>(), st);
-        launch_prefix_raw(mp_ssz.as<uint32_t>(), ne, mp_sp[c].as<uint64_t>(), d_scan_tmp.as<uint64_t>(), st);
+        launch_prefix_raw(mp_ssz.as<uint32_t>(), ne, mp_sp[c].as<uint64_t>(), &seg_, st);
+        if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
         sp[c] = mp_sp[c].as<uint64_t>();
     }
     std::vector<int32_t> bstream(nc, -1);   // v2: planner stream of each BOOLEAN column's values
     if (v2_)
         for (size_t k = 0; k < bool_idx_.size(); k++) bstream[bool_idx_[k]] = (int32_t)(opt_idx_.size() + k);
     ENS(mp_spp, nc * sizeof(uint64_t *)); ENS(mp_cstream, nc * 4); ENS(mp_bstream, nc * 4);
-    CK(hipMemcpyAsync(mp_spp.p, sp.data(), nc * sizeof(uint64_t *), hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(mp_cstream.p, cstream.data(), nc * 4, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(mp_bstream.p, bstream.data(), nc * 4, hipMemcpyHostToDevice, st));
+    CK(xh2d(mp_spp.p, sp.data(), nc * sizeof(uint64_t *), st));
+    CK(xh2d(mp_cstream.p, cstream.data(), nc * 4, st));
+    CK(xh2d(mp_bstream.p, bstream.data(), nc * 4, st));
     uint64_t Ptot = 0;
-    CK(hipMemcpyAsync(&Ptot, d_P.as<uint64_t>() + ne, 8, hipMemcpyDeviceToHost, st));
-    CK(hipStreamSynchronize(st));
+    CK(xd2h(&Ptot, d_P.as<uint64_t>() + ne, 8, st));
+    CK(xsync(st));
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
 
     PageCutArgs a{};
@@ -559,7 +560,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         }
         out.records_consumed = 0;
         out.open_records = (int64_t)ne;
-        CK(hipStreamSynchronize(st));
+        CK(xsync(st));
         return KPW_OK;
     }
     uint64_t acc_len = 0;
@@ -613,15 +614,15 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
             pb.push_back(0);
             ENS(mp_pbytes, pb.size() * 8); ENS(mp_pboff, nc * 8);
             // (pb / pboff outlive the copies: the stream is synchronised below)
-            CK(hipMemcpyAsync(mp_pbytes.p, pb.data(), pb.size() * 8, hipMemcpyHostToDevice, st));
-            CK(hipMemcpyAsync(mp_pboff.p, pboff.data(), nc * 8, hipMemcpyHostToDevice, st));
+            CK(xh2d(mp_pbytes.p, pb.data(), pb.size() * 8, st));
+            CK(xh2d(mp_pboff.p, pboff.data(), nc * 8, st));
             a.pbytes = mp_pbytes.as<uint64_t>();
             a.pb_off = mp_pboff.as<uint64_t>();
             a.s = s0; a.h = h;
             launch_plan_mp(a, st);
             CK(hipGetLastError());
-            CK(hipMemcpyAsync(po, a.out, 16, hipMemcpyDeviceToHost, st));
-            CK(hipStreamSynchronize(st));
+            CK(xd2h(po, a.out, 16, st));
+            CK(xsync(st));
             if (po[0] >= 0 || h == (int64_t)ne) break;
             h = std::min<int64_t>((int64_t)ne, s0 + 2 * (h - s0));
         }
@@ -646,7 +647,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         }
         break;
     }
-    CK(hipStreamSynchronize(st));
+    CK(xsync(st));
     out.records_consumed = s0;
     out.open_records = (int64_t)ne - s0;
     if (final_flush) out.open_buffered = 0;

@@ -16,13 +16,14 @@
 // partial group is zero padded (toBytes).  An RLE run costs varint(len<<1) +
 // ceil(bw/8) value bytes.
 //
-// Pipeline per batch of jobs (all launched back to back, no host sync):
-//   bounds -> [seg max-scan] -> longruns(count) -> [scan] -> longruns(write)
-//   -> phase_reduce -> [seg compose-scan] -> phase_apply(count) -> [scan] -> phase_apply(write)
-//   -> r_sizes -> [seg scans] -> r_finalize -> (write_runs + write_groups) | events
+// Pipeline per batch of jobs (launched back to back, no host sync; every scan a single-pass
+// decoupled look-back inside the kernel that needs it, kpw_lookback.h):
+//   longruns (break max-scan, count, sum-scan, write) -> phase (compose-scan, RLE runs,
+//   sum-scan, write) -> sizes (two sum-scans, job totals) -> write (runs + groups) | events
 #include "kpw_device.h"
 #include "kpw_kernels.h"
 #include "kpw_scan.h"
+#include "kpw_lookback.h"
 
 namespace kpw {
 
@@ -73,44 +74,26 @@ __device__ __forceinline__ void src_get8(const ValSrc &s, int64_t p0, int64_t le
 }
 
 // ------------------------------------------------------------------ long runs
+// One launch over the position tiles: the last value break before the tile (a max-scan,
+// look-back 0), then the long runs ending in the tile, counted, placed (a sum-scan, look-back
+// 1) and written as (a, b).  A tile with a break publishes its inclusive max at once (break
+// positions grow with the tile), so look-back 0 is one step in practice.  The job's last
+// tile stores n_long.
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_bounds(const RleJob *jobs, const uint32_t *ptile_job, int64_t *last_brk)
-{
-    __shared__ int64_t lds[KPW_BLOCK];
-    const uint32_t t = blockIdx.x;
-    const RleJob &J = jobs[ptile_job[t]];
-    const ValSrc src = job_src(J);
-    const int64_t len = J.len;
-    const int64_t p0 = (int64_t)(t - J.tile0) * KPW_TILE_P + threadIdx.x * 8;
-    int64_t last = -1;
-    if (p0 < len) {
-        uint32_t prev = p0 > 0 ? src_get(src, p0 - 1) : 0;
-        uint32_t vv[8];
-        src_get8(src, p0, len, vv);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int64_t i = p0 + k;
-            if (i >= len) break;
-            const uint32_t v = vv[k];
-            if (i == 0 || v != prev) last = i;
-            prev = v;
-        }
-    }
-    last = block_reduce<int64_t, OpMaxI64>(last, lds);
-    if (threadIdx.x == 0) last_brk[t] = last;
-}
-
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(const RleJob *jobs, const uint32_t *ptile_job, const int64_t *prev_brk,
-                                                            uint32_t *cnt, const uint32_t *off, uint32_t *lr_a, uint32_t *lr_b,
-                                                            int write)
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const uint32_t *ptile_job, uint32_t *lr_a, uint32_t *lr_b,
+                                                            uint32_t nt, LbView L)
 {
     __shared__ int64_t ldsi[KPW_BLOCK];
     __shared__ uint32_t ldsu[KPW_BLOCK];
-    const uint32_t t = blockIdx.x;
-    const RleJob &J = jobs[ptile_job[t]];
+    __shared__ uint32_t slot;
+    __shared__ int64_t c0;
+    __shared__ uint32_t c1;
+    const uint32_t t = lb_ticket(L, nt, &slot);
+    RleJob &J = jobs[ptile_job[t]];
     const ValSrc src = job_src(J);
     const int64_t len = J.len;
-    const int64_t p0 = (int64_t)(t - J.tile0) * KPW_TILE_P + threadIdx.x * 8;
+    const uint32_t tile0 = J.tile0;
+    const int64_t p0 = (int64_t)(t - tile0) * KPW_TILE_P + threadIdx.x * 8;
     uint32_t brk = 0;
     int64_t local_last = -1;
     if (p0 < len) {
@@ -128,17 +111,20 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(const RleJob *jobs, 
     }
     int64_t tot_i;
     int64_t incoming = block_scan_excl<int64_t, OpMaxI64>(local_last, ldsi, &tot_i);
-    const int64_t pb = (t == J.tile0) ? -1 : prev_brk[t];
+    const int64_t pb = lb_tile<int64_t, OpMaxI64>(L, 0, t, tile0, tot_i, t == tile0 || tot_i >= 0, t != tile0, &c0);
     if (pb > incoming) incoming = pb;
 
-    // pass: count (and optionally write) long runs ending in this thread's positions
+    // long runs ending in this thread's positions: count, then write
     uint32_t c = 0;
-    for (int pass = 0; pass < (write ? 2 : 1); pass++) {
+    for (int pass = 0; pass < 2; pass++) {
         uint64_t base = 0;
         if (pass == 1) {
             uint32_t tot;
-            uint32_t ex = block_scan_excl<uint32_t, OpSum32>(c, ldsu, &tot);
-            base = J.e0 + off[t] + ex;
+            const uint32_t ex = block_scan_excl<uint32_t, OpSum32>(c, ldsu, &tot);
+            const uint32_t off = lb_tile<uint32_t, OpSum32>(L, nt, t, tile0, tot, t == tile0, t != tile0, &c1);
+            if (t == tile0 + J.ntiles - 1 && threadIdx.x == 0) J.n_long = off + tot;
+            if (!tot) break;
+            base = J.e0 + off + ex;
         }
         int64_t prev = incoming;
         uint32_t k2 = 0;
@@ -159,55 +145,40 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(const RleJob *jobs, 
         }
         c = k2;
     }
-    if (!write) {
-        uint32_t s = block_reduce<uint32_t, OpSum32>(c, ldsu);
-        if (threadIdx.x == 0) cnt[t] = s;
-    }
 }
 
 // ------------------------------------------------------------------ phase scan over long runs
+// One launch over the element tiles: the phase entering each long run (an 8-state map
+// composition scan, look-back 0), the RLE runs among them, placed (sum-scan, look-back 1) and
+// written as (g, b).  The job's last element tile stores n_rle.
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_phase_reduce(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *lr_a,
-                                                            const uint32_t *lr_b, uint32_t *emap)
+__global__ void __launch_bounds__(KPW_BLOCK) k_phase(RleJob *jobs, const uint32_t *etile_job, const uint32_t *lr_a,
+                                                     const uint32_t *lr_b, uint32_t *r_g, uint32_t *r_b, uint32_t nt, LbView L)
 {
     __shared__ uint32_t lds[KPW_BLOCK];
-    const uint32_t u = blockIdx.x;
-    const RleJob &J = jobs[etile_job[u]];
-    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
-    uint32_t m = OpMapCompose::id();
-    if (k < J.n_long) m = run_map(lr_a[J.e0 + k], lr_b[J.e0 + k]);
-    m = block_reduce<uint32_t, OpMapCompose>(m, lds);
-    if (threadIdx.x == 0) emap[u] = m;
-}
-
-__global__ void __launch_bounds__(KPW_BLOCK) k_phase_apply(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *lr_a,
-                                                           const uint32_t *lr_b, const uint32_t *emap_pre, uint32_t *r_cnt,
-                                                           const uint32_t *r_off, uint32_t *r_g, uint32_t *r_b, int write)
-{
-    __shared__ uint32_t lds[KPW_BLOCK];
-    const uint32_t u = blockIdx.x;
-    const RleJob &J = jobs[etile_job[u]];
-    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
+    __shared__ uint32_t slot, c0, c1;
+    const uint32_t u = lb_ticket(L, nt, &slot);
+    RleJob &J = jobs[etile_job[u]];
+    const uint32_t et0 = J.etile0;
+    const uint64_t k = (uint64_t)(u - et0) * KPW_TILE_E + threadIdx.x;
     const bool valid = k < J.n_long;
     uint32_t a = 0, b = 0, m = OpMapCompose::id();
     if (valid) { a = lr_a[J.e0 + k]; b = lr_b[J.e0 + k]; m = run_map(a, b); }
     uint32_t tot;
     const uint32_t ex = block_scan_excl<uint32_t, OpMapCompose>(m, lds, &tot);
-    const uint32_t phi = pm_get(ex, pm_get(emap_pre[u], 0));
+    const uint32_t pre = lb_tile<uint32_t, OpMapCompose>(L, 0, u, et0, tot, u == et0, u != et0, &c0);
+    const uint32_t phi = pm_get(ex, pm_get(pre, 0));
     const uint32_t g = a + ((phi - a) & 7u);
     const uint32_t rle = (valid && g + 8 <= b) ? 1u : 0u;
-    if (!write) {
-        uint32_t s = block_reduce<uint32_t, OpSum32>(rle, lds);
-        if (threadIdx.x == 0) r_cnt[u] = s;
-    } else {
-        uint32_t t2;
-        uint32_t idx = block_scan_excl<uint32_t, OpSum32>(rle, lds, &t2);
-        if (rle) {
-            const uint64_t o = J.e0 + r_off[u] + idx;
-            r_g[o] = g;
-            r_b[o] = b;
-        }
+    uint32_t t2;
+    const uint32_t idx = block_scan_excl<uint32_t, OpSum32>(rle, lds, &t2);
+    const uint32_t off = lb_tile<uint32_t, OpSum32>(L, nt, u, et0, t2, u == et0, u != et0, &c1);
+    if (rle) {
+        const uint64_t o = J.e0 + off + idx;
+        r_g[o] = g;
+        r_b[o] = b;
     }
+    if (u == et0 + J.netiles - 1 && threadIdx.x == 0) J.n_rle = off + t2;
 }
 
 // ------------------------------------------------------------------ sizes / offsets
@@ -215,55 +186,44 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_phase_apply(const RleJob *jobs, c
 __device__ __forceinline__ uint64_t gap_bytes(uint64_t G, uint32_t bw) { return G * bw + (G + 62) / 63; }
 __device__ __forceinline__ uint32_t rle_bytes(uint32_t L, uint32_t bw) { return varint_len32(L << 1) + (bw + 7) / 8; }
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_r_sizes(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
-                                                       const uint32_t *r_b, uint64_t *r_bytes, uint64_t *r_groups,
-                                                       uint64_t *et_bytes, uint64_t *et_groups)
+// One launch over the element tiles: per RLE run the bytes and groups of (gap before it + the
+// run), their offsets (two sum-scans, look-backs 0 and 1), and the job totals (the job's last
+// run, or its first tile when it has none).
+__global__ void __launch_bounds__(KPW_BLOCK) k_r_sizes(RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
+                                                       const uint32_t *r_b, uint64_t *r_boff, uint64_t *r_goff, uint32_t nt,
+                                                       LbView L)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
-    const uint32_t u = blockIdx.x;
-    const RleJob &J = jobs[etile_job[u]];
-    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
+    __shared__ uint32_t slot;
+    __shared__ uint64_t c0, c1;
+    const uint32_t u = lb_ticket(L, nt, &slot);
+    RleJob &J = jobs[etile_job[u]];
+    const uint32_t et0 = J.etile0;
+    const uint64_t k = (uint64_t)(u - et0) * KPW_TILE_E + threadIdx.x;
+    const uint32_t nrle = J.n_rle;
+    const bool valid = k < nrle;
     uint64_t by = 0, gr = 0;
-    if (k < J.n_rle) {
+    if (valid) {
         const uint32_t g = r_g[J.e0 + k], b = r_b[J.e0 + k];
         const uint32_t pe = k ? r_b[J.e0 + k - 1] : 0;
         gr = (g - pe) >> 3;
         by = gap_bytes(gr, J.bw) + rle_bytes(b - g, J.bw);
-        r_bytes[J.e0 + k] = by;
-        r_groups[J.e0 + k] = gr;
     }
-    uint64_t sb = block_reduce<uint64_t, OpSum64>(by, lds);
-    uint64_t sg = block_reduce<uint64_t, OpSum64>(gr, lds);
-    if (threadIdx.x == 0) { et_bytes[u] = sb; et_groups[u] = sg; }
-}
-
-__global__ void __launch_bounds__(KPW_BLOCK) k_r_finalize(RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_b,
-                                                          const uint64_t *r_bytes, const uint64_t *r_groups,
-                                                          const uint64_t *et_boff, const uint64_t *et_goff,
-                                                          const uint64_t *job_btot, const uint64_t *job_gtot,
-                                                          uint64_t *r_boff, uint64_t *r_goff)
-{
-    __shared__ uint64_t lds[KPW_BLOCK];
-    const uint32_t u = blockIdx.x;
-    const uint32_t j = etile_job[u];
-    RleJob &J = jobs[j];
-    const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
-    const bool valid = k < J.n_rle;
-    const uint64_t by = valid ? r_bytes[J.e0 + k] : 0;
-    const uint64_t gr = valid ? r_groups[J.e0 + k] : 0;
     uint64_t t1, t2;
     const uint64_t eb = block_scan_excl<uint64_t, OpSum64>(by, lds, &t1);
     const uint64_t eg = block_scan_excl<uint64_t, OpSum64>(gr, lds, &t2);
+    const uint64_t boff = lb_tile<uint64_t, OpSum64>(L, 0, u, et0, t1, u == et0, u != et0, &c0);
+    const uint64_t goff = lb_tile<uint64_t, OpSum64>(L, nt, u, et0, t2, u == et0, u != et0, &c1);
     if (valid) {
-        r_boff[J.e0 + k] = et_boff[u] + eb;
-        r_goff[J.e0 + k] = et_goff[u] + eg;
+        r_boff[J.e0 + k] = boff + eb;
+        r_goff[J.e0 + k] = goff + eg;
     }
-    const bool owner = (J.n_rle == 0) ? (u == J.etile0 && threadIdx.x == 0) : (k == (uint64_t)J.n_rle - 1);
+    const bool owner = (nrle == 0) ? (u == et0 && threadIdx.x == 0) : (k == (uint64_t)nrle - 1);
     if (owner) {
-        const uint64_t last_end = J.n_rle ? r_b[J.e0 + J.n_rle - 1] : 0;
+        const uint64_t last_end = nrle ? r_b[J.e0 + nrle - 1] : 0;
         const uint64_t fg = (J.len > last_end) ? ((uint64_t)J.len - last_end + 7) / 8 : 0;
-        const uint64_t rb = J.n_rle ? job_btot[j] : 0;
-        const uint64_t rg = J.n_rle ? job_gtot[j] : 0;
+        const uint64_t rb = nrle ? boff + eb + by : 0;
+        const uint64_t rg = nrle ? goff + eg + gr : 0;
         J.final_gap_start = last_end;
         J.final_gap_off = rb;
         J.final_gap_groups = fg;
@@ -274,10 +234,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_r_finalize(RleJob *jobs, const ui
 
 // ------------------------------------------------------------------ writers
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_write_runs(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
-                                                              const uint32_t *r_b, const uint64_t *r_boff, uint8_t *out)
+__device__ __forceinline__ void rle_write_runs(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
+                                               const uint32_t *r_b, const uint64_t *r_boff, uint8_t *out, uint32_t u)
 {
-    const uint32_t u = blockIdx.x;
     const RleJob &J = jobs[etile_job[u]];
     const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
     if (k >= J.n_rle) return;
@@ -317,11 +276,10 @@ __device__ __forceinline__ GroupLoc locate_group(const RleJob &J, uint64_t q, co
     return L;
 }
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_write_groups(const RleJob *jobs, const uint32_t *ptile_job, const uint32_t *r_g,
-                                                                const uint32_t *r_b, const uint64_t *r_boff, const uint64_t *r_goff,
-                                                                uint8_t *out)
+__device__ __forceinline__ void rle_write_groups(const RleJob *jobs, const uint32_t *ptile_job, const uint32_t *r_g,
+                                                 const uint32_t *r_b, const uint64_t *r_boff, const uint64_t *r_goff, uint8_t *out,
+                                                 uint32_t t)
 {
-    const uint32_t t = blockIdx.x;
     const RleJob &J = jobs[ptile_job[t]];
     const uint64_t q = (uint64_t)(t - J.tile0) * KPW_BLOCK + threadIdx.x;
     if (q >= J.total_groups) return;
@@ -353,10 +311,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_write_groups(const RleJob *jo
 
 // Planning mode: per-position emitted-byte events (event at the position whose write
 // emits the bytes) and a bitmask of RLE-run end positions.
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_ev_runs(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
-                                                           const uint32_t *r_b, uint8_t *ev, uint64_t *gend, uint64_t gend_stride)
+__device__ __forceinline__ void rle_ev_runs(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
+                                            const uint32_t *r_b, uint8_t *ev, uint64_t *gend, uint64_t gend_stride, uint32_t u)
 {
-    const uint32_t u = blockIdx.x;
     const uint32_t j = etile_job[u];
     const RleJob &J = jobs[j];
     const uint64_t k = (uint64_t)(u - J.etile0) * KPW_TILE_E + threadIdx.x;
@@ -367,11 +324,10 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_ev_runs(const RleJob *jobs, c
     atomicOr((unsigned long long *)&gend[j * gend_stride + (b >> 6)], 1ull << (b & 63));
 }
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_ev_groups(const RleJob *jobs, const uint32_t *ptile_job, const uint32_t *r_g,
-                                                             const uint32_t *r_b, const uint64_t *r_boff, const uint64_t *r_goff,
-                                                             uint8_t *ev)
+__device__ __forceinline__ void rle_ev_groups(const RleJob *jobs, const uint32_t *ptile_job, const uint32_t *r_g,
+                                              const uint32_t *r_b, const uint64_t *r_boff, const uint64_t *r_goff, uint8_t *ev,
+                                              uint32_t t)
 {
-    const uint32_t t = blockIdx.x;
     const RleJob &J = jobs[ptile_job[t]];
     const uint64_t q = (uint64_t)(t - J.tile0) * KPW_BLOCK + threadIdx.x;
     if (q >= J.total_groups) return;
@@ -381,65 +337,57 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_ev_groups(const RleJob *jobs,
     ev[J.out_off + last] = (uint8_t)(J.bw + ((L.within % 63) == 0 ? 1 : 0));
 }
 
+// one launch each: blocks [0, n_etiles) the RLE runs, the rest the bit-packed groups
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_write(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *ptile_job,
+                                                         const uint32_t *r_g, const uint32_t *r_b, const uint64_t *r_boff,
+                                                         const uint64_t *r_goff, uint8_t *out, uint32_t n_etiles)
+{
+    if (blockIdx.x < n_etiles) rle_write_runs(jobs, etile_job, r_g, r_b, r_boff, out, blockIdx.x);
+    else rle_write_groups(jobs, ptile_job, r_g, r_b, r_boff, r_goff, out, blockIdx.x - n_etiles);
+}
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_ev(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *ptile_job,
+                                                      const uint32_t *r_g, const uint32_t *r_b, const uint64_t *r_boff,
+                                                      const uint64_t *r_goff, uint8_t *ev, uint64_t *gend, uint64_t gend_stride,
+                                                      uint32_t n_etiles)
+{
+    if (blockIdx.x < n_etiles) rle_ev_runs(jobs, etile_job, r_g, r_b, ev, gend, gend_stride, blockIdx.x);
+    else rle_ev_groups(jobs, ptile_job, r_g, r_b, r_boff, r_goff, ev, blockIdx.x - n_etiles);
+}
+
 // ------------------------------------------------------------------ host launchers
 
-// copy per-job totals from a u32 array into RleJob.n_long / n_rle
-__global__ void k_store_counts(RleJob *jobs, int njobs, const uint32_t *tot, int which)
-{
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= njobs) return;
-    if (which == 0) jobs[j].n_long = tot[j]; else jobs[j].n_rle = tot[j];
-}
-void launch_rle_store_counts(RleJob *jobs_d, int njobs, const uint32_t *tot, int which, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_store_counts, dim3((njobs + 255) / 256), dim3(256), 0, s, jobs_d, njobs, tot, which);
-}
-
-
+// Three launches (long runs, phases, sizes), each a chain of single-pass scans; a launch whose
+// scan scratch cannot grow is skipped with sc.seg->failed set (the engine fails the encode).
 void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc,
                           hipStream_t s)
 {
     if (!njobs || !n_ptiles) return;
-    hipLaunchKernelGGL(k_rle_bounds, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.last_brk);
-    seg_tile_scan<int64_t, OpMaxI64>(sc.last_brk, sc.prev_brk, sc.ptile_job, n_ptiles, nullptr, sc.seg, s);
-    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.prev_brk,
-                       sc.lr_cnt, sc.lr_off, sc.lr_a, sc.lr_b, 0);
-    // n_long per job lands in jobs[j].n_long via the job-total pointer trick below
-    seg_tile_scan<uint32_t, OpSum32>(sc.lr_cnt, sc.lr_off, sc.ptile_job, n_ptiles, sc.job_nlong, sc.seg, s);
-    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.prev_brk,
-                       sc.lr_cnt, sc.lr_off, sc.lr_a, sc.lr_b, 1);
-    launch_rle_store_counts(jobs_d, njobs, sc.job_nlong, 0, s);
-    hipLaunchKernelGGL(k_phase_reduce, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b, sc.emap);
-    seg_tile_scan<uint32_t, OpMapCompose>(sc.emap, sc.emap_pre, sc.etile_job, n_etiles, nullptr, sc.seg, s);
-    hipLaunchKernelGGL(k_phase_apply, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b,
-                       sc.emap_pre, sc.r_cnt, sc.r_off, sc.r_g, sc.r_b, 0);
-    seg_tile_scan<uint32_t, OpSum32>(sc.r_cnt, sc.r_off, sc.etile_job, n_etiles, sc.job_nrle, sc.seg, s);
-    hipLaunchKernelGGL(k_phase_apply, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b,
-                       sc.emap_pre, sc.r_cnt, sc.r_off, sc.r_g, sc.r_b, 1);
-    launch_rle_store_counts(jobs_d, njobs, sc.job_nrle, 1, s);
-    hipLaunchKernelGGL(k_r_sizes, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b,
-                       sc.r_bytes, sc.r_groups, sc.et_bytes, sc.et_groups);
-    seg_tile_scan<uint64_t, OpSum64>(sc.et_bytes, sc.et_bytes, sc.etile_job, n_etiles, sc.job_btot, sc.seg, s);
-    seg_tile_scan<uint64_t, OpSum64>(sc.et_groups, sc.et_groups, sc.etile_job, n_etiles, sc.job_gtot, sc.seg, s);
-    hipLaunchKernelGGL(k_r_finalize, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_b, sc.r_bytes,
-                       sc.r_groups, sc.et_bytes, sc.et_groups, sc.job_btot, sc.job_gtot, sc.r_boff, sc.r_goff);
+    LbView L = lb_prepare(sc.seg, 2ull * n_ptiles, s);
+    if (!L.w) return;
+    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.lr_a, sc.lr_b, n_ptiles, L);
+    L = lb_prepare(sc.seg, 2ull * n_etiles, s);
+    if (!L.w) return;
+    hipLaunchKernelGGL(k_phase, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b, sc.r_g, sc.r_b,
+                       n_etiles, L);
+    L = lb_prepare(sc.seg, 2ull * n_etiles, s);
+    if (!L.w) return;
+    hipLaunchKernelGGL(k_r_sizes, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b, sc.r_boff, sc.r_goff,
+                       n_etiles, L);
 }
 
 void launch_rle_write(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc, uint8_t *out, hipStream_t s)
 {
     if (!n_ptiles) return;
-    hipLaunchKernelGGL(k_rle_write_runs, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b, sc.r_boff, out);
-    hipLaunchKernelGGL(k_rle_write_groups, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.r_g, sc.r_b,
-                       sc.r_boff, sc.r_goff, out);
+    hipLaunchKernelGGL(k_rle_write, dim3(n_etiles + n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.ptile_job, sc.r_g,
+                       sc.r_b, sc.r_boff, sc.r_goff, out, n_etiles);
 }
 
 void launch_rle_events(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc, uint8_t *ev,
                        uint64_t *gend, uint64_t gend_stride, hipStream_t s)
 {
     if (!n_ptiles) return;
-    hipLaunchKernelGGL(k_rle_ev_runs, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b, ev, gend, gend_stride);
-    hipLaunchKernelGGL(k_rle_ev_groups, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.r_g, sc.r_b,
-                       sc.r_boff, sc.r_goff, ev);
+    hipLaunchKernelGGL(k_rle_ev, dim3(n_etiles + n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.ptile_job, sc.r_g,
+                       sc.r_b, sc.r_boff, sc.r_goff, ev, gend, gend_stride, n_etiles);
 }
 
 }  // namespace kpw

@@ -130,12 +130,59 @@ struct FIn {
         return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, s) << 32);
     }
     __device__ __forceinline__ uint8_t ld8(uint32_t p) const { return ((sgg_cu8 *)base)[p]; }
+    // D dwords starting at byte p (D + 1 aligned loads, all in flight together)
+    template <int D> __device__ __forceinline__ void ldw(uint32_t p, uint32_t *o) const
+    {
+        const uintptr_t a = (uintptr_t)(base + p);
+        sgg_cu32 *w = (sgg_cu32 *)(a & ~(uintptr_t)3);
+        const uint32_t s = (uint32_t)(a & 3);
+        uint32_t v[D + 1];
+#pragma unroll
+        for (int i = 0; i <= D; i++) v[i] = w[i];
+#pragma unroll
+        for (int i = 0; i < D; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], s);
+    }
 };
 
-// FindMatchLength(s1, s2, limit); stops early (returns > cap) past cap bytes
-__device__ __forceinline__ uint32_t sg_fml(const FIn &in, uint32_t s1, uint32_t s2, uint32_t limit, uint32_t cap)
+// FindMatchLength(s1, s2, limit); stops early (returns > cap) past cap bytes.  `memo`: the
+// match length (4 + this function's result) the previous round computed for the same copy
+// (0: none); the data is fixed within a fragment, so once the first 16 bytes agree the rest is
+// known.  Past the first step the comparison runs SG_FMLW bytes per dependent load round trip.
+#ifndef SG_MEMO
+#define SG_MEMO 1
+#endif
+#ifndef SG_FMLW
+#define SG_FMLW 32
+#endif
+__device__ __forceinline__ uint32_t sg_fml(const FIn &in, uint32_t s1, uint32_t s2, uint32_t limit, uint32_t cap,
+                                           uint32_t memo)
 {
     uint32_t m = 0;
+    if (s2 + 16 <= limit) {
+        const uint64_t x0 = in.ld64(s1) ^ in.ld64(s2);
+        const uint64_t x1 = in.ld64(s1 + 8) ^ in.ld64(s2 + 8);
+        if (x0) return (uint32_t)__builtin_ctzll(x0) >> 3;
+        if (x1) return 8 + ((uint32_t)__builtin_ctzll(x1) >> 3);
+        if (SG_MEMO && memo) return memo - 4;
+        m = 16;
+#if SG_FMLW > 16
+        constexpr int D = SG_FMLW / 4;   // dwords compared per step
+        while (s2 + m + SG_FMLW <= limit) {
+            uint32_t a[D], b[D];
+            in.ldw<D>(s1 + m, a);
+            in.ldw<D>(s2 + m, b);
+            uint32_t r = 0xffffffffu;
+#pragma unroll
+            for (int i = D - 1; i >= 0; i--) {
+                const uint32_t x = a[i] ^ b[i];
+                if (x) r = (uint32_t)i * 4 + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
+            if (r != 0xffffffffu) return m + r;
+            m += SG_FMLW;
+            if (m > cap) return m;
+        }
+#endif
+    }
     while (s2 + m + 16 <= limit) {   // 16 bytes per step: both words' loads in flight together
         const uint64_t x0 = in.ld64(s1 + m) ^ in.ld64(s2 + m);
         const uint64_t x1 = in.ld64(s1 + m + 8) ^ in.ld64(s2 + m + 8);
@@ -294,7 +341,7 @@ struct ParseOut {
     uint32_t nrec;
 };
 __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, const FIn &in, PS st, uint32_t t, uint32_t n,
-                                             uint32_t ip_limit)
+                                             uint32_t ip_limit, uint32_t nprev)
 {
     const uint32_t sk = t * SG_SEG, sk1 = sk + SG_SEG;
     ParseOut o{st, 0, false, false, false, 0};
@@ -347,7 +394,12 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
             for (int k = 1; k < (int)SG_PB; k++) if (hit == k) { base = q[k]; c = cc[k]; }
             lit = true;
         }
-        const uint32_t len = 4 + sg_fml(in, c + 4, base + 4, n, SG_MAXLEN);
+        uint32_t memo = 0;
+        if (SG_MEMO && o.nrec < nprev) {   // the previous round's copy at this index, if it is this copy
+            const uint64_t pr = G.rec[o.nrec * SG_T + t];
+            if ((uint32_t)pr == (base | ((base - c) << 16))) memo = (uint32_t)(pr >> 32) & 0xffffu;
+        }
+        const uint32_t len = 4 + sg_fml(in, c + 4, base + 4, n, SG_MAXLEN, memo);
         if (len > SG_MAXLEN) { o.lng = true; break; }
         o.fnd = true;
         G.rec[(o.nrec++) * SG_T + t] = (uint64_t)base | ((uint64_t)(base - c) << 16) | ((uint64_t)len << 32) | ((uint64_t)lit << 48);
@@ -638,7 +690,8 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             __syncthreads();
             PMARK(1);
             // ---------------------------------------------- parse my segment
-            po = t < nseg ? sg_parse(S, G, in, upk(S.b.entry[t]), t, n, ip_limit) : ParseOut{upk(S.b.entry[t]), 0, false, false, false, 0};
+            po = t < nseg ? sg_parse(S, G, in, upk(S.b.entry[t]), t, n, ip_limit, po.nrec)
+                          : ParseOut{upk(S.b.entry[t]), 0, false, false, false, 0};
             S.b.exitst[t] = pk(po.st);
             if (po.lfl) atomicOr(&S.lfl[t >> 5], 1u << (t & 31));
             {

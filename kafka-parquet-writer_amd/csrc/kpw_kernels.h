@@ -47,8 +47,9 @@ struct DecodeArgs {
 // handle (Engine::seg_) and grown on demand.  Scans of one handle run in order on its own
 // stream, so they share it; handles never share one (concurrent writers, C5).
 struct SegScratch {
-    void *p = nullptr;
+    void *p = nullptr;             // single-pass scans: ticket counter + tile status words
     size_t bytes = 0;
+    uint32_t epoch = 0;            // of the last launch (status words carry it)
     bool failed = false;           // an allocation failed since the engine last checked
 };
 
@@ -76,23 +77,12 @@ struct RleJob {
 };
 
 struct RleScratch {
-    // position tiles
-    uint32_t *ptile_job;
-    int64_t *first_brk, *last_brk, *prev_brk;
-    uint32_t *lr_cnt, *lr_off;     // long runs per position tile / exclusive offsets
-    // element tiles
-    uint32_t *etile_job;
+    uint32_t *ptile_job;           // position tile -> job
+    uint32_t *etile_job;           // element tile -> job
     uint32_t *lr_a, *lr_b;         // long runs (a, b)
-    uint32_t *emap, *emap_pre;     // element-tile phase map aggregate / exclusive prefix
-    uint32_t *r_cnt, *r_off;       // RLE runs per element tile / offsets
     uint32_t *r_g, *r_b;           // RLE runs (g, b)
-    uint64_t *r_bytes, *r_groups;  // per RLE run: gap+run bytes, gap groups (then exclusive offsets)
-    uint64_t *et_bytes, *et_groups;        // element-tile sums -> offsets
     uint64_t *r_boff, *r_goff;     // per RLE run: byte offset of its gap, groups before its gap
-    // per job
-    uint32_t *job_nlong, *job_nrle;
-    uint64_t *job_btot, *job_gtot;
-    SegScratch *seg;               // the handle's segmented-scan scratch
+    SegScratch *seg;               // the handle's scan scratch (look-back status words)
 };
 
 // Plan / chunk descriptors -------------------------------------------------------------
@@ -228,13 +218,12 @@ struct DeltaJob {
 
 // ---------------------------------------------------------------- launch wrappers
 void launch_decode(const DecodeArgs &a, hipStream_t s);
-void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, uint64_t *tile_tmp, hipStream_t s);
+void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s);
 // P[0] = 0, P[k] = base + raw[1] + ... + raw[k-1] (k >= 1) for u8 (width 1) / u16 (width 2) raw
-void launch_prefix_narrow(const void *raw, int width, uint64_t base, uint64_t n, uint64_t *P, uint64_t *tile_tmp, hipStream_t s);
+void launch_prefix_narrow(const void *raw, int width, uint64_t base, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s);
 
 void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t n_etiles,
                           const RleScratch &sc, hipStream_t s);
-void launch_rle_store_counts(RleJob *jobs_d, int njobs, const uint32_t *tot, int which, hipStream_t s);
 void launch_rle_write(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc,
                       uint8_t *out, hipStream_t s);
 void launch_rle_events(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc,

@@ -1,0 +1,129 @@
+// kpw_lookback.h — single-pass chained scans (decoupled look-back), shared by the scan and
+// RLE kernels.
+//
+// Every tile publishes its aggregate as soon as its own elements are reduced, then its
+// inclusive prefix once its look-back (one wave, 64 predecessors per step) has found a
+// predecessor whose inclusive prefix is out.  One launch per scan instead of reduce / carry /
+// apply, and a kernel can chain several scans (status words of scan k at k * ntiles).
+//
+// Status word of tile i (u64, written and read as one agent-scope atomic, so value and state
+// arrive together): value << 17 | epoch << 2 | state (1: aggregate, 2: inclusive prefix).
+// The epoch changes every launch on the scratch, so stale words read as "not yet" without a
+// clear; values fit 47 bits (byte counts and positions of one encode, < 2^40).  Tiles take
+// their index from a ticket counter (word 0): a block waits only on tiles already taken by
+// running blocks, whatever order the 8 XCDs dispatch in; the block holding the last ticket
+// resets the counter for the next launch.
+#pragma once
+#include "kpw_device.h"
+
+namespace kpw {
+
+struct LbView {
+    uint64_t *w;      // [0]: ticket counter (u32); status words from w[8]
+    uint32_t epoch;
+};
+constexpr uint32_t LB_ST_AGG = 1, LB_ST_INC = 2;
+
+__device__ __forceinline__ uint32_t lb_ticket(const LbView &L, uint32_t nt, uint32_t *slot)
+{
+    if (threadIdx.x == 0) {
+        const uint32_t t = atomicAdd((uint32_t *)L.w, 1u);
+        if (t == nt - 1) atomicExch((uint32_t *)L.w, 0u);
+        *slot = t;
+    }
+    __syncthreads();
+    const uint32_t t = *slot;
+    __syncthreads();
+    return t;
+}
+
+// status word idx (= scan * ntiles + tile)
+__device__ __forceinline__ void lb_publish(const LbView &L, uint32_t idx, uint64_t enc, uint32_t st)
+{
+    __hip_atomic_store(&L.w[8 + idx], (enc << 17) | ((uint64_t)L.epoch << 2) | st, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0: the combination (in order) of tiles [first, tile) of scan `sbase` (= scan * ntiles)
+// that enters `tile`, where `first` is the first tile of its run (the job); the look-back also
+// ends at any tile that published its inclusive value.  Values travel encoded (Enc).
+template <typename T, typename Op, typename Enc>
+__device__ __forceinline__ T lb_lookback(const LbView &L, uint32_t sbase, uint32_t tile, uint32_t first)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    T acc = Op::id();
+    int64_t base = (int64_t)tile - 1;
+    for (;;) {
+        const int64_t q = base - (int64_t)lane;
+        const bool valid = q >= (int64_t)first;
+        uint64_t wv = 0;
+        if (valid) {
+            // (bounded: a predecessor that never publishes would be a bug; the scan then
+            // produces wrong values, which the parity tests catch, instead of hanging the GPU)
+            for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+                wv = __hip_atomic_load(&L.w[8 + sbase + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)((wv >> 2) & 0x7fff) == L.epoch && (wv & 3) != 0) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        const bool term = !valid || (wv & 3) == LB_ST_INC;
+        const uint64_t tm = __ballot(term);
+        const uint32_t stop = tm ? (uint32_t)__builtin_ctzll(tm) : 64u;   // nearest terminal lane
+        T v = (valid && lane <= stop) ? Enc::dec(wv >> 17) : Op::id();
+        // ordered reduction: higher lanes are earlier tiles
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const T o = __shfl_down(v, d, 64);
+            if (lane + d < 64) v = Op::op(o, v);
+        }
+        v = __shfl(v, 0, 64);
+        acc = Op::op(v, acc);
+        if (tm) return acc;
+        base -= 64;
+    }
+}
+
+struct EncU64 {
+    __device__ static uint64_t enc(uint64_t v) { return v; }
+    __device__ static uint64_t dec(uint64_t e) { return e; }
+};
+struct EncU32 {
+    __device__ static uint64_t enc(uint32_t v) { return v; }
+    __device__ static uint32_t dec(uint64_t e) { return (uint32_t)e; }
+};
+struct EncI64 {   // max-scan values are >= -1 (OpMaxI64's identity)
+    __device__ static uint64_t enc(int64_t v) { return (uint64_t)(v + 1); }
+    __device__ static int64_t dec(uint64_t e) { return (int64_t)e - 1; }
+};
+template <typename T> struct EncOf;
+template <> struct EncOf<uint64_t> { using E = EncU64; };
+template <> struct EncOf<uint32_t> { using E = EncU32; };
+template <> struct EncOf<int64_t> { using E = EncI64; };
+
+// One scan's tile (exclusive prefix within its run returned to every thread; `agg` = the
+// tile's own aggregate, valid in thread 0).  `inc_now`: the tile's inclusive value does not
+// depend on earlier tiles (first of its run, or a segment head inside it), so it is published
+// at once; `need`: the tile needs its carry-in.  Returns Op::id() when !need.
+template <typename T, typename Op>
+__device__ __forceinline__ T lb_tile(const LbView &L, uint32_t sbase, uint32_t tile, uint32_t first, T agg, bool inc_now,
+                                     bool need, T *slot)
+{
+    using Enc = typename EncOf<T>::E;
+    if (threadIdx.x == 0) {
+        *slot = Op::id();
+        lb_publish(L, sbase + tile, Enc::enc(agg), inc_now ? LB_ST_INC : LB_ST_AGG);
+    }
+    if (need && threadIdx.x < 64) {
+        const T c = lb_lookback<T, Op, Enc>(L, sbase, tile, first);
+        if (threadIdx.x == 0) {
+            *slot = c;
+            if (!inc_now) lb_publish(L, sbase + tile, Enc::enc(Op::op(c, agg)), LB_ST_INC);
+        }
+    }
+    __syncthreads();
+    const T c = *slot;
+    __syncthreads();
+    return c;
+}
+
+}  // namespace kpw

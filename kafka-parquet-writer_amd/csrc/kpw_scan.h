@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "kpw_kernels.h"
+#include "kpw_lookback.h"
 
 namespace kpw {
 
@@ -11,12 +12,17 @@ struct OpSum32;
 struct OpMaxI64;
 struct OpMapCompose;
 
-uint64_t mj_scan_tmp_words(uint64_t len, uint32_t njobs);
-void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, uint64_t *tmp, hipStream_t s);
-void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, uint64_t *tmp, hipStream_t s);
+// Single-pass scans (decoupled look-back, k_scan.hip); `sc` holds their tile status words.
+// If the scratch cannot grow, the scan is skipped and sc->failed is set: the caller must fail
+// the encode.
+void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, SegScratch *sc, hipStream_t s);
+void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, SegScratch *sc, hipStream_t s);
 
-// Exclusive segmented scan over tile aggregates.  If the scratch cannot grow, the scan is
-// skipped and sc->failed is set: the caller must fail the encode.
+// Status words for one single-pass launch over `nwords` tiles x scans (w == nullptr: the
+// scratch could not grow, sc->failed set; the caller skips the launch).
+LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s);
+
+// Exclusive segmented scan over tile aggregates (same scratch contract).
 template <typename T, typename Op>
 void seg_tile_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, SegScratch *sc, hipStream_t s);
 void seg_scratch_free(SegScratch &sc);

@@ -198,7 +198,11 @@ struct Worker {
     PinnedBuf h_off;                   // host record boundaries of the running job
     PinnedBuf h_len;                   // record lengths, u8 / u16 / u32 (H2D source: 1/8 .. 1/2 the bytes of offsets)
     int len_width = 1;                 // narrowest length width a job tries (KPW_LEN_BYTES)
-    DevBuf d_len, d_tmp;               // device lengths, prefix-scan scratch
+    DevBuf d_len;                      // device lengths
+    struct ScanScratch {               // the offsets scan's tile status words
+        SegScratch sc;
+        ~ScanScratch() { seg_scratch_free(sc); }
+    } scan;
     const uint64_t *offs = nullptr;    // device record offsets handed to the engine
     hipEvent_t carry_ev = nullptr;     // recorded after this worker placed a job's carried records
     hipEvent_t enc_done = nullptr;     // recorded after a job's encode (the D2H of its pages waits on it)
@@ -712,9 +716,7 @@ static int upload_offsets(Worker &W, size_t count, hipStream_t s)
         W.offs = W.d_off.as<uint64_t>();
         return hipMemcpyAsync(W.d_off.p, hb, count * 8, hipMemcpyHostToDevice, s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
     }
-    if (W.h_len.ensure(count * 4) || W.d_len.ensure(count * 4) || W.d_off.ensure((count + 1) * 8) ||
-        W.d_tmp.ensure(mj_scan_tmp_words(count, 1) * 8 + 64))
-        return KPW_ERR_NOMEM;
+    if (W.h_len.ensure(count * 4) || W.d_len.ensure(count * 4) || W.d_off.ensure((count + 1) * 8)) return KPW_ERR_NOMEM;
     // Every job starts at u8 (no ratchet: one long record must not keep the worker on wide
     // lengths for the rest of the file); the u8 pass ORs the lengths, so a job that
     // does not fit goes straight to the width that holds it (at most two host passes).
@@ -744,8 +746,9 @@ static int upload_offsets(Worker &W, size_t count, hipStream_t s)
             if (over) { width = all_or.load() <= 0xffff ? 2 : 4; continue; }
         }
         if (hipMemcpyAsync(W.d_len.p, W.h_len.p, count * width, hipMemcpyHostToDevice, s) != hipSuccess) return KPW_ERR_DEVICE;
-        if (width == 4) launch_prefix_raw(W.d_len.as<uint32_t>(), count, W.d_off.as<uint64_t>(), W.d_tmp.as<uint64_t>(), s);
-        else launch_prefix_narrow(W.d_len.p, width, hb[0], count, W.d_off.as<uint64_t>(), W.d_tmp.as<uint64_t>(), s);
+        if (width == 4) launch_prefix_raw(W.d_len.as<uint32_t>(), count, W.d_off.as<uint64_t>(), &W.scan.sc, s);
+        else launch_prefix_narrow(W.d_len.p, width, hb[0], count, W.d_off.as<uint64_t>(), &W.scan.sc, s);
+        if (W.scan.sc.failed) { W.scan.sc.failed = false; return KPW_ERR_NOMEM; }
         if (hipGetLastError() != hipSuccess) return KPW_ERR_DEVICE;
         W.offs = W.d_off.as<uint64_t>() + 1;   // P[k + 1] = boundary k
         return KPW_OK;

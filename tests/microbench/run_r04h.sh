@@ -1,6 +1,11 @@
 #!/bin/bash
 OUT=gpurun_out/r04h
 mkdir -p $OUT
+python tests/microbench/dump_any.py 1 2200000 /tmp/p2.bin > /dev/null
+python tests/microbench/dump_any.py 2 300000 /tmp/p4.bin > /dev/null
+for b in tests/microbench/build/seg_bench*; do
+  for k in 2 4; do timeout -k 10 120 $b /tmp/p$k.bin 3 > $OUT/seg_$(basename $b)_c$k.log 2>&1 || exit $?; done
+done
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -k "multipage or rotation or v2 or fullsize or async" > $OUT/pytest_mp.log 2>&1 || exit $?
 KPW_TRACE=1 timeout -k 10 300 python tests/microbench/mp_leg.py 10000000 1048576 3 > $OUT/mp_trace.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py --steps 1 --warmup 0 --no-resident --no-cpu-baseline --secondary-steps 0 --per-record-records 3000000 > $OUT/per_record.log 2>&1 || exit $?
