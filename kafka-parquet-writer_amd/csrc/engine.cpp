@@ -65,7 +65,6 @@ Engine::~Engine()
     for (auto &e : kev_) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamSynchronize(stream);
     seg_scratch_free(seg_);
-    pin_free(xfer_);
     if (stream) (void)hipStreamDestroy(stream);
     if (tr)
         fprintf(stderr, "[kpw] engine free: events+stream %.1f ms\n",
@@ -162,60 +161,22 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
 
 #define ENS(buf, bytes) do { if ((buf).ensure(bytes)) return fail(KPW_ERR_NOMEM, "device allocation failed: " #buf); } while (0)
 
-hipError_t Engine::xreserve(size_t bytes, hipStream_t s, size_t *off)
-{
-    const size_t need = (bytes + 255) & ~(size_t)255;
-    if (xfer_off_ + need > xfer_cap_) {
-        // queued copies may still read the arena (and readbacks land in it): drain, then grow
-        if (hipError_t e = xsync(s)) return e;
-        if (need > xfer_cap_) {
-            pin_free(xfer_);
-            xfer_cap_ = std::max<size_t>(need * 2, xfer_cap_ * 2 + (1u << 20));
-            xfer_ = (uint8_t *)pin_alloc(xfer_cap_);
-            if (!xfer_) { xfer_cap_ = 0; return hipErrorOutOfMemory; }
-        }
-    }
-    *off = xfer_off_;
-    xfer_off_ += need;
-    return hipSuccess;
-}
-
-// KPW_XFER=0: plain pageable copies (A/B)
-static bool xfer_pinned()
-{
-    static const bool on = [] { const char *e = getenv("KPW_XFER"); return !(e && e[0] == '0'); }();
-    return on;
-}
-
+// The engine's small host tables and readbacks.  Measured (r04, C2 writer A/B on one box):
+// staging them through a pinned arena so they run on SDMA instead of one blit kernel each cost
+// 7-10 % (every SDMA copy between two kernels of the stream is a cross-engine wait), so they
+// stay plain pageable copies; the readbacks are synchronous, xsync keeps the call sites'
+// ordering explicit.
 hipError_t Engine::xh2d(void *dst, const void *src, size_t bytes, hipStream_t s)
 {
-    if (!bytes) return hipSuccess;
-    if (!xfer_pinned()) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
-    size_t off;
-    if (hipError_t e = xreserve(bytes, s, &off)) return e;
-    memcpy(xfer_ + off, src, bytes);
-    return hipMemcpyAsync(dst, xfer_ + off, bytes, hipMemcpyHostToDevice, s);
+    return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
 }
 
 hipError_t Engine::xd2h(void *dst, const void *src, size_t bytes, hipStream_t s)
 {
-    if (!bytes) return hipSuccess;
-    if (!xfer_pinned()) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
-    size_t off;
-    if (hipError_t e = xreserve(bytes, s, &off)) return e;
-    xpend_.push_back(XPend{dst, off, bytes});
-    return hipMemcpyAsync(xfer_ + off, src, bytes, hipMemcpyDeviceToHost, s);
+    return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s) : hipSuccess;
 }
 
-hipError_t Engine::xsync(hipStream_t s)
-{
-    const hipError_t e = hipStreamSynchronize(s);
-    if (e == hipSuccess)
-        for (const XPend &p : xpend_) memcpy(p.host, xfer_ + p.off, p.bytes);
-    xpend_.clear();
-    xfer_off_ = 0;   // every queued copy has run
-    return e;
-}
+hipError_t Engine::xsync(hipStream_t s) { return hipStreamSynchronize(s); }
 
 // Lays out tiles for the given jobs, uploads them and runs the structure pass.
 int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, RleScratch &sc)

@@ -177,18 +177,10 @@ private:
     int mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s, int64_t e,
                     const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask = nullptr);
     int grow_keep(DevBuf &b, size_t bytes, size_t keep);
-    // Small host tables and readbacks cross through one pinned arena (SDMA copies: a pageable
-    // hipMemcpyAsync runs as a blit kernel, which on a busy GPU also queues for CUs behind K7).
-    // xd2h copies land in `dst` at the next xsync (a stream synchronisation), which also frees
-    // the arena for reuse.
+    // the engine's small host <-> device transfers (engine.cpp: why they stay pageable copies)
     hipError_t xh2d(void *dst, const void *src, size_t bytes, hipStream_t s);
     hipError_t xd2h(void *dst, const void *src, size_t bytes, hipStream_t s);
     hipError_t xsync(hipStream_t s);
-    hipError_t xreserve(size_t bytes, hipStream_t s, size_t *off);
-    struct XPend { void *host; size_t off, bytes; };
-    uint8_t *xfer_ = nullptr;
-    size_t xfer_cap_ = 0, xfer_off_ = 0;
-    std::vector<XPend> xpend_;
     std::vector<DevBuf> mp_sp;
     DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_pboff, mp_flag, mp_dch, mp_dtile_chunk, mp_dtile_first, mp_dtile_count, mp_dtile_raw,
         mp_dtile_smin, mp_dtile_smax, mp_dtile_cnt, mp_dtile_sz, mp_ssz, mp_spp, mp_cstream, mp_bstream, mp_acc;

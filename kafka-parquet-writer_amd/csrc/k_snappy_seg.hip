@@ -55,6 +55,7 @@ constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the wh
 #ifndef SG_SW
 #define SG_SW 4u                 // sort scatter: waves (each owns the hashes h % SG_SW)
 #endif
+
 constexpr uint32_t SG_NOMATCH = 0xffff;  // cand[]: the table entry's 4 bytes differ (positions < 65521)
 
 enum : uint32_t { MS = 0, MP = 1, MT = 2 };
@@ -144,18 +145,14 @@ struct FIn {
     }
 };
 
-// FindMatchLength(s1, s2, limit); stops early (returns > cap) past cap bytes.  `memo`: the
-// match length (4 + this function's result) the previous round computed for the same copy
-// (0: none); the data is fixed within a fragment, so once the first 16 bytes agree the rest is
-// known.  Past the first step the comparison runs SG_FMLW bytes per dependent load round trip.
-#ifndef SG_MEMO
-#define SG_MEMO 1
-#endif
+// FindMatchLength(s1, s2, limit); stops early (returns > cap) past cap bytes.  Past the first
+// 16 bytes the comparison runs SG_FMLW bytes per dependent load round trip (r04: 32 bytes,
+// C4 parse 578 -> 561 K cycles per fragment; 64 measured slower, and re-using the previous
+// round's length of the same copy cost more in record loads than it saved).
 #ifndef SG_FMLW
 #define SG_FMLW 32
 #endif
-__device__ __forceinline__ uint32_t sg_fml(const FIn &in, uint32_t s1, uint32_t s2, uint32_t limit, uint32_t cap,
-                                           uint32_t memo)
+__device__ __forceinline__ uint32_t sg_fml(const FIn &in, uint32_t s1, uint32_t s2, uint32_t limit, uint32_t cap)
 {
     uint32_t m = 0;
     if (s2 + 16 <= limit) {
@@ -163,7 +160,6 @@ __device__ __forceinline__ uint32_t sg_fml(const FIn &in, uint32_t s1, uint32_t 
         const uint64_t x1 = in.ld64(s1 + 8) ^ in.ld64(s2 + 8);
         if (x0) return (uint32_t)__builtin_ctzll(x0) >> 3;
         if (x1) return 8 + ((uint32_t)__builtin_ctzll(x1) >> 3);
-        if (SG_MEMO && memo) return memo - 4;
         m = 16;
 #if SG_FMLW > 16
         constexpr int D = SG_FMLW / 4;   // dwords compared per step
@@ -341,7 +337,7 @@ struct ParseOut {
     uint32_t nrec;
 };
 __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, const FIn &in, PS st, uint32_t t, uint32_t n,
-                                             uint32_t ip_limit, uint32_t nprev)
+                                             uint32_t ip_limit)
 {
     const uint32_t sk = t * SG_SEG, sk1 = sk + SG_SEG;
     ParseOut o{st, 0, false, false, false, 0};
@@ -394,12 +390,7 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
             for (int k = 1; k < (int)SG_PB; k++) if (hit == k) { base = q[k]; c = cc[k]; }
             lit = true;
         }
-        uint32_t memo = 0;
-        if (SG_MEMO && o.nrec < nprev) {   // the previous round's copy at this index, if it is this copy
-            const uint64_t pr = G.rec[o.nrec * SG_T + t];
-            if ((uint32_t)pr == (base | ((base - c) << 16))) memo = (uint32_t)(pr >> 32) & 0xffffu;
-        }
-        const uint32_t len = 4 + sg_fml(in, c + 4, base + 4, n, SG_MAXLEN, memo);
+        const uint32_t len = 4 + sg_fml(in, c + 4, base + 4, n, SG_MAXLEN);
         if (len > SG_MAXLEN) { o.lng = true; break; }
         o.fnd = true;
         G.rec[(o.nrec++) * SG_T + t] = (uint64_t)base | ((uint64_t)(base - c) << 16) | ((uint64_t)len << 32) | ((uint64_t)lit << 48);
@@ -690,7 +681,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             __syncthreads();
             PMARK(1);
             // ---------------------------------------------- parse my segment
-            po = t < nseg ? sg_parse(S, G, in, upk(S.b.entry[t]), t, n, ip_limit, po.nrec)
+            po = t < nseg ? sg_parse(S, G, in, upk(S.b.entry[t]), t, n, ip_limit)
                           : ParseOut{upk(S.b.entry[t]), 0, false, false, false, 0};
             S.b.exitst[t] = pk(po.st);
             if (po.lfl) atomicOr(&S.lfl[t >> 5], 1u << (t & 31));

@@ -289,6 +289,18 @@ def test_data_size_every_record_multipage_200k():
     assert dt < 5, dt   # measured 0.56 s on one MI355X (r03b); the single-page loop's bar is 3 s
 
 
+def test_data_size_every_record_reference_defaults_64k_pages():
+    """the reference's default 128 MiB row groups with 64 KiB pages
+    (KafkaProtoParquetWriter.java:656-659 -> ParquetFile.java:47), 300 000 one-record writes:
+    every getDataSize() equals the oracle's and the file is byte-identical.  The open row group
+    never closes here, so every page cut probes a growing prefix (the O(rowgroup^2 / page)
+    regime the verdict names); the loop's rate is printed."""
+    n = 300_000
+    dt, nrg = _per_record_against_oracle(synth.REC8, synth.KIND_REC8, 59, n, 128 * MiB, 64 * 1024)
+    print("128 MiB / 64 KiB per-record loop: %.3f s (%.2f M records/s), %d row groups" % (dt, n / dt / 1e6, nrg))
+    assert nrg == 1
+
+
 def test_data_size_every_record_multipage_small_pages():
     """Many page cuts per row group and many row groups (SampleMessage, 64 KiB blocks, 2 KiB
     pages, uncompressed and SNAPPY)."""
