@@ -232,6 +232,18 @@ static inline uint64_t next_pow2(uint64_t x)
 int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
                    hipStream_t user_stream, BatchOut &out)
 {
+    const int st = encode_impl(d_data, d_off, n, final_flush, next_rg_size, user_stream, out);
+    if (st) return st;
+    // the single-pass scans count a look-back that waited past its bound (kpw_lookback.h):
+    // their results would be wrong, so the encode fails loudly instead
+    const int lf = lb_failures(&seg_, stream);
+    if (lf != 0) return fail(KPW_ERR_DEVICE, lf < 0 ? "scan status unreadable" : "scan look-back timed out");
+    return KPW_OK;
+}
+
+int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
+                        hipStream_t user_stream, BatchOut &out)
+{
     out = BatchOut();
     CK(hipSetDevice(device));
     StreamOrder order(stream);

@@ -102,8 +102,11 @@ public:
     // ColumnChunkPageWriter.getMemSize() adds to getBufferedSize() (the writer's size model).
     // `cols_mask` (optional): only those columns are encoded (the ones that cut a page since the
     // last probe; the others' pages are unchanged, so their npages / flushed come back as -1).
+    // `rg_token` names the open row group (the caller's fill-buffer generation): a cut page never
+    // changes afterwards, so its header + compressed size is kept per (column, page) across the
+    // probes of one token and only the pages cut since are compressed.
     int probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, std::vector<int32_t> &npages,
-                    std::vector<int64_t> &flushed, const std::vector<char> *cols_mask = nullptr);
+                    std::vector<int64_t> &flushed, const std::vector<char> *cols_mask = nullptr, uint64_t rg_token = ~0ull);
     const std::string &error() const { return err_; }
     // Alternate the page output buffers between encodes, so the previous encode's pages can
     // still be read (D2H on another stream) while this one runs.  The caller orders this
@@ -129,6 +132,8 @@ public:
     float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 K7 (k_snappy_v, k_snappy_seg, k_snappy_s_rest)
 
 private:
+    int encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
+                    hipStream_t user_stream, BatchOut &out);
     int fail(int code, const std::string &msg);
     SegScratch seg_;   // segmented-scan scratch of this handle (freed in ~Engine)
     bool seg_failed_reset() { const bool f = seg_.failed; seg_.failed = false; return f; }
@@ -170,12 +175,19 @@ private:
     bool probe_ = false;                 // encode() is a probe_pages call
     std::vector<int32_t> probe_npages_;
     const std::vector<char> *probe_mask_ = nullptr;
+    uint64_t probe_token_ = ~0ull;       // open row group of the cached page sizes (~0: none)
+    struct CutPage { int64_t end; int64_t bytes; };   // a cut page: end record, header + compressed bytes
+    std::vector<std::vector<CutPage>> probe_cache_;   // per column, in page order
     std::vector<int64_t> probe_flushed_;
     int encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                   const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out);
     int mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vector<int64_t>> &cuts);
+    // k7_from (probe): per column the first cut page to compress; the dictionary page, the open
+    // page and the cut pages before k7_from[c] are not compressed (their compressed sizes in
+    // `run` are then meaningless)
     int mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s, int64_t e,
-                    const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask = nullptr);
+                    const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask = nullptr,
+                    const std::vector<uint32_t> *k7_from = nullptr);
     int grow_keep(DevBuf &b, size_t bytes, size_t keep);
     // the engine's small host <-> device transfers (engine.cpp: why they stay pageable copies)
     hipError_t xh2d(void *dst, const void *src, size_t bytes, hipStream_t s);

@@ -100,7 +100,8 @@ int Engine::mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vecto
 // Encode the column chunks [s, e) split at `cuts` (page ends <= e).  Result pages are in
 // pages_dev_ (PageOut offsets), grouped per column: optional dictionary page, data pages.
 int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s,
-                        int64_t e, const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask)
+                        int64_t e, const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask,
+                        const std::vector<uint32_t> *k7_from)
 {
     hipStream_t st = stream;
     const int nc = (int)cols.size();
@@ -113,6 +114,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     for (size_t i = 0; i < bool_idx_.size(); i++) bool_pos[bool_idx_[i]] = (int)i;
     uint64_t ht_off = 0, ids_off = 0;
     std::vector<uint32_t> dtj, dfirst(nc), dcount(nc), ptj, pfirst, pcount;
+    std::vector<char> k7_on;           // per page: its data page is compressed (k7_from)
     for (int c = 0; c < nc; c++) {
         ChunkDesc &D = dch[c];
         memset(&D, 0, sizeof(D));
@@ -202,6 +204,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             pcount.push_back(pt);
             ptj.insert(ptj.end(), pt, (uint32_t)pg.size());
             pg.push_back(P);
+            k7_on.push_back(!k7_from || (i >= (*k7_from)[c] && i < cuts[c].size()));
             q = pe;
         }
         D.npages = (int32_t)pg.size() - D.first_page;
@@ -356,6 +359,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         std::vector<uint32_t> fpage, fidx, pfrag0(2 * npg);
         for (int p = 0; p < 2 * npg; p++) {
             pfrag0[p] = (uint32_t)fpage.size();
+            if (k7_from && (!(p & 1) || !k7_on[p >> 1])) continue;   // a probe: only the newly cut pages
             const uint64_t nf = (plen[p] + SNAPPY_FRAG - 1) / SNAPPY_FRAG;
             for (uint64_t k = 0; k < nf; k++) { fpage.push_back((uint32_t)p); fidx.push_back((uint32_t)k); }
         }
@@ -542,21 +546,33 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         MpRun pr;
         int rs = mp_cuts(a, 0, (int64_t)ne, pc);
         if (rs) return rs;
-        rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_);
+        // pages cut in an earlier probe of this row group keep their sizes: only the ones cut
+        // since are compressed (a cached page whose end moved would be a bug: recompute them all)
+        probe_cache_.resize(nc);
+        std::vector<uint32_t> from(nc, 0);
+        for (int c = 0; c < nc; c++) {
+            std::vector<CutPage> &pcache = probe_cache_[c];
+            bool ok = pcache.size() <= pc[c].size();
+            for (size_t i = 0; ok && i < pcache.size(); i++) ok = pcache[i].end == pc[c][i];
+            if (!ok) pcache.clear();
+            from[c] = (uint32_t)pcache.size();
+        }
+        rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
         if (rs) return rs;
         probe_npages_.assign(nc, 0);
         probe_flushed_.assign(nc, 0);
         for (int c = 0; c < nc; c++) {
             if (probe_mask_ && !(*probe_mask_)[c]) { probe_npages_[c] = -1; probe_flushed_[c] = -1; continue; }
+            std::vector<CutPage> &pcache = probe_cache_[c];
             size_t i = 0;
             for (const PageOut &p : pr.cols[c]) {
                 if (p.page_type == KPW_DICTIONARY_PAGE) continue;
-                if (i < pc[c].size()) {
-                    probe_flushed_[c] += (int64_t)page_header(p, cols[c].phys).size() + p.compressed_size;
-                    probe_npages_[c]++;
-                }
+                if (i < pc[c].size() && i >= pcache.size())
+                    pcache.push_back(CutPage{pc[c][i], (int64_t)page_header(p, cols[c].phys).size() + p.compressed_size});
                 i++;
             }
+            for (const CutPage &cp : pcache) probe_flushed_[c] += cp.bytes;
+            probe_npages_[c] = (int32_t)pcache.size();
         }
         out.records_consumed = 0;
         out.open_records = (int64_t)ne;
@@ -664,9 +680,11 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
 }
 
 int Engine::probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, std::vector<int32_t> &npages,
-                        std::vector<int64_t> &flushed, const std::vector<char> *cols_mask)
+                        std::vector<int64_t> &flushed, const std::vector<char> *cols_mask, uint64_t rg_token)
 {
     if (!mp_) return fail(KPW_ERR_STATE, "probe_pages: single-page regime (no page cuts inside row groups)");
+    if (rg_token != probe_token_ || rg_token == ~0ull) probe_cache_.clear();
+    probe_token_ = rg_token;
     BatchOut out;
     probe_ = true;
     probe_mask_ = cols_mask;

@@ -85,10 +85,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const 
 {
     __shared__ int64_t ldsi[KPW_BLOCK];
     __shared__ uint32_t ldsu[KPW_BLOCK];
-    __shared__ uint32_t slot;
     __shared__ int64_t c0;
     __shared__ uint32_t c1;
-    const uint32_t t = lb_ticket(L, nt, &slot);
+    const uint32_t t = blockIdx.x;
     RleJob &J = jobs[ptile_job[t]];
     const ValSrc src = job_src(J);
     const int64_t len = J.len;
@@ -156,12 +155,17 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_phase(RleJob *jobs, const uint32_
                                                      const uint32_t *lr_b, uint32_t *r_g, uint32_t *r_b, uint32_t nt, LbView L)
 {
     __shared__ uint32_t lds[KPW_BLOCK];
-    __shared__ uint32_t slot, c0, c1;
-    const uint32_t u = lb_ticket(L, nt, &slot);
+    __shared__ uint32_t c0, c1;
+    const uint32_t u = blockIdx.x;
     RleJob &J = jobs[etile_job[u]];
     const uint32_t et0 = J.etile0;
+    const uint32_t nlong = J.n_long;
+    // element tiles are laid out for the job's capacity (len / 8 + 2); past its long runs a
+    // tile has nothing to scan or write, and no later tile of the job needs its status
+    const uint32_t last = et0 + (nlong ? (nlong - 1) / KPW_TILE_E : 0);
+    if (u > last) return;
     const uint64_t k = (uint64_t)(u - et0) * KPW_TILE_E + threadIdx.x;
-    const bool valid = k < J.n_long;
+    const bool valid = k < nlong;
     uint32_t a = 0, b = 0, m = OpMapCompose::id();
     if (valid) { a = lr_a[J.e0 + k]; b = lr_b[J.e0 + k]; m = run_map(a, b); }
     uint32_t tot;
@@ -178,7 +182,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_phase(RleJob *jobs, const uint32_
         r_g[o] = g;
         r_b[o] = b;
     }
-    if (u == et0 + J.netiles - 1 && threadIdx.x == 0) J.n_rle = off + t2;
+    if (u == last && threadIdx.x == 0) J.n_rle = off + t2;
 }
 
 // ------------------------------------------------------------------ sizes / offsets
@@ -194,13 +198,13 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_r_sizes(RleJob *jobs, const uint3
                                                        LbView L)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
-    __shared__ uint32_t slot;
     __shared__ uint64_t c0, c1;
-    const uint32_t u = lb_ticket(L, nt, &slot);
+    const uint32_t u = blockIdx.x;
     RleJob &J = jobs[etile_job[u]];
     const uint32_t et0 = J.etile0;
     const uint64_t k = (uint64_t)(u - et0) * KPW_TILE_E + threadIdx.x;
     const uint32_t nrle = J.n_rle;
+    if (u > et0 + (nrle ? (nrle - 1) / KPW_TILE_E : 0)) return;   // past the job's RLE runs
     const bool valid = k < nrle;
     uint64_t by = 0, gr = 0;
     if (valid) {

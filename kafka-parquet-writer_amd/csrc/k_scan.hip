@@ -42,9 +42,8 @@ template <class F>
 __global__ void __launch_bounds__(KPW_BLOCK) k_mj_scan(F f, uint64_t len, uint32_t tpj, uint32_t nt, LbView L)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
-    __shared__ uint32_t slot;
     __shared__ uint64_t cslot;
-    const uint32_t t = lb_ticket(L, nt, &slot), j = t / tpj, tile = t % tpj;
+    const uint32_t t = blockIdx.x, j = t / tpj, tile = t % tpj;
     const uint64_t i0 = (uint64_t)tile * KPW_TILE_P + (uint64_t)threadIdx.x * 8;
     uint64_t v[8], s = 0;
 #pragma unroll
@@ -64,6 +63,16 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_mj_scan(F f, uint64_t len, uint32
 // Status words of one single-pass launch (nwords: ntiles x scans; w == nullptr: allocation
 // failed, sc->failed set).  Grown buffers start zeroed; the epoch wraps after 2^15 - 1
 // launches with a clear.
+int lb_failures(SegScratch *sc, hipStream_t s)
+{
+    if (!sc->p) return 0;
+    uint32_t n = 0;
+    if (hipMemcpyAsync(&n, (const uint64_t *)sc->p + 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    return (int)n;
+}
+
 LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s)
 {
     const size_t need = 64 + (size_t)nwords * 8;
@@ -154,9 +163,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_seg_scan(const T *in, T *out, con
 {
     __shared__ T lv[KPW_BLOCK];
     __shared__ uint32_t lh[KPW_BLOCK];
-    __shared__ uint32_t slot;
     __shared__ T lcarry_s;
-    const uint32_t blk = lb_ticket(L, nb, &slot);
+    const uint32_t blk = blockIdx.x;
     const uint32_t b = blk * SEG_CH;
     const uint32_t k0 = b + threadIdx.x * SEG_PER;
     T v[SEG_PER];

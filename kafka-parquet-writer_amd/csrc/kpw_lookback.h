@@ -9,33 +9,25 @@
 // Status word of tile i (u64, written and read as one agent-scope atomic, so value and state
 // arrive together): value << 17 | epoch << 2 | state (1: aggregate, 2: inclusive prefix).
 // The epoch changes every launch on the scratch, so stale words read as "not yet" without a
-// clear; values fit 47 bits (byte counts and positions of one encode, < 2^40).  Tiles take
-// their index from a ticket counter (word 0): a block waits only on tiles already taken by
-// running blocks, whatever order the 8 XCDs dispatch in; the block holding the last ticket
-// resets the counter for the next launch.
+// clear; values fit 47 bits (byte counts and positions of one encode, < 2^40).
+//
+// Tile index = blockIdx.x.  A tile waits only on lower-numbered tiles, and each XCD dispatches
+// its workgroups in index order, so the lowest unfinished tile always runs (by induction every
+// tile does).  A ticket counter would not need that, but one atomic per tile on a single
+// address serialised the launch (r04: the element-tile kernels over ~50 k tiles took 0.7 ms
+// where the multi-launch scans took 0.1).  The spin is bounded: a tile that waits past the
+// bound counts a failure in w[1] (the engine fails the encode on it, lb_failures) and goes on
+// with a wrong value rather than hang the GPU.
 #pragma once
 #include "kpw_device.h"
 
 namespace kpw {
 
 struct LbView {
-    uint64_t *w;      // [0]: ticket counter (u32); status words from w[8]
+    uint64_t *w;      // w[1] (low u32): look-back timeouts; status words from w[8]
     uint32_t epoch;
 };
 constexpr uint32_t LB_ST_AGG = 1, LB_ST_INC = 2;
-
-__device__ __forceinline__ uint32_t lb_ticket(const LbView &L, uint32_t nt, uint32_t *slot)
-{
-    if (threadIdx.x == 0) {
-        const uint32_t t = atomicAdd((uint32_t *)L.w, 1u);
-        if (t == nt - 1) atomicExch((uint32_t *)L.w, 0u);
-        *slot = t;
-    }
-    __syncthreads();
-    const uint32_t t = *slot;
-    __syncthreads();
-    return t;
-}
 
 // status word idx (= scan * ntiles + tile)
 __device__ __forceinline__ void lb_publish(const LbView &L, uint32_t idx, uint64_t enc, uint32_t st)
@@ -58,13 +50,13 @@ __device__ __forceinline__ T lb_lookback(const LbView &L, uint32_t sbase, uint32
         const bool valid = q >= (int64_t)first;
         uint64_t wv = 0;
         if (valid) {
-            // (bounded: a predecessor that never publishes would be a bug; the scan then
-            // produces wrong values, which the parity tests catch, instead of hanging the GPU)
+            bool ok = false;
             for (uint32_t spin = 0; spin < (1u << 22); spin++) {
                 wv = __hip_atomic_load(&L.w[8 + sbase + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)((wv >> 2) & 0x7fff) == L.epoch && (wv & 3) != 0) break;
+                if ((uint32_t)((wv >> 2) & 0x7fff) == L.epoch && (wv & 3) != 0) { ok = true; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
+            if (!ok) { atomicAdd((uint32_t *)(L.w + 1), 1u); wv = LB_ST_INC; }   // counted; value 0, terminal
         }
         const bool term = !valid || (wv & 3) == LB_ST_INC;
         const uint64_t tm = __ballot(term);

@@ -21,6 +21,10 @@ void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njo
 // Status words for one single-pass launch over `nwords` tiles x scans (w == nullptr: the
 // scratch could not grow, sc->failed set; the caller skips the launch).
 LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s);
+// look-back timeouts counted on this scratch since it was allocated (kpw_lookback.h; 0 unless a
+// tile waited past the spin bound: the scans' results are then wrong), -1 if unreadable.
+// Synchronises `s` (the stream the scans ran on).
+int lb_failures(SegScratch *sc, hipStream_t s);
 
 // Exclusive segmented scan over tile aggregates (same scratch contract).
 template <typename T, typename Op>

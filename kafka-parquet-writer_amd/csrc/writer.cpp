@@ -293,6 +293,8 @@ struct kpw_writer {
     int64_t open_buffered = 0;         // open row group's buffered size after the last PLANNED job
     std::atomic<int> n_materialize{0};
     double t_open = 0, t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0;
+    double t_probe = 0;          // page-size probes (multi-page per-record path): wall time, count, records
+    uint64_t n_probe = 0, probe_recs = 0;
     double stats[16] = {0};            // kpw_writer_stats (job order; read after drain)
 
     ~kpw_writer();
@@ -934,6 +936,8 @@ static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
         const int st = E.encode(B.d, W.offs + s0, (uint64_t)(lim - s0), j.kind == JOB_FINAL, T, nullptr, out);
         E.max_cuts = 0;
         if (st) return jfail(st, E.error());
+        if (s0 == 0 && lb_failures(&W.scan.sc, s) != 0)   // the offsets scan (kpw_lookback.h)
+            return jfail(KPW_ERR_DEVICE, "offsets scan look-back timed out");
         W.njobs++;   // page buffer sets alternate per encode
         if (out.invalid_record >= 0) {
             // records from the invalid one on are never written (KafkaProtoParquetWriter.java:270-276)
@@ -1370,7 +1374,9 @@ static int probe_flushed(kpw_writer *w, size_t m, std::vector<int32_t> &np, std:
     // hence their flushed bytes, are unchanged)
     std::vector<char> mask;
     w->model.cut_columns(mask);
-    if (int st = P.probe_pages(F.d, w->pr_off.as<uint64_t>(), m, np, fl, &mask)) return wfail(w, st, P.error());
+    const double tp = trace_on() ? now_ms() : 0.0;
+    if (int st = P.probe_pages(F.d, w->pr_off.as<uint64_t>(), m, np, fl, &mask, w->fill_gen)) return wfail(w, st, P.error());
+    if (trace_on()) { w->t_probe += now_ms() - tp; w->n_probe++; w->probe_recs += m; }
     return KPW_OK;
 }
 
@@ -1841,6 +1847,9 @@ extern "C" int kpw_writer_close(kpw_writer *w)
                             "a carry %d, gap %.0f MiB\n",
                     w->t_encode, w->t_dma, w->t_acquire, w->t_d2h_alloc, w->t_asm, w->n_materialize.load(),
                     w->gap_.load() / 1048576.0);
+        if (trace_on() && w->n_probe)
+            fprintf(stderr, "[kpw] close: %llu page-size probes, %.1f ms (%.3f ms each, %.0f records each)\n",
+                    (unsigned long long)w->n_probe, w->t_probe, w->t_probe / w->n_probe, (double)w->probe_recs / w->n_probe);
         return KPW_OK;
     } catch (...) {
         set_fatal(w, KPW_ERR_DEVICE, "close failed");
