@@ -622,7 +622,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_snappy_page_sizes(SnappyArgs a, c
             if (len) {
                 uint32_t v = (uint32_t)len;
                 uint64_t fo = pre + varint_len32(v);
-                const uint32_t nf = (uint32_t)((len + SNAPPY_FRAG - 1) / SNAPPY_FRAG);
+                // the page's fragments as listed (a page-size probe lists only the pages it
+                // needs: the others have none, and their sizes here are not used)
+                const uint32_t nf = (p + 1 < a.npages ? page_frag0[p + 1] : a.nfrags) - page_frag0[p];
                 for (uint32_t k = 0; k < nf; k++) {
                     a.frag_coff[page_frag0[p] + k] = fo;
                     fo += a.frag_len[page_frag0[p] + k];
