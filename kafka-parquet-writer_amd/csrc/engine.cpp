@@ -349,9 +349,11 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             S.rank_col = cols[c].optional ? (int32_t)c : -1;   // optional: length set on the device
         }
     }
+    // a v1 page-size probe with the size model's page cuts needs no planner inputs
+    const bool plan = nstreams && !(probe_ && probe_cuts_);
     ENS(d_streams, std::max<size_t>(1, nstreams) * sizeof(PlanStream));
-    if (nstreams) CK(xh2d(d_streams.p, hs.data(), nstreams * sizeof(PlanStream), s));
-    if (nstreams) {
+    if (plan) CK(xh2d(d_streams.p, hs.data(), nstreams * sizeof(PlanStream), s));
+    if (plan) {
         pj.resize(nstreams);
         for (uint32_t k = 0; k < nstreams; k++) {
             RleJob &J = pj[k];

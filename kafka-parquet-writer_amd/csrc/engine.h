@@ -105,8 +105,11 @@ public:
     // `rg_token` names the open row group (the caller's fill-buffer generation): a cut page never
     // changes afterwards, so its header + compressed size is kept per (column, page) across the
     // probes of one token and only the pages cut since are compressed.
+    // `cuts` (optional, v1): the page cuts of [0, n) per column as the caller's size model has
+    // them, so the probe skips the GPU planner's page-cut pass and its inputs.
     int probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, std::vector<int32_t> &npages,
-                    std::vector<int64_t> &flushed, const std::vector<char> *cols_mask = nullptr, uint64_t rg_token = ~0ull);
+                    std::vector<int64_t> &flushed, const std::vector<char> *cols_mask = nullptr, uint64_t rg_token = ~0ull,
+                    const std::vector<std::vector<int64_t>> *cuts = nullptr);
     const std::string &error() const { return err_; }
     // Alternate the page output buffers between encodes, so the previous encode's pages can
     // still be read (D2H on another stream) while this one runs.  The caller orders this
@@ -176,12 +179,15 @@ private:
     std::vector<int32_t> probe_npages_;
     const std::vector<char> *probe_mask_ = nullptr;
     uint64_t probe_token_ = ~0ull;       // open row group of the cached page sizes (~0: none)
+    const std::vector<std::vector<int64_t>> *probe_cuts_ = nullptr;   // v1 probe: the caller's page cuts
     struct CutPage { int64_t end; int64_t bytes; };   // a cut page: end record, header + compressed bytes
     std::vector<std::vector<CutPage>> probe_cache_;   // per column, in page order
     std::vector<int64_t> probe_flushed_;
     int encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                   const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out);
     int mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vector<int64_t>> &cuts);
+    int probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, const std::vector<DevCol> &hc,
+                 const std::vector<std::vector<int64_t>> &pc, BatchOut &out);
     // k7_from (probe): per column the first cut page to compress; the dictionary page, the open
     // page and the cut pages before k7_from[c] are not compressed (their compressed sizes in
     // `run` are then meaningless)

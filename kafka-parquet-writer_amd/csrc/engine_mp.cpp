@@ -414,7 +414,19 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             boff[p] = blob_len;
             if (cols[pg[p].col].phys == KPW_BYTE_ARRAY && pg[p].has_minmax) blob_len += smeta[4 * p + 1] + smeta[4 * p + 3];
         }
-        if (blob_len) {
+        // a probe needs the page headers' sizes only: the min / max lengths, and whether min ==
+        // max (write_stats then also writes the deprecated fields), which differing lengths decide
+        bool need_bytes = !probe_;
+        for (int p = 0; p < npg && !need_bytes; p++)
+            if (cols[pg[p].col].phys == KPW_BYTE_ARRAY && pg[p].has_minmax && smeta[4 * p + 1] == smeta[4 * p + 3])
+                need_bytes = true;
+        if (blob_len && !need_bytes) {
+            for (int p = 0; p < npg; p++)
+                if (cols[pg[p].col].phys == KPW_BYTE_ARRAY && pg[p].has_minmax) {
+                    bmin[p].assign(smeta[4 * p + 1], 'a');
+                    bmax[p].assign(smeta[4 * p + 3], 'b');
+                }
+        } else if (blob_len) {
             std::vector<uint8_t> blob(blob_len);
             ENS(d_sblob, blob_len);
             launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(),
@@ -500,11 +512,55 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     return KPW_OK;
 }
 
+// probe_pages: the open row group's prefix [0, ne) with its page cuts `pc` (cuts <= ne, a cut at
+// ne included) -> per probed column the pages cut inside it and their header + compressed
+// bytes, i.e. ColumnChunkPageWriter.getMemSize() after record ne - 1
+int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, const std::vector<DevCol> &hc,
+                     const std::vector<std::vector<int64_t>> &pc, BatchOut &out)
+{
+    hipStream_t st = stream;
+    const int nc = (int)cols.size();
+    MpRun pr;
+    // pages cut in an earlier probe of this row group keep their sizes: only the ones cut since
+    // are compressed (a cached page whose end moved would be a bug: recompute them all)
+    probe_cache_.resize(nc);
+    std::vector<uint32_t> from(nc, 0);
+    for (int c = 0; c < nc; c++) {
+        std::vector<CutPage> &pcache = probe_cache_[c];
+        bool ok = pcache.size() <= pc[c].size();
+        for (size_t i = 0; ok && i < pcache.size(); i++) ok = pcache[i].end == pc[c][i];
+        if (!ok) pcache.clear();
+        from[c] = (uint32_t)pcache.size();
+    }
+    int rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
+    if (rs) return rs;
+    probe_npages_.assign(nc, 0);
+    probe_flushed_.assign(nc, 0);
+    for (int c = 0; c < nc; c++) {
+        if (probe_mask_ && !(*probe_mask_)[c]) { probe_npages_[c] = -1; probe_flushed_[c] = -1; continue; }
+        std::vector<CutPage> &pcache = probe_cache_[c];
+        size_t i = 0;
+        for (const PageOut &p : pr.cols[c]) {
+            if (p.page_type == KPW_DICTIONARY_PAGE) continue;
+            if (i < pc[c].size() && i >= pcache.size())
+                pcache.push_back(CutPage{pc[c][i], (int64_t)page_header(p, cols[c].phys).size() + p.compressed_size});
+            i++;
+        }
+        for (const CutPage &cp : pcache) probe_flushed_[c] += cp.bytes;
+        probe_npages_[c] = (int32_t)pcache.size();
+    }
+    out.records_consumed = 0;
+    out.open_records = (int64_t)ne;
+    CK(xsync(st));
+    return KPW_OK;
+}
+
 int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                       const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out)
 {
     hipStream_t st = stream;
     const int nc = (int)cols.size();
+    if (probe_ && probe_cuts_) return probe_mp(d_data, d_off, n, ne, hc, *probe_cuts_, out);
     // per BYTE_ARRAY column: exclusive prefix of (4 + len) over present values
     std::vector<const uint64_t *> sp(nc, nullptr);
     std::vector<int32_t> cstream(nc, -1);
@@ -538,46 +594,11 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     a.col_bstream = mp_bstream.as<int32_t>(); a.streams = d_streams.as<PlanStream>(); a.v2 = v2_ ? 1 : 0;
     if (opt_idx_.empty() && !(v2_ && !bool_idx_.empty())) { a.E = nullptr; a.gend = nullptr; }   // no planner streams
 
-    if (probe_) {
-        // probe_pages: the open row group's prefix [0, ne) -> the pages every column cut inside it
-        // (cuts <= ne, a cut at ne included) and their header + compressed bytes, i.e.
-        // ColumnChunkPageWriter.getMemSize() after record ne - 1
+    if (probe_) {   // probe_pages: the open row group's prefix [0, ne); its page cuts from the GPU planner
         std::vector<std::vector<int64_t>> pc;
-        MpRun pr;
         int rs = mp_cuts(a, 0, (int64_t)ne, pc);
         if (rs) return rs;
-        // pages cut in an earlier probe of this row group keep their sizes: only the ones cut
-        // since are compressed (a cached page whose end moved would be a bug: recompute them all)
-        probe_cache_.resize(nc);
-        std::vector<uint32_t> from(nc, 0);
-        for (int c = 0; c < nc; c++) {
-            std::vector<CutPage> &pcache = probe_cache_[c];
-            bool ok = pcache.size() <= pc[c].size();
-            for (size_t i = 0; ok && i < pcache.size(); i++) ok = pcache[i].end == pc[c][i];
-            if (!ok) pcache.clear();
-            from[c] = (uint32_t)pcache.size();
-        }
-        rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
-        if (rs) return rs;
-        probe_npages_.assign(nc, 0);
-        probe_flushed_.assign(nc, 0);
-        for (int c = 0; c < nc; c++) {
-            if (probe_mask_ && !(*probe_mask_)[c]) { probe_npages_[c] = -1; probe_flushed_[c] = -1; continue; }
-            std::vector<CutPage> &pcache = probe_cache_[c];
-            size_t i = 0;
-            for (const PageOut &p : pr.cols[c]) {
-                if (p.page_type == KPW_DICTIONARY_PAGE) continue;
-                if (i < pc[c].size() && i >= pcache.size())
-                    pcache.push_back(CutPage{pc[c][i], (int64_t)page_header(p, cols[c].phys).size() + p.compressed_size});
-                i++;
-            }
-            for (const CutPage &cp : pcache) probe_flushed_[c] += cp.bytes;
-            probe_npages_[c] = (int32_t)pcache.size();
-        }
-        out.records_consumed = 0;
-        out.open_records = (int64_t)ne;
-        CK(xsync(st));
-        return KPW_OK;
+        return probe_mp(d_data, d_off, n, ne, hc, pc, out);
     }
     uint64_t acc_len = 0;
     const uint64_t per_rec = std::max<uint64_t>(1, Ptot / ne);
@@ -680,17 +701,20 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
 }
 
 int Engine::probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, std::vector<int32_t> &npages,
-                        std::vector<int64_t> &flushed, const std::vector<char> *cols_mask, uint64_t rg_token)
+                        std::vector<int64_t> &flushed, const std::vector<char> *cols_mask, uint64_t rg_token,
+                        const std::vector<std::vector<int64_t>> *cuts)
 {
     if (!mp_) return fail(KPW_ERR_STATE, "probe_pages: single-page regime (no page cuts inside row groups)");
     if (rg_token != probe_token_ || rg_token == ~0ull) probe_cache_.clear();
     probe_token_ = rg_token;
+    probe_cuts_ = v2_ || !cuts || cuts->size() != cols.size() ? nullptr : cuts;
     BatchOut out;
     probe_ = true;
     probe_mask_ = cols_mask;
     const int st = encode(d_data, d_off, n, false, props.block_size, nullptr, out);
     probe_ = false;
     probe_mask_ = nullptr;
+    probe_cuts_ = nullptr;
     if (st) return st;
     if (out.invalid_record >= 0) return fail(KPW_ERR_INVALID_PROTO, "probe_pages: invalid record in a modelled row group");
     npages = probe_npages_;

@@ -168,6 +168,7 @@ void SizeModel::reset_store()
         k.flushed = 0;
         k.pages = 0;
         k.pages_known = 0;
+        k.cut_at.clear();
         k.value_count = 0;
         k.next_check = 100;   // props.getMinRowCountForPageSizeCheck()
         k.bv = RleCount();
@@ -260,6 +261,7 @@ int SizeModel::add(const uint8_t *rec, uint64_t len)
                 k.dl = RleCount();
                 k.data = 0;
                 k.pages++;
+                k.cut_at.push_back(record_count_ + 1);   // the page ends after this record
                 cut = true;
                 continue;
             }
@@ -285,6 +287,7 @@ int SizeModel::add(const uint8_t *rec, uint64_t len)
                 k.bv = RleCount();
                 k.data = 0;
                 k.pages++;
+                k.cut_at.push_back(record_count_);
                 cut = true;
                 rem = page_size_;
             }
@@ -309,6 +312,12 @@ int SizeModel::finish_pages(const std::vector<int32_t> &npages, const std::vecto
         cols_[c].pages_known = cols_[c].pages;
     }
     return block_check();
+}
+
+void SizeModel::page_cuts(std::vector<std::vector<int64_t>> &cuts) const
+{
+    cuts.resize(cols_.size());
+    for (size_t c = 0; c < cols_.size(); c++) cuts[c] = cols_[c].cut_at;
 }
 
 void SizeModel::cut_columns(std::vector<char> &mask) const

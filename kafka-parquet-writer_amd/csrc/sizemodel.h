@@ -67,6 +67,8 @@ public:
     int finish_pages(const std::vector<int32_t> &npages, const std::vector<int64_t> &flushed);
     // the columns that cut a page since the last finish_pages (the ones a probe must encode)
     void cut_columns(std::vector<char> &mask) const;
+    // per column: the open row group's page cuts so far (a page ends before record cut_at[i])
+    void page_cuts(std::vector<std::vector<int64_t>> &cuts) const;
     int64_t buffered() const;               // columnStore.getBufferedSize()
     int64_t record_count() const { return record_count_; }
     bool multi_page() const { return multi_; }
@@ -84,6 +86,7 @@ private:
         int64_t flushed = 0;                // pageWriter.getMemSize(): cut pages, header + compressed
         int32_t pages = 0;                  // pages cut in the open row group
         int32_t pages_known = 0;            // pages whose flushed bytes `flushed` holds
+        std::vector<int64_t> cut_at;        // record count of the open row group at each page cut
         int32_t value_count = 0, next_check = 100;
         RleCount bv;                        // v2 BOOLEAN: RunLengthBitPackingHybridValuesWriter of the values
         int64_t rows_written = 0;           // v2: rowCount at this column's last page

@@ -1374,8 +1374,11 @@ static int probe_flushed(kpw_writer *w, size_t m, std::vector<int32_t> &np, std:
     // hence their flushed bytes, are unchanged)
     std::vector<char> mask;
     w->model.cut_columns(mask);
+    std::vector<std::vector<int64_t>> cuts;   // the model's page cuts: the probe skips the GPU's page-cut pass
+    w->model.page_cuts(cuts);
     const double tp = trace_on() ? now_ms() : 0.0;
-    if (int st = P.probe_pages(F.d, w->pr_off.as<uint64_t>(), m, np, fl, &mask, w->fill_gen)) return wfail(w, st, P.error());
+    if (int st = P.probe_pages(F.d, w->pr_off.as<uint64_t>(), m, np, fl, &mask, w->fill_gen, &cuts))
+        return wfail(w, st, P.error());
     if (trace_on()) { w->t_probe += now_ms() - tp; w->n_probe++; w->probe_recs += m; }
     return KPW_OK;
 }
