@@ -4,6 +4,8 @@
 //    elements per 256-thread tile, 16-byte-friendly sequential per-thread ranges;
 //  * multi-block segmented scans over tile aggregates (one entry per 2048 positions / 256
 //    elements), generic over the combine operator.
+#include <algorithm>
+
 #include "kpw_device.h"
 #include "kpw_kernels.h"
 #include "kpw_scan.h"
@@ -37,29 +39,34 @@ struct EvF {
     __device__ void put(uint32_t j, uint64_t i, uint64_t v) const { E[j * stride + i] = (uint32_t)v; }
 };
 
-// multi-job equal-length exclusive sum: tile t of job t / tpj covers KPW_TILE_P elements
+// multi-job equal-length exclusive sum: tile t of job t / tpj covers MJ_TILE elements, MJ_PER
+// consecutive ones per thread (r04: 8 per thread made the look-back's latency per tile the
+// bound on 400 M-element event scans; 32 per thread gives it 4x the work to hide behind)
+constexpr int MJ_PER = 32;
+constexpr uint64_t MJ_TILE = (uint64_t)KPW_BLOCK * MJ_PER;
 template <class F>
 __global__ void __launch_bounds__(KPW_BLOCK) k_mj_scan(F f, uint64_t len, uint32_t tpj, uint32_t nt, LbView L)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
     __shared__ uint64_t cslot;
     const uint32_t t = blockIdx.x, j = t / tpj, tile = t % tpj;
-    const uint64_t i0 = (uint64_t)tile * KPW_TILE_P + (uint64_t)threadIdx.x * 8;
-    uint64_t v[8], s = 0;
+    const uint64_t i0 = (uint64_t)tile * MJ_TILE + (uint64_t)threadIdx.x * MJ_PER;
+    uint64_t v[MJ_PER], s = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) { v[k] = (i0 + k < len) ? f.get(j, i0 + k) : 0; s += v[k]; }
+    for (int k = 0; k < MJ_PER; k++) { v[k] = (i0 + k < len) ? f.get(j, i0 + k) : 0; s += v[k]; }
     uint64_t tot;
     uint64_t ex = block_scan_excl<uint64_t, OpSum64>(s, lds, &tot);
     const uint64_t carry = lb_tile<uint64_t, OpSum64>(L, 0, t, t - tile, tot, tile == 0, tile != 0, &cslot);
     ex += carry;
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < MJ_PER; k++) {
         if (i0 + k < len) f.put(j, i0 + k, ex);
         ex += v[k];
     }
     if (tile == tpj - 1 && threadIdx.x == 0) f.put(j, len, carry + tot);
 }
 
+// look-back timeouts counted on the scratch (kpw_lookback.h)
 // Status words of one single-pass launch (nwords: ntiles x scans; w == nullptr: allocation
 // failed, sc->failed set).  Grown buffers start zeroed; the epoch wraps after 2^15 - 1
 // launches with a clear.
@@ -73,6 +80,9 @@ int lb_failures(SegScratch *sc, hipStream_t s)
     return (int)n;
 }
 
+// Status words of one single-pass launch (nwords: ntiles x scans; w == nullptr: allocation
+// failed, sc->failed set).  Grown buffers start zeroed; the epoch wraps after 2^15 - 1
+// launches with a clear.
 LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s)
 {
     const size_t need = 64 + (size_t)nwords * 8;
@@ -97,7 +107,7 @@ template <class F>
 static void mj_scan(F f, uint64_t len, uint32_t njobs, SegScratch *sc, hipStream_t s)
 {
     if (!njobs) return;
-    const uint32_t tpj = (uint32_t)((len + KPW_TILE_P - 1) / KPW_TILE_P) ? (uint32_t)((len + KPW_TILE_P - 1) / KPW_TILE_P) : 1;
+    const uint32_t tpj = (uint32_t)std::max<uint64_t>(1, (len + MJ_TILE - 1) / MJ_TILE);
     const uint32_t nt = tpj * njobs;
     const LbView L = lb_prepare(sc, nt, s);
     if (!L.w) return;
