@@ -205,12 +205,17 @@ int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, Rle
         etj.insert(etj.end(), J.netiles, (uint32_t)j);
     }
     const size_t nj = jobs.size();
-    ENS(r_ptile_job, npt * 4); ENS(r_etile_job, net * 4); ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_rg, e0 * 4);
+    ENS(r_ptile_job, npt * 4); ENS(r_last, npt * 8); ENS(r_prev, npt * 8); ENS(r_lrcnt, npt * 4); ENS(r_lroff, npt * 4);
+    ENS(r_etile_job, net * 4); ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_rg, e0 * 4);
     ENS(r_rb, e0 * 4); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8); ENS(d_jobs, nj * sizeof(RleJob));
     CK(xh2d(r_ptile_job.p, ptj.data(), npt * 4, s));
     CK(xh2d(r_etile_job.p, etj.data(), net * 4, s));
     CK(xh2d(d_jobs.p, jobs.data(), nj * sizeof(RleJob), s));
     sc.ptile_job = r_ptile_job.as<uint32_t>();
+    sc.last_brk = r_last.as<int64_t>();
+    sc.prev_brk = r_prev.as<int64_t>();
+    sc.lr_cnt = r_lrcnt.as<uint32_t>();
+    sc.lr_off = r_lroff.as<uint32_t>();
     sc.etile_job = r_etile_job.as<uint32_t>();
     sc.lr_a = r_lra.as<uint32_t>();
     sc.lr_b = r_lrb.as<uint32_t>();

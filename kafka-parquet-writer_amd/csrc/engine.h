@@ -148,7 +148,7 @@ private:
     // planning
     DevBuf d_ev, d_E, d_gend, d_rg_start, d_rg_end, d_plan_out;
     // rle scratch (shared by planning and encoding)
-    DevBuf r_ptile_job, r_etile_job, r_lra, r_lrb, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;
+    DevBuf r_ptile_job, r_last, r_prev, r_lrcnt, r_lroff, r_etile_job, r_lra, r_lrb, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;
     // chunks
     DevBuf d_chunks, d_ctile_chunk, d_ctile_first, d_ctile_count, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
         d_tile_cnt, d_tile_sz, d_ht, d_ids, d_ent_rec, d_ent_boff, d_page_off, d_page_len, d_tot,

@@ -18,8 +18,9 @@
 //
 // Pipeline per batch of jobs (launched back to back, no host sync; every scan a single-pass
 // decoupled look-back inside the kernel that needs it, kpw_lookback.h):
-//   longruns (break max-scan, count, sum-scan, write) -> phase (compose-scan, RLE runs,
-//   sum-scan, write) -> sizes (two sum-scans, job totals) -> write (runs + groups) | events
+//   bounds -> [max-scan] -> longruns(count) -> [sum-scan] -> longruns(write) -> phase
+//   (compose-scan, RLE runs, sum-scan, write) -> sizes (two sum-scans, job totals) -> write
+//   (runs + groups) | events
 #include "kpw_device.h"
 #include "kpw_kernels.h"
 #include "kpw_scan.h"
@@ -74,25 +75,51 @@ __device__ __forceinline__ void src_get8(const ValSrc &s, int64_t p0, int64_t le
 }
 
 // ------------------------------------------------------------------ long runs
-// One launch over the position tiles: the last value break before the tile (a max-scan,
-// look-back 0), then the long runs ending in the tile, counted, placed (a sum-scan, look-back
-// 1) and written as (a, b).  A tile with a break publishes its inclusive max at once (break
-// positions grow with the tile), so look-back 0 is one step in practice.  The job's last
-// tile stores n_long.
+// Over the position tiles: the last value break per tile, a segmented max-scan of those (the
+// break before each tile), the long runs ending in each tile counted, a sum-scan of the counts,
+// then the runs written as (a, b); the job's last tile stores n_long.  (r04: one launch with
+// both scans as in-kernel look-backs measured 2x slower here: every tile has full work, and
+// its look-back round trips are exposed; the element-tile kernels below keep theirs, since
+// most of their tiles are past the job's runs and exit at once.)
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const uint32_t *ptile_job, uint32_t *lr_a, uint32_t *lr_b,
-                                                            uint32_t nt, LbView L)
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_bounds(const RleJob *jobs, const uint32_t *ptile_job, int64_t *last_brk)
+{
+    __shared__ int64_t lds[KPW_BLOCK];
+    const uint32_t t = blockIdx.x;
+    const RleJob &J = jobs[ptile_job[t]];
+    const ValSrc src = job_src(J);
+    const int64_t len = J.len;
+    const int64_t p0 = (int64_t)(t - J.tile0) * KPW_TILE_P + threadIdx.x * 8;
+    int64_t last = -1;
+    if (p0 < len) {
+        uint32_t prev = p0 > 0 ? src_get(src, p0 - 1) : 0;
+        uint32_t vv[8];
+        src_get8(src, p0, len, vv);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int64_t i = p0 + k;
+            if (i >= len) break;
+            const uint32_t v = vv[k];
+            if (i == 0 || v != prev) last = i;
+            prev = v;
+        }
+    }
+    last = block_reduce<int64_t, OpMaxI64>(last, lds);
+    if (threadIdx.x == 0) last_brk[t] = last;
+}
+
+// write = 0: long runs per tile into cnt[t]; write = 1: the runs at their offsets off[t]
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const uint32_t *ptile_job, const int64_t *prev_brk,
+                                                            uint32_t *cnt, const uint32_t *off, uint32_t *lr_a, uint32_t *lr_b,
+                                                            int write)
 {
     __shared__ int64_t ldsi[KPW_BLOCK];
     __shared__ uint32_t ldsu[KPW_BLOCK];
-    __shared__ int64_t c0;
-    __shared__ uint32_t c1;
     const uint32_t t = blockIdx.x;
     RleJob &J = jobs[ptile_job[t]];
     const ValSrc src = job_src(J);
     const int64_t len = J.len;
-    const uint32_t tile0 = J.tile0;
-    const int64_t p0 = (int64_t)(t - tile0) * KPW_TILE_P + threadIdx.x * 8;
+    const int64_t p0 = (int64_t)(t - J.tile0) * KPW_TILE_P + threadIdx.x * 8;
     uint32_t brk = 0;
     int64_t local_last = -1;
     if (p0 < len) {
@@ -110,20 +137,18 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const 
     }
     int64_t tot_i;
     int64_t incoming = block_scan_excl<int64_t, OpMaxI64>(local_last, ldsi, &tot_i);
-    const int64_t pb = lb_tile<int64_t, OpMaxI64>(L, 0, t, tile0, tot_i, t == tile0 || tot_i >= 0, t != tile0, &c0);
+    const int64_t pb = (t == J.tile0) ? -1 : prev_brk[t];
     if (pb > incoming) incoming = pb;
 
-    // long runs ending in this thread's positions: count, then write
+    // pass: count (and optionally write) long runs ending in this thread's positions
     uint32_t c = 0;
-    for (int pass = 0; pass < 2; pass++) {
+    for (int pass = 0; pass < (write ? 2 : 1); pass++) {
         uint64_t base = 0;
         if (pass == 1) {
             uint32_t tot;
             const uint32_t ex = block_scan_excl<uint32_t, OpSum32>(c, ldsu, &tot);
-            const uint32_t off = lb_tile<uint32_t, OpSum32>(L, nt, t, tile0, tot, t == tile0, t != tile0, &c1);
-            if (t == tile0 + J.ntiles - 1 && threadIdx.x == 0) J.n_long = off + tot;
-            if (!tot) break;
-            base = J.e0 + off + ex;
+            if (t == J.tile0 + J.ntiles - 1 && threadIdx.x == 0) J.n_long = off[t] + tot;
+            base = J.e0 + off[t] + ex;
         }
         int64_t prev = incoming;
         uint32_t k2 = 0;
@@ -143,6 +168,10 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const 
             }
         }
         c = k2;
+    }
+    if (!write) {
+        const uint32_t s = block_reduce<uint32_t, OpSum32>(c, ldsu);
+        if (threadIdx.x == 0) cnt[t] = s;
     }
 }
 
@@ -360,16 +389,21 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_ev(const RleJob *jobs, const 
 
 // ------------------------------------------------------------------ host launchers
 
-// Three launches (long runs, phases, sizes), each a chain of single-pass scans; a launch whose
-// scan scratch cannot grow is skipped with sc.seg->failed set (the engine fails the encode).
+// Long runs (5 launches: bounds, max-scan, count, sum-scan, write), then phases and sizes (one
+// launch each, chaining two look-back scans); a launch whose scan scratch cannot grow is
+// skipped with sc.seg->failed set (the engine fails the encode).
 void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc,
                           hipStream_t s)
 {
     if (!njobs || !n_ptiles) return;
-    LbView L = lb_prepare(sc.seg, 2ull * n_ptiles, s);
-    if (!L.w) return;
-    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.lr_a, sc.lr_b, n_ptiles, L);
-    L = lb_prepare(sc.seg, 2ull * n_etiles, s);
+    hipLaunchKernelGGL(k_rle_bounds, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.last_brk);
+    seg_tile_scan<int64_t, OpMaxI64>(sc.last_brk, sc.prev_brk, sc.ptile_job, n_ptiles, nullptr, sc.seg, s);
+    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, (const int64_t *)sc.prev_brk,
+                       sc.lr_cnt, (const uint32_t *)sc.lr_off, sc.lr_a, sc.lr_b, 0);
+    seg_tile_scan<uint32_t, OpSum32>(sc.lr_cnt, sc.lr_off, sc.ptile_job, n_ptiles, nullptr, sc.seg, s);
+    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, (const int64_t *)sc.prev_brk,
+                       sc.lr_cnt, (const uint32_t *)sc.lr_off, sc.lr_a, sc.lr_b, 1);
+    LbView L = lb_prepare(sc.seg, 2ull * n_etiles, s);
     if (!L.w) return;
     hipLaunchKernelGGL(k_phase, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b, sc.r_g, sc.r_b,
                        n_etiles, L);

@@ -39,31 +39,71 @@ struct EvF {
     __device__ void put(uint32_t j, uint64_t i, uint64_t v) const { E[j * stride + i] = (uint32_t)v; }
 };
 
-// multi-job equal-length exclusive sum: tile t of job t / tpj covers MJ_TILE elements, MJ_PER
-// consecutive ones per thread (r04: 8 per thread made the look-back's latency per tile the
-// bound on 400 M-element event scans; 32 per thread gives it 4x the work to hide behind)
-constexpr int MJ_PER = 32;
-constexpr uint64_t MJ_TILE = (uint64_t)KPW_BLOCK * MJ_PER;
+// Multi-job equal-length exclusive sums, reduce -> scan tile sums -> apply (three launches).
+// r04: a single-pass look-back version measured 1.8x slower on the planner's 400 M-element
+// event scans (each tile's look-back is a round trip of uncached agent-scope loads; these
+// scans stream their input once more instead).  Tiles of KPW_TILE_P elements, 8 consecutive
+// ones per thread.
 template <class F>
-__global__ void __launch_bounds__(KPW_BLOCK) k_mj_scan(F f, uint64_t len, uint32_t tpj, uint32_t nt, LbView L)
+__global__ void __launch_bounds__(KPW_BLOCK) k_mj_tsum(F f, uint64_t len, uint32_t tpj, uint64_t *tsum)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
-    __shared__ uint64_t cslot;
     const uint32_t t = blockIdx.x, j = t / tpj, tile = t % tpj;
-    const uint64_t i0 = (uint64_t)tile * MJ_TILE + (uint64_t)threadIdx.x * MJ_PER;
-    uint64_t v[MJ_PER], s = 0;
+    const uint64_t i0 = (uint64_t)tile * KPW_TILE_P + (uint64_t)threadIdx.x * 8;
+    uint64_t s = 0;
 #pragma unroll
-    for (int k = 0; k < MJ_PER; k++) { v[k] = (i0 + k < len) ? f.get(j, i0 + k) : 0; s += v[k]; }
+    for (int k = 0; k < 8; k++) if (i0 + k < len) s += f.get(j, i0 + k);
+    s = block_reduce<uint64_t, OpSum64>(s, lds);
+    if (threadIdx.x == 0) tsum[t] = s;
+}
+
+// one block per job: exclusive scan of its tiles' sums; writes the job total to tsum[njobs*tpj + j]
+__global__ void __launch_bounds__(KPW_BLOCK) k_mj_tscan(uint64_t *tsum, uint32_t tpj, uint32_t njobs)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    const uint32_t j = blockIdx.x;
+    uint64_t carry = 0;
+    for (uint32_t b = 0; b < tpj; b += KPW_BLOCK) {
+        const uint32_t k = b + threadIdx.x;
+        uint64_t v = k < tpj ? tsum[(uint64_t)j * tpj + k] : 0;
+        uint64_t tot;
+        uint64_t ex = block_scan_excl<uint64_t, OpSum64>(v, lds, &tot);
+        if (k < tpj) tsum[(uint64_t)j * tpj + k] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) tsum[(uint64_t)njobs * tpj + j] = carry;
+}
+
+template <class F>
+__global__ void __launch_bounds__(KPW_BLOCK) k_mj_tapply(F f, uint64_t len, uint32_t tpj, uint32_t njobs, const uint64_t *tsum)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    const uint32_t t = blockIdx.x, j = t / tpj, tile = t % tpj;
+    const uint64_t i0 = (uint64_t)tile * KPW_TILE_P + (uint64_t)threadIdx.x * 8;
+    uint64_t v[8], s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) { v[k] = (i0 + k < len) ? f.get(j, i0 + k) : 0; s += v[k]; }
     uint64_t tot;
-    uint64_t ex = block_scan_excl<uint64_t, OpSum64>(s, lds, &tot);
-    const uint64_t carry = lb_tile<uint64_t, OpSum64>(L, 0, t, t - tile, tot, tile == 0, tile != 0, &cslot);
-    ex += carry;
+    uint64_t ex = block_scan_excl<uint64_t, OpSum64>(s, lds, &tot) + tsum[t];
 #pragma unroll
-    for (int k = 0; k < MJ_PER; k++) {
+    for (int k = 0; k < 8; k++) {
         if (i0 + k < len) f.put(j, i0 + k, ex);
         ex += v[k];
     }
-    if (tile == tpj - 1 && threadIdx.x == 0) f.put(j, len, carry + tot);
+    if (tile == tpj - 1 && threadIdx.x == 0) f.put(j, len, tsum[(uint64_t)njobs * tpj + j]);
+}
+
+// the reduce-then-scan scratch (tile sums): w == nullptr if it cannot grow (sc->failed set)
+uint64_t *scan_tmp(SegScratch *sc, uint64_t words, hipStream_t s)
+{
+    const size_t need = (size_t)words * 8 + 64;
+    if (need > sc->tmp_bytes) {
+        if (sc->tmp) dev_free_after(sc->tmp, s);   // earlier scans may still use it on `s`
+        sc->tmp_bytes = need * 2;
+        sc->tmp = dev_alloc(sc->tmp_bytes);
+        if (!sc->tmp) { sc->tmp_bytes = 0; sc->failed = true; return nullptr; }
+    }
+    return (uint64_t *)sc->tmp;
 }
 
 // look-back timeouts counted on the scratch (kpw_lookback.h)
@@ -107,11 +147,13 @@ template <class F>
 static void mj_scan(F f, uint64_t len, uint32_t njobs, SegScratch *sc, hipStream_t s)
 {
     if (!njobs) return;
-    const uint32_t tpj = (uint32_t)std::max<uint64_t>(1, (len + MJ_TILE - 1) / MJ_TILE);
+    const uint32_t tpj = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P - 1) / KPW_TILE_P);
     const uint32_t nt = tpj * njobs;
-    const LbView L = lb_prepare(sc, nt, s);
-    if (!L.w) return;
-    hipLaunchKernelGGL(k_mj_scan<F>, dim3(nt), dim3(KPW_BLOCK), 0, s, f, len, tpj, nt, L);
+    uint64_t *tmp = scan_tmp(sc, (uint64_t)nt + njobs + 1, s);
+    if (!tmp) return;
+    hipLaunchKernelGGL(k_mj_tsum<F>, dim3(nt), dim3(KPW_BLOCK), 0, s, f, len, tpj, tmp);
+    hipLaunchKernelGGL(k_mj_tscan, dim3(njobs), dim3(KPW_BLOCK), 0, s, tmp, tpj, njobs);
+    hipLaunchKernelGGL(k_mj_tapply<F>, dim3(nt), dim3(KPW_BLOCK), 0, s, f, len, tpj, njobs, (const uint64_t *)tmp);
 }
 
 void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s)
@@ -222,8 +264,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_seg_scan(const T *in, T *out, con
 void seg_scratch_free(SegScratch &sc)
 {
     dev_free(sc.p);
-    sc.p = nullptr;
-    sc.bytes = 0;
+    dev_free(sc.tmp);
+    sc.p = sc.tmp = nullptr;
+    sc.bytes = sc.tmp_bytes = 0;
 }
 
 template <typename T, typename Op>

@@ -47,9 +47,11 @@ struct DecodeArgs {
 // handle (Engine::seg_) and grown on demand.  Scans of one handle run in order on its own
 // stream, so they share it; handles never share one (concurrent writers, C5).
 struct SegScratch {
-    void *p = nullptr;             // single-pass scans: ticket counter + tile status words
+    void *p = nullptr;             // single-pass scans: tile status words (kpw_lookback.h)
     size_t bytes = 0;
     uint32_t epoch = 0;            // of the last launch (status words carry it)
+    void *tmp = nullptr;           // reduce-then-scan tile sums (never the status words: any
+    size_t tmp_bytes = 0;          // value written there could pose as a status of a later epoch)
     bool failed = false;           // an allocation failed since the engine last checked
 };
 
@@ -78,6 +80,8 @@ struct RleJob {
 
 struct RleScratch {
     uint32_t *ptile_job;           // position tile -> job
+    int64_t *last_brk, *prev_brk;  // per position tile: its last value break / the one before it
+    uint32_t *lr_cnt, *lr_off;     // per position tile: long runs ending in it / their offset
     uint32_t *etile_job;           // element tile -> job
     uint32_t *lr_a, *lr_b;         // long runs (a, b)
     uint32_t *r_g, *r_b;           // RLE runs (g, b)

@@ -12,9 +12,9 @@ struct OpSum32;
 struct OpMaxI64;
 struct OpMapCompose;
 
-// Single-pass scans (decoupled look-back, k_scan.hip); `sc` holds their tile status words.
-// If the scratch cannot grow, the scan is skipped and sc->failed is set: the caller must fail
-// the encode.
+// Multi-job scans (reduce -> scan -> apply, k_scan.hip); `sc` holds their tile sums.  If the
+// scratch cannot grow, the scan is skipped and sc->failed is set: the caller must fail the
+// encode.
 void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, SegScratch *sc, hipStream_t s);
 void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, SegScratch *sc, hipStream_t s);
 
