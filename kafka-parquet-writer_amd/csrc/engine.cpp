@@ -166,6 +166,24 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
 // 7-10 % (every SDMA copy between two kernels of the stream is a cross-engine wait), so they
 // stay plain pageable copies; the readbacks are synchronous, xsync keeps the call sites'
 // ordering explicit.
+int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::vector<uint8_t *> &dev)
+{
+    static thread_local std::vector<uint8_t> host;
+    size_t tot = 0;
+    for (const HostPart &q : parts) tot += (q.bytes + 255) & ~(size_t)255;
+    ENS(buf, std::max<size_t>(tot, 256));
+    host.resize(tot);
+    dev.clear();
+    size_t at = 0;
+    for (const HostPart &q : parts) {
+        if (q.bytes) memcpy(host.data() + at, q.p, q.bytes);
+        dev.push_back(buf.as<uint8_t>() + at);
+        at += (q.bytes + 255) & ~(size_t)255;
+    }
+    CK(xh2d(buf.p, host.data(), tot, stream));
+    return KPW_OK;
+}
+
 hipError_t Engine::xh2d(void *dst, const void *src, size_t bytes, hipStream_t s)
 {
     return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
@@ -205,18 +223,18 @@ int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, Rle
         etj.insert(etj.end(), J.netiles, (uint32_t)j);
     }
     const size_t nj = jobs.size();
-    ENS(r_ptile_job, npt * 4); ENS(r_last, npt * 8); ENS(r_prev, npt * 8); ENS(r_lrcnt, npt * 4); ENS(r_lroff, npt * 4);
-    ENS(r_etile_job, net * 4); ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_rg, e0 * 4);
-    ENS(r_rb, e0 * 4); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8); ENS(d_jobs, nj * sizeof(RleJob));
-    CK(xh2d(r_ptile_job.p, ptj.data(), npt * 4, s));
-    CK(xh2d(r_etile_job.p, etj.data(), net * 4, s));
-    CK(xh2d(d_jobs.p, jobs.data(), nj * sizeof(RleJob), s));
-    sc.ptile_job = r_ptile_job.as<uint32_t>();
+    ENS(r_last, npt * 8); ENS(r_prev, npt * 8); ENS(r_lrcnt, npt * 4); ENS(r_lroff, npt * 4);
+    ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_rg, e0 * 4);
+    ENS(r_rb, e0 * 4); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8);
+    std::vector<uint8_t *> dp;   // jobs first: d_jobs.as<RleJob>() is the job table
+    if (int st = upload_parts(d_jobs, {{jobs.data(), nj * sizeof(RleJob)}, {ptj.data(), npt * 4}, {etj.data(), net * 4}}, dp))
+        return st;
+    sc.ptile_job = (uint32_t *)dp[1];
     sc.last_brk = r_last.as<int64_t>();
     sc.prev_brk = r_prev.as<int64_t>();
     sc.lr_cnt = r_lrcnt.as<uint32_t>();
     sc.lr_off = r_lroff.as<uint32_t>();
-    sc.etile_job = r_etile_job.as<uint32_t>();
+    sc.etile_job = (uint32_t *)dp[2];
     sc.lr_a = r_lra.as<uint32_t>();
     sc.lr_b = r_lrb.as<uint32_t>();
     sc.r_g = r_rg.as<uint32_t>();
@@ -541,38 +559,43 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             for (int ci = 0; ci < nch; ci++)
                 if (ch[ci].is_dict && k < ccount[ci]) dorder.push_back(cfirst[ci] + k);
     }
-    ENS(d_dict_order, std::max<size_t>(1, dorder.size()) * 4);
-    if (!dorder.empty()) CK(xh2d(d_dict_order.p, dorder.data(), dorder.size() * 4, s));
-    ENS(d_chunks, nch * sizeof(ChunkDesc)); ENS(d_ctile_chunk, nct * 4); ENS(d_ctile_first, nch * 4); ENS(d_ctile_count, nch * 4);
+    ENS(d_chunks, nch * sizeof(ChunkDesc));
     ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
     ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8);
     ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
     ENS(d_ids, std::max<uint64_t>(1, ids_off) * 4); ENS(d_ent_rec, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
-    ENS(d_page_off, 2 * nch * 8); ENS(d_page_len, 2 * nch * 8); ENS(d_tot, 64);
+    // page table (u64 words): [body / compressed totals 2 | collision flags 1 | pad 1 | page offsets,
+    // lengths, level prefixes, compressed offsets, compressed lengths: 2 per chunk each], so the
+    // layout's results come back in one copy and K7's in another
+    const size_t P2 = 2 * (size_t)nch;
+    ENS(d_ptab, (4 + 5 * P2) * 8);
+    uint64_t *const pt = d_ptab.as<uint64_t>();
+    uint64_t *const d_poff = pt + 4, *const d_plen = d_poff + P2, *const d_ppre = d_plen + P2;
+    uint64_t *const d_pcoff = d_ppre + P2, *const d_pclen = d_pcoff + P2;
+    uint32_t *const d_coll = (uint32_t *)(pt + 2);
     for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
-    CK(xh2d(d_ctile_chunk.p, ctj.data(), nct * 4, s));
-    CK(xh2d(d_ctile_first.p, cfirst.data(), nch * 4, s));
-    CK(xh2d(d_ctile_count.p, ccount.data(), nch * 4, s));
-    ENS(d_collision, 64);
+    std::vector<uint8_t *> ctp;   // chunk tile -> chunk, first tile and tile count per chunk, insertion order
+    if (int st = upload_parts(d_ctile, {{ctj.data(), (size_t)nct * 4}, {cfirst.data(), (size_t)nch * 4}, {ccount.data(), (size_t)nch * 4},
+                                        {dorder.data(), dorder.size() * 4}}, ctp))
+        return st;
     ChunkArgs a{};
     a.ch = d_chunks.as<ChunkDesc>(); a.nchunks = nch; a.nctiles = nct; a.cols = d_cols.as<DevCol>(); a.data = d_data;
-    a.ctile_chunk = d_ctile_chunk.as<uint32_t>(); a.ctile_first = d_ctile_first.as<uint32_t>();
-    a.ctile_count = d_ctile_count.as<uint32_t>(); a.tile_raw = d_tile_raw.as<uint64_t>();
+    a.ctile_chunk = (uint32_t *)ctp[0]; a.ctile_first = (uint32_t *)ctp[1];
+    a.ctile_count = (uint32_t *)ctp[2]; a.tile_raw = d_tile_raw.as<uint64_t>();
     a.tile_raw_off = d_tile_raw_off.as<uint64_t>(); a.tile_smin = d_tile_smin.as<uint64_t>();
     a.tile_smax = d_tile_smax.as<uint64_t>(); a.tile_cnt = d_tile_cnt.as<uint32_t>(); a.tile_sz = d_tile_sz.as<uint64_t>();
     a.ht = d_ht.as<HtSlot>();
     a.ids = d_ids.as<uint32_t>(); a.ent_rec = d_ent_rec.as<uint64_t>(); a.ent_boff = d_ent_boff.as<uint64_t>();
     a.max_dict_bytes = (uint32_t)props.dictionary_page_size;
     a.data_end = d_off + n;
-    a.collision = d_collision.as<uint32_t>();
-    a.dict_order = d_dict_order.as<uint32_t>(); a.ndict_tiles = (uint32_t)dorder.size();
+    a.collision = d_coll;
+    a.dict_order = (uint32_t *)ctp[3]; a.ndict_tiles = (uint32_t)dorder.size();
     a.v2 = v2_ ? 1 : 0;
     a.seg = &seg_;
     // v2 DELTA streams: dense inputs share the chunks' rank-indexed id space (ids_off)
     DeltaArgs dla{};
-    ENS(d_page_pre, 2 * nch * 8);
-    a.page_pre = d_page_pre.as<uint64_t>();
+    a.page_pre = d_ppre;
     if (v2_) {
         ENS(d_dense, std::max<uint64_t>(1, ids_off) * 8); ENS(d_pre, std::max<uint64_t>(1, ids_off) * 4);
         ENS(d_sfx, std::max<uint64_t>(1, ids_off) * 4);
@@ -596,6 +619,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     uint32_t enpt = 0, enet = 0;
     RleScratch esc{};
+    std::vector<uint64_t> ptab;   // host copy of the page table
     uint64_t body_tot = 0;
     // BYTE_ARRAY dictionaries are keyed by a 64-bit hash and verified byte-for-byte; a
     // verified collision re-runs the chunk phase with byte comparisons (exact_strings).
@@ -603,7 +627,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     for (bool exact = false;;) {
         a.exact_strings = exact ? 1 : 0;
         CK(xh2d(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), s));
-        CK(hipMemsetAsync(d_collision.p, 0, 8, s));
+        CK(hipMemsetAsync(d_coll, 0, 8, s));
         if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), s));
         if (v2_ && !dj.empty()) CK(xh2d(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), s));
         // ------------------------------------------------------------ K6 + K2
@@ -630,11 +654,13 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         }
         CK(hipEventRecord(ev_[4], s));
         // ------------------------------------------------------------ layout
-        launch_layout(a, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), s);
-        uint32_t flags[2] = {0, 0};
-        CK(xd2h(&body_tot, d_tot.p, 8, s));
-        CK(xd2h(flags, d_collision.p, 8, s));
+        launch_layout(a, d_jobs.as<RleJob>(), d_poff, d_plen, pt, s);
+        ptab.resize(4 + 5 * P2);
+        CK(xd2h(ptab.data(), pt, (4 + (v2_ ? 3 : 2) * P2) * 8, s));   // totals, flags, offsets, lengths (v2: prefixes)
         CK(xsync(s));
+        body_tot = ptab[0];
+        uint32_t flags[2];
+        memcpy(flags, &ptab[2], 8);
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
         if (flags[1]) {
             assign_tables(false);
@@ -661,11 +687,10 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     CK(hipGetLastError());
     CK(hipEventRecord(ev_[5], s));
-    std::vector<uint64_t> poff(2 * nch), plen(2 * nch), ppre(2 * nch, 0), pcoff, pclen;
-    CK(xd2h(poff.data(), d_page_off.p, 2 * nch * 8, s));
-    CK(xd2h(plen.data(), d_page_len.p, 2 * nch * 8, s));
-    if (v2_) CK(xd2h(ppre.data(), d_page_pre.p, 2 * nch * 8, s));
-    CK(xsync(s));
+    // (no sync here: the page offsets and lengths came back with the layout)
+    std::vector<uint64_t> poff(ptab.begin() + 4, ptab.begin() + 4 + P2), plen(ptab.begin() + 4 + P2, ptab.begin() + 4 + 2 * P2);
+    std::vector<uint64_t> ppre(P2, 0), pcoff, pclen;
+    if (v2_) ppre.assign(ptab.begin() + 4 + 2 * P2, ptab.begin() + 4 + 3 * P2);
     // ---------------------------------------------------------------- K7
     if (props.codec == KPW_SNAPPY) {
         std::vector<uint32_t> fpage, fidx, pfrag0(2 * nch);
@@ -675,23 +700,16 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             for (uint64_t k = 0; k < nf; k++) { fpage.push_back((uint32_t)p); fidx.push_back((uint32_t)k); }
         }
         const uint32_t nf = (uint32_t)fpage.size();
-        ENS(d_frag_page, std::max<uint32_t>(1, nf) * 4); ENS(d_frag_idx, std::max<uint32_t>(1, nf) * 4);
         ENS(d_frag_out, (uint64_t)std::max<uint32_t>(1, nf) * SNAPPY_FRAG_CAP); ENS(d_frag_len, std::max<uint32_t>(1, nf) * 4);
-        ENS(d_frag_coff, std::max<uint32_t>(1, nf) * 8); ENS(d_page_coff, 2 * nch * 8); ENS(d_page_clen, 2 * nch * 8);
-        ENS(d_page_frag0, 2 * nch * 4);
+        ENS(d_frag_coff, std::max<uint32_t>(1, nf) * 8);
         ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * nch * 8 + 64 + 4096);
-        if (nf) {
-            CK(xh2d(d_frag_page.p, fpage.data(), nf * 4, s));
-            CK(xh2d(d_frag_idx.p, fidx.data(), nf * 4, s));
-        }
-        CK(xh2d(d_page_frag0.p, pfrag0.data(), 2 * nch * 4, s));
         SnappyArgs sa{};
-        sa.in = d_body.as<uint8_t>(); sa.page_off = d_page_off.as<uint64_t>(); sa.page_len = d_page_len.as<uint64_t>();
-        sa.npages = 2 * nch; sa.nfrags = nf; sa.frag_page = d_frag_page.as<uint32_t>(); sa.frag_idx = d_frag_idx.as<uint32_t>();
+        sa.in = d_body.as<uint8_t>(); sa.page_off = d_poff; sa.page_len = d_plen;
+        sa.npages = 2 * nch; sa.nfrags = nf;
         sa.frag_out = d_frag_out.as<uint8_t>(); sa.frag_len = d_frag_len.as<uint32_t>();
-        sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
-        sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
-        sa.page_pre = v2_ ? d_page_pre.as<uint64_t>() : nullptr;
+        sa.page_coff = d_pcoff; sa.page_clen = d_pclen;
+        sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = pt + 1;
+        sa.page_pre = v2_ ? d_ppre : nullptr;
         // Longest-first dispatch.  K7's waves are latency-bound and a fragment's time depends on
         // its data (one PLAIN int64 fragment of slowly-growing timestamps: ~9 ms; an
         // incompressible one: ~50 us), so the kernel's tail is set by the long fragments
@@ -709,6 +727,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         };
         bool have_cost = false;
         for (double c : sn_cost_) have_cost |= c > 0;
+        sn_order_.clear();
         if (nf) {
             ENS(d_sprof, (uint64_t)nf * 16);
             sa.ftime = d_sprof.as<uint64_t>();
@@ -718,31 +737,34 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
                 for (uint32_t f = 0; f < nf; f++) ranked[f] = {-cost_of(f), f};
                 std::sort(ranked.begin(), ranked.end());
                 for (uint32_t f = 0; f < nf; f++) sn_order_[f] = ranked[f].second;
-                ENS(d_sorder, (uint64_t)nf * 4);
-                CK(xh2d(d_sorder.p, sn_order_.data(), (size_t)nf * 4, s));
-                sa.order = d_sorder.as<uint32_t>();
             }
         }
+        // fragment -> page, index in page, first fragment per page, dispatch order: one copy
+        std::vector<uint8_t *> kt;
+        if (int st = upload_parts(d_ktab, {{fpage.data(), (size_t)nf * 4}, {fidx.data(), (size_t)nf * 4},
+                                           {pfrag0.data(), (size_t)2 * nch * 4}, {sn_order_.data(), sn_order_.size() * 4}}, kt))
+            return st;
+        sa.frag_page = (uint32_t *)kt[0]; sa.frag_idx = (uint32_t *)kt[1];
+        const uint32_t *page_frag0 = (const uint32_t *)kt[2];
+        if (!sn_order_.empty()) sa.order = (uint32_t *)kt[3];
         if (seg_args(sa)) return KPW_ERR_NOMEM;
         // K7 window (stage_ms[9]): every kernel from the first fragment kernel to the compressed
         // pages in place (k_snappy_v, k_snappy_s_rest, k_snappy_seg, k_snappy_v, k_snappy_s_rest,
         // k_snappy_page_sizes, k_snappy_copy; one 4-byte fill of the fragment counter)
         CK(hipEventRecord(kev_[2], s));
         launch_snappy(sa, s);
-        launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), s);
+        launch_snappy_finish(sa, page_frag0, s);
         CK(hipEventRecord(kev_[3], s));
         if (nf) {
             sn_ft_.resize(2 * (size_t)nf);
             CK(xd2h(sn_ft_.data(), d_sprof.p, sn_ft_.size() * 8, s));
         }
         CK(hipGetLastError());
-        pcoff.resize(2 * nch);
-        pclen.resize(2 * nch);
-        uint64_t ctot = 0;
-        CK(xd2h(pcoff.data(), d_page_coff.p, 2 * nch * 8, s));
-        CK(xd2h(pclen.data(), d_page_clen.p, 2 * nch * 8, s));
-        CK(xd2h(&ctot, d_tot.as<uint64_t>() + 1, 8, s));
+        CK(xd2h(ptab.data(), pt, (4 + 5 * P2) * 8, s));   // compressed total, offsets, lengths
         CK(xsync(s));
+        const uint64_t ctot = ptab[1];
+        pcoff.assign(ptab.begin() + 4 + 3 * P2, ptab.begin() + 4 + 4 * P2);
+        pclen.assign(ptab.begin() + 4 + 4 * P2, ptab.begin() + 4 + 5 * P2);
         if (nf) {
             // per-kind mean duration (fragments handed to k_snappy_s_rest count their short
             // k_snappy_v attempt); KPW_SNAPPY_PROFILE=<file> also dumps the raw records
@@ -946,7 +968,10 @@ int Engine::seg_args(SnappyArgs &sa)
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     ENS(d_seg_scratch, snappy_seg_scratch_bytes((uint32_t)cus));
+    void *const old_counter = d_seg_counter.p;
     ENS(d_seg_counter, 64);
+    if (d_seg_counter.p != old_counter && hipMemsetAsync(d_seg_counter.p, 0, 64, stream) != hipSuccess)   // once
+        return fail(KPW_ERR_DEVICE, "fragment counter clear failed");
     sa.seg_scratch = d_seg_scratch.as<uint8_t>();
     sa.seg_counter = d_seg_counter.as<uint32_t>();
     {   // KPW_SEG_RESERVE_CUS: CUs kept out of the persistent segment kernel's grid (its workgroup

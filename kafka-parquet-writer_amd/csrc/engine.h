@@ -148,14 +148,14 @@ private:
     // planning
     DevBuf d_ev, d_E, d_gend, d_rg_start, d_rg_end, d_plan_out;
     // rle scratch (shared by planning and encoding)
-    DevBuf r_ptile_job, r_last, r_prev, r_lrcnt, r_lroff, r_etile_job, r_lra, r_lrb, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;
+    DevBuf r_last, r_prev, r_lrcnt, r_lroff, r_lra, r_lrb, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;   // d_jobs: jobs + tile maps
     // chunks
-    DevBuf d_chunks, d_ctile_chunk, d_ctile_first, d_ctile_count, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
-        d_tile_cnt, d_tile_sz, d_ht, d_ids, d_ent_rec, d_ent_boff, d_page_off, d_page_len, d_tot,
+    DevBuf d_chunks, d_ctile, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
+        d_tile_cnt, d_tile_sz, d_ht, d_ids, d_ent_rec, d_ent_boff, d_ptab,   // d_ptab: page table (engine.cpp)
         d_body;
     // snappy
-    DevBuf d_frag_page, d_frag_idx, d_frag_out, d_frag_len, d_page_coff, d_page_clen, d_frag_coff, d_comp, d_page_frag0;
-    DevBuf d_smeta, d_sblob, d_collision, d_dict_order, d_sprof, d_sorder;
+    DevBuf d_ktab, d_frag_out, d_frag_len, d_frag_coff, d_comp;   // d_ktab: K7's host tables
+    DevBuf d_smeta, d_sblob, d_sprof;
     DevBuf d_seg_scratch, d_seg_counter;   // k_snappy_seg (one scratch block per CU)
     int seg_args(SnappyArgs &sa);          // fills sa.seg_* (KPW_SNAPPY_SEG=0: sequential kernels only)
     DevBuf d_body_alt, d_comp_alt;
@@ -168,7 +168,7 @@ private:
     std::vector<DevBuf> col_cbits;
     std::vector<uint64_t *> cbits_;    // per BOOLEAN column (bool_idx_ order): its value stream bits (this encode)
     DevBuf d_cbits_ptr, d_streams, d_djobs, d_blk_job, d_blk_min, d_blk_w, d_blk_sz, d_blk_off, d_btot, d_dense, d_pre, d_sfx,
-        d_tile_sfx, d_tile_sfx_off, d_chunk_sfx, d_page_pre;
+        d_tile_sfx, d_tile_sfx_off, d_chunk_sfx;
     hipEvent_t ev_[9] = {};
     hipEvent_t kev_[4] = {};
     std::vector<uint32_t> opt_idx_, bool_idx_;
@@ -196,11 +196,15 @@ private:
                     const std::vector<uint32_t> *k7_from = nullptr);
     int grow_keep(DevBuf &b, size_t bytes, size_t keep);
     // the engine's small host <-> device transfers (engine.cpp: why they stay pageable copies)
+    // Several host tables in one H2D copy into `buf` (256-byte aligned parts): their device
+    // addresses in `dev`.  One copy instead of one per table (each is a blit kernel).
+    struct HostPart { const void *p; size_t bytes; };
+    int upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::vector<uint8_t *> &dev);
     hipError_t xh2d(void *dst, const void *src, size_t bytes, hipStream_t s);
     hipError_t xd2h(void *dst, const void *src, size_t bytes, hipStream_t s);
     hipError_t xsync(hipStream_t s);
     std::vector<DevBuf> mp_sp;
-    DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_pboff, mp_flag, mp_dch, mp_dtile_chunk, mp_dtile_first, mp_dtile_count, mp_dtile_raw,
+    DevBuf mp_ncuts, mp_cutpos, mp_pbytes, mp_pboff, mp_flag, mp_dch, mp_dtile_raw,
         mp_dtile_smin, mp_dtile_smax, mp_dtile_cnt, mp_dtile_sz, mp_ssz, mp_spp, mp_cstream, mp_bstream, mp_acc;
     uint8_t *pages_dev_ = nullptr;
     uint64_t pages_len_ = 0;

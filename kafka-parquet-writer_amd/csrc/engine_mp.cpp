@@ -222,16 +222,24 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         }
     }
     // page descriptors use the engine's chunk buffers; dictionary descriptors their own
-    ENS(d_chunks, npg * sizeof(ChunkDesc)); ENS(d_ctile_chunk, npt * 4); ENS(d_ctile_first, npg * 4); ENS(d_ctile_count, npg * 4);
+    ENS(d_chunks, npg * sizeof(ChunkDesc));
     ENS(d_tile_raw, npt * 8); ENS(d_tile_raw_off, npt * 8); ENS(d_tile_smin, npt * 8); ENS(d_tile_smax, npt * 8);
     ENS(d_tile_cnt, npt * 4); ENS(d_tile_sz, npt * 8);
-    ENS(mp_dch, nc * sizeof(ChunkDesc)); ENS(mp_dtile_chunk, ndt * 4); ENS(mp_dtile_first, nc * 4); ENS(mp_dtile_count, nc * 4);
+    ENS(mp_dch, nc * sizeof(ChunkDesc));
     ENS(mp_dtile_raw, ndt * 8); ENS(mp_dtile_smin, ndt * 8); ENS(mp_dtile_smax, ndt * 8); ENS(mp_dtile_cnt, ndt * 4);
-    ENS(mp_dtile_sz, ndt * 8); ENS(d_dict_order, std::max<size_t>(1, dorder.size()) * 4);
+    ENS(mp_dtile_sz, ndt * 8);
     ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
     ENS(d_ids, std::max<uint64_t>(1, ids_off) * 4); ENS(d_ent_rec, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
-    ENS(d_page_off, 2 * npg * 8); ENS(d_page_len, 2 * npg * 8); ENS(d_page_pre, 2 * npg * 8); ENS(d_tot, 64); ENS(d_collision, 64);
+    // page table as in Engine::encode: totals, collision flags, then per page slot its offset,
+    // length, level prefix, compressed offset and length
+    const size_t P2 = 2 * (size_t)npg;
+    ENS(d_ptab, (4 + 5 * P2) * 8);
+    uint64_t *const pt = d_ptab.as<uint64_t>();
+    uint64_t *const d_poff = pt + 4, *const d_plen = d_poff + P2, *const d_ppre = d_plen + P2;
+    uint64_t *const d_pcoff = d_ppre + P2, *const d_pclen = d_pcoff + P2;
+    uint32_t *const d_coll = (uint32_t *)(pt + 2);
+    std::vector<uint64_t> ptab(4 + 5 * P2);
     for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
     DeltaArgs dla{};
     if (v2_) {
@@ -253,37 +261,35 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         dla.blk_sz = d_blk_sz.as<uint64_t>(); dla.blk_off = d_blk_off.as<uint64_t>(); dla.btot = d_btot.as<uint64_t>();
         dla.seg = &seg_;
     }
-    CK(xh2d(d_ctile_chunk.p, ptj.data(), npt * 4, st));
-    CK(xh2d(d_ctile_first.p, pfirst.data(), npg * 4, st));
-    CK(xh2d(d_ctile_count.p, pcount.data(), npg * 4, st));
-    CK(xh2d(mp_dtile_chunk.p, dtj.data(), ndt * 4, st));
-    CK(xh2d(mp_dtile_first.p, dfirst.data(), nc * 4, st));
-    CK(xh2d(mp_dtile_count.p, dcount.data(), nc * 4, st));
-    if (!dorder.empty()) CK(xh2d(d_dict_order.p, dorder.data(), dorder.size() * 4, st));
+    std::vector<uint8_t *> tp;   // page tiles, dictionary tiles and the insertion order in one copy
+    if (int rs = upload_parts(d_ctile, {{ptj.data(), (size_t)npt * 4}, {pfirst.data(), (size_t)npg * 4}, {pcount.data(), (size_t)npg * 4},
+                                        {dtj.data(), (size_t)ndt * 4}, {dfirst.data(), (size_t)nc * 4}, {dcount.data(), (size_t)nc * 4},
+                                        {dorder.data(), dorder.size() * 4}}, tp))
+        return rs;
 
     ChunkArgs ap{};
     ap.ch = d_chunks.as<ChunkDesc>(); ap.nchunks = npg; ap.nctiles = npt; ap.cols = d_cols.as<DevCol>(); ap.data = d_data;
-    ap.ctile_chunk = d_ctile_chunk.as<uint32_t>(); ap.ctile_first = d_ctile_first.as<uint32_t>();
-    ap.ctile_count = d_ctile_count.as<uint32_t>(); ap.tile_raw = d_tile_raw.as<uint64_t>();
+    ap.ctile_chunk = (uint32_t *)tp[0]; ap.ctile_first = (uint32_t *)tp[1];
+    ap.ctile_count = (uint32_t *)tp[2]; ap.tile_raw = d_tile_raw.as<uint64_t>();
     ap.tile_raw_off = d_tile_raw_off.as<uint64_t>(); ap.tile_smin = d_tile_smin.as<uint64_t>();
     ap.tile_smax = d_tile_smax.as<uint64_t>(); ap.tile_cnt = d_tile_cnt.as<uint32_t>(); ap.tile_sz = d_tile_sz.as<uint64_t>();
     ap.ht = d_ht.as<HtSlot>();
     ap.ids = d_ids.as<uint32_t>(); ap.ent_rec = d_ent_rec.as<uint64_t>(); ap.ent_boff = d_ent_boff.as<uint64_t>();
     ap.max_dict_bytes = (uint32_t)props.dictionary_page_size;
-    ap.data_end = d_off + n; ap.collision = d_collision.as<uint32_t>();
-    ap.page_pre = d_page_pre.as<uint64_t>();
+    ap.data_end = d_off + n; ap.collision = d_coll;
+    ap.page_pre = d_ppre;
     ap.mp = 1;
     ap.seg = &seg_;
     ap.v2 = v2_ ? 1 : 0;
     if (v2_) { ap.djobs = dla.jobs; ap.djobs_w = dla.jobs; ap.chunk_sfx = d_chunk_sfx.as<uint64_t>(); }
     ChunkArgs ad = ap;
     ad.ch = mp_dch.as<ChunkDesc>(); ad.nchunks = nc; ad.nctiles = ndt;
-    ad.ctile_chunk = mp_dtile_chunk.as<uint32_t>(); ad.ctile_first = mp_dtile_first.as<uint32_t>();
-    ad.ctile_count = mp_dtile_count.as<uint32_t>(); ad.tile_raw = mp_dtile_raw.as<uint64_t>(); ad.tile_raw_off = nullptr;
+    ad.ctile_chunk = (uint32_t *)tp[3]; ad.ctile_first = (uint32_t *)tp[4];
+    ad.ctile_count = (uint32_t *)tp[5]; ad.tile_raw = mp_dtile_raw.as<uint64_t>(); ad.tile_raw_off = nullptr;
     ad.tile_smin = mp_dtile_smin.as<uint64_t>(); ad.tile_smax = mp_dtile_smax.as<uint64_t>();
     ad.tile_cnt = mp_dtile_cnt.as<uint32_t>(); ad.tile_sz = mp_dtile_sz.as<uint64_t>();
     ad.max_dict_bytes = 0xFFFFFFFFu;   // the dictPageSize limit is applied per page (k_mp_dict_decide)
-    ad.dict_order = d_dict_order.as<uint32_t>(); ad.ndict_tiles = (uint32_t)dorder.size();
+    ad.dict_order = (uint32_t *)tp[6]; ad.ndict_tiles = (uint32_t)dorder.size();
     ad.mp_round_tiles = kMpRoundTiles; ad.mp_nrounds = (uint32_t)rlen.size(); ad.mp_round_len = rlen.data();
     ad.mp_dict_limit = (uint32_t)props.dictionary_page_size;
 
@@ -294,7 +300,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         ap.exact_strings = ad.exact_strings = attempt;
         CK(xh2d(d_chunks.p, pg.data(), npg * sizeof(ChunkDesc), st));
         CK(xh2d(mp_dch.p, dch.data(), nc * sizeof(ChunkDesc), st));
-        CK(hipMemsetAsync(d_collision.p, 0, 4, st));
+        CK(hipMemsetAsync(d_coll, 0, 4, st));
         if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), st));
         if (v2_ && !dj.empty()) CK(xh2d(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), st));
         launch_chunk_stats(ap, st);                          // K6 per page (+ nn, raw bytes)
@@ -317,13 +323,13 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
                             d_tile_sfx_off.as<uint64_t>(), d_chunk_sfx.as<uint64_t>(), st);
             launch_delta_structure(dla, st);
         }
-        launch_layout(ap, d_jobs.as<RleJob>(), d_page_off.as<uint64_t>(), d_page_len.as<uint64_t>(), d_tot.as<uint64_t>(), st);
+        launch_layout(ap, d_jobs.as<RleJob>(), d_poff, d_plen, pt, st);
         CK(hipGetLastError());
-        uint32_t coll = 0;
-        CK(xd2h(&body_tot, d_tot.p, 8, st));
-        CK(xd2h(&coll, d_collision.p, 4, st));
+        CK(xd2h(ptab.data(), pt, (4 + (v2_ ? 3 : 2) * P2) * 8, st));   // totals, flags, offsets, lengths (v2: prefixes)
         CK(xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st));
         CK(xsync(st));
+        body_tot = ptab[0];
+        const uint32_t coll = (uint32_t)ptab[2];
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
         for (int c = 0; c < nc; c++)
             if (dch[c].is_dict && dch[c].overflow) return fail(KPW_ERR_DEVICE, "multi-page dictionary table overflow");
@@ -349,11 +355,10 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         launch_dba_suffixes(ap, d_pre.as<uint32_t>(), dla.jobs, d_tile_sfx_off.as<uint64_t>(), d_body.as<uint8_t>(), st);
     }
     CK(hipGetLastError());
-    std::vector<uint64_t> poff(2 * npg), plen(2 * npg), pcoff(2 * npg), pclen(2 * npg), ppre(2 * npg, 0);
-    CK(xd2h(poff.data(), d_page_off.p, 2 * npg * 8, st));
-    CK(xd2h(plen.data(), d_page_len.p, 2 * npg * 8, st));
-    if (v2_) CK(xd2h(ppre.data(), d_page_pre.p, 2 * npg * 8, st));
-    CK(xsync(st));
+    // (no sync here: the page offsets and lengths came back with the layout)
+    std::vector<uint64_t> poff(ptab.begin() + 4, ptab.begin() + 4 + P2), plen(ptab.begin() + 4 + P2, ptab.begin() + 4 + 2 * P2);
+    std::vector<uint64_t> pcoff(P2), pclen(P2), ppre(P2, 0);
+    if (v2_) ppre.assign(ptab.begin() + 4 + 2 * P2, ptab.begin() + 4 + 3 * P2);
     // ---------------------------------------------------------------- K7
     if (props.codec == KPW_SNAPPY) {
         std::vector<uint32_t> fpage, fidx, pfrag0(2 * npg);
@@ -364,32 +369,29 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             for (uint64_t k = 0; k < nf; k++) { fpage.push_back((uint32_t)p); fidx.push_back((uint32_t)k); }
         }
         const uint32_t nf = (uint32_t)fpage.size();
-        ENS(d_frag_page, std::max<uint32_t>(1, nf) * 4); ENS(d_frag_idx, std::max<uint32_t>(1, nf) * 4);
         ENS(d_frag_out, (uint64_t)std::max<uint32_t>(1, nf) * SNAPPY_FRAG_CAP); ENS(d_frag_len, std::max<uint32_t>(1, nf) * 4);
-        ENS(d_frag_coff, std::max<uint32_t>(1, nf) * 8); ENS(d_page_coff, 2 * npg * 8); ENS(d_page_clen, 2 * npg * 8);
-        ENS(d_page_frag0, 2 * npg * 4);
+        ENS(d_frag_coff, std::max<uint32_t>(1, nf) * 8);
         ENS(d_comp, body_tot + (uint64_t)nf * 64 + 2 * npg * 8 + 64 + 4096);
-        if (nf) {
-            CK(xh2d(d_frag_page.p, fpage.data(), nf * 4, st));
-            CK(xh2d(d_frag_idx.p, fidx.data(), nf * 4, st));
-        }
-        CK(xh2d(d_page_frag0.p, pfrag0.data(), 2 * npg * 4, st));
+        std::vector<uint8_t *> kt;   // fragment -> page, index in page, first fragment per page: one copy
+        if (int rs = upload_parts(d_ktab, {{fpage.data(), (size_t)nf * 4}, {fidx.data(), (size_t)nf * 4}, {pfrag0.data(), (size_t)2 * npg * 4}},
+                                  kt))
+            return rs;
         SnappyArgs sa{};
-        sa.in = d_body.as<uint8_t>(); sa.page_off = d_page_off.as<uint64_t>(); sa.page_len = d_page_len.as<uint64_t>();
-        sa.npages = 2 * npg; sa.nfrags = nf; sa.frag_page = d_frag_page.as<uint32_t>(); sa.frag_idx = d_frag_idx.as<uint32_t>();
+        sa.in = d_body.as<uint8_t>(); sa.page_off = d_poff; sa.page_len = d_plen;
+        sa.npages = 2 * npg; sa.nfrags = nf; sa.frag_page = (uint32_t *)kt[0]; sa.frag_idx = (uint32_t *)kt[1];
         sa.frag_out = d_frag_out.as<uint8_t>(); sa.frag_len = d_frag_len.as<uint32_t>();
-        sa.page_coff = d_page_coff.as<uint64_t>(); sa.page_clen = d_page_clen.as<uint64_t>();
-        sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = d_tot.as<uint64_t>() + 1;
-        sa.page_pre = v2_ ? d_page_pre.as<uint64_t>() : nullptr;   // v2: levels in front, uncompressed
+        sa.page_coff = d_pcoff; sa.page_clen = d_pclen;
+        sa.frag_coff = d_frag_coff.as<uint64_t>(); sa.out = d_comp.as<uint8_t>(); sa.tot = pt + 1;
+        sa.page_pre = v2_ ? d_ppre : nullptr;   // v2: levels in front, uncompressed
         if (seg_args(sa)) return KPW_ERR_NOMEM;
         launch_snappy(sa, st);
-        launch_snappy_finish(sa, d_page_frag0.as<uint32_t>(), st);
+        launch_snappy_finish(sa, (const uint32_t *)kt[2], st);
         CK(hipGetLastError());
-        uint64_t ctot = 0;
-        CK(xd2h(pcoff.data(), d_page_coff.p, 2 * npg * 8, st));
-        CK(xd2h(pclen.data(), d_page_clen.p, 2 * npg * 8, st));
-        CK(xd2h(&ctot, d_tot.as<uint64_t>() + 1, 8, st));
+        CK(xd2h(ptab.data(), pt, (4 + 5 * P2) * 8, st));   // compressed total, offsets, lengths
         CK(xsync(st));
+        const uint64_t ctot = ptab[1];
+        pcoff.assign(ptab.begin() + 4 + 3 * P2, ptab.begin() + 4 + 4 * P2);
+        pclen.assign(ptab.begin() + 4 + 4 * P2, ptab.begin() + 4 + 5 * P2);
         pages_dev_ = d_comp.as<uint8_t>();
         pages_len_ = ctot;
     } else {   // uncompressed: a (v2) page body starts at its level prefix

@@ -695,8 +695,7 @@ void launch_snappy(const SnappyArgs &a, hipStream_t s)
             r.s_budget = sbudget;
             hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, s, r);
         }
-        (void)hipMemsetAsync(a.seg_counter, 0, 4, s);
-        SnappyArgs g = a;
+        SnappyArgs g = a;   // (the fragment counter is 0: zeroed once, left at 0 by every launch)
         g.order = nullptr;
         g.seg_only_marked = vbudget ? 1 : 0;
         hipLaunchKernelGGL(k_snappy_seg, dim3(a.seg_grid), dim3(1024), 0, s, g);

@@ -420,7 +420,14 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
 #define PMARK(i) do { if (pf) { const uint64_t now_ = clock64(); prof[i] += now_ - plast; plast = now_; } if (a.seg_dbg && t == 0) a.seg_dbg[blockIdx.x * 4 + 2] = (i); } while (0)
 
     for (;;) {
-        if (t == 0) S.frag = (int)atomicAdd(a.seg_counter, 1u);
+        if (t == 0) {
+            // every workgroup draws once past the last fragment, so the draw numbered
+            // nfrags + grid - 1 is the launch's last: it leaves the counter at 0 for the next
+            // launch (no fill before each launch)
+            const uint32_t d = atomicAdd(a.seg_counter, 1u);
+            if (d == a.nfrags + gridDim.x - 1) atomicExch(a.seg_counter, 0u);
+            S.frag = (int)d;
+        }
         __syncthreads();
         const uint32_t fslot = (uint32_t)S.frag;
         __syncthreads();
