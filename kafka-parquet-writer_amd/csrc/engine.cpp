@@ -308,13 +308,15 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             d.vbits = col_vbits[c].as<uint64_t>();
         }
     }
-    ENS(d_cols, nc * sizeof(DevCol));
-    CK(xh2d(d_cols.p, hc.data(), nc * sizeof(DevCol), s));
-    ENS(d_raw, n * 4); ENS(d_err, 64);
-    CK(hipMemsetAsync(d_err.p, 0xFF, 8, s));
+    // column descriptors and K1's first-invalid-record word (all ones: none) in one copy
+    static const uint64_t kNoErr = ~0ull;
+    std::vector<uint8_t *> cp;
+    if (int st = upload_parts(d_cols, {{hc.data(), nc * sizeof(DevCol)}, {&kNoErr, 8}}, cp)) return st;
+    unsigned long long *const d_err = (unsigned long long *)cp[1];
+    ENS(d_raw, n * 4);
     DecodeArgs da;
     da.data = d_data; da.off = d_off; da.n = n; da.cols = d_cols.as<DevCol>(); da.ncols = nc; da.pad = 0;
-    da.fmap = d_fmap.as<int16_t>(); da.raw = d_raw.as<uint32_t>(); da.err_min = d_err.as<unsigned long long>();
+    da.fmap = d_fmap.as<int16_t>(); da.raw = d_raw.as<uint32_t>(); da.err_min = d_err;
     da.nwords = nwords;
     CK(hipEventRecord(kev_[0], s));
     launch_decode(da, s);
@@ -322,7 +324,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     CK(hipGetLastError());
     CK(hipEventRecord(ev_[1], s));
     uint64_t err_idx = ~0ull;
-    CK(xd2h(&err_idx, d_err.p, 8, s));
+    CK(xd2h(&err_idx, d_err, 8, s));
     CK(xsync(s));
     const uint64_t ne = std::min<uint64_t>(n, err_idx);
     out.invalid_record = err_idx < n ? (int64_t)err_idx : -1;
@@ -408,31 +410,38 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     if (mp_) return encode_mp(d_data, d_off, n, ne, final_flush, next_rg_size, hc, nwords, out);
     // ---------------------------------------------------------------- A9 plan
+    // plan buffer (int64): [out 4 | pad 4 | (start, end) per row group]: the result and the first
+    // kPlanHead row groups come back in one copy
+    constexpr int32_t kPlanHead = 64;
     const int32_t max_rgs = (int32_t)(ne / 100 + 4);
-    ENS(d_rg_start, max_rgs * 8); ENS(d_rg_end, max_rgs * 8); ENS(d_plan_out, 64);
+    ENS(d_plan, (8 + 2 * (size_t)max_rgs) * 8);
     PlanArgs pa{};
     pa.n = ne; pa.final_flush = final_flush ? 1 : 0; pa.ncols = nc; pa.next_rg_size = next_rg_size;
     pa.P = d_P.as<uint64_t>(); pa.cols = d_cols.as<DevCol>();
     pa.streams = d_streams.as<PlanStream>(); pa.nstreams = (int32_t)nstreams;
     pa.nbool = v2_ ? 0 : (int32_t)nbool; pa.bool_cols = d_bool.as<uint32_t>();
     pa.E = nstreams ? d_E.as<uint32_t>() : nullptr; pa.gend = nstreams ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
-    pa.rg_start = d_rg_start.as<int64_t>(); pa.rg_end = d_rg_end.as<int64_t>(); pa.max_rgs = max_rgs;
+    pa.rg = d_plan.as<int64_t>() + 8; pa.max_rgs = max_rgs;
     pa.max_cuts = max_cuts;
-    pa.out = d_plan_out.as<int64_t>();
+    pa.out = d_plan.as<int64_t>();
     launch_plan(pa, s);
     CK(hipGetLastError());
-    int64_t po[4];
-    CK(xd2h(po, d_plan_out.p, 32, s));
+    const int32_t head = std::min<int32_t>(max_rgs, kPlanHead);
+    std::vector<int64_t> pl(8 + 2 * (size_t)head);
+    CK(xd2h(pl.data(), d_plan.p, pl.size() * 8, s));
     CK(xsync(s));
     CK(hipEventRecord(ev_[2], s));
+    const int64_t *po = pl.data();
     const int nrg = (int)po[0];
     if (po[3]) return fail(KPW_ERR_DEVICE, "planner row-group table overflow");
-    std::vector<int64_t> rs(nrg), re(nrg);
-    if (nrg) {
-        CK(xd2h(rs.data(), d_rg_start.p, nrg * 8, s));
-        CK(xd2h(re.data(), d_rg_end.p, nrg * 8, s));
+    if (nrg > head) {   // more row groups than the first copy held
+        pl.resize(8 + 2 * (size_t)nrg);
+        CK(xd2h(pl.data() + 8 + 2 * head, d_plan.as<int64_t>() + 8 + 2 * head, 2 * (size_t)(nrg - head) * 8, s));
         CK(xsync(s));
+        po = pl.data();
     }
+    std::vector<int64_t> rs(nrg), re(nrg);
+    for (int r = 0; r < nrg; r++) { rs[r] = pl[8 + 2 * r]; re[r] = pl[8 + 2 * r + 1]; }
     out.records_consumed = po[1];
     out.open_records = (int64_t)ne - po[1];
     out.open_buffered = po[2];
@@ -559,7 +568,9 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             for (int ci = 0; ci < nch; ci++)
                 if (ch[ci].is_dict && k < ccount[ci]) dorder.push_back(cfirst[ci] + k);
     }
-    ENS(d_chunks, nch * sizeof(ChunkDesc));
+    // chunk descriptors, then 4 words of string-statistics metadata per chunk (one readback)
+    static_assert(sizeof(ChunkDesc) % 8 == 0, "metadata words follow the descriptors");
+    ENS(d_chunks, nch * (sizeof(ChunkDesc) + 32));
     ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
     ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8);
     ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
@@ -805,13 +816,18 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     CK(hipEventRecord(ev_[6], s));
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
     // ---------------------------------------------------------------- metadata
-    CK(xd2h(ch.data(), d_chunks.p, nch * sizeof(ChunkDesc), s));
     // binary min/max bytes: gather (offset, len) pairs, then the bytes into one blob
     std::vector<uint64_t> smeta(4 * nch, 0);
-    ENS(d_smeta, 4 * nch * 8);
-    launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(), nullptr, s);
-    CK(xd2h(smeta.data(), d_smeta.p, 4 * nch * 8, s));
-    CK(xsync(s));
+    uint64_t *const d_smeta = (uint64_t *)(d_chunks.as<ChunkDesc>() + nch);
+    launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta, nullptr, s);
+    {   // descriptors + metadata in one copy
+        static thread_local std::vector<uint8_t> md;
+        md.resize(nch * (sizeof(ChunkDesc) + 32));
+        CK(xd2h(md.data(), d_chunks.p, md.size(), s));
+        CK(xsync(s));
+        memcpy(ch.data(), md.data(), nch * sizeof(ChunkDesc));
+        memcpy(smeta.data(), md.data() + nch * sizeof(ChunkDesc), nch * 32);
+    }
     {   // next encode's table hints: the most entries of each column's chunks, none after a fallback
         std::vector<uint32_t> most(nc, 0);
         std::vector<char> seen(nc, 0), fell(nc, 0);
@@ -836,7 +852,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         if (blob_len) {
             std::vector<uint8_t> blob(blob_len);
             ENS(d_sblob, blob_len);
-            launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(),
+            launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta,
                                 d_sblob.as<uint8_t>(), s);
             CK(xd2h(blob.data(), d_sblob.p, blob_len, s));
             CK(xsync(s));

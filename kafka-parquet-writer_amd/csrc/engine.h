@@ -144,9 +144,9 @@ private:
     // decode buffers
     std::vector<DevBuf> col_vals, col_shash, col_spfx, col_soff, col_slen, col_pres, col_vbits, col_pcnt;
     std::vector<uint32_t> dict_hint_;  // per column: most dictionary entries in the previous encode (0: none)
-    DevBuf d_cols, d_fmap, d_raw, d_P, d_err, d_opt, d_bool;
+    DevBuf d_cols, d_fmap, d_raw, d_P, d_opt, d_bool;   // d_cols: descriptors + error word
     // planning
-    DevBuf d_ev, d_E, d_gend, d_rg_start, d_rg_end, d_plan_out;
+    DevBuf d_ev, d_E, d_gend, d_plan;
     // rle scratch (shared by planning and encoding)
     DevBuf r_last, r_prev, r_lrcnt, r_lroff, r_lra, r_lrb, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;   // d_jobs: jobs + tile maps
     // chunks
@@ -155,7 +155,7 @@ private:
         d_body;
     // snappy
     DevBuf d_ktab, d_frag_out, d_frag_len, d_frag_coff, d_comp;   // d_ktab: K7's host tables
-    DevBuf d_smeta, d_sblob, d_sprof;
+    DevBuf d_sblob, d_sprof;
     DevBuf d_seg_scratch, d_seg_counter;   // k_snappy_seg (one scratch block per CU)
     int seg_args(SnappyArgs &sa);          // fills sa.seg_* (KPW_SNAPPY_SEG=0: sequential kernels only)
     DevBuf d_body_alt, d_comp_alt;

@@ -222,7 +222,9 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         }
     }
     // page descriptors use the engine's chunk buffers; dictionary descriptors their own
-    ENS(d_chunks, npg * sizeof(ChunkDesc));
+    // chunk descriptors, then 4 words of string-statistics metadata per chunk (one readback)
+    static_assert(sizeof(ChunkDesc) % 8 == 0, "metadata words follow the descriptors");
+    ENS(d_chunks, npg * (sizeof(ChunkDesc) + 32));
     ENS(d_tile_raw, npt * 8); ENS(d_tile_raw_off, npt * 8); ENS(d_tile_smin, npt * 8); ENS(d_tile_smax, npt * 8);
     ENS(d_tile_cnt, npt * 4); ENS(d_tile_sz, npt * 8);
     ENS(mp_dch, nc * sizeof(ChunkDesc));
@@ -401,13 +403,18 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
     // ---------------------------------------------------------------- page metadata
-    CK(xd2h(pg.data(), d_chunks.p, npg * sizeof(ChunkDesc), st));
     CK(xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st));
     std::vector<uint64_t> smeta(4 * npg, 0);
-    ENS(d_smeta, 4 * npg * 8);
-    launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(), nullptr, st);
-    CK(xd2h(smeta.data(), d_smeta.p, 4 * npg * 8, st));
-    CK(xsync(st));
+    uint64_t *const d_smeta = (uint64_t *)(d_chunks.as<ChunkDesc>() + npg);
+    launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta, nullptr, st);
+    {   // descriptors + metadata in one copy
+        static thread_local std::vector<uint8_t> md;
+        md.resize(npg * (sizeof(ChunkDesc) + 32));
+        CK(xd2h(md.data(), d_chunks.p, md.size(), st));
+        CK(xsync(st));
+        memcpy(pg.data(), md.data(), npg * sizeof(ChunkDesc));
+        memcpy(smeta.data(), md.data() + npg * sizeof(ChunkDesc), npg * 32);
+    }
     std::vector<std::string> bmin(npg), bmax(npg);
     {
         uint64_t blob_len = 0;
@@ -431,7 +438,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         } else if (blob_len) {
             std::vector<uint8_t> blob(blob_len);
             ENS(d_sblob, blob_len);
-            launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta.as<uint64_t>(),
+            launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta,
                                 d_sblob.as<uint8_t>(), st);
             CK(xd2h(blob.data(), d_sblob.p, blob_len, st));
             CK(xsync(st));

@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
             rc = nc;
         }
         if (cut) {
-            if (nrg < a.max_rgs) { if (tid == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = r; } }
+            if (nrg < a.max_rgs) { if (tid == 0) { a.rg[2 * nrg] = s; a.rg[2 * nrg + 1] = r; } }
             else overflow = 1;
             nrg++;
             s = r;
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
         int64_t open_buf = 0;
         if (s < n) open_buf = (int64_t)eval_mem<PLAN_T>(a, W, s, n);
         if (a.final_flush && s < n) {
-            if (nrg < a.max_rgs) { if (tid == 0) { a.rg_start[nrg] = s; a.rg_end[nrg] = n; } }
+            if (nrg < a.max_rgs) { if (tid == 0) { a.rg[2 * nrg] = s; a.rg[2 * nrg + 1] = n; } }
             else overflow = 1;
             nrg++;
             s = n;

@@ -118,8 +118,7 @@ struct PlanArgs {
     const uint64_t *gend;          // per stream k: bitmask of global RLE ends [(n/64+2)]
     uint64_t gend_stride;          // words per stream
     // outputs
-    int64_t *rg_start;             // [max_rgs]
-    int64_t *rg_end;
+    int64_t *rg;                   // [max_rgs] (start, end) pairs
     int32_t max_rgs;
     int32_t max_cuts;              // > 0: stop after this many cuts (HDFS alignment plans one row group at a time)
     int64_t *out;                  // [0]=n_rgs [1]=open_start [2]=open_buffered [3]=overflow
