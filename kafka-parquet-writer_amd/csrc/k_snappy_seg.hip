@@ -56,9 +56,6 @@ constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the wh
 #define SG_SW 4u                 // sort scatter: waves (each owns the hashes h % SG_SW)
 #endif
 
-#ifndef SG_HALF
-#define SG_HALF 0                // the fragment stays in LDS; cand[] holds one half of it per pass
-#endif
 constexpr uint32_t SG_NOMATCH = 0xffff;  // cand[]: the table entry's 4 bytes differ (positions < 65521)
 
 enum : uint32_t { MS = 0, MP = 1, MT = 2 };
@@ -148,32 +145,6 @@ struct FIn {
     }
 };
 
-// fragment bytes from its LDS copy (SG_HALF): the interface of FIn
-struct FInL {
-    const uint32_t *d;   // the fragment, dword-aligned, + 64 bytes of padding
-    __device__ __forceinline__ uint32_t ld32(uint32_t p) const
-    {
-        const uint32_t i = p >> 2;
-        return __builtin_amdgcn_alignbyte(d[i + 1], d[i], p & 3);
-    }
-    __device__ __forceinline__ uint64_t ld64(uint32_t p) const
-    {
-        const uint32_t i = p >> 2, s = p & 3;
-        const uint32_t w0 = d[i], w1 = d[i + 1], w2 = d[i + 2];
-        return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, s) << 32);
-    }
-    __device__ __forceinline__ uint8_t ld8(uint32_t p) const { return (uint8_t)(d[p >> 2] >> ((p & 3) * 8)); }
-    template <int D> __device__ __forceinline__ void ldw(uint32_t p, uint32_t *o) const
-    {
-        const uint32_t i = p >> 2, s = p & 3;
-        uint32_t v[D + 1];
-#pragma unroll
-        for (int k = 0; k <= D; k++) v[k] = d[i + k];
-#pragma unroll
-        for (int k = 0; k < D; k++) o[k] = __builtin_amdgcn_alignbyte(v[k + 1], v[k], s);
-    }
-};
-
 // FindMatchLength(s1, s2, limit); stops early (returns > cap) past cap bytes.  Past the first
 // 16 bytes the comparison runs SG_FMLW bytes per dependent load round trip (r04: 32 bytes,
 // C4 parse 578 -> 561 K cycles per fragment; 64 measured slower, and re-using the previous
@@ -181,8 +152,7 @@ struct FInL {
 #ifndef SG_FMLW
 #define SG_FMLW 32
 #endif
-template <class In>
-__device__ __forceinline__ uint32_t sg_fml(const In &in, uint32_t s1, uint32_t s2, uint32_t limit, uint32_t cap)
+__device__ __forceinline__ uint32_t sg_fml(const FIn &in, uint32_t s1, uint32_t s2, uint32_t limit, uint32_t cap)
 {
     uint32_t m = 0;
     if (s2 + 16 <= limit) {
@@ -195,8 +165,8 @@ __device__ __forceinline__ uint32_t sg_fml(const In &in, uint32_t s1, uint32_t s
         constexpr int D = SG_FMLW / 4;   // dwords compared per step
         while (s2 + m + SG_FMLW <= limit) {
             uint32_t a[D], b[D];
-            in.template ldw<D>(s1 + m, a);
-            in.template ldw<D>(s2 + m, b);
+            in.ldw<D>(s1 + m, a);
+            in.ldw<D>(s2 + m, b);
             uint32_t r = 0xffffffffu;
 #pragma unroll
             for (int i = D - 1; i >= 0; i--) {
@@ -273,9 +243,7 @@ __device__ __forceinline__ uint32_t put_lit_tag(sgg_u8 *o, uint32_t op, uint32_t
 // at rec[r * SG_T + t], so a wave's loads and stores cover contiguous 1 KiB / 512 B spans.
 struct SgScratch {
     uint4 sig4[8 * SG_T];         // positions sorted by (hash, position), 8 entries per piece
-#if !SG_HALF
     uint4 key4[16 * SG_T];        // the 4 bytes at each sorted entry's position
-#endif
     uint64_t bflag[SG_T];         // bit j of word t: sorted entry 64t+j starts a hash bucket
     uint64_t rec[SG_T * SG_RECS]; // copies found by the last parse, per segment
     uint32_t job[2 * SG_T][4];    // long literals: src, dst, len
@@ -284,33 +252,7 @@ struct SgScratch {
 // uint16 slot of sorted entry i
 __device__ __forceinline__ uint32_t sig_slot(uint32_t i) { return i; }
 
-constexpr uint32_t SG_DATA = 65536 + 64;   // the fragment's bytes (+ read padding)
-#if SG_HALF
-// LDS: the fragment (64 KiB, whole kernel) next to cand[] for one half of its positions
-// (64 KiB: the parse runs per half, rounds compute cand[] twice), the bucket counters of the
-// sort in cand[]'s place.  156 KiB, one workgroup per CU.
-struct SgShared {
-    uint32_t data[SG_DATA / 4];
-    union {
-        uint16_t cand[32768];     // rounds: candidate (table entry) per position of the half
-        uint32_t cnt[8192 + 2];   // setup: bucket counters, two uint16 per word; + a dummy
-    } a;
-    struct {
-        uint64_t entry[SG_T];
-        uint64_t exitst[SG_T];
-    } b;
-    uint64_t ibits[SG_T];
-    uint64_t found[SG_W];
-    uint32_t lfl[SG_T / 32];
-    uint32_t wf[SG_W], wv[SG_W];
-    uint32_t njobs;
-    int frag;
-    uint64_t prof[16];
-};
-#define SG_DATA_ARR(S) ((S).data)
-#define SG_CNT_ARR(S) ((S).a.cnt)
-#define SG_CAND(S, p) ((S).a.cand[(p) & 32767u])
-#else
+constexpr uint32_t SG_DATA = 65536 + 64;   // setup: the fragment's bytes (+ read padding)
 struct SgShared {
     union {
         uint16_t cand[65536];     // rounds: candidate (table entry) per position
@@ -331,22 +273,18 @@ struct SgShared {
     int frag;
     uint64_t prof[16];            // microbench phase counters (thread 0)
 };
-#define SG_DATA_ARR(S) ((S).a.su.data)
-#define SG_CNT_ARR(S) ((S).a.su.cnt)
-#define SG_CAND(S, p) ((S).a.cand[p])
-#endif
 
 // 4 bytes at position p of the LDS-staged fragment
 __device__ __forceinline__ uint32_t lds_ld32(const SgShared &S, uint32_t p)
 {
     const uint32_t d = p >> 2;
-    return __builtin_amdgcn_alignbyte(SG_DATA_ARR(S)[d + 1], SG_DATA_ARR(S)[d], p & 3);
+    return __builtin_amdgcn_alignbyte(S.a.su.data[d + 1], S.a.su.data[d], p & 3);
 }
 
 __device__ __forceinline__ uint32_t cnt_add(SgShared &S, uint32_t h)
 {
     const uint32_t sh = (h & 1) * 16;
-    return (atomicAdd(&SG_CNT_ARR(S)[h >> 1], 1u << sh) >> sh) & 0xffffu;
+    return (atomicAdd(&S.a.su.cnt[h >> 1], 1u << sh) >> sh) & 0xffffu;
 }
 
 // exclusive scan of u32 over the workgroup; *total = sum
@@ -398,8 +336,7 @@ struct ParseOut {
     bool lfl, fnd, lng;
     uint32_t nrec;
 };
-template <class In>
-__device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, const In &in, PS st, uint32_t t, uint32_t n,
+__device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, const FIn &in, PS st, uint32_t t, uint32_t n,
                                              uint32_t ip_limit)
 {
     const uint32_t sk = t * SG_SEG, sk1 = sk + SG_SEG;
@@ -410,7 +347,7 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
         if (st.mode == MP) {
             const uint32_t ipe = st.ip;
             if (ipe - 1 >= sk) o.own |= 1ull << (ipe - 1 - sk); else o.lfl = true;
-            c = SG_CAND(S, ipe);
+            c = S.a.cand[ipe];
             o.own |= 1ull << (ipe - sk);
             if (c == SG_NOMATCH) { st = PS{MS, ipe + 1, 32, ipe}; continue; }
             base = ipe; lit = false;
@@ -435,7 +372,7 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
                 if (v[k]) { ipk = nx; skk++; }
             }
 #pragma unroll
-            for (int k = 0; k < (int)SG_PB; k++) cc[k] = SG_CAND(S, q[k]);
+            for (int k = 0; k < (int)SG_PB; k++) cc[k] = S.a.cand[q[k]];
             int hit = -1;
 #pragma unroll
             for (int k = (int)SG_PB - 1; k >= 0; k--)
@@ -546,9 +483,9 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
 #pragma unroll
             for (int i = 0; i < 17; i++) v[i] = (t * 16 + i < nw) ? src[t * 16 + i] : 0u;
 #pragma unroll
-            for (int i = 0; i < 16; i++) SG_DATA_ARR(S)[t * 16 + i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
-            if (t < 16) SG_DATA_ARR(S)[SG_T * 16 + t] = 0;
-            for (uint32_t i = t; i <= tsize / 2; i += SG_T) SG_CNT_ARR(S)[i] = 0;
+            for (int i = 0; i < 16; i++) S.a.su.data[t * 16 + i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+            if (t < 16) S.a.su.data[SG_T * 16 + t] = 0;
+            for (uint32_t i = t; i <= tsize / 2; i += SG_T) S.a.su.cnt[i] = 0;
             S.ibits[t] = 0;   // bucket-start bits during the sort
         }
         __syncthreads();
@@ -565,13 +502,13 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             const uint32_t words = tsize / 2, wpt = (words + SG_T - 1) / SG_T, w0 = t * wpt;
             uint32_t loc = 0;
             for (uint32_t i = 0; i < wpt; i++)
-                if (w0 + i < words) { const uint32_t x = SG_CNT_ARR(S)[w0 + i]; loc += (x & 0xffffu) + (x >> 16); }
+                if (w0 + i < words) { const uint32_t x = S.a.su.cnt[w0 + i]; loc += (x & 0xffffu) + (x >> 16); }
             uint32_t tot;
             uint32_t run = sg_scan_excl(loc, S, &tot);
             for (uint32_t i = 0; i < wpt; i++)
                 if (w0 + i < words) {
-                    const uint32_t x = SG_CNT_ARR(S)[w0 + i], lo = x & 0xffffu, hi = x >> 16;
-                    SG_CNT_ARR(S)[w0 + i] = run | ((run + lo) << 16);
+                    const uint32_t x = S.a.su.cnt[w0 + i], lo = x & 0xffffu, hi = x >> 16;
+                    S.a.su.cnt[w0 + i] = run | ((run + lo) << 16);
                     if (lo) atomicOr((unsigned long long *)&S.ibits[run >> 6], 1ull << (run & 63));   // bucket starts
                     if (hi) atomicOr((unsigned long long *)&S.ibits[(run + lo) >> 6], 1ull << ((run + lo) & 63));
                     run += lo + hi;
@@ -596,7 +533,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     idx[u] = 0;
-                    if (h[u] != 0xffffffffu) idx[u] = atomicAdd(&SG_CNT_ARR(S)[h[u] >> 1], 1u << ((h[u] & 1) * 16));
+                    if (h[u] != 0xffffffffu) idx[u] = atomicAdd(&S.a.su.cnt[h[u] >> 1], 1u << ((h[u] & 1) * 16));
                 }
 #pragma unroll
                 for (int u = 0; u < 16; u++) asm volatile("" : "+v"(idx[u]));   // one wait for the batch
@@ -622,9 +559,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             // fragment: the rounds compare a position with its candidate there, so the parse's
             // probes are LDS reads
             sgg_cu4 *sp4 = (sgg_cu4 *)(G.sig4 + t * 8);
-#if !SG_HALF
             sgg_u4 *kp = (sgg_u4 *)(G.key4 + t);
-#endif
 #pragma unroll
             for (int q0 = 0; q0 < 8; q0 += 4) {
             sg_u32x4 vq[4];
@@ -633,7 +568,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
                 const int q = q0 + qq;
-                uint32_t pp[8];
+                uint32_t pp[8], kk[8];
 #pragma unroll
                 for (int e = 0; e < 8; e++) pp[e] = (vq[qq][e >> 1] >> ((e & 1) * 16)) & 0xffffu;
 #pragma unroll
@@ -641,14 +576,10 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                     const uint32_t j = q * 8 + e;
                     if (i0 + j < npos && !((bf >> j) & 1) && pp[e] <= prevp) bad = 1;
                     prevp = pp[e];
+                    kk[e] = lds_ld32(S, pp[e]);
                 }
-#if !SG_HALF
-                uint32_t kk[8];
-#pragma unroll
-                for (int e = 0; e < 8; e++) kk[e] = lds_ld32(S, pp[e]);
                 kp[(2 * q) * SG_T] = sg_u32x4{kk[0], kk[1], kk[2], kk[3]};
                 kp[(2 * q + 1) * SG_T] = sg_u32x4{kk[4], kk[5], kk[6], kk[7]};
-#endif
             }
             }
             G.bflag[t] = bf;
@@ -675,77 +606,6 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         while (!bad && rounds < SG_MAXR) {
             rounds++;
             if (a.seg_dbg && t == 0) a.seg_dbg[blockIdx.x * 4 + 1] = rounds;
-#if SG_HALF
-            // ---------------------------------------------- per half: cand[] (segmented max-scan), parse
-            {
-                const uint32_t i0 = t * SG_SEG;
-                uint32_t sg2[SG_SEG / 2];
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const uint4 v = G.sig4[t * 8 + q];
-                    sg2[4 * q] = v.x; sg2[4 * q + 1] = v.y; sg2[4 * q + 2] = v.z; sg2[4 * q + 3] = v.w;
-                }
-                const uint64_t bf = G.bflag[t];
-                uint32_t m = 0;
-                uint64_t insm = 0;   // bit j: sorted entry i0+j is an inserted position
-                const uint32_t *ib32 = (const uint32_t *)S.ibits;
-#pragma unroll
-                for (int j0 = 0; j0 < (int)SG_SEG; j0 += 16) {
-                    uint32_t wv[16];
-#pragma unroll
-                    for (int u = 0; u < 16; u++) {
-                        const int j = j0 + u;
-                        const uint32_t p = (sg2[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-                        wv[u] = ib32[p >> 5];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 16; u++) asm volatile("" : "+v"(wv[u]));
-#pragma unroll
-                    for (int u = 0; u < 16; u++) {
-                        const int j = j0 + u;
-                        const uint32_t p = (sg2[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-                        const uint32_t ins = (i0 + j < npos) ? ((wv[u] >> (p & 31)) & 1) : 0u;
-                        insm |= (uint64_t)ins << j;
-                        if ((bf >> j) & 1) m = 0;
-                        if (ins) m = p;
-                    }
-                }
-                PMARK(13);
-                const uint32_t mc = sg_segmax_carry(i0 < npos && bf != 0, i0 < npos ? m : 0, S);
-                PMARK(14);
-                const FInL inl{SG_DATA_ARR(S)};
-                po = ParseOut{upk(S.b.entry[t]), 0, false, false, false, 0};
-                // positions [0, 32 Ki) then [32 Ki, 64 Ki): cand[] holds one half, and the threads
-                // whose segments lie in it parse (their probes never leave their segment)
-                const uint32_t nhalf = nseg > SG_T / 2 ? 2u : 1u;
-                for (uint32_t h = 0; h < nhalf; h++) {
-                    if (h) {
-#pragma unroll
-                        for (int q = 0; q < 8; q++) {
-                            const uint4 v = G.sig4[t * 8 + q];
-                            sg2[4 * q] = v.x; sg2[4 * q + 1] = v.y; sg2[4 * q + 2] = v.z; sg2[4 * q + 3] = v.w;
-                        }
-                    }
-                    uint32_t mm = mc;
-                    uint32_t km = mm ? lds_ld32(S, mm) : key0;
-#pragma unroll
-                    for (int j = 0; j < (int)SG_SEG; j++) {
-                        const uint32_t p = (sg2[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-                        if ((bf >> j) & 1) { mm = 0; km = key0; }
-                        const bool mine = (p >> 15) == h;
-                        const bool ins = (insm >> j) & 1;
-                        const uint32_t kp = (mine || ins) ? lds_ld32(S, p) : 0u;
-                        if (mine && i0 + j < npos) SG_CAND(S, p) = (uint16_t)(km == kp ? mm : SG_NOMATCH);
-                        if (ins) { mm = p; km = kp; }
-                    }
-                    PMARK(15);
-                    __syncthreads();
-                    PMARK(1);
-                    if ((t >> 9) == h && t < nseg) po = sg_parse(S, G, inl, upk(S.b.entry[t]), t, n, ip_limit);
-                    __syncthreads();
-                }
-            }
-#else
             // ---------------------------------------------- cand[] from ibits (segmented max-scan)
             {
                 const uint32_t i0 = t * SG_SEG;
@@ -830,7 +690,6 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             // ---------------------------------------------- parse my segment
             po = t < nseg ? sg_parse(S, G, in, upk(S.b.entry[t]), t, n, ip_limit)
                           : ParseOut{upk(S.b.entry[t]), 0, false, false, false, 0};
-#endif
             S.b.exitst[t] = pk(po.st);
             if (po.lfl) atomicOr(&S.lfl[t >> 5], 1u << (t & 31));
             {
@@ -878,11 +737,6 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             continue;
         }
         // ---------------------------------------------- emit the converged parse's copies
-#if SG_HALF
-        const FInL src_in{SG_DATA_ARR(S)};   // literals from the LDS copy
-#else
-        const FIn &src_in = in;
-#endif
         const PS e0 = upk(S.b.entry[t]);
         uint32_t osz = 0;
         uint32_t ne = e0.ne;
@@ -909,11 +763,11 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
 #if SG_LITW
                     // dword stores once the output is aligned (the thread owns [op, op + len))
                     uint32_t i = 0;
-                    for (; i < len && ((op + i) & 3); i++) out[op + i] = src_in.ld8(src + i);
-                    for (; i + 4 <= len; i += 4) *(__attribute__((address_space(1))) uint32_t *)(out + op + i) = src_in.ld32(src + i);
-                    for (; i < len; i++) out[op + i] = src_in.ld8(src + i);
+                    for (; i < len && ((op + i) & 3); i++) out[op + i] = in.ld8(src + i);
+                    for (; i + 4 <= len; i += 4) *(__attribute__((address_space(1))) uint32_t *)(out + op + i) = in.ld32(src + i);
+                    for (; i < len; i++) out[op + i] = in.ld8(src + i);
 #else
-                    for (uint32_t i = 0; i < len; i++) out[op + i] = src_in.ld8(src + i);
+                    for (uint32_t i = 0; i < len; i++) out[op + i] = in.ld8(src + i);
 #endif
                 } else {
                     const uint32_t jx = atomicAdd(&S.njobs, 1u);
@@ -937,7 +791,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
             const uint32_t nj = S.njobs;
             for (uint32_t jx = 0; jx < nj; jx++) {
                 const uint32_t src = G.job[jx][0], dst = G.job[jx][1], len = G.job[jx][2];
-                for (uint32_t i = t; i < len; i += SG_T) out[dst + i] = src_in.ld8(src + i);
+                for (uint32_t i = t; i < len; i += SG_T) out[dst + i] = in.ld8(src + i);
             }
         }
         if (t == 0) {
