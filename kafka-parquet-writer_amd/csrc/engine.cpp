@@ -347,6 +347,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     const uint32_t nstreams = nopt + (v2_ ? nbool : 0);
     RleScratch sc{};
     uint32_t npt = 0, net = 0;
+    const uint64_t ev_stride = (ne + 1 + 7) & ~7ull;   // event bytes per stream (positions 0..ne, 8-aligned)
     std::vector<RleJob> pj;
     std::vector<PlanStream> hs(nstreams);
     std::vector<uint64_t *> &cbits = cbits_;
@@ -388,7 +389,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             J.src.base = 0;
             J.len = (uint32_t)ne;    // upper bound; optional boolean streams are shortened on the device
             J.bw = 1;
-            J.out_off = (uint64_t)k * (ne + 1);
+            J.out_off = (uint64_t)k * ev_stride;
         }
         int st = run_rle(pj, npt, net, sc);
         if (st) return st;
@@ -398,17 +399,17 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             launch_bool_streams(d_cols.as<DevCol>(), d_bool.as<uint32_t>(), nbool, ne, d_cbits_ptr.as<uint64_t *>(),
                                 d_jobs.as<RleJob>(), nopt, d_streams.as<PlanStream>(), nopt, s);
         }
-        ENS(d_ev, (uint64_t)nstreams * (ne + 1));
-        ENS(d_E, (uint64_t)nstreams * (ne + 1) * 4);
+        ENS(d_ev, (uint64_t)nstreams * ev_stride);
+        ENS(d_E, (uint64_t)nstreams * (ev_stride / 8 + 1) * 4);
         ENS(d_gend, (uint64_t)nstreams * nwords * 8);
-        CK(hipMemsetAsync(d_ev.p, 0, (uint64_t)nstreams * (ne + 1), s));
+        CK(hipMemsetAsync(d_ev.p, 0, (uint64_t)nstreams * ev_stride, s));
         CK(hipMemsetAsync(d_gend.p, 0, (uint64_t)nstreams * nwords * 8, s));
         launch_rle_structure(d_jobs.as<RleJob>(), (int)nstreams, npt, net, sc, s);
         launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), d_gend.as<uint64_t>(), nwords, s);
-        launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ne, nstreams, &seg_, s);
+        launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ev_stride, nstreams, &seg_, s);
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     }
-    if (mp_) return encode_mp(d_data, d_off, n, ne, final_flush, next_rg_size, hc, nwords, out);
+    if (mp_) return encode_mp(d_data, d_off, n, ne, final_flush, next_rg_size, hc, nwords, ev_stride, out);
     // ---------------------------------------------------------------- A9 plan
     // plan buffer (int64): [out 4 | pad 4 | (start, end) per row group]: the result and the first
     // kPlanHead row groups come back in one copy
@@ -420,7 +421,8 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     pa.P = d_P.as<uint64_t>(); pa.cols = d_cols.as<DevCol>();
     pa.streams = d_streams.as<PlanStream>(); pa.nstreams = (int32_t)nstreams;
     pa.nbool = v2_ ? 0 : (int32_t)nbool; pa.bool_cols = d_bool.as<uint32_t>();
-    pa.E = nstreams ? d_E.as<uint32_t>() : nullptr; pa.gend = nstreams ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
+    pa.E8 = nstreams ? d_E.as<uint32_t>() : nullptr; pa.ev = nstreams ? d_ev.as<uint8_t>() : nullptr; pa.ev_stride = ev_stride;
+    pa.gend = nstreams ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
     pa.rg = d_plan.as<int64_t>() + 8; pa.max_rgs = max_rgs;
     pa.max_cuts = max_cuts;
     pa.out = d_plan.as<int64_t>();

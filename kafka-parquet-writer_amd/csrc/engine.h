@@ -184,7 +184,7 @@ private:
     std::vector<std::vector<CutPage>> probe_cache_;   // per column, in page order
     std::vector<int64_t> probe_flushed_;
     int encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
-                  const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out);
+                  const std::vector<DevCol> &hc, uint64_t gend_stride, uint64_t ev_stride, BatchOut &out);
     int mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vector<int64_t>> &cuts);
     int probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, const std::vector<DevCol> &hc,
                  const std::vector<std::vector<int64_t>> &pc, BatchOut &out);

@@ -565,7 +565,7 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
 }
 
 int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
-                      const std::vector<DevCol> &hc, uint64_t gend_stride, BatchOut &out)
+                      const std::vector<DevCol> &hc, uint64_t gend_stride, uint64_t ev_stride, BatchOut &out)
 {
     hipStream_t st = stream;
     const int nc = (int)cols.size();
@@ -597,11 +597,12 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
 
     PageCutArgs a{};
     a.n = ne; a.ncols = nc; a.page_size = props.page_size; a.cols = d_cols.as<DevCol>();
-    a.col_stream = mp_cstream.as<int32_t>(); a.E = d_E.as<uint32_t>(); a.gend = d_gend.as<uint64_t>();
+    a.col_stream = mp_cstream.as<int32_t>(); a.E8 = d_E.as<uint32_t>(); a.ev = d_ev.as<uint8_t>(); a.ev_stride = ev_stride;
+    a.gend = d_gend.as<uint64_t>();
     a.gend_stride = gend_stride;
     a.sp = mp_spp.as<const uint64_t *>(); a.next_rg_size = T;
     a.col_bstream = mp_bstream.as<int32_t>(); a.streams = d_streams.as<PlanStream>(); a.v2 = v2_ ? 1 : 0;
-    if (opt_idx_.empty() && !(v2_ && !bool_idx_.empty())) { a.E = nullptr; a.gend = nullptr; }   // no planner streams
+    if (opt_idx_.empty() && !(v2_ && !bool_idx_.empty())) { a.E8 = nullptr; a.ev = nullptr; a.gend = nullptr; }   // no planner streams
 
     if (probe_) {   // probe_pages: the open row group's prefix [0, ne); its page cuts from the GPU planner
         std::vector<std::vector<int64_t>> pc;

@@ -65,8 +65,32 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v)
     return v;
 }
 
+// the global parse's emitted bytes of one stream before position x: the group-of-8 prefix plus
+// the event bytes of the positions before x in its group
+struct EvView {
+    const uint32_t *E8;
+    const uint8_t *ev;
+};
+__device__ __forceinline__ uint64_t ev_prefix(const EvView &v, uint64_t x)
+{
+    const uint64_t g = x >> 3;
+    uint64_t s = v.E8[g];
+    if (x & 7) {
+        uint64_t b = *(const uint64_t *)(v.ev + 8 * g) & ((1ull << (8 * (x & 7))) - 1);
+        b = (b & 0x00ff00ff00ff00ffull) + ((b >> 8) & 0x00ff00ff00ff00ffull);
+        b += b >> 16;
+        b += b >> 32;
+        s += b & 0xffffu;
+    }
+    return s;
+}
+template <class A> __device__ __forceinline__ EvView ev_view(const A &a, uint32_t k)
+{
+    return EvView{a.E8 + (uint64_t)k * (a.ev_stride / 8 + 1), a.ev + (uint64_t)k * a.ev_stride};
+}
+
 // E_s(r) for one optional column (dl width 1).
-__device__ uint64_t walker_query(Walker &w, int64_t r, const uint64_t *pres, uint64_t n, const uint32_t *Eg,
+__device__ uint64_t walker_query(Walker &w, int64_t r, const uint64_t *pres, uint64_t n, const EvView &Eg,
                                  const uint64_t *gend)
 {
     while (w.state == 0) {
@@ -123,14 +147,14 @@ __device__ uint64_t walker_query(Walker &w, int64_t r, const uint64_t *pres, uin
             if ((gend[b >> 6] >> (b & 63)) & 1) {
                 w.state = 1;
                 w.conv_pos = (int64_t)b;
-                w.delta = (int64_t)w.eacc - (int64_t)Eg[b + 1];
+                w.delta = (int64_t)w.eacc - (int64_t)ev_prefix(Eg, b + 1);
             }
         } else {
             w.grp++;
         }
         w.pend_pos = -1;
     }
-    if (w.state == 1 && r > w.conv_pos) return (uint64_t)((int64_t)Eg[r] + w.delta);
+    if (w.state == 1 && r > w.conv_pos) return (uint64_t)((int64_t)ev_prefix(Eg, (uint64_t)r) + w.delta);
     return w.eacc;
 }
 
@@ -160,7 +184,7 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
     uint64_t part = 0;
     for (int k = tid; k < a.nstreams; k += PLAN_T) {
         const PlanStream &S = a.streams[k];
-        part += walker_query(W[k], stream_pos(a, S, r), S.bits, S.len, a.E + (uint64_t)k * (a.n + 1),
+        part += walker_query(W[k], stream_pos(a, S, r), S.bits, S.len, ev_view(a, k),
                              a.gend + (uint64_t)k * a.gend_stride);
     }
     for (int k = tid; k < a.nbool; k += PLAN_T) {
@@ -196,7 +220,7 @@ __device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, int64_t 
         if (g == 0) part = a.P[r] - a.P[s];
         for (int k = g; k < a.nstreams; k += NW) {
             const Walker &w = W[k];
-            part += w.state == 1 ? (uint64_t)((int64_t)a.E[(uint64_t)k * (a.n + 1) + stream_pos(a, a.streams[k], r)] + w.delta)
+            part += w.state == 1 ? (uint64_t)((int64_t)ev_prefix(ev_view(a, k), (uint64_t)stream_pos(a, a.streams[k], r)) + w.delta)
                                  : w.eacc;
         }
         for (int k = g; k < a.nbool; k += NW) {
@@ -357,7 +381,7 @@ __device__ __forceinline__ uint64_t col_bool_rle(const PageCutArgs &a, int c, Wa
     const DevCol &col = a.cols[c];
     const PlanStream &S = a.streams[k];
     const int64_t pos = col.optional ? (int64_t)pc_at(col, (uint64_t)r) : r;
-    return walker_query(wb, pos, S.bits, S.len, a.E + (uint64_t)k * (a.n + 1), a.gend + (uint64_t)k * a.gend_stride);
+    return walker_query(wb, pos, S.bits, S.len, ev_view(a, k), a.gend + (uint64_t)k * a.gend_stride);
 }
 // rl(0) + dl + data buffered sizes of column c over the page [q, r):
 // dl = RunLengthBitPackingHybridEncoder bytes emitted since q (walker), data =
@@ -377,7 +401,7 @@ __device__ __forceinline__ uint64_t col_dl_bytes(const PageCutArgs &a, int c, Wa
     const int k = a.col_stream[c];
     if (k < 0) return 0;
     const DevCol &col = a.cols[c];
-    return walker_query(w, r, col.pres, a.n, a.E + (uint64_t)k * (a.n + 1), a.gend + (uint64_t)k * a.gend_stride);
+    return walker_query(w, r, col.pres, a.n, ev_view(a, k), a.gend + (uint64_t)k * a.gend_stride);
 }
 
 // ColumnWriterV1.accountForValueWritten (estimateNextSizeCheck = true), one thread per

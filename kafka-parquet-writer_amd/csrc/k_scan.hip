@@ -33,10 +33,19 @@ struct PcntF {
     __device__ uint64_t get(uint32_t j, uint64_t w) const { return __popcll(cols[opt[j]].pres[w]); }
     __device__ void put(uint32_t j, uint64_t w, uint64_t v) const { cols[opt[j]].pcnt[w] = (uint32_t)v; }
 };
+// planner events per group of 8 positions: element g of stream j = the 8 event bytes of
+// positions [8g, 8g + 8) summed (one 8-byte load); E8[j * (groups + 1) + g] = the prefix
 struct EvF {
-    const uint8_t *ev; uint32_t *E; uint64_t stride;
-    __device__ uint64_t get(uint32_t j, uint64_t i) const { return ev[j * stride + i]; }
-    __device__ void put(uint32_t j, uint64_t i, uint64_t v) const { E[j * stride + i] = (uint32_t)v; }
+    const uint64_t *ev; uint32_t *E8; uint64_t groups;
+    __device__ uint64_t get(uint32_t j, uint64_t g) const
+    {
+        uint64_t b = ev[j * groups + g];
+        b = (b & 0x00ff00ff00ff00ffull) + ((b >> 8) & 0x00ff00ff00ff00ffull);
+        b += b >> 16;
+        b += b >> 32;
+        return b & 0xffffu;
+    }
+    __device__ void put(uint32_t j, uint64_t g, uint64_t v) const { E8[j * (groups + 1) + g] = (uint32_t)v; }
 };
 
 // Multi-job equal-length exclusive sums, reduce -> scan tile sums -> apply (three launches).
@@ -174,10 +183,10 @@ void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt
     mj_scan(f, nwords, nopt, sc, s);
 }
 
-void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, SegScratch *sc, hipStream_t s)
+void launch_scan_events(const uint8_t *ev, uint32_t *E8, uint64_t ev_stride, uint32_t njobs, SegScratch *sc, hipStream_t s)
 {
-    EvF f{ev, E, n + 1};
-    mj_scan(f, n, njobs, sc, s);
+    EvF f{(const uint64_t *)ev, E8, ev_stride / 8};
+    mj_scan(f, ev_stride / 8, njobs, sc, s);
 }
 
 // ------------------------------------------------------------------ segmented tile scans

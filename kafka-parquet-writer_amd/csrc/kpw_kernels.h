@@ -114,7 +114,12 @@ struct PlanArgs {
     int32_t nstreams;
     int32_t nbool;                 // boolean columns counted as ceil(values/8) (v1); 0 in v2
     const uint32_t *bool_cols;     // indices of boolean columns
-    const uint32_t *E;             // per stream k: E[k*(n+1) + q] global emitted bytes before position q
+    // emitted bytes of the global parse of stream k before position q (ev_prefix): per group of 8
+    // positions E8[k * (ev_stride / 8 + 1) + q / 8], plus the event bytes ev[k * ev_stride + ...]
+    // of the positions before q in its group (one 8-byte load)
+    const uint32_t *E8;
+    const uint8_t *ev;
+    uint64_t ev_stride;            // bytes per stream in ev (a multiple of 8, > n)
     const uint64_t *gend;          // per stream k: bitmask of global RLE ends [(n/64+2)]
     uint64_t gend_stride;          // words per stream
     // outputs
@@ -136,7 +141,9 @@ struct PageCutArgs {
     int64_t page_size;
     const DevCol *cols;
     const int32_t *col_stream;     // per column: definition-level stream (E/gend index) or -1
-    const uint32_t *E;             // as PlanArgs
+    const uint32_t *E8;            // as PlanArgs
+    const uint8_t *ev;
+    uint64_t ev_stride;
     const uint64_t *gend;
     uint64_t gend_stride;
     const uint64_t *const *sp;     // per column: exclusive prefix of (4 + len) over present BYTE_ARRAY values

@@ -16,7 +16,9 @@ struct OpMapCompose;
 // scratch cannot grow, the scan is skipped and sc->failed is set: the caller must fail the
 // encode.
 void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, SegScratch *sc, hipStream_t s);
-void launch_scan_events(const uint8_t *ev, uint32_t *E, uint64_t n, uint32_t njobs, SegScratch *sc, hipStream_t s);
+// per stream j: E8[j * (ev_stride / 8 + 1) + g] = event bytes of positions [0, 8g) (ev_stride: bytes
+// per stream in ev, a multiple of 8)
+void launch_scan_events(const uint8_t *ev, uint32_t *E8, uint64_t ev_stride, uint32_t njobs, SegScratch *sc, hipStream_t s);
 
 // Status words for one single-pass launch over `nwords` tiles x scans (w == nullptr: the
 // scratch could not grow, sc->failed set; the caller skips the launch).
