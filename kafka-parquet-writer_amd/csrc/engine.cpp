@@ -330,9 +330,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     out.invalid_record = err_idx < n ? (int64_t)err_idx : -1;
 
     // ---------------------------------------------------------------- planning inputs
-    ENS(d_P, (ne + 1) * 8);
     if (nopt) launch_pcnt_scan(d_cols.as<DevCol>(), d_opt.as<uint32_t>(), nopt, nwords, &seg_, s);
-    launch_prefix_raw(d_raw.as<uint32_t>(), ne, d_P.as<uint64_t>(), &seg_, s);
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     if (ne == 0) {
         out.records_consumed = 0;
@@ -409,6 +407,24 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ev_stride, nstreams, &seg_, s);
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     }
+    // raw-byte prefix P; for the single-page planner also Q = P + the record-indexed streams'
+    // global event bytes (k_plan folds converged streams into one load), in the same scan
+    uint32_t nfold = 0;
+    for (uint32_t k = 0; k < nstreams; k++) nfold += hs[k].rank_col < 0 ? 1 : 0;
+    // (few streams: the planner's evaluations are cheap already and the fold's extra pass over
+    // the batch costs more, C2 4 streams: +0.8 ms per 100 M records; C3 199 streams: -6 ms per 10 M)
+    const bool fold = plan && !mp_ && nfold >= 16 && !fold_off();
+    ENS(d_P, (ne + 1) * 8);
+    if (fold) {
+        ENS(d_Q, (ne + 1) * 8);
+        ENS(d_qv, ne * 4);
+        launch_plan_fold(d_ev.as<uint8_t>(), ev_stride, d_streams.as<PlanStream>(), nstreams, d_raw.as<uint32_t>(), ne,
+                         d_qv.as<uint32_t>(), s);
+        launch_prefix_raw2(d_raw.as<uint32_t>(), d_qv.as<uint32_t>(), ne, d_P.as<uint64_t>(), d_Q.as<uint64_t>(), &seg_, s);
+    } else {
+        launch_prefix_raw(d_raw.as<uint32_t>(), ne, d_P.as<uint64_t>(), &seg_, s);
+    }
+    if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     if (mp_) return encode_mp(d_data, d_off, n, ne, final_flush, next_rg_size, hc, nwords, ev_stride, out);
     // ---------------------------------------------------------------- A9 plan
     // plan buffer (int64): [out 4 | pad 4 | (start, end) per row group]: the result and the first
@@ -418,7 +434,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ENS(d_plan, (8 + 2 * (size_t)max_rgs) * 8);
     PlanArgs pa{};
     pa.n = ne; pa.final_flush = final_flush ? 1 : 0; pa.ncols = nc; pa.next_rg_size = next_rg_size;
-    pa.P = d_P.as<uint64_t>(); pa.cols = d_cols.as<DevCol>();
+    pa.P = d_P.as<uint64_t>(); pa.Q = fold ? d_Q.as<uint64_t>() : nullptr; pa.cols = d_cols.as<DevCol>();
     pa.streams = d_streams.as<PlanStream>(); pa.nstreams = (int32_t)nstreams;
     pa.nbool = v2_ ? 0 : (int32_t)nbool; pa.bool_cols = d_bool.as<uint32_t>();
     pa.E8 = nstreams ? d_E.as<uint32_t>() : nullptr; pa.ev = nstreams ? d_ev.as<uint8_t>() : nullptr; pa.ev_stride = ev_stride;
@@ -435,6 +451,11 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     CK(hipEventRecord(ev_[2], s));
     const int64_t *po = pl.data();
     const int nrg = (int)po[0];
+#ifdef KPW_PLAN_PROF
+    fprintf(stderr, "[plan_prof] rgs %d total %.3f ms walk %.3f ms (%lld) conv %.3f ms (%lld) points %lld\n", nrg,
+            po[4] / 1e5, po[5] / 1e5, (long long)(po[7] & 0x1fffff), po[6] / 1e5, (long long)((po[7] >> 21) & 0x1fffff),
+            (long long)(po[7] >> 42));
+#endif
     if (po[3]) return fail(KPW_ERR_DEVICE, "planner row-group table overflow");
     if (nrg > head) {   // more row groups than the first copy held
         pl.resize(8 + 2 * (size_t)nrg);

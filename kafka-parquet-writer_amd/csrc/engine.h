@@ -19,6 +19,13 @@ inline bool body_poison()
     static const bool on = [] { const char *e = getenv("KPW_BODY_POISON"); return e && e[0] == '1'; }();
     return on;
 }
+// KPW_PLAN_FOLD=0: the planner evaluates every stream per check point instead of the folded
+// prefix Q (A/B and parity of the two evaluations)
+inline bool fold_off()
+{
+    static const bool off = [] { const char *e = getenv("KPW_PLAN_FOLD"); return e && e[0] == '0'; }();
+    return off;
+}
 struct SnappyArgs;
 
 struct ColInfo {
@@ -144,7 +151,7 @@ private:
     // decode buffers
     std::vector<DevBuf> col_vals, col_shash, col_spfx, col_soff, col_slen, col_pres, col_vbits, col_pcnt;
     std::vector<uint32_t> dict_hint_;  // per column: most dictionary entries in the previous encode (0: none)
-    DevBuf d_cols, d_fmap, d_raw, d_P, d_opt, d_bool;   // d_cols: descriptors + error word
+    DevBuf d_cols, d_fmap, d_raw, d_P, d_Q, d_qv, d_opt, d_bool;   // d_cols: descriptors + error word
     // planning
     DevBuf d_ev, d_E, d_gend, d_plan;
     // rle scratch (shared by planning and encoding)

@@ -25,6 +25,11 @@
 //
 // One block walks the row groups sequentially; its 1024 threads split the streams / boolean
 // columns (every thread takes the same decisions from block-wide sums).
+//
+// Folding: once every record-indexed stream's walker has converged in a row group, their sum
+// is sum_s (E_g,s(r) + delta_s) = sum_s E_g,s(r) + D, so memSize(r) = Q[r] - P[s] + D (+ the
+// value-rank streams and v1 booleans), with Q = P + sum_s E_g,s precomputed for every r
+// (k_plan_fold + one scan): one load per evaluation instead of one per stream (C3: 199).
 #include "kpw_device.h"
 #include "kpw_kernels.h"
 
@@ -89,39 +94,44 @@ template <class A> __device__ __forceinline__ EvView ev_view(const A &a, uint32_
     return EvView{a.E8 + (uint64_t)k * (a.ev_stride / 8 + 1), a.ev + (uint64_t)k * a.ev_stride};
 }
 
+// A walker's bits: the stream's 64-bit windows and the global parse's run-end flags.
+struct SrcDirect {
+    const uint64_t *bits, *gend;
+    __device__ uint64_t win(uint64_t p) const { return bits_window(bits, p); }
+    __device__ bool gend_at(uint64_t b) const { return (gend[b >> 6] >> (b & 63)) & 1; }
+};
 // E_s(r) for one optional column (dl width 1).
-__device__ uint64_t walker_query(Walker &w, int64_t r, const uint64_t *pres, uint64_t n, const EvView &Eg,
-                                 const uint64_t *gend)
+template <class Src>
+__device__ uint64_t walker_query(Walker &w, int64_t r, const Src &src, uint64_t n, const EvView &Eg)
 {
     while (w.state == 0) {
         if (w.pend_pos < 0) {
             const int64_t p = w.p;
             if (p + 8 > (int64_t)n) { w.state = 2; break; }
-            const uint64_t x64 = bits_window(pres, (uint64_t)p);
+            const uint64_t x64 = src.win((uint64_t)p);
             const uint32_t x8 = (uint32_t)(x64 & 0xffu);
             if (x8 != 0 && x8 != 0xffu && p + 7 < r) {
-                // bit-packed groups straight from the 64-bit window: every mixed group that ends
-                // before r is consumed (1 byte, +1 for a new run header every 63 groups) without
-                // reloading; the first group that is not is left to the general path below
-                int64_t q = p;
-                int k = 0;
-                do {
-                    w.eacc += 1 + ((w.grp % 63) == 0 ? 1 : 0);
-                    w.grp++;
-                    q += 8;
-                    k++;
-                    if (k == 8 || q + 8 > (int64_t)n || q + 7 >= r) break;
-                    const uint32_t y8 = (uint32_t)((x64 >> (8 * k)) & 0xffu);
-                    if (y8 == 0 || y8 == 0xffu) break;
-                } while (true);
-                w.p = q;
+                // bit-packed groups straight from the 64-bit window: the mixed groups before the
+                // first pure byte (0x00 / 0xff: SWAR zero-byte tests of x and ~x), that end before
+                // r and inside the batch, are consumed at once (1 byte each, +1 for a new run
+                // header every 63 groups); the next group goes to the general path below
+                const uint64_t lo7 = 0x0101010101010101ull, hi7 = 0x8080808080808080ull;
+                const uint64_t nx = ~x64;
+                const uint64_t pm = ((x64 - lo7) & nx & hi7) | ((nx - lo7) & x64 & hi7);
+                int64_t k = pm ? (int64_t)(__builtin_ctzll(pm) >> 3) : 8;   // >= 1: byte 0 is mixed
+                const int64_t kn = ((int64_t)n - p) >> 3, kr = (r - p) >> 3;
+                k = k < kn ? k : kn;
+                k = k < kr ? k : kr;
+                w.eacc += (uint64_t)k + (w.grp + (uint32_t)k + 62) / 63 - (w.grp + 62) / 63;
+                w.grp += (uint32_t)k;
+                w.p = p + 8 * k;
                 continue;
             }
             if (x8 == 0 || x8 == 0xffu) {
                 const uint64_t fill = x8 ? ~0ull : 0ull;
                 int64_t pos = p + 8, b = (int64_t)n;
                 while (pos < (int64_t)n) {
-                    uint64_t d = bits_window(pres, (uint64_t)pos) ^ fill;
+                    uint64_t d = src.win((uint64_t)pos) ^ fill;
                     if (d) { b = pos + __ffsll((long long)d) - 1; break; }
                     pos += 64;
                 }
@@ -144,7 +154,7 @@ __device__ uint64_t walker_query(Walker &w, int64_t r, const uint64_t *pres, uin
         if (w.pend_rle) {
             w.grp = 0;
             const uint64_t b = (uint64_t)w.pend_pos;
-            if ((gend[b >> 6] >> (b & 63)) & 1) {
+            if (src.gend_at(b)) {
                 w.state = 1;
                 w.conv_pos = (int64_t)b;
                 w.delta = (int64_t)w.eacc - (int64_t)ev_prefix(Eg, b + 1);
@@ -165,10 +175,34 @@ __device__ __forceinline__ uint64_t pc_at(const DevCol &c, uint64_t x)
     return (uint64_t)c.pcnt[wi] + (uint64_t)__popcll(m);
 }
 
-// position of record r in stream k (the record itself, or its value rank)
-__device__ __forceinline__ int64_t stream_pos(const PlanArgs &a, const PlanStream &S, int64_t r)
+// k_plan's copies of the stream and boolean-column tables in LDS: every evaluation reads
+// them, and from global memory each read added a dependent load ahead of the stream's own
+// (C3: 199 streams, ~20 evaluations per row group)
+struct PlanSt {
+    const uint64_t *bits;
+    uint64_t len;
+    const uint64_t *rpres;   // rank-indexed stream: the presence bits and counts of its column
+    const uint32_t *rpcnt;
+};
+struct PlanBool {
+    const uint64_t *pres;    // null: REQUIRED
+    const uint32_t *pcnt;
+};
+__device__ __forceinline__ uint64_t pc_at_p(const uint64_t *pres, const uint32_t *pcnt, uint64_t x)
 {
-    return S.rank_col < 0 ? r : (int64_t)pc_at(a.cols[S.rank_col], (uint64_t)r);
+    const uint64_t wi = x >> 6;
+    const uint64_t m = (x & 63) ? (pres[wi] & ((1ull << (x & 63)) - 1)) : 0ull;
+    return (uint64_t)pcnt[wi] + (uint64_t)__popcll(m);
+}
+// position of record r in stream k (the record itself, or its value rank)
+__device__ __forceinline__ int64_t st_pos(const PlanSt &S, int64_t r)
+{
+    return S.rpres ? (int64_t)pc_at_p(S.rpres, S.rpcnt, (uint64_t)r) : r;
+}
+__device__ __forceinline__ uint64_t bool_bytes(const PlanBool &B, int64_t s, int64_t r)
+{
+    const uint64_t cnt = B.pres ? pc_at_p(B.pres, B.pcnt, (uint64_t)r) - pc_at_p(B.pres, B.pcnt, (uint64_t)s) : (uint64_t)(r - s);
+    return (cnt + 7) / 8;
 }
 
 // k_plan block: PLAN_T threads, each owning streams tid, tid + PLAN_T, ...; 1024 (16 waves) for
@@ -176,22 +210,23 @@ __device__ __forceinline__ int64_t stream_pos(const PlanArgs &a, const PlanStrea
 // waves; 1.72 -> 1.46 ms per job), 256 for few (C2: 4 streams, where 16 waves only add barrier
 // cost: resident plan stage 13.1 -> 17.2 ms per 100 M records with 1024)
 
+// folded (F = D - P[s]): the record-indexed streams are in Q[r] + F
 template <int PLAN_T>
-__device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
+__device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, const PlanSt *St, const PlanBool *Bo, int64_t s, int64_t r, bool folded,
+                             int64_t F)
 {
     __shared__ uint64_t red[PLAN_T / 64];
     const int tid = threadIdx.x;
-    uint64_t part = 0;
+    uint64_t part = 0;   // issued first: its latency overlaps the streams'
+    if (tid == 0) part = folded ? (uint64_t)((int64_t)a.Q[r] + F) : a.P[r] - a.P[s];
     for (int k = tid; k < a.nstreams; k += PLAN_T) {
-        const PlanStream &S = a.streams[k];
-        part += walker_query(W[k], stream_pos(a, S, r), S.bits, S.len, ev_view(a, k),
-                             a.gend + (uint64_t)k * a.gend_stride);
+        const PlanSt &S = St[k];
+        if (folded && !S.rpres) continue;
+        Walker w = W[k];   // in registers for the walk
+        part += walker_query(w, st_pos(S, r), SrcDirect{S.bits, a.gend + (uint64_t)k * a.gend_stride}, S.len, ev_view(a, k));
+        W[k] = w;
     }
-    for (int k = tid; k < a.nbool; k += PLAN_T) {
-        const DevCol &c = a.cols[a.bool_cols[k]];
-        const uint64_t cnt = c.optional ? pc_at(c, (uint64_t)r) - pc_at(c, (uint64_t)s) : (uint64_t)(r - s);
-        part += (cnt + 7) / 8;
-    }
+    for (int k = tid; k < a.nbool; k += PLAN_T) part += bool_bytes(Bo[k], s, r);
     part = wave_sum(part);
     if ((tid & 63) == 0) red[tid >> 6] = part;
     __syncthreads();   // also publishes the walkers to eval_mem_points
@@ -199,7 +234,7 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 #pragma unroll
     for (int i = 0; i < PLAN_T / 64; i++) tot += red[i];
     __syncthreads();
-    return tot + (a.P[r] - a.P[s]);
+    return tot;
 }
 
 // memSize at the 64 clamp-step check points s + rc + 10000*j, valid only when every walker is
@@ -208,7 +243,8 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, int64_t s, int64_t r)
 // g, g + 16, ... (independent loads, no walking), and the 16 partial sums meet in LDS; every
 // lane j returns the memSize of point j.
 template <int PLAN_T>
-__device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, int64_t s, int64_t rc)
+__device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, const PlanSt *St, const PlanBool *Bo, int64_t s,
+                                    int64_t rc, bool folded, int64_t F)
 {
     __shared__ uint64_t red[PLAN_T];
     constexpr int NW = PLAN_T / 64;
@@ -217,17 +253,14 @@ __device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, int64_t 
     const int64_t r = s + rc + 10000 * (int64_t)j;
     uint64_t part = 0;
     if (r <= (int64_t)a.n) {
-        if (g == 0) part = a.P[r] - a.P[s];
+        if (g == 0) part = folded ? (uint64_t)((int64_t)a.Q[r] + F) : a.P[r] - a.P[s];
         for (int k = g; k < a.nstreams; k += NW) {
+            if (folded && !St[k].rpres) continue;
             const Walker &w = W[k];
-            part += w.state == 1 ? (uint64_t)((int64_t)ev_prefix(ev_view(a, k), (uint64_t)stream_pos(a, a.streams[k], r)) + w.delta)
+            part += w.state == 1 ? (uint64_t)((int64_t)ev_prefix(ev_view(a, k), (uint64_t)st_pos(St[k], r)) + w.delta)
                                  : w.eacc;
         }
-        for (int k = g; k < a.nbool; k += NW) {
-            const DevCol &c = a.cols[a.bool_cols[k]];
-            const uint64_t cnt = c.optional ? pc_at(c, (uint64_t)r) - pc_at(c, (uint64_t)s) : (uint64_t)(r - s);
-            part += (cnt + 7) / 8;
-        }
+        for (int k = g; k < a.nbool; k += NW) part += bool_bytes(Bo[k], s, r);
     }
     red[tid] = part;
     __syncthreads();
@@ -239,29 +272,78 @@ __device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, int64_t 
 }
 
 template <int PLAN_T>
-__device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walker *W, int64_t r)
+__device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walker *W, const PlanSt *St, int64_t r)
 {
     bool ok = true;
     for (int k = threadIdx.x; k < a.nstreams; k += PLAN_T)
-        ok = ok && (W[k].state == 2 || (W[k].state == 1 && W[k].conv_pos < stream_pos(a, a.streams[k], r)));
+        ok = ok && (W[k].state == 2 || (W[k].state == 1 && W[k].conv_pos < st_pos(St[k], r)));
     return __syncthreads_and(ok ? 1 : 0) != 0;
+}
+
+// Every record-indexed stream's walker converged: F = D - P[s] (D = the sum of their deltas).
+template <int PLAN_T>
+__device__ bool try_fold(const PlanArgs &a, const Walker *W, const PlanSt *St, int64_t s, int64_t &F)
+{
+    __shared__ uint64_t red[PLAN_T / 64];
+    const int tid = threadIdx.x;
+    bool ok = true;
+    int64_t d = 0;
+    for (int k = tid; k < a.nstreams; k += PLAN_T)
+        if (!St[k].rpres) { ok = ok && W[k].state == 1; d += W[k].delta; }
+    if (!__syncthreads_and(ok ? 1 : 0)) return false;
+    const uint64_t w = wave_sum((uint64_t)d);
+    if ((tid & 63) == 0) red[tid >> 6] = w;
+    __syncthreads();
+    uint64_t D = 0;
+#pragma unroll
+    for (int i = 0; i < PLAN_T / 64; i++) D += red[i];
+    __syncthreads();
+    F = (int64_t)D - (int64_t)a.P[s];
+    return true;
 }
 
 template <int PLAN_T>
 __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
 {
     __shared__ Walker W[MAX_STREAMS];
+    __shared__ PlanSt St[MAX_STREAMS];
+    __shared__ PlanBool Bo[MAX_COLS];
     const int tid = threadIdx.x;
+    for (int k = tid; k < a.nstreams; k += PLAN_T) {
+        const PlanStream S = a.streams[k];
+        PlanSt t;
+        t.bits = S.bits; t.len = S.len; t.rpres = nullptr; t.rpcnt = nullptr;
+        if (S.rank_col >= 0) { t.rpres = a.cols[S.rank_col].pres; t.rpcnt = a.cols[S.rank_col].pcnt; }
+        St[k] = t;
+    }
+    for (int k = tid; k < a.nbool; k += PLAN_T) {
+        const DevCol &c = a.cols[a.bool_cols[k]];
+        Bo[k] = PlanBool{c.optional ? c.pres : nullptr, c.optional ? c.pcnt : nullptr};
+    }
+    __syncthreads();
     const int lane = tid & 63;
     const int64_t n = (int64_t)a.n;
     const int64_t T = a.next_rg_size;
     int64_t s = 0;
     int32_t nrg = 0;
     int64_t overflow = 0;
+#ifdef KPW_PLAN_PROF
+    // profiling build (tests/microbench): wall-clock ticks (100 MHz) per evaluation kind in
+    // out[4..7]: total, walking evaluations, converged single evaluations, counts
+    const uint64_t pp_t0 = wall_clock64();
+    uint64_t pp_unc = 0, pp_cnv = 0, pp_nu = 0, pp_nc = 0, pp_np = 0;
+#define PP_OUT()                                                                                   \
+    if (tid == 0) {                                                                                \
+        a.out[4] = (int64_t)(wall_clock64() - pp_t0); a.out[5] = (int64_t)pp_unc;                  \
+        a.out[6] = (int64_t)pp_cnv; a.out[7] = (int64_t)(pp_nu | pp_nc << 21 | pp_np << 42);       \
+    }
+#else
+#define PP_OUT()
+#endif
     for (;;) {
         for (int k = tid; k < a.nstreams; k += PLAN_T) {
             Walker w;
-            w.p = stream_pos(a, a.streams[k], s); w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
+            w.p = st_pos(St[k], s); w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
             w.pend_bytes = 0; w.pend_rle = 0; w.grp = 0; w.state = 0;
             W[k] = w;
         }
@@ -269,38 +351,65 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
         int64_t rc = 100;
         bool cut = false;
         bool clamp = true;   // the previous decision took the recordCount + 10000 clamp
+        bool folded = false;
+        int64_t F = 0;
         int64_t r = 0;
         while (s + rc <= n) {
+            if (a.Q && !folded) folded = try_fold<PLAN_T>(a, W, St, s, F);
             // Far from the cut every next check is recordCount + 10000 (the clamp): once the
             // walkers are converged, the block evaluates memSize at the next 64 clamp-step
-            // check points and the scalar replay below takes parquet-mr's decisions over them,
-            // stopping where a decision leaves the clamp path (or cuts).  Near the cut (the
+            // check points and takes parquet-mr's decisions over them (one lane each), stopping
+            // where a decision leaves the clamp path (or cuts).  Near the cut (the
             // estimate halves the distance each check) one point at a time is cheaper.
-            if (clamp && walkers_converged<PLAN_T>(a, W, s + rc)) {
-                const uint64_t Mj = eval_mem_points<PLAN_T>(a, W, s, rc);
-                bool left = false;
-                for (int j = 0; j < 64; j++) {
-                    const int64_t rcv = rc + 10000 * (int64_t)j;
-                    if (s + rcv > n) { rc = rcv; left = true; break; }
-                    const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)Mj, j);
-                    const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(Mj >> 32), j);
-                    const int64_t M = (int64_t)(((uint64_t)mhi << 32) | mlo);
+            if (clamp && walkers_converged<PLAN_T>(a, W, St, s + rc)) {
+#ifdef KPW_PLAN_PROF
+                pp_np++;
+#endif
+                const uint64_t Mj = eval_mem_points<PLAN_T>(a, W, St, Bo, s, rc, folded, F);
+                // parquet-mr's decision at every point, lane j for point j (each depends only on
+                // its own memSize); the replay stops at the first point past the batch, that cuts,
+                // or whose next check leaves the clamp path
+                const int64_t rcv = rc + 10000 * (int64_t)lane;
+                const bool past = s + rcv > n;
+                bool cut_j = false;
+                int64_t nc = rcv + 10000;
+                if (!past) {
+                    const int64_t M = (int64_t)Mj;
                     const int64_t rs = M / rcv;
-                    if (M > T - 2 * rs) { cut = true; r = s + rcv; left = true; break; }
-                    const float q = __fdiv_rn((float)T, (float)rs);
-                    const int64_t est = jadd(rcv, java_f2l(q)) / 2;
-                    const int64_t lo = est > 100 ? est : 100;
-                    const int64_t hi = jadd(rcv, 10000);
-                    int64_t nc = lo < hi ? lo : hi;
-                    if (nc < rcv + 1) nc = rcv + 1;
-                    if (nc != rcv + 10000) { rc = nc; left = true; clamp = false; break; }
+                    cut_j = M > T - 2 * rs;
+                    if (!cut_j) {
+                        const float q = __fdiv_rn((float)T, (float)rs);
+                        const int64_t est = jadd(rcv, java_f2l(q)) / 2;
+                        const int64_t lo = est > 100 ? est : 100;
+                        const int64_t hi = jadd(rcv, 10000);
+                        nc = lo < hi ? lo : hi;
+                        if (nc < rcv + 1) nc = rcv + 1;
+                    }
                 }
-                if (cut) break;
-                if (!left) rc += 10000 * 64;
+                const uint64_t stop = __ballot(past || cut_j || nc != rcv + 10000);
+                if (!stop) { rc += 10000 * 64; continue; }
+                const int js = __builtin_ctzll(stop);   // uniform
+                const int64_t rcs = rc + 10000 * (int64_t)js;
+                if (s + rcs > n) { rc = rcs; continue; }   // leaves the loop
+                if (__builtin_amdgcn_readlane((int)cut_j, js)) { cut = true; r = s + rcs; break; }
+                const uint32_t nlo = __builtin_amdgcn_readlane((uint32_t)nc, js);
+                const uint32_t nhi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)nc >> 32), js);
+                rc = (int64_t)(((uint64_t)nhi << 32) | nlo);
+                clamp = false;
                 continue;
             }
             r = s + rc;
-            const int64_t M = (int64_t)eval_mem<PLAN_T>(a, W, s, r);
+#ifdef KPW_PLAN_PROF
+            bool pp_walk = false;
+            for (int k = tid; k < a.nstreams; k += PLAN_T) pp_walk = pp_walk || W[k].state == 0;
+            pp_walk = __syncthreads_or(pp_walk ? 1 : 0) != 0;
+            const uint64_t pp_e0 = wall_clock64();
+#endif
+            const int64_t M = (int64_t)eval_mem<PLAN_T>(a, W, St, Bo, s, r, folded, F);
+#ifdef KPW_PLAN_PROF
+            if (pp_walk) { pp_unc += wall_clock64() - pp_e0; pp_nu++; }
+            else { pp_cnv += wall_clock64() - pp_e0; pp_nc++; }
+#endif
             const int64_t rs = M / rc;
             if (M > T - 2 * rs) { cut = true; break; }
             const float q = __fdiv_rn((float)T, (float)rs);
@@ -319,6 +428,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
             s = r;
             if (a.max_cuts > 0 && nrg >= a.max_cuts) {   // the caller re-plans from s with the next limit
                 if (tid == 0) { a.out[0] = nrg; a.out[1] = s; a.out[2] = 0; a.out[3] = overflow; }
+                PP_OUT();
                 break;
             }
             __syncthreads();
@@ -326,7 +436,10 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
         }
         // the open row group [s, n)
         int64_t open_buf = 0;
-        if (s < n) open_buf = (int64_t)eval_mem<PLAN_T>(a, W, s, n);
+        if (s < n) {
+            if (a.Q && !folded) folded = try_fold<PLAN_T>(a, W, St, s, F);
+            open_buf = (int64_t)eval_mem<PLAN_T>(a, W, St, Bo, s, n, folded, F);
+        }
         if (a.final_flush && s < n) {
             if (nrg < a.max_rgs) { if (tid == 0) { a.rg[2 * nrg] = s; a.rg[2 * nrg + 1] = n; } }
             else overflow = 1;
@@ -340,8 +453,44 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
             a.out[2] = open_buf;
             a.out[3] = overflow;
         }
+        PP_OUT();
         break;
     }
+#undef PP_OUT
+}
+
+// val[x] = raw[x] + the event bytes at position x of every record-indexed stream (the input
+// of Q's scan); one thread per group of 8 positions, one 8-byte load per stream, byte lanes
+// summed as u16 (< 2^16: at most MAX_STREAMS streams x 6 bytes)
+__global__ void __launch_bounds__(256) k_plan_fold(const uint8_t *ev, uint64_t ev_stride, const PlanStream *streams, uint32_t nstreams,
+                                                   const uint32_t *raw, uint64_t n, uint32_t *val)
+{
+    const uint64_t x0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    if (x0 >= n) return;
+    uint64_t lo = 0, hi = 0;
+#pragma unroll 4
+    for (uint32_t k = 0; k < nstreams; k++) {
+        if (streams[k].rank_col >= 0) continue;
+        const uint64_t b = *(const uint64_t *)(ev + (uint64_t)k * ev_stride + x0);
+        lo += b & 0x00ff00ff00ff00ffull;
+        hi += (b >> 8) & 0x00ff00ff00ff00ffull;
+    }
+    uint32_t e[8];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { e[2 * i] = (uint32_t)(lo >> (16 * i)) & 0xffffu; e[2 * i + 1] = (uint32_t)(hi >> (16 * i)) & 0xffffu; }
+    if (x0 + 8 <= n) {
+        const uint4 r0 = *(const uint4 *)(raw + x0), r1 = *(const uint4 *)(raw + x0 + 4);
+        *(uint4 *)(val + x0) = make_uint4(r0.x + e[0], r0.y + e[1], r0.z + e[2], r0.w + e[3]);
+        *(uint4 *)(val + x0 + 4) = make_uint4(r1.x + e[4], r1.y + e[5], r1.z + e[6], r1.w + e[7]);
+    } else {
+        for (uint64_t i = 0; x0 + i < n; i++) val[x0 + i] = raw[x0 + i] + e[i];
+    }
+}
+
+void launch_plan_fold(const uint8_t *ev, uint64_t ev_stride, const PlanStream *streams, uint32_t nstreams, const uint32_t *raw,
+                      uint64_t n, uint32_t *val, hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_plan_fold, dim3((unsigned)((n + 2047) / 2048)), dim3(256), 0, s, ev, ev_stride, streams, nstreams, raw, n, val);
 }
 
 void launch_plan(const PlanArgs &a, hipStream_t s)
@@ -381,7 +530,7 @@ __device__ __forceinline__ uint64_t col_bool_rle(const PageCutArgs &a, int c, Wa
     const DevCol &col = a.cols[c];
     const PlanStream &S = a.streams[k];
     const int64_t pos = col.optional ? (int64_t)pc_at(col, (uint64_t)r) : r;
-    return walker_query(wb, pos, S.bits, S.len, ev_view(a, k), a.gend + (uint64_t)k * a.gend_stride);
+    return walker_query(wb, pos, SrcDirect{S.bits, a.gend + (uint64_t)k * a.gend_stride}, S.len, ev_view(a, k));
 }
 // rl(0) + dl + data buffered sizes of column c over the page [q, r):
 // dl = RunLengthBitPackingHybridEncoder bytes emitted since q (walker), data =
@@ -401,7 +550,7 @@ __device__ __forceinline__ uint64_t col_dl_bytes(const PageCutArgs &a, int c, Wa
     const int k = a.col_stream[c];
     if (k < 0) return 0;
     const DevCol &col = a.cols[c];
-    return walker_query(w, r, col.pres, a.n, ev_view(a, k), a.gend + (uint64_t)k * a.gend_stride);
+    return walker_query(w, r, SrcDirect{col.pres, a.gend + (uint64_t)k * a.gend_stride}, a.n, ev_view(a, k));
 }
 
 // ColumnWriterV1.accountForValueWritten (estimateNextSizeCheck = true), one thread per

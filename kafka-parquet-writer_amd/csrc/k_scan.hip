@@ -21,6 +21,12 @@ struct RawF {
     __device__ uint64_t get(uint32_t, uint64_t i) const { return raw[i]; }
     __device__ void put(uint32_t, uint64_t i, uint64_t v) const { P[i] = v; }
 };
+// job 0: raw -> P, job 1: val -> Q (the planner's folded prefix, k_plan_fold)
+struct Raw2F {
+    const uint32_t *raw, *val; uint64_t *P, *Q;
+    __device__ uint64_t get(uint32_t j, uint64_t i) const { return j ? val[i] : raw[i]; }
+    __device__ void put(uint32_t j, uint64_t i, uint64_t v) const { (j ? Q : P)[i] = v; }
+};
 // record lengths narrowed to T (u8 / u16) on the host; element 0 is `base` (the first boundary)
 template <typename T>
 struct NarrowF {
@@ -169,6 +175,13 @@ void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, SegScratch 
 {
     RawF f{raw, P};
     mj_scan(f, n, 1, sc, s);
+}
+
+void launch_prefix_raw2(const uint32_t *raw, const uint32_t *val, uint64_t n, uint64_t *P, uint64_t *Q, SegScratch *sc,
+                        hipStream_t s)
+{
+    Raw2F f{raw, val, P, Q};
+    mj_scan(f, n, 2, sc, s);
 }
 
 void launch_prefix_narrow(const void *raw, int width, uint64_t base, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s)

@@ -109,6 +109,8 @@ struct PlanArgs {
     int32_t ncols;
     int64_t next_rg_size;          // nextRowGroupSize
     const uint64_t *P;             // exclusive prefix of raw bytes [n+1]
+    const uint64_t *Q;             // [n+1] P + the global parse's bytes of every record-indexed stream
+                                   // (null: not folded); see k_plan_fold
     const DevCol *cols;
     const PlanStream *streams;     // RLE streams counted by emitted bytes
     int32_t nstreams;
@@ -229,6 +231,9 @@ struct DeltaJob {
 // ---------------------------------------------------------------- launch wrappers
 void launch_decode(const DecodeArgs &a, hipStream_t s);
 void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s);
+// P = exclusive prefix of raw and Q = of val, in one scan
+void launch_prefix_raw2(const uint32_t *raw, const uint32_t *val, uint64_t n, uint64_t *P, uint64_t *Q, SegScratch *sc,
+                        hipStream_t s);
 // P[0] = 0, P[k] = base + raw[1] + ... + raw[k-1] (k >= 1) for u8 (width 1) / u16 (width 2) raw
 void launch_prefix_narrow(const void *raw, int width, uint64_t base, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s);
 
@@ -240,6 +245,8 @@ void launch_rle_events(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, con
                        uint8_t *ev, uint64_t *gend, uint64_t gend_stride, hipStream_t s);
 
 void launch_plan(const PlanArgs &a, hipStream_t s);
+void launch_plan_fold(const uint8_t *ev, uint64_t ev_stride, const PlanStream *streams, uint32_t nstreams, const uint32_t *raw,
+                      uint64_t n, uint32_t *val, hipStream_t s);
 // k_asm.hip: one job's file bytes gathered in HBM (pieces of <= 64 KiB: dst offset in `out`,
 // src = device address (dev) or offset into the host-built header blob)
 struct AsmPiece {
