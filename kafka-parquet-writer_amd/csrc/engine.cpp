@@ -224,7 +224,7 @@ int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, Rle
     }
     const size_t nj = jobs.size();
     ENS(r_last, npt * 8); ENS(r_prev, npt * 8); ENS(r_lrcnt, npt * 4); ENS(r_lroff, npt * 4);
-    ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_rg, e0 * 4);
+    ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_lrf, e0); ENS(r_rg, e0 * 4);
     ENS(r_rb, e0 * 4); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8);
     std::vector<uint8_t *> dp;   // jobs first: d_jobs.as<RleJob>() is the job table
     if (int st = upload_parts(d_jobs, {{jobs.data(), nj * sizeof(RleJob)}, {ptj.data(), npt * 4}, {etj.data(), net * 4}}, dp))
@@ -237,6 +237,7 @@ int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, Rle
     sc.etile_job = (uint32_t *)dp[2];
     sc.lr_a = r_lra.as<uint32_t>();
     sc.lr_b = r_lrb.as<uint32_t>();
+    sc.lr_rle = nullptr;   // kept by the planning jobs only (set by the caller)
     sc.r_g = r_rg.as<uint32_t>();
     sc.r_b = r_rb.as<uint32_t>();
     sc.r_boff = r_rboff.as<uint64_t>();
@@ -391,6 +392,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         }
         int st = run_rle(pj, npt, net, sc);
         if (st) return st;
+        sc.lr_rle = r_lrf.as<uint8_t>();   // k_plan's walkers read the global parse's decision per long run
         if (v2_ && nbool) {
             ENS(d_cbits_ptr, nbool * sizeof(uint64_t *));
             CK(xh2d(d_cbits_ptr.p, cbits.data(), nbool * sizeof(uint64_t *), s));
@@ -399,11 +401,15 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         }
         ENS(d_ev, (uint64_t)nstreams * ev_stride);
         ENS(d_E, (uint64_t)nstreams * (ev_stride / 8 + 1) * 4);
-        ENS(d_gend, (uint64_t)nstreams * nwords * 8);
         CK(hipMemsetAsync(d_ev.p, 0, (uint64_t)nstreams * ev_stride, s));
-        CK(hipMemsetAsync(d_gend.p, 0, (uint64_t)nstreams * nwords * 8, s));
+        // the RLE-run end bitmaps: only the multi-page planners' walkers read them (k_plan's
+        // read the per-long-run decisions)
+        if (mp_) {
+            ENS(d_gend, (uint64_t)nstreams * nwords * 8);
+            CK(hipMemsetAsync(d_gend.p, 0, (uint64_t)nstreams * nwords * 8, s));
+        }
         launch_rle_structure(d_jobs.as<RleJob>(), (int)nstreams, npt, net, sc, s);
-        launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), d_gend.as<uint64_t>(), nwords, s);
+        launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), mp_ ? d_gend.as<uint64_t>() : nullptr, nwords, s);
         launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ev_stride, nstreams, &seg_, s);
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     }
@@ -435,6 +441,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     PlanArgs pa{};
     pa.n = ne; pa.final_flush = final_flush ? 1 : 0; pa.ncols = nc; pa.next_rg_size = next_rg_size;
     pa.P = d_P.as<uint64_t>(); pa.Q = fold ? d_Q.as<uint64_t>() : nullptr; pa.cols = d_cols.as<DevCol>();
+    pa.jobs = d_jobs.as<RleJob>(); pa.lr_a = sc.lr_a; pa.lr_b = sc.lr_b; pa.lr_off = sc.lr_off; pa.lr_rle = sc.lr_rle;
     pa.streams = d_streams.as<PlanStream>(); pa.nstreams = (int32_t)nstreams;
     pa.nbool = v2_ ? 0 : (int32_t)nbool; pa.bool_cols = d_bool.as<uint32_t>();
     pa.E8 = nstreams ? d_E.as<uint32_t>() : nullptr; pa.ev = nstreams ? d_ev.as<uint8_t>() : nullptr; pa.ev_stride = ev_stride;

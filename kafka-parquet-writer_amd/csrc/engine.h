@@ -155,7 +155,7 @@ private:
     // planning
     DevBuf d_ev, d_E, d_gend, d_plan;
     // rle scratch (shared by planning and encoding)
-    DevBuf r_last, r_prev, r_lrcnt, r_lroff, r_lra, r_lrb, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;   // d_jobs: jobs + tile maps
+    DevBuf r_last, r_prev, r_lrcnt, r_lroff, r_lra, r_lrb, r_lrf, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;   // d_jobs: jobs + tile maps
     // chunks
     DevBuf d_chunks, d_ctile, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
         d_tile_cnt, d_tile_sz, d_ht, d_ids, d_ent_rec, d_ent_boff, d_ptab,   // d_ptab: page table (engine.cpp)

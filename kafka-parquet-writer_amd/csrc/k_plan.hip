@@ -179,11 +179,103 @@ __device__ __forceinline__ uint64_t pc_at(const DevCol &c, uint64_t x)
 // them, and from global memory each read added a dependent load ahead of the stream's own
 // (C3: 199 streams, ~20 evaluations per row group)
 struct PlanSt {
-    const uint64_t *bits;
-    uint64_t len;
     const uint64_t *rpres;   // rank-indexed stream: the presence bits and counts of its column
     const uint32_t *rpcnt;
+    const uint32_t *lra, *lrb;   // the stream's long runs (K3 structure of the planning jobs)
+    const uint32_t *lroff;       // per position tile of the stream: its first long run ending there
+    const uint8_t *lrle;         // per long run: the global parse took it as an RLE run
+    uint32_t nlong, ntiles;
+    int64_t len;
 };
+
+// k_plan's walker: the parse started at the row group's first position, stepped over the long
+// runs (maximal runs of >= 8 equal values, k_rle.hip) rather than over positions.  Its groups
+// start at gs, gs + 8, ... (phase gs mod 8) until an RLE run: a long run [a, b) is one iff its
+// first group start g = a + ((gs - a) mod 8) has g + 8 <= b; the (g - gs) / 8 groups before it
+// cost 1 byte each (+1 run header per 63), the run varint((b - g) << 1) + 1 at position b, and
+// the next gap starts at b.  The parse has converged with the global one (started at 0) once
+// both take the same long run as an RLE run (lr_rle), and from there E_s = E_g + delta.
+struct LWalker {
+    int64_t gs;         // start of the open gap (bit-packed groups from here)
+    uint64_t eacc;      // bytes of the events before gs
+    int64_t conv_pos;
+    int64_t delta;
+    uint32_t cur;       // next long run
+    uint32_t state;     // 0 walking, 1 converged, 2 no long runs left (closed form)
+};
+__device__ __forceinline__ uint64_t bp_bytes(uint64_t G) { return G + (G + 62) / 63; }
+
+__device__ __forceinline__ void lw_init(LWalker &w, const PlanSt &S, int64_t p)
+{
+    w.gs = p; w.eacc = 0; w.conv_pos = -1; w.delta = 0; w.state = 0;
+    // first long run ending after p: a binary search among the runs ending in p's tile
+    const uint32_t t = (uint32_t)((uint64_t)p / KPW_TILE_P);
+    uint32_t lo = t < S.ntiles ? S.lroff[t] : S.nlong;
+    uint32_t hi = t + 1 < S.ntiles ? S.lroff[t + 1] : S.nlong;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((int64_t)S.lrb[mid] <= p) lo = mid + 1; else hi = mid;
+    }
+    w.cur = lo;
+}
+
+// the walker's value at r once it no longer walks: converged, or the closed-form final gap
+__device__ __forceinline__ uint64_t lw_value(const LWalker &w, int64_t r, int64_t n, const EvView &Eg)
+{
+    if (w.state == 1) return (uint64_t)((int64_t)ev_prefix(Eg, (uint64_t)r) + w.delta);
+    const int64_t lim = r < n ? r : n;
+    return w.eacc + (lim > w.gs ? bp_bytes((uint64_t)(lim - w.gs) >> 3) : 0);
+}
+
+// E_s(r): the bytes the parse started at the row group's start emitted before position r
+// (queries come in increasing r)
+__device__ uint64_t lw_query(LWalker &w, int64_t r, const PlanSt &S, const EvView &Eg)
+{
+    const int64_t n = S.len;
+    uint64_t cap = ~0ull;   // groups of the open gap before the next RLE run
+    bool stop = false;
+    while (!stop && w.state == 0) {
+        if (w.cur >= S.nlong) { w.state = 2; break; }
+        // 8 long runs per round: their loads issue together (one latency per 8 runs; C3 walks
+        // ~150 runs before the parses meet)
+        const uint32_t nb = S.nlong - w.cur < 8 ? S.nlong - w.cur : 8;
+        uint32_t A[8], B[8], Fl[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const bool v = (uint32_t)i < nb;
+            A[i] = v ? S.lra[w.cur + i] : 0;
+            B[i] = v ? S.lrb[w.cur + i] : 0;
+            Fl[i] = v ? S.lrle[w.cur + i] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            if ((uint32_t)i >= nb) break;
+            const int64_t b = B[i];
+            int64_t a = A[i];
+            if (a >= r) { stop = true; break; }        // every later event of the gap's groups: >= r
+            if (a < w.gs) a = w.gs;                    // the run the row group starts in
+            const int64_t g = a + ((w.gs - a) & 7);
+            if (g + 8 > b) { w.cur++; continue; }      // bit-packed in this phase
+            const uint64_t G = (uint64_t)(g - w.gs) >> 3;
+            if (r <= b) { cap = G; stop = true; break; }   // the run's event (at b) is not before r
+            w.eacc += bp_bytes(G) + varint_len32((uint32_t)(b - g) << 1) + 1;
+            w.gs = b;
+            w.cur++;
+            if (Fl[i]) {   // the global parse ends an RLE run at b too
+                w.state = 1;
+                w.conv_pos = b;
+                w.delta = (int64_t)w.eacc - (int64_t)ev_prefix(Eg, (uint64_t)b + 1);
+                stop = true;
+                break;
+            }
+        }
+    }
+    if (w.state != 0) return lw_value(w, r, n, Eg);
+    const int64_t lim = r < n ? r : n;
+    uint64_t G = lim > w.gs ? (uint64_t)(lim - w.gs) >> 3 : 0;
+    if (G > cap) G = cap;
+    return w.eacc + bp_bytes(G);
+}
 struct PlanBool {
     const uint64_t *pres;    // null: REQUIRED
     const uint32_t *pcnt;
@@ -212,7 +304,7 @@ __device__ __forceinline__ uint64_t bool_bytes(const PlanBool &B, int64_t s, int
 
 // folded (F = D - P[s]): the record-indexed streams are in Q[r] + F
 template <int PLAN_T>
-__device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, const PlanSt *St, const PlanBool *Bo, int64_t s, int64_t r, bool folded,
+__device__ uint64_t eval_mem(const PlanArgs &a, LWalker *W, const PlanSt *St, const PlanBool *Bo, int64_t s, int64_t r, bool folded,
                              int64_t F)
 {
     __shared__ uint64_t red[PLAN_T / 64];
@@ -222,8 +314,8 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, const PlanSt *St, con
     for (int k = tid; k < a.nstreams; k += PLAN_T) {
         const PlanSt &S = St[k];
         if (folded && !S.rpres) continue;
-        Walker w = W[k];   // in registers for the walk
-        part += walker_query(w, st_pos(S, r), SrcDirect{S.bits, a.gend + (uint64_t)k * a.gend_stride}, S.len, ev_view(a, k));
+        LWalker w = W[k];   // in registers for the walk
+        part += lw_query(w, st_pos(S, r), S, ev_view(a, k));
         W[k] = w;
     }
     for (int k = tid; k < a.nbool; k += PLAN_T) part += bool_bytes(Bo[k], s, r);
@@ -243,7 +335,7 @@ __device__ uint64_t eval_mem(const PlanArgs &a, Walker *W, const PlanSt *St, con
 // g, g + 16, ... (independent loads, no walking), and the 16 partial sums meet in LDS; every
 // lane j returns the memSize of point j.
 template <int PLAN_T>
-__device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, const PlanSt *St, const PlanBool *Bo, int64_t s,
+__device__ uint64_t eval_mem_points(const PlanArgs &a, const LWalker *W, const PlanSt *St, const PlanBool *Bo, int64_t s,
                                     int64_t rc, bool folded, int64_t F)
 {
     __shared__ uint64_t red[PLAN_T];
@@ -256,9 +348,7 @@ __device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, const Pl
         if (g == 0) part = folded ? (uint64_t)((int64_t)a.Q[r] + F) : a.P[r] - a.P[s];
         for (int k = g; k < a.nstreams; k += NW) {
             if (folded && !St[k].rpres) continue;
-            const Walker &w = W[k];
-            part += w.state == 1 ? (uint64_t)((int64_t)ev_prefix(ev_view(a, k), (uint64_t)st_pos(St[k], r)) + w.delta)
-                                 : w.eacc;
+            part += lw_value(W[k], st_pos(St[k], r), St[k].len, ev_view(a, k));
         }
         for (int k = g; k < a.nbool; k += NW) part += bool_bytes(Bo[k], s, r);
     }
@@ -272,7 +362,7 @@ __device__ uint64_t eval_mem_points(const PlanArgs &a, const Walker *W, const Pl
 }
 
 template <int PLAN_T>
-__device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walker *W, const PlanSt *St, int64_t r)
+__device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const LWalker *W, const PlanSt *St, int64_t r)
 {
     bool ok = true;
     for (int k = threadIdx.x; k < a.nstreams; k += PLAN_T)
@@ -282,7 +372,7 @@ __device__ __forceinline__ bool walkers_converged(const PlanArgs &a, const Walke
 
 // Every record-indexed stream's walker converged: F = D - P[s] (D = the sum of their deltas).
 template <int PLAN_T>
-__device__ bool try_fold(const PlanArgs &a, const Walker *W, const PlanSt *St, int64_t s, int64_t &F)
+__device__ bool try_fold(const PlanArgs &a, const LWalker *W, const PlanSt *St, int64_t s, int64_t &F)
 {
     __shared__ uint64_t red[PLAN_T / 64];
     const int tid = threadIdx.x;
@@ -305,15 +395,19 @@ __device__ bool try_fold(const PlanArgs &a, const Walker *W, const PlanSt *St, i
 template <int PLAN_T>
 __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
 {
-    __shared__ Walker W[MAX_STREAMS];
+    __shared__ LWalker W[MAX_STREAMS];
     __shared__ PlanSt St[MAX_STREAMS];
     __shared__ PlanBool Bo[MAX_COLS];
     const int tid = threadIdx.x;
     for (int k = tid; k < a.nstreams; k += PLAN_T) {
         const PlanStream S = a.streams[k];
+        const RleJob &J = a.jobs[k];
         PlanSt t;
-        t.bits = S.bits; t.len = S.len; t.rpres = nullptr; t.rpcnt = nullptr;
+        t.rpres = nullptr; t.rpcnt = nullptr;
         if (S.rank_col >= 0) { t.rpres = a.cols[S.rank_col].pres; t.rpcnt = a.cols[S.rank_col].pcnt; }
+        t.lra = a.lr_a + J.e0; t.lrb = a.lr_b + J.e0; t.lroff = a.lr_off + J.tile0;
+        t.lrle = a.lr_rle + J.e0;
+        t.nlong = J.n_long; t.ntiles = J.ntiles; t.len = J.len;
         St[k] = t;
     }
     for (int k = tid; k < a.nbool; k += PLAN_T) {
@@ -341,12 +435,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
 #define PP_OUT()
 #endif
     for (;;) {
-        for (int k = tid; k < a.nstreams; k += PLAN_T) {
-            Walker w;
-            w.p = st_pos(St[k], s); w.conv_pos = -1; w.delta = 0; w.eacc = 0; w.pend_pos = -1; w.pend_next = 0;
-            w.pend_bytes = 0; w.pend_rle = 0; w.grp = 0; w.state = 0;
-            W[k] = w;
-        }
+        for (int k = tid; k < a.nstreams; k += PLAN_T) lw_init(W[k], St[k], st_pos(St[k], s));
         __syncthreads();
         int64_t rc = 100;
         bool cut = false;

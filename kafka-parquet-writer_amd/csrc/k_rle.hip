@@ -181,7 +181,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const 
 // written as (g, b).  The job's last element tile stores n_rle.
 
 __global__ void __launch_bounds__(KPW_BLOCK) k_phase(RleJob *jobs, const uint32_t *etile_job, const uint32_t *lr_a,
-                                                     const uint32_t *lr_b, uint32_t *r_g, uint32_t *r_b, uint32_t nt, LbView L)
+                                                     const uint32_t *lr_b, uint32_t *r_g, uint32_t *r_b, uint8_t *lr_rle, uint32_t nt,
+                                                     LbView L)
 {
     __shared__ uint32_t lds[KPW_BLOCK];
     __shared__ uint32_t c0, c1;
@@ -203,6 +204,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_phase(RleJob *jobs, const uint32_
     const uint32_t phi = pm_get(ex, pm_get(pre, 0));
     const uint32_t g = a + ((phi - a) & 7u);
     const uint32_t rle = (valid && g + 8 <= b) ? 1u : 0u;
+    if (lr_rle && valid) lr_rle[J.e0 + k] = (uint8_t)rle;
     uint32_t t2;
     const uint32_t idx = block_scan_excl<uint32_t, OpSum32>(rle, lds, &t2);
     const uint32_t off = lb_tile<uint32_t, OpSum32>(L, nt, u, et0, t2, u == et0, u != et0, &c1);
@@ -343,7 +345,7 @@ __device__ __forceinline__ void rle_write_groups(const RleJob *jobs, const uint3
 }
 
 // Planning mode: per-position emitted-byte events (event at the position whose write
-// emits the bytes) and a bitmask of RLE-run end positions.
+// emits the bytes) and a bitmask of RLE-run end positions (gend; null: not kept).
 __device__ __forceinline__ void rle_ev_runs(const RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
                                             const uint32_t *r_b, uint8_t *ev, uint64_t *gend, uint64_t gend_stride, uint32_t u)
 {
@@ -354,7 +356,7 @@ __device__ __forceinline__ void rle_ev_runs(const RleJob *jobs, const uint32_t *
     const uint32_t g = r_g[J.e0 + k], b = r_b[J.e0 + k];
     if (b >= J.len) return;  // emitted only by toBytes()
     ev[J.out_off + b] = (uint8_t)rle_bytes(b - g, J.bw);
-    atomicOr((unsigned long long *)&gend[j * gend_stride + (b >> 6)], 1ull << (b & 63));
+    if (gend) atomicOr((unsigned long long *)&gend[j * gend_stride + (b >> 6)], 1ull << (b & 63));
 }
 
 __device__ __forceinline__ void rle_ev_groups(const RleJob *jobs, const uint32_t *ptile_job, const uint32_t *r_g,
@@ -406,7 +408,7 @@ void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t
     LbView L = lb_prepare(sc.seg, 2ull * n_etiles, s);
     if (!L.w) return;
     hipLaunchKernelGGL(k_phase, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.lr_a, sc.lr_b, sc.r_g, sc.r_b,
-                       n_etiles, L);
+                       sc.lr_rle, n_etiles, L);
     L = lb_prepare(sc.seg, 2ull * n_etiles, s);
     if (!L.w) return;
     hipLaunchKernelGGL(k_r_sizes, dim3(n_etiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.etile_job, sc.r_g, sc.r_b, sc.r_boff, sc.r_goff,

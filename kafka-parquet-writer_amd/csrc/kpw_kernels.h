@@ -84,6 +84,7 @@ struct RleScratch {
     uint32_t *lr_cnt, *lr_off;     // per position tile: long runs ending in it / their offset
     uint32_t *etile_job;           // element tile -> job
     uint32_t *lr_a, *lr_b;         // long runs (a, b)
+    uint8_t *lr_rle;               // per long run: the parse took it as an RLE run (planning; null: not kept)
     uint32_t *r_g, *r_b;           // RLE runs (g, b)
     uint64_t *r_boff, *r_goff;     // per RLE run: byte offset of its gap, groups before its gap
     SegScratch *seg;               // the handle's scan scratch (look-back status words)
@@ -109,6 +110,9 @@ struct PlanArgs {
     int32_t ncols;
     int64_t next_rg_size;          // nextRowGroupSize
     const uint64_t *P;             // exclusive prefix of raw bytes [n+1]
+    const RleJob *jobs;            // the streams' K3 planning jobs (job k = stream k) and long runs
+    const uint32_t *lr_a, *lr_b, *lr_off;
+    const uint8_t *lr_rle;
     const uint64_t *Q;             // [n+1] P + the global parse's bytes of every record-indexed stream
                                    // (null: not folded); see k_plan_fold
     const DevCol *cols;
