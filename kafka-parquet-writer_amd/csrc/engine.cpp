@@ -324,15 +324,22 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     CK(hipEventRecord(kev_[1], s));
     CK(hipGetLastError());
     CK(hipEventRecord(ev_[1], s));
+    // K1's first invalid record bounds the batch.  The single-page path does not wait for it: it
+    // plans over all n records and learns the verdict with the plan (k_plan copies it), re-planning
+    // over the valid prefix in the rare batch that has one; the multi-page path reads it now.
     uint64_t err_idx = ~0ull;
-    CK(xd2h(&err_idx, d_err, 8, s));
-    CK(xsync(s));
-    const uint64_t ne = std::min<uint64_t>(n, err_idx);
-    out.invalid_record = err_idx < n ? (int64_t)err_idx : -1;
+    const bool optimistic = !mp_;
+    if (!optimistic) {
+        CK(xd2h(&err_idx, d_err, 8, s));
+        CK(xsync(s));
+    }
+    uint64_t ne = std::min<uint64_t>(n, err_idx);
 
     // ---------------------------------------------------------------- planning inputs
     if (nopt) launch_pcnt_scan(d_cols.as<DevCol>(), d_opt.as<uint32_t>(), nopt, nwords, &seg_, s);
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
+replan:
+    out.invalid_record = err_idx < n ? (int64_t)err_idx : -1;
     if (ne == 0) {
         out.records_consumed = 0;
         out.open_records = 0;
@@ -410,26 +417,26 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         }
         launch_rle_structure(d_jobs.as<RleJob>(), (int)nstreams, npt, net, sc, s);
         launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), mp_ ? d_gend.as<uint64_t>() : nullptr, nwords, s);
-        launch_scan_events(d_ev.as<uint8_t>(), d_E.as<uint32_t>(), ev_stride, nstreams, &seg_, s);
-        if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     }
-    // raw-byte prefix P; for the single-page planner also Q = P + the record-indexed streams'
-    // global event bytes (k_plan folds converged streams into one load), in the same scan
+    // one scan for the planner's prefixes per group of 8 positions: the event streams' E8, the raw
+    // record sizes' P8 and, for the single-page planner of a wide schema, Q8 over raw + the
+    // record-indexed streams' global event bytes (k_plan folds converged streams into one load)
     uint32_t nfold = 0;
     for (uint32_t k = 0; k < nstreams; k++) nfold += hs[k].rank_col < 0 ? 1 : 0;
     // (few streams: the planner's evaluations are cheap already and the fold's extra pass over
     // the batch costs more, C2 4 streams: +0.8 ms per 100 M records; C3 199 streams: -6 ms per 10 M)
     const bool fold = plan && !mp_ && nfold >= 16 && !fold_off();
-    ENS(d_P, (ne + 1) * 8);
+    const uint64_t groups = ev_stride / 8;
+    ENS(d_P, (groups + 1) * 8);
     if (fold) {
-        ENS(d_Q, (ne + 1) * 8);
+        ENS(d_Q, (groups + 1) * 8);
         ENS(d_qv, ne * 4);
         launch_plan_fold(d_ev.as<uint8_t>(), ev_stride, d_streams.as<PlanStream>(), nstreams, d_raw.as<uint32_t>(), ne,
                          d_qv.as<uint32_t>(), s);
-        launch_prefix_raw2(d_raw.as<uint32_t>(), d_qv.as<uint32_t>(), ne, d_P.as<uint64_t>(), d_Q.as<uint64_t>(), &seg_, s);
-    } else {
-        launch_prefix_raw(d_raw.as<uint32_t>(), ne, d_P.as<uint64_t>(), &seg_, s);
     }
+    launch_plan_prefix(plan ? d_ev.as<uint8_t>() : nullptr, plan ? d_E.as<uint32_t>() : nullptr, plan ? nstreams : 0, ev_stride,
+                       d_raw.as<uint32_t>(), fold ? d_qv.as<uint32_t>() : nullptr, ne, d_P.as<uint64_t>(),
+                       fold ? d_Q.as<uint64_t>() : nullptr, &seg_, s);
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     if (mp_) return encode_mp(d_data, d_off, n, ne, final_flush, next_rg_size, hc, nwords, ev_stride, out);
     // ---------------------------------------------------------------- A9 plan
@@ -440,13 +447,15 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ENS(d_plan, (8 + 2 * (size_t)max_rgs) * 8);
     PlanArgs pa{};
     pa.n = ne; pa.final_flush = final_flush ? 1 : 0; pa.ncols = nc; pa.next_rg_size = next_rg_size;
-    pa.P = d_P.as<uint64_t>(); pa.Q = fold ? d_Q.as<uint64_t>() : nullptr; pa.cols = d_cols.as<DevCol>();
+    pa.P8 = d_P.as<uint64_t>(); pa.raw = d_raw.as<uint32_t>(); pa.cols = d_cols.as<DevCol>();
+    pa.Q8 = fold ? d_Q.as<uint64_t>() : nullptr; pa.qv = fold ? d_qv.as<uint32_t>() : nullptr;
     pa.jobs = d_jobs.as<RleJob>(); pa.lr_a = sc.lr_a; pa.lr_b = sc.lr_b; pa.lr_off = sc.lr_off; pa.lr_rle = sc.lr_rle;
     pa.streams = d_streams.as<PlanStream>(); pa.nstreams = (int32_t)nstreams;
     pa.nbool = v2_ ? 0 : (int32_t)nbool; pa.bool_cols = d_bool.as<uint32_t>();
     pa.E8 = nstreams ? d_E.as<uint32_t>() : nullptr; pa.ev = nstreams ? d_ev.as<uint8_t>() : nullptr; pa.ev_stride = ev_stride;
     pa.gend = nstreams ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
     pa.rg = d_plan.as<int64_t>() + 8; pa.max_rgs = max_rgs;
+    pa.err = d_err;
     pa.max_cuts = max_cuts;
     pa.out = d_plan.as<int64_t>();
     launch_plan(pa, s);
@@ -457,11 +466,14 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     CK(xsync(s));
     CK(hipEventRecord(ev_[2], s));
     const int64_t *po = pl.data();
+    if (optimistic && ne == n && (uint64_t)po[4] < n) {   // K1 found an invalid record: plan its prefix
+        err_idx = ne = (uint64_t)po[4];
+        goto replan;
+    }
     const int nrg = (int)po[0];
 #ifdef KPW_PLAN_PROF
-    fprintf(stderr, "[plan_prof] rgs %d total %.3f ms walk %.3f ms (%lld) conv %.3f ms (%lld) points %lld\n", nrg,
-            po[4] / 1e5, po[5] / 1e5, (long long)(po[7] & 0x1fffff), po[6] / 1e5, (long long)((po[7] >> 21) & 0x1fffff),
-            (long long)(po[7] >> 42));
+    fprintf(stderr, "[plan_prof] rgs %d total %.3f ms walk %.3f ms (%lld) conv (%lld) points %lld\n", nrg, po[5] / 1e5,
+            po[6] / 1e5, (long long)(po[7] & 0x1fffff), (long long)((po[7] >> 21) & 0x1fffff), (long long)(po[7] >> 42));
 #endif
     if (po[3]) return fail(KPW_ERR_DEVICE, "planner row-group table overflow");
     if (nrg > head) {   // more row groups than the first copy held
@@ -600,7 +612,6 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     // chunk descriptors, then 4 words of string-statistics metadata per chunk (one readback)
     static_assert(sizeof(ChunkDesc) % 8 == 0, "metadata words follow the descriptors");
-    ENS(d_chunks, nch * (sizeof(ChunkDesc) + 32));
     ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
     ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8);
     ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
@@ -616,10 +627,16 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     uint64_t *const d_pcoff = d_ppre + P2, *const d_pclen = d_pcoff + P2;
     uint32_t *const d_coll = (uint32_t *)(pt + 2);
     for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
-    std::vector<uint8_t *> ctp;   // chunk tile -> chunk, first tile and tile count per chunk, insertion order
-    if (int st = upload_parts(d_ctile, {{ctj.data(), (size_t)nct * 4}, {cfirst.data(), (size_t)nch * 4}, {ccount.data(), (size_t)nch * 4},
-                                        {dorder.data(), dorder.size() * 4}}, ctp))
+    // one upload: descriptors (+ room for their statistics metadata), then chunk tile -> chunk,
+    // first tile and tile count per chunk, dictionary insertion order
+    static thread_local std::vector<uint8_t> chbuf;
+    chbuf.assign((size_t)nch * (sizeof(ChunkDesc) + 32), 0);
+    memcpy(chbuf.data(), ch.data(), (size_t)nch * sizeof(ChunkDesc));
+    std::vector<uint8_t *> ctp;
+    if (int st = upload_parts(d_chunks, {{chbuf.data(), chbuf.size()}, {ctj.data(), (size_t)nct * 4}, {cfirst.data(), (size_t)nch * 4},
+                                         {ccount.data(), (size_t)nch * 4}, {dorder.data(), dorder.size() * 4}}, ctp))
         return st;
+    ctp.erase(ctp.begin());   // (the descriptors: d_chunks.p)
     ChunkArgs a{};
     a.ch = d_chunks.as<ChunkDesc>(); a.nchunks = nch; a.nctiles = nct; a.cols = d_cols.as<DevCol>(); a.data = d_data;
     a.ctile_chunk = (uint32_t *)ctp[0]; a.ctile_first = (uint32_t *)ctp[1];
@@ -665,13 +682,13 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     // BYTE_ARRAY dictionaries are keyed by a 64-bit hash and verified byte-for-byte; a
     // verified collision re-runs the chunk phase with byte comparisons (exact_strings).
     // A hint-sized table that overflowed (flag word 1) re-runs the phase at full size.
-    for (bool exact = false;;) {
+    for (bool exact = false, first = true;; first = false) {
         a.exact_strings = exact ? 1 : 0;
-        CK(xh2d(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), s));
-        CK(hipMemsetAsync(d_coll, 0, 8, s));
-        if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), s));
+        if (!first) CK(xh2d(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), s));   // a re-run starts from the host's
         if (v2_ && !dj.empty()) CK(xh2d(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), s));
         // ------------------------------------------------------------ K6 + K2
+        a.ht_clear = d_ht.as<HtSlot>(); a.ht_clear_n = ht_off;   // K6 empties the hash tables and the flags
+        a.flags_clear = (uint64_t *)d_coll;
         launch_chunk_stats(a, s);
         CK(hipGetLastError());
         if (!ej.empty()) {
@@ -715,11 +732,11 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     }
     // +512: K7 reads its input through 256-byte register windows that may run past the last page
     ENS(d_body, body_tot + 512 + 4096);   // + 4 KiB: the writer D2Hs whole 4 KiB units
-    // only the tail K7's windows may read is cleared here; the PLAIN boolean values are zeroed
-    // by k_zero_bool (launch_chunk_write) and every other body byte is written by its kernel
-    // (KPW_BODY_POISON=1 fills the body with 0xAB first: the GPU parity suite checks that)
+    // only the tail K7's windows may read and the PLAIN boolean values are cleared (k_chunk_prep,
+    // launch_chunk_write); every other body byte is written by its kernel (KPW_BODY_POISON=1 fills
+    // the body with 0xAB first: the GPU parity suite checks that)
     if (body_poison()) CK(hipMemsetAsync(d_body.p, 0xAB, body_tot, s));
-    CK(hipMemsetAsync(d_body.as<uint8_t>() + body_tot, 0, 512, s));
+    a.body_tail = body_tot;
     launch_chunk_write(a, d_jobs.as<RleJob>(), d_body.as<uint8_t>(), s);
     if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), s);
     if (v2_) {
@@ -856,6 +873,7 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         CK(xd2h(md.data(), d_chunks.p, md.size(), s));
         CK(xsync(s));
         memcpy(ch.data(), md.data(), nch * sizeof(ChunkDesc));
+        for (auto &C : ch) chunk_stats_derive(C);
         memcpy(smeta.data(), md.data() + nch * sizeof(ChunkDesc), nch * 32);
     }
     {   // next encode's table hints: the most entries of each column's chunks, none after a fallback

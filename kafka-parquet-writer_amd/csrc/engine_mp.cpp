@@ -302,9 +302,9 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         ap.exact_strings = ad.exact_strings = attempt;
         CK(xh2d(d_chunks.p, pg.data(), npg * sizeof(ChunkDesc), st));
         CK(xh2d(mp_dch.p, dch.data(), nc * sizeof(ChunkDesc), st));
-        CK(hipMemsetAsync(d_coll, 0, 4, st));
-        if (ht_off) CK(hipMemsetAsync(d_ht.p, 0xFF, ht_off * sizeof(HtSlot), st));
         if (v2_ && !dj.empty()) CK(xh2d(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), st));
+        ap.ht_clear = d_ht.as<HtSlot>(); ap.ht_clear_n = ht_off;   // K6 empties the hash tables and the flags
+        ap.flags_clear = (uint64_t *)d_coll;
         launch_chunk_stats(ap, st);                          // K6 per page (+ nn, raw bytes)
         if (!ej.empty()) {
             int rs = run_rle(ej, enpt, enet, esc);
@@ -343,11 +343,11 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         }
     }
     ENS(d_body, body_tot + 512 + 4096);   // + 4 KiB: the writer D2Hs whole 4 KiB units
-    // only the tail K7's windows may read is cleared here; the PLAIN boolean values are zeroed
-    // by k_zero_bool (launch_chunk_write) and every other body byte is written by its kernel
-    // (KPW_BODY_POISON=1 fills the body with 0xAB first: the GPU parity suite checks that)
+    // only the tail K7's windows may read and the PLAIN boolean values are cleared (k_chunk_prep,
+    // launch_chunk_write); every other body byte is written by its kernel (KPW_BODY_POISON=1 fills
+    // the body with 0xAB first: the GPU parity suite checks that)
     if (body_poison()) CK(hipMemsetAsync(d_body.p, 0xAB, body_tot, st));
-    CK(hipMemsetAsync(d_body.as<uint8_t>() + body_tot, 0, 512, st));
+    ap.body_tail = body_tot;
     launch_mp_dictpage_off(ap.ch, ad.ch, nc, st);
     launch_dict_page(ad, d_body.as<uint8_t>(), st);
     launch_chunk_write(ap, d_jobs.as<RleJob>(), d_body.as<uint8_t>(), st);
@@ -413,6 +413,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         CK(xd2h(md.data(), d_chunks.p, md.size(), st));
         CK(xsync(st));
         memcpy(pg.data(), md.data(), npg * sizeof(ChunkDesc));
+        for (auto &C : pg) chunk_stats_derive(C);
         memcpy(smeta.data(), md.data() + npg * sizeof(ChunkDesc), npg * 32);
     }
     std::vector<std::string> bmin(npg), bmax(npg);
@@ -591,7 +592,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     CK(xh2d(mp_cstream.p, cstream.data(), nc * 4, st));
     CK(xh2d(mp_bstream.p, bstream.data(), nc * 4, st));
     uint64_t Ptot = 0;
-    CK(xd2h(&Ptot, d_P.as<uint64_t>() + ne, 8, st));
+    CK(xd2h(&Ptot, d_P.as<uint64_t>() + ev_stride / 8, 8, st));   // P8's total
     CK(xsync(st));
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
 

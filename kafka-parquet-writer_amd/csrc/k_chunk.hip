@@ -106,8 +106,12 @@ __device__ __forceinline__ bool str_eq(const DevCol &col, const uint8_t *data, u
 __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
                                                            const uint32_t *ctile_chunk, const uint32_t *ctile_first,
                                                            uint64_t *tile_raw, uint64_t *tile_smin, uint64_t *tile_smax,
-                                                           const uint64_t *data_end_p)
+                                                           const uint64_t *data_end_p, uint4 *ht_clear, uint64_t ht_clear_n,
+                                                           uint64_t *flags_clear)
 {
+    if (flags_clear && blockIdx.x == 0 && threadIdx.x == 0) *flags_clear = 0;   // set by the dictionary kernels after
+    for (uint64_t i = (uint64_t)blockIdx.x * KPW_BLOCK + threadIdx.x; i < ht_clear_n; i += (uint64_t)gridDim.x * KPW_BLOCK)
+        ht_clear[i] = make_uint4(~0u, ~0u, ~0u, ~0u);   // empty dictionary slots for the phase after
     const uint64_t data_end = *data_end_p;
     __shared__ uint64_t lds[KPW_BLOCK];
     const uint32_t t = blockIdx.x;
@@ -166,15 +170,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_stats(ChunkDesc *ch, const 
     }
 }
 
-// per chunk: null count, has_minmax (BYTE_ARRAY min/max: k_str_final)
-__global__ void k_chunk_stats_final(ChunkDesc *ch, int nchunks)
-{
-    const int ci = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ci >= nchunks) return;
-    ChunkDesc &C = ch[ci];
-    C.null_count = (uint64_t)(C.e - C.s) - C.nn;
-    C.has_minmax = C.nn > 0;
-}
+// (null_count = records - nn and has_minmax = nn > 0 are derived by the host from the read-back
+// descriptors, chunk_stats_derive)
 
 // BYTE_ARRAY min/max, after the dictionary phase: a complete dictionary holds every
 // distinct value of its chunk, so its entries stand in for the values (one entry per
@@ -435,11 +432,28 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
 // count (write=0) / assign (write=1) first occurrences in record order.  In the coalesced
 // tile layout record order is (k, wave, lane); the write pass ranks a thread's first
 // occurrences with one ballot + one wave scan per k and 32 (k, wave) totals in LDS.
+// per dictionary chunk after the insert pass: fallback, id width and id-job length
+__device__ void dict_jobs(ChunkDesc &C, RleJob *jobs, uint32_t max_dict_bytes, uint32_t *retry)
+{
+    if (!C.is_dict) return;
+    if (C.overflow && C.ht_plim) atomicOr(retry, 1u);   // hint-sized table too small: the host redoes the phase
+    if (C.dict_bytes > max_dict_bytes || C.overflow) C.fallback = 1;
+    if (C.id_job < 0) return;   // multi-page dictionary descriptor: pages carry the id jobs
+    RleJob &J = jobs[C.id_job];
+    if (C.fallback) { J.len = 0; J.bw = 0; return; }
+    // DictionaryValuesWriter.getBytes: bitWidth = getWidthFromMaxInt(dictSize - 1)
+    const uint32_t m = C.dict_n - 1;
+    C.bw = m ? 32 - __clz(m) : (C.dict_n ? 0 : 32);
+    J.len = C.nn;
+    J.bw = C.bw;
+}
+
 __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const DevCol *cols, const uint32_t *ctile_chunk,
                                                            const uint32_t *ctile_first, HtSlot *ht,
                                                            const uint32_t *slotof, uint32_t *tile_cnt, uint64_t *tile_sz,
                                                            const uint32_t *tile_cnt_off, const uint64_t *tile_sz_off,
-                                                           uint64_t *ent_rec, uint64_t *ent_boff, int write)
+                                                           uint64_t *ent_rec, uint64_t *ent_boff, int write, RleJob *jobs,
+                                                           uint32_t max_dict_bytes, uint32_t *retry)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
     __shared__ uint32_t ldu[KPW_BLOCK];
@@ -447,8 +461,12 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
     __shared__ uint64_t wsz[8][KPW_BLOCK / 64];
     const uint32_t t = blockIdx.x;
     const uint32_t ci = ctile_chunk[t];
-    const ChunkDesc &C = ch[ci];
-    const bool active = C.is_dict && !C.fallback && !(C.stop_tile && t - ctile_first[ci] >= C.stop_tile);
+    ChunkDesc &C = ch[ci];
+    // the dictionary outcome (dict_jobs, stored by the chunk's first tile) from the insert pass, so no tile
+    // depends on whether that store has happened yet
+    const bool fb = C.fallback || C.dict_bytes > max_dict_bytes || C.overflow;
+    if (!write && t == ctile_first[ci] && threadIdx.x == 0) dict_jobs(C, jobs, max_dict_bytes, retry);
+    const bool active = C.is_dict && !fb && !(C.stop_tile && t - ctile_first[ci] >= C.stop_tile);
     const DevCol col = cols[C.col];   // by value: not reloaded after stores
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
     uint32_t cnt = 0;
@@ -560,23 +578,6 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_ids(const ChunkDesc *ch, con
     }
 }
 
-__global__ void k_dict_jobs(ChunkDesc *ch, int nchunks, RleJob *jobs, uint32_t max_dict_bytes, uint32_t *retry)
-{
-    const int ci = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ci >= nchunks) return;
-    ChunkDesc &C = ch[ci];
-    if (!C.is_dict) return;
-    if (C.overflow && C.ht_plim) atomicOr(retry, 1u);   // hint-sized table too small: the host redoes the phase
-    if (C.dict_bytes > max_dict_bytes || C.overflow) C.fallback = 1;
-    if (C.id_job < 0) return;   // multi-page dictionary descriptor: pages carry the id jobs
-    RleJob &J = jobs[C.id_job];
-    if (C.fallback) { J.len = 0; J.bw = 0; return; }
-    // DictionaryValuesWriter.getBytes: bitWidth = getWidthFromMaxInt(dictSize - 1)
-    const uint32_t m = C.dict_n - 1;
-    C.bw = m ? 32 - __clz(m) : (C.dict_n ? 0 : 32);
-    J.len = C.nn;
-    J.bw = C.bw;
-}
 
 // ------------------------------------------------------------------ layout (one block, all chunks)
 
@@ -678,10 +679,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_layout(ChunkDesc *ch, int nchunks
 
 // ------------------------------------------------------------------ writers
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_chunk_headers(const ChunkDesc *ch, int nchunks, const DevCol *cols, uint8_t *out, int v2,
-                                                             const RleJob *jobs)
+__device__ __forceinline__ void chunk_header(const ChunkDesc *ch, int nchunks, const DevCol *cols, uint8_t *out, int v2,
+                                             const RleJob *jobs, int ci)
 {
-    const int ci = blockIdx.x * blockDim.x + threadIdx.x;
     if (ci >= nchunks) return;
     const ChunkDesc &C = ch[ci];
     const DevCol col = cols[C.col];   // by value: not reloaded after stores
@@ -862,15 +862,16 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_plain_bool(const ChunkDesc *ch, c
 
 // Zero the values part of the PLAIN boolean pages before k_plain_bool ORs its words in (the rest
 // of the page body is written in full by its kernels, so the body is not cleared as a whole).
-// Grid (chunks, 16): the dwords inside the range with dword stores, the edge bytes with byte stores.
-__global__ void __launch_bounds__(KPW_BLOCK) k_zero_bool(const ChunkDesc *ch, const DevCol *cols, uint8_t *out)
+// 16 blocks per chunk: the dwords inside the range with dword stores, the edge bytes with byte stores.
+constexpr uint32_t ZB_BLOCKS = 16;
+__device__ __forceinline__ void zero_bool(const ChunkDesc *ch, const DevCol *cols, uint8_t *out, uint32_t chunk, uint32_t y)
 {
-    const ChunkDesc &C = ch[blockIdx.x];
+    const ChunkDesc &C = ch[chunk];
     const DevCol col = cols[C.col];
     if (col.phys != 0 || C.bool_job >= 0 || C.val_len == 0) return;
     const uint64_t b = C.val_off, e = C.val_off + C.val_len;
     const uint64_t wb = (b + 3) & ~3ull, we = e & ~3ull;
-    const uint64_t tid = (uint64_t)blockIdx.y * KPW_BLOCK + threadIdx.x, nth = (uint64_t)gridDim.y * KPW_BLOCK;
+    const uint64_t tid = (uint64_t)y * KPW_BLOCK + threadIdx.x, nth = (uint64_t)ZB_BLOCKS * KPW_BLOCK;
     if (wb >= we) {
         for (uint64_t i = b + tid; i < e; i += nth) out[i] = 0;
         return;
@@ -879,6 +880,19 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_zero_bool(const ChunkDesc *ch, co
     for (uint64_t w = (wb >> 2) + tid; w < (we >> 2); w += nth) o32[w] = 0u;
     if (tid < wb - b) out[b + tid] = 0;
     if (tid < e - we) out[we + tid] = 0;
+}
+
+// One launch before the page writers: blocks [0, hb) the chunks' level-stream headers (a thread
+// per chunk), then ZB_BLOCKS per chunk zeroing the PLAIN boolean ranges, then one block clearing
+// the 512 bytes at tail_off (the body's end) that K7's read windows may reach past the last page.
+__global__ void __launch_bounds__(KPW_BLOCK) k_chunk_prep(const ChunkDesc *ch, int nchunks, const DevCol *cols, uint8_t *out, int v2,
+                                                          const RleJob *jobs, uint32_t hb, uint64_t tail_off)
+{
+    if (blockIdx.x < hb) { chunk_header(ch, nchunks, cols, out, v2, jobs, (int)(blockIdx.x * KPW_BLOCK + threadIdx.x)); return; }
+    const uint32_t b = blockIdx.x - hb;
+    if (b < (uint32_t)nchunks * ZB_BLOCKS) { zero_bool(ch, cols, out, b / ZB_BLOCKS, b % ZB_BLOCKS); return; }
+    out[tail_off + threadIdx.x] = 0;
+    out[tail_off + KPW_BLOCK + threadIdx.x] = 0;
 }
 
 // Binary statistics: meta[4c..4c+3] = (min offset, min len, max offset, max len) of chunk c
@@ -895,7 +909,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_stats_gather(const ChunkDesc *ch,
         if (ci < nchunks) {
             const ChunkDesc &C = ch[ci];
             const DevCol &col = cols[C.col];
-            bin = col.phys == 6 && C.has_minmax;
+            bin = col.phys == 6 && C.nn > 0;   // has_minmax
             if (!blob) {
                 if (bin) {
                     meta[4 * ci] = col.soff[C.smin]; meta[4 * ci + 1] = col.slen[C.smin];
@@ -930,8 +944,8 @@ void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, c
 void launch_chunk_stats(const ChunkArgs &a, hipStream_t s)
 {
     hipLaunchKernelGGL(k_chunk_stats, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
-                       a.tile_raw, a.tile_smin, a.tile_smax, a.data_end);
-    hipLaunchKernelGGL(k_chunk_stats_final, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks);
+                       a.tile_raw, a.tile_smin, a.tile_smax, a.data_end, (uint4 *)a.ht_clear, a.ht_clear_n,
+                       a.flags_clear);
 }
 
 // multi-page dictionary rounds: a chunk whose dictionary passed dictPageSize with the tiles of
@@ -964,14 +978,14 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
         hipLaunchKernelGGL(k_dict_insert, dim3(a.ndict_tiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order,
                            a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
     }
-    hipLaunchKernelGGL(k_dict_jobs, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, jobs, a.max_dict_bytes,
-                       a.collision + 1);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
-                       a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0);
+                       a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0, jobs, a.max_dict_bytes,
+                       a.collision + 1);
     seg_tile_scan_u32(a.tile_cnt, a.tile_cnt, a.ctile_chunk, a.nctiles, a.seg, s);
     seg_tile_scan_u64(a.tile_sz, a.tile_sz, a.ctile_chunk, a.nctiles, a.seg, s);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
-                       a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1);
+                       a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1, jobs, a.max_dict_bytes,
+                       a.collision + 1);
     hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht, a.ids,
                        a.data, a.ent_rec, a.data_end, a.collision);
     // BYTE_ARRAY statistics need the dictionary outcome (entries stand in for the values);
@@ -999,14 +1013,15 @@ void launch_layout(const ChunkArgs &a, RleJob *jobs, uint64_t *page_off, uint64_
 
 void launch_chunk_write(const ChunkArgs &a, const RleJob *jobs, uint8_t *out, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_chunk_headers, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a.ch, a.nchunks, a.cols, out, a.v2, jobs);
+    const uint32_t hb = (uint32_t)((a.nchunks + KPW_BLOCK - 1) / KPW_BLOCK);
+    hipLaunchKernelGGL(k_chunk_prep, dim3(hb + (uint32_t)a.nchunks * ZB_BLOCKS + 1), dim3(KPW_BLOCK), 0, s, a.ch, a.nchunks, a.cols, out,
+                       a.v2, jobs, hb, a.body_tail);
     if (!a.mp)   // multi-page: the dictionary page is written from the dictionary descriptors
         hipLaunchKernelGGL(k_dict_page, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
                            a.ent_rec, a.ent_boff, out);
     seg_tile_scan_u64(a.tile_raw, a.tile_raw_off, a.ctile_chunk, a.nctiles, a.seg, s);
     hipLaunchKernelGGL(k_plain, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.ctile_chunk, a.ctile_first,
                        a.tile_raw_off, out);
-    if (a.nchunks) hipLaunchKernelGGL(k_zero_bool, dim3(a.nchunks, 16), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, out);
     hipLaunchKernelGGL(k_plain_bool, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, out);
 }
 

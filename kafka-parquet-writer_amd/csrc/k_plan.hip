@@ -175,6 +175,18 @@ __device__ __forceinline__ uint64_t pc_at(const DevCol &c, uint64_t x)
     return (uint64_t)c.pcnt[wi] + (uint64_t)__popcll(m);
 }
 
+// prefix at position r of a sequence scanned per group of 8 (k_scan.hip PlanPrefixF): the
+// group's prefix plus the group's elements before r (independent loads)
+__device__ __forceinline__ uint64_t pref8(const uint64_t *X8, const uint32_t *x, int64_t r)
+{
+    const uint64_t g = (uint64_t)r >> 3;
+    uint64_t s = X8[g];
+    const uint32_t k = (uint32_t)r & 7;
+#pragma unroll
+    for (uint32_t i = 0; i < 7; i++) s += i < k ? x[8 * g + i] : 0u;
+    return s;
+}
+
 // k_plan's copies of the stream and boolean-column tables in LDS: every evaluation reads
 // them, and from global memory each read added a dependent load ahead of the stream's own
 // (C3: 199 streams, ~20 evaluations per row group)
@@ -310,7 +322,7 @@ __device__ uint64_t eval_mem(const PlanArgs &a, LWalker *W, const PlanSt *St, co
     __shared__ uint64_t red[PLAN_T / 64];
     const int tid = threadIdx.x;
     uint64_t part = 0;   // issued first: its latency overlaps the streams'
-    if (tid == 0) part = folded ? (uint64_t)((int64_t)a.Q[r] + F) : a.P[r] - a.P[s];
+    if (tid == 0) part = folded ? (uint64_t)((int64_t)pref8(a.Q8, a.qv, r) + F) : pref8(a.P8, a.raw, r) - pref8(a.P8, a.raw, s);
     for (int k = tid; k < a.nstreams; k += PLAN_T) {
         const PlanSt &S = St[k];
         if (folded && !S.rpres) continue;
@@ -345,7 +357,7 @@ __device__ uint64_t eval_mem_points(const PlanArgs &a, const LWalker *W, const P
     const int64_t r = s + rc + 10000 * (int64_t)j;
     uint64_t part = 0;
     if (r <= (int64_t)a.n) {
-        if (g == 0) part = folded ? (uint64_t)((int64_t)a.Q[r] + F) : a.P[r] - a.P[s];
+        if (g == 0) part = folded ? (uint64_t)((int64_t)pref8(a.Q8, a.qv, r) + F) : pref8(a.P8, a.raw, r) - pref8(a.P8, a.raw, s);
         for (int k = g; k < a.nstreams; k += NW) {
             if (folded && !St[k].rpres) continue;
             part += lw_value(W[k], st_pos(St[k], r), St[k].len, ev_view(a, k));
@@ -388,7 +400,7 @@ __device__ bool try_fold(const PlanArgs &a, const LWalker *W, const PlanSt *St, 
 #pragma unroll
     for (int i = 0; i < PLAN_T / 64; i++) D += red[i];
     __syncthreads();
-    F = (int64_t)D - (int64_t)a.P[s];
+    F = (int64_t)D - (int64_t)pref8(a.P8, a.raw, s);
     return true;
 }
 
@@ -423,13 +435,13 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
     int64_t overflow = 0;
 #ifdef KPW_PLAN_PROF
     // profiling build (tests/microbench): wall-clock ticks (100 MHz) per evaluation kind in
-    // out[4..7]: total, walking evaluations, converged single evaluations, counts
+    // out[5..7]: total, walking evaluations, counts
     const uint64_t pp_t0 = wall_clock64();
     uint64_t pp_unc = 0, pp_cnv = 0, pp_nu = 0, pp_nc = 0, pp_np = 0;
 #define PP_OUT()                                                                                   \
     if (tid == 0) {                                                                                \
-        a.out[4] = (int64_t)(wall_clock64() - pp_t0); a.out[5] = (int64_t)pp_unc;                  \
-        a.out[6] = (int64_t)pp_cnv; a.out[7] = (int64_t)(pp_nu | pp_nc << 21 | pp_np << 42);       \
+        a.out[5] = (int64_t)(wall_clock64() - pp_t0); a.out[6] = (int64_t)pp_unc;                  \
+        a.out[7] = (int64_t)(pp_nu | pp_nc << 21 | pp_np << 42);                                   \
     }
 #else
 #define PP_OUT()
@@ -444,7 +456,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
         int64_t F = 0;
         int64_t r = 0;
         while (s + rc <= n) {
-            if (a.Q && !folded) folded = try_fold<PLAN_T>(a, W, St, s, F);
+            if (a.Q8 && !folded) folded = try_fold<PLAN_T>(a, W, St, s, F);
             // Far from the cut every next check is recordCount + 10000 (the clamp): once the
             // walkers are converged, the block evaluates memSize at the next 64 clamp-step
             // check points and takes parquet-mr's decisions over them (one lane each), stopping
@@ -516,7 +528,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
             nrg++;
             s = r;
             if (a.max_cuts > 0 && nrg >= a.max_cuts) {   // the caller re-plans from s with the next limit
-                if (tid == 0) { a.out[0] = nrg; a.out[1] = s; a.out[2] = 0; a.out[3] = overflow; }
+                if (tid == 0) { a.out[0] = nrg; a.out[1] = s; a.out[2] = 0; a.out[3] = overflow; a.out[4] = (int64_t)*a.err; }
                 PP_OUT();
                 break;
             }
@@ -526,7 +538,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
         // the open row group [s, n)
         int64_t open_buf = 0;
         if (s < n) {
-            if (a.Q && !folded) folded = try_fold<PLAN_T>(a, W, St, s, F);
+            if (a.Q8 && !folded) folded = try_fold<PLAN_T>(a, W, St, s, F);
             open_buf = (int64_t)eval_mem<PLAN_T>(a, W, St, Bo, s, n, folded, F);
         }
         if (a.final_flush && s < n) {
@@ -541,6 +553,7 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
             a.out[1] = s;
             a.out[2] = open_buf;
             a.out[3] = overflow;
+            a.out[4] = (int64_t)*a.err;
         }
         PP_OUT();
         break;

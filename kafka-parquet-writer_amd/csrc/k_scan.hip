@@ -21,12 +21,6 @@ struct RawF {
     __device__ uint64_t get(uint32_t, uint64_t i) const { return raw[i]; }
     __device__ void put(uint32_t, uint64_t i, uint64_t v) const { P[i] = v; }
 };
-// job 0: raw -> P, job 1: val -> Q (the planner's folded prefix, k_plan_fold)
-struct Raw2F {
-    const uint32_t *raw, *val; uint64_t *P, *Q;
-    __device__ uint64_t get(uint32_t j, uint64_t i) const { return j ? val[i] : raw[i]; }
-    __device__ void put(uint32_t j, uint64_t i, uint64_t v) const { (j ? Q : P)[i] = v; }
-};
 // record lengths narrowed to T (u8 / u16) on the host; element 0 is `base` (the first boundary)
 template <typename T>
 struct NarrowF {
@@ -39,19 +33,39 @@ struct PcntF {
     __device__ uint64_t get(uint32_t j, uint64_t w) const { return __popcll(cols[opt[j]].pres[w]); }
     __device__ void put(uint32_t j, uint64_t w, uint64_t v) const { cols[opt[j]].pcnt[w] = (uint32_t)v; }
 };
-// planner events per group of 8 positions: element g of stream j = the 8 event bytes of
-// positions [8g, 8g + 8) summed (one 8-byte load); E8[j * (groups + 1) + g] = the prefix
-struct EvF {
-    const uint64_t *ev; uint32_t *E8; uint64_t groups;
+// The planner's prefixes, one multi-job scan over groups of 8 positions: jobs [0, nev) the event
+// streams (element g = the 8 event bytes of positions [8g, 8g + 8) summed from one 8-byte load;
+// E8[j * (groups + 1) + g] = the prefix), job nev the raw record sizes (P8[g] = the bytes of
+// records [0, 8g)) and job nev + 1, when val is given, the folded sizes (Q8).  A position's prefix
+// is its group's plus up to 7 elements (k_plan pref8).
+struct PlanPrefixF {
+    const uint64_t *ev; uint32_t *E8; uint64_t groups; uint32_t nev;
+    const uint32_t *raw, *val; uint64_t n; uint64_t *P8, *Q8;
     __device__ uint64_t get(uint32_t j, uint64_t g) const
     {
-        uint64_t b = ev[j * groups + g];
-        b = (b & 0x00ff00ff00ff00ffull) + ((b >> 8) & 0x00ff00ff00ff00ffull);
-        b += b >> 16;
-        b += b >> 32;
-        return b & 0xffffu;
+        if (j < nev) {
+            uint64_t b = ev[j * groups + g];
+            b = (b & 0x00ff00ff00ff00ffull) + ((b >> 8) & 0x00ff00ff00ff00ffull);
+            b += b >> 16;
+            b += b >> 32;
+            return b & 0xffffu;
+        }
+        const uint32_t *x = j == nev ? raw : val;
+        const uint64_t i0 = g * 8;
+        uint64_t s = 0;
+        if (i0 + 8 <= n) {
+            const uint4 u = *(const uint4 *)(x + i0), v = *(const uint4 *)(x + i0 + 4);
+            s = (uint64_t)u.x + u.y + u.z + u.w + v.x + v.y + v.z + v.w;
+        } else {
+            for (uint64_t i = i0; i < n; i++) s += x[i];
+        }
+        return s;
     }
-    __device__ void put(uint32_t j, uint64_t g, uint64_t v) const { E8[j * (groups + 1) + g] = (uint32_t)v; }
+    __device__ void put(uint32_t j, uint64_t g, uint64_t v) const
+    {
+        if (j < nev) E8[j * (groups + 1) + g] = (uint32_t)v;
+        else (j == nev ? P8 : Q8)[g] = v;
+    }
 };
 
 // Multi-job equal-length exclusive sums, reduce -> scan tile sums -> apply (three launches).
@@ -70,6 +84,35 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_mj_tsum(F f, uint64_t len, uint32
     for (int k = 0; k < 8; k++) if (i0 + k < len) s += f.get(j, i0 + k);
     s = block_reduce<uint64_t, OpSum64>(s, lds);
     if (threadIdx.x == 0) tsum[t] = s;
+}
+
+// Two-launch version when the tile sums are few (MJ2_MAX_READS: all apply blocks together read
+// about nt * tpj / 2 of them): each apply block sums the tile sums before it itself (L2-resident)
+// instead of a third launch scanning them (the writer's record offsets: 4.4 k tiles per job).
+// (r04: a single-pass look-back version of these scans took 0.48 ms per writer job on the
+// record offsets where the three launches took 0.09: each tile's look-back polls its
+// predecessors' status through uncached device-scope loads.)
+constexpr uint64_t MJ2_MAX_READS = 16ull << 20;
+template <class F>
+__global__ void __launch_bounds__(KPW_BLOCK) k_mj_tapply_c(F f, uint64_t len, uint32_t tpj, const uint64_t *tsum)
+{
+    __shared__ uint64_t lds[KPW_BLOCK];
+    const uint32_t t = blockIdx.x, j = t / tpj, tile = t % tpj;
+    uint64_t c = 0;
+    for (uint32_t k = threadIdx.x; k < tile; k += KPW_BLOCK) c += tsum[(uint64_t)j * tpj + k];
+    const uint64_t carry = block_reduce<uint64_t, OpSum64>(c, lds);
+    const uint64_t i0 = (uint64_t)tile * KPW_TILE_P + (uint64_t)threadIdx.x * 8;
+    uint64_t v[8], s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) { v[k] = (i0 + k < len) ? f.get(j, i0 + k) : 0; s += v[k]; }
+    uint64_t tot;
+    uint64_t ex = block_scan_excl<uint64_t, OpSum64>(s, lds, &tot) + carry;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (i0 + k < len) f.put(j, i0 + k, ex);
+        ex += v[k];
+    }
+    if (tile == tpj - 1 && threadIdx.x == 0) f.put(j, len, carry + tot);
 }
 
 // one block per job: exclusive scan of its tiles' sums; writes the job total to tsum[njobs*tpj + j]
@@ -167,6 +210,10 @@ static void mj_scan(F f, uint64_t len, uint32_t njobs, SegScratch *sc, hipStream
     uint64_t *tmp = scan_tmp(sc, (uint64_t)nt + njobs + 1, s);
     if (!tmp) return;
     hipLaunchKernelGGL(k_mj_tsum<F>, dim3(nt), dim3(KPW_BLOCK), 0, s, f, len, tpj, tmp);
+    if ((uint64_t)nt * tpj / 2 <= MJ2_MAX_READS) {
+        hipLaunchKernelGGL(k_mj_tapply_c<F>, dim3(nt), dim3(KPW_BLOCK), 0, s, f, len, tpj, (const uint64_t *)tmp);
+        return;
+    }
     hipLaunchKernelGGL(k_mj_tscan, dim3(njobs), dim3(KPW_BLOCK), 0, s, tmp, tpj, njobs);
     hipLaunchKernelGGL(k_mj_tapply<F>, dim3(nt), dim3(KPW_BLOCK), 0, s, f, len, tpj, njobs, (const uint64_t *)tmp);
 }
@@ -175,13 +222,6 @@ void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, SegScratch 
 {
     RawF f{raw, P};
     mj_scan(f, n, 1, sc, s);
-}
-
-void launch_prefix_raw2(const uint32_t *raw, const uint32_t *val, uint64_t n, uint64_t *P, uint64_t *Q, SegScratch *sc,
-                        hipStream_t s)
-{
-    Raw2F f{raw, val, P, Q};
-    mj_scan(f, n, 2, sc, s);
 }
 
 void launch_prefix_narrow(const void *raw, int width, uint64_t base, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s)
@@ -196,10 +236,11 @@ void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt
     mj_scan(f, nwords, nopt, sc, s);
 }
 
-void launch_scan_events(const uint8_t *ev, uint32_t *E8, uint64_t ev_stride, uint32_t njobs, SegScratch *sc, hipStream_t s)
+void launch_plan_prefix(const uint8_t *ev, uint32_t *E8, uint32_t nev, uint64_t ev_stride, const uint32_t *raw, const uint32_t *val,
+                        uint64_t n, uint64_t *P8, uint64_t *Q8, SegScratch *sc, hipStream_t s)
 {
-    EvF f{(const uint64_t *)ev, E8, ev_stride / 8};
-    mj_scan(f, ev_stride / 8, njobs, sc, s);
+    PlanPrefixF f{(const uint64_t *)ev, E8, ev_stride / 8, nev, raw, val, n, P8, Q8};
+    mj_scan(f, ev_stride / 8, nev + 1 + (val ? 1 : 0), sc, s);
 }
 
 // ------------------------------------------------------------------ segmented tile scans

@@ -16,6 +16,13 @@ struct HtSlot {
     uint32_t id;
 };
 
+// host side of the statistics K6 leaves in a read-back descriptor
+inline void chunk_stats_derive(ChunkDesc &C)
+{
+    C.null_count = (uint64_t)(C.e - C.s) - C.nn;
+    C.has_minmax = C.nn > 0;
+}
+
 struct ChunkArgs {
     ChunkDesc *ch;
     int32_t nchunks;
@@ -29,6 +36,10 @@ struct ChunkArgs {
     uint32_t *tile_cnt;
     uint64_t *tile_sz;
     HtSlot *ht;                    // dictionary hash tables (per chunk at ChunkDesc::ht_off)
+    HtSlot *ht_clear;              // k_chunk_stats empties these slots (all ones) on the way: the
+    uint64_t ht_clear_n;           // dictionary phase follows it (one dispatch fewer than a fill)
+    uint64_t *flags_clear;         // and zeroes this word (the collision / retry flags)
+    uint64_t body_tail;            // page writers: the body's end (k_chunk_prep clears 512 bytes from there)
     uint32_t *ids;
     uint64_t *ent_rec, *ent_boff;
     uint32_t max_dict_bytes;

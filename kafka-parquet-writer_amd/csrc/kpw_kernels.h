@@ -109,12 +109,14 @@ struct PlanArgs {
     int32_t final_flush;           // close(): flush the trailing row group
     int32_t ncols;
     int64_t next_rg_size;          // nextRowGroupSize
-    const uint64_t *P;             // exclusive prefix of raw bytes [n+1]
+    const uint64_t *P8;            // raw record bytes before record 8g [n/8 + 1] ...
+    const uint32_t *raw;           // ... plus those of the group's records before r (pref8)
+    const unsigned long long *err; // K1's first invalid record (copied to out[4])
     const RleJob *jobs;            // the streams' K3 planning jobs (job k = stream k) and long runs
     const uint32_t *lr_a, *lr_b, *lr_off;
     const uint8_t *lr_rle;
-    const uint64_t *Q;             // [n+1] P + the global parse's bytes of every record-indexed stream
-                                   // (null: not folded); see k_plan_fold
+    const uint64_t *Q8;            // the same over val = raw + the global parse's event bytes of every
+    const uint32_t *qv;            // record-indexed stream (null: not folded); see k_plan_fold
     const DevCol *cols;
     const PlanStream *streams;     // RLE streams counted by emitted bytes
     int32_t nstreams;
@@ -235,9 +237,6 @@ struct DeltaJob {
 // ---------------------------------------------------------------- launch wrappers
 void launch_decode(const DecodeArgs &a, hipStream_t s);
 void launch_prefix_raw(const uint32_t *raw, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s);
-// P = exclusive prefix of raw and Q = of val, in one scan
-void launch_prefix_raw2(const uint32_t *raw, const uint32_t *val, uint64_t n, uint64_t *P, uint64_t *Q, SegScratch *sc,
-                        hipStream_t s);
 // P[0] = 0, P[k] = base + raw[1] + ... + raw[k-1] (k >= 1) for u8 (width 1) / u16 (width 2) raw
 void launch_prefix_narrow(const void *raw, int width, uint64_t base, uint64_t n, uint64_t *P, SegScratch *sc, hipStream_t s);
 

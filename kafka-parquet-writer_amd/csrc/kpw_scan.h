@@ -18,7 +18,10 @@ struct OpMapCompose;
 void launch_pcnt_scan(const DevCol *cols_d, const uint32_t *opt_d, uint32_t nopt, uint64_t nwords, SegScratch *sc, hipStream_t s);
 // per stream j: E8[j * (ev_stride / 8 + 1) + g] = event bytes of positions [0, 8g) (ev_stride: bytes
 // per stream in ev, a multiple of 8)
-void launch_scan_events(const uint8_t *ev, uint32_t *E8, uint64_t ev_stride, uint32_t njobs, SegScratch *sc, hipStream_t s);
+// the planner's prefixes over groups of 8 positions (k_scan.hip PlanPrefixF): E8 of nev event
+// streams, P8 of the raw record sizes, Q8 of the folded sizes when val != null
+void launch_plan_prefix(const uint8_t *ev, uint32_t *E8, uint32_t nev, uint64_t ev_stride, const uint32_t *raw, const uint32_t *val,
+                        uint64_t n, uint64_t *P8, uint64_t *Q8, SegScratch *sc, hipStream_t s);
 
 // Status words for one single-pass launch over `nwords` tiles x scans (w == nullptr: the
 // scratch could not grow, sc->failed set; the caller skips the launch).
