@@ -196,13 +196,11 @@ hipError_t Engine::xd2h(void *dst, const void *src, size_t bytes, hipStream_t s)
 
 hipError_t Engine::xsync(hipStream_t s) { return hipStreamSynchronize(s); }
 
-// Lays out tiles for the given jobs, uploads them and runs the structure pass.
-int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, RleScratch &sc)
+// Lays out tiles for the given jobs (ptj / etj: tile -> job) and sizes the scratch.
+int Engine::rle_layout(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, std::vector<uint32_t> &ptj, std::vector<uint32_t> &etj)
 {
-    hipStream_t s = stream;
     npt = net = 0;
     uint64_t e0 = 0;
-    static thread_local std::vector<uint32_t> ptj, etj;
     ptj.clear();
     etj.clear();
     for (size_t j = 0; j < jobs.size(); j++) {
@@ -222,19 +220,21 @@ int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, Rle
         ptj.insert(ptj.end(), J.ntiles, (uint32_t)j);
         etj.insert(etj.end(), J.netiles, (uint32_t)j);
     }
-    const size_t nj = jobs.size();
     ENS(r_last, npt * 8); ENS(r_prev, npt * 8); ENS(r_lrcnt, npt * 4); ENS(r_lroff, npt * 4);
     ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_lrf, e0); ENS(r_rg, e0 * 4);
     ENS(r_rb, e0 * 4); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8);
-    std::vector<uint8_t *> dp;   // jobs first: d_jobs.as<RleJob>() is the job table
-    if (int st = upload_parts(d_jobs, {{jobs.data(), nj * sizeof(RleJob)}, {ptj.data(), npt * 4}, {etj.data(), net * 4}}, dp))
-        return st;
-    sc.ptile_job = (uint32_t *)dp[1];
+    return KPW_OK;
+}
+
+// The scratch of the jobs laid out last, with their uploaded tile maps.
+void Engine::rle_bind(RleScratch &sc, const uint8_t *ptj_d, const uint8_t *etj_d)
+{
+    sc.ptile_job = (uint32_t *)ptj_d;
     sc.last_brk = r_last.as<int64_t>();
     sc.prev_brk = r_prev.as<int64_t>();
     sc.lr_cnt = r_lrcnt.as<uint32_t>();
     sc.lr_off = r_lroff.as<uint32_t>();
-    sc.etile_job = (uint32_t *)dp[2];
+    sc.etile_job = (uint32_t *)etj_d;
     sc.lr_a = r_lra.as<uint32_t>();
     sc.lr_b = r_lrb.as<uint32_t>();
     sc.lr_rle = nullptr;   // kept by the planning jobs only (set by the caller)
@@ -243,6 +243,17 @@ int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, Rle
     sc.r_boff = r_rboff.as<uint64_t>();
     sc.r_goff = r_rgoff.as<uint64_t>();
     sc.seg = &seg_;
+}
+
+// Lays out tiles for the given jobs, uploads them (d_jobs: the job table first) and binds the scratch.
+int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, RleScratch &sc)
+{
+    static thread_local std::vector<uint32_t> ptj, etj;
+    if (int st = rle_layout(jobs, npt, net, ptj, etj)) return st;
+    std::vector<uint8_t *> dp;
+    if (int st = upload_parts(d_jobs, {{jobs.data(), jobs.size() * sizeof(RleJob)}, {ptj.data(), npt * 4}, {etj.data(), net * 4}}, dp))
+        return st;
+    rle_bind(sc, dp[1], dp[2]);
     return KPW_OK;
 }
 
@@ -251,6 +262,55 @@ static inline uint64_t next_pow2(uint64_t x)
     uint64_t p = 1;
     while (p < x) p <<= 1;
     return p;
+}
+
+// RLE streams whose emitted bytes count in checkBlockSizeReached: definition levels of optional
+// columns; in v2 also the boolean values (RunLengthBitPackingHybridValuesWriter).  Job k = stream
+// k, its events at k * ev_stride.
+int Engine::plan_inputs(const std::vector<DevCol> &hc, uint64_t ne, uint64_t nwords, std::vector<PlanStream> &hs,
+                        std::vector<RleJob> &pj)
+{
+    hipStream_t s = stream;
+    const uint32_t nopt = (uint32_t)opt_idx_.size();
+    const uint32_t nbool = (uint32_t)bool_idx_.size();
+    const uint32_t nstreams = nopt + (v2_ ? nbool : 0);
+    const uint64_t ev_stride = (ne + 1 + 7) & ~7ull;
+    std::vector<uint64_t *> &cbits = cbits_;
+    cbits.assign(nbool, nullptr);
+    if (v2_) {
+        for (uint32_t i = 0; i < nbool; i++) {
+            const uint32_t c = bool_idx_[i];
+            if (cols[c].optional) {
+                ENS(col_cbits[i], nwords * 8);
+                CK(hipMemsetAsync(col_cbits[i].p, 0, nwords * 8, s));
+                cbits[i] = col_cbits[i].as<uint64_t>();
+            } else {
+                cbits[i] = hc[c].vbits;   // required: the record-indexed value bits are the stream
+            }
+        }
+    }
+    hs.resize(nstreams);
+    pj.resize(nstreams);
+    for (uint32_t k = 0; k < nstreams; k++) {
+        PlanStream &S = hs[k];
+        S.pad = 0;
+        S.len = ne;
+        if (k < nopt) { S.bits = hc[opt_idx_[k]].pres; S.rank_col = -1; }
+        else {
+            const uint32_t c = bool_idx_[k - nopt];
+            S.bits = cbits[k - nopt];
+            S.rank_col = cols[c].optional ? (int32_t)c : -1;   // optional: length set on the device
+        }
+        RleJob &J = pj[k];
+        memset(&J, 0, sizeof(J));
+        J.src.kind = 0;
+        J.src.ptr = S.bits;
+        J.src.base = 0;
+        J.len = (uint32_t)ne;    // upper bound; optional boolean streams are shortened on the device
+        J.bw = 1;
+        J.out_off = (uint64_t)k * ev_stride;
+    }
+    return KPW_OK;
 }
 
 int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
@@ -309,10 +369,29 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             d.vbits = col_vbits[c].as<uint64_t>();
         }
     }
-    // column descriptors and K1's first-invalid-record word (all ones: none) in one copy
+    // column descriptors and K1's first-invalid-record word (all ones: none) in one copy; the
+    // single-page path (which plans before it knows K1's verdict) adds the planner's inputs for
+    // all n records: its RLE jobs, their tile maps and the stream table
+    const uint32_t nbool = (uint32_t)bool_idx_.size();
+    const uint32_t nstreams = nopt + (v2_ ? nbool : 0);
+    const bool plan = nstreams && !(probe_ && probe_cuts_);   // (a v1 probe with the size model's page cuts: none)
+    const bool pre = plan && !mp_;
+    std::vector<PlanStream> hs;
+    std::vector<RleJob> pj;
+    uint32_t npt = 0, net = 0;
+    static thread_local std::vector<uint32_t> pptj, petj;
     static const uint64_t kNoErr = ~0ull;
+    std::vector<HostPart> parts{{hc.data(), nc * sizeof(DevCol)}, {&kNoErr, 8}};
+    if (pre) {
+        if (int st = plan_inputs(hc, n, nwords, hs, pj)) return st;
+        if (int st = rle_layout(pj, npt, net, pptj, petj)) return st;
+        parts.push_back({pj.data(), pj.size() * sizeof(RleJob)});
+        parts.push_back({pptj.data(), (size_t)npt * 4});
+        parts.push_back({petj.data(), (size_t)net * 4});
+        parts.push_back({hs.data(), hs.size() * sizeof(PlanStream)});
+    }
     std::vector<uint8_t *> cp;
-    if (int st = upload_parts(d_cols, {{hc.data(), nc * sizeof(DevCol)}, {&kNoErr, 8}}, cp)) return st;
+    if (int st = upload_parts(d_cols, parts, cp)) return st;
     unsigned long long *const d_err = (unsigned long long *)cp[1];
     ENS(d_raw, n * 4);
     DecodeArgs da;
@@ -347,64 +426,28 @@ replan:
         CK(xsync(s));
         return KPW_OK;
     }
-    // RLE streams whose emitted bytes count in checkBlockSizeReached: definition levels of
-    // optional columns; in v2 also the boolean values (RunLengthBitPackingHybridValuesWriter)
-    const uint32_t nbool = (uint32_t)bool_idx_.size();
-    const uint32_t nstreams = nopt + (v2_ ? nbool : 0);
     RleScratch sc{};
-    uint32_t npt = 0, net = 0;
     const uint64_t ev_stride = (ne + 1 + 7) & ~7ull;   // event bytes per stream (positions 0..ne, 8-aligned)
-    std::vector<RleJob> pj;
-    std::vector<PlanStream> hs(nstreams);
-    std::vector<uint64_t *> &cbits = cbits_;
-    cbits.assign(nbool, nullptr);
-    if (v2_) {
-        for (uint32_t i = 0; i < nbool; i++) {
-            const uint32_t c = bool_idx_[i];
-            if (cols[c].optional) {
-                ENS(col_cbits[i], nwords * 8);
-                CK(hipMemsetAsync(col_cbits[i].p, 0, nwords * 8, s));
-                cbits[i] = col_cbits[i].as<uint64_t>();
-            } else {
-                cbits[i] = hc[c].vbits;   // required: the record-indexed value bits are the stream
-            }
-        }
-    }
-    for (uint32_t k = 0; k < nstreams; k++) {
-        PlanStream &S = hs[k];
-        S.pad = 0;
-        S.len = ne;
-        if (k < nopt) { S.bits = hc[opt_idx_[k]].pres; S.rank_col = -1; }
-        else {
-            const uint32_t c = bool_idx_[k - nopt];
-            S.bits = cbits[k - nopt];
-            S.rank_col = cols[c].optional ? (int32_t)c : -1;   // optional: length set on the device
-        }
-    }
-    // a v1 page-size probe with the size model's page cuts needs no planner inputs
-    const bool plan = nstreams && !(probe_ && probe_cuts_);
-    ENS(d_streams, std::max<size_t>(1, nstreams) * sizeof(PlanStream));
-    if (plan) CK(xh2d(d_streams.p, hs.data(), nstreams * sizeof(PlanStream), s));
+    const bool pre_ok = pre && ne == n;   // the uploaded inputs are this plan's
+    RleJob *pjobs = pre_ok ? (RleJob *)cp[2] : nullptr;   // (d_jobs is set, and may move, in run_rle)
+    PlanStream *pstreams = pre_ok ? (PlanStream *)cp[5] : nullptr;
     if (plan) {
-        pj.resize(nstreams);
-        for (uint32_t k = 0; k < nstreams; k++) {
-            RleJob &J = pj[k];
-            memset(&J, 0, sizeof(J));
-            J.src.kind = 0;
-            J.src.ptr = hs[k].bits;
-            J.src.base = 0;
-            J.len = (uint32_t)ne;    // upper bound; optional boolean streams are shortened on the device
-            J.bw = 1;
-            J.out_off = (uint64_t)k * ev_stride;
+        if (pre_ok) {
+            rle_bind(sc, cp[3], cp[4]);
+        } else {
+            if (int st = plan_inputs(hc, ne, nwords, hs, pj)) return st;
+            ENS(d_streams, nstreams * sizeof(PlanStream));
+            CK(xh2d(d_streams.p, hs.data(), nstreams * sizeof(PlanStream), s));
+            pstreams = d_streams.as<PlanStream>();
+            if (int st = run_rle(pj, npt, net, sc)) return st;
+            pjobs = d_jobs.as<RleJob>();
         }
-        int st = run_rle(pj, npt, net, sc);
-        if (st) return st;
         sc.lr_rle = r_lrf.as<uint8_t>();   // k_plan's walkers read the global parse's decision per long run
         if (v2_ && nbool) {
             ENS(d_cbits_ptr, nbool * sizeof(uint64_t *));
-            CK(xh2d(d_cbits_ptr.p, cbits.data(), nbool * sizeof(uint64_t *), s));
-            launch_bool_streams(d_cols.as<DevCol>(), d_bool.as<uint32_t>(), nbool, ne, d_cbits_ptr.as<uint64_t *>(),
-                                d_jobs.as<RleJob>(), nopt, d_streams.as<PlanStream>(), nopt, s);
+            CK(xh2d(d_cbits_ptr.p, cbits_.data(), nbool * sizeof(uint64_t *), s));
+            launch_bool_streams(d_cols.as<DevCol>(), d_bool.as<uint32_t>(), nbool, ne, d_cbits_ptr.as<uint64_t *>(), pjobs, nopt,
+                                pstreams, nopt, s);
         }
         ENS(d_ev, (uint64_t)nstreams * ev_stride);
         ENS(d_E, (uint64_t)nstreams * (ev_stride / 8 + 1) * 4);
@@ -415,14 +458,14 @@ replan:
             ENS(d_gend, (uint64_t)nstreams * nwords * 8);
             CK(hipMemsetAsync(d_gend.p, 0, (uint64_t)nstreams * nwords * 8, s));
         }
-        launch_rle_structure(d_jobs.as<RleJob>(), (int)nstreams, npt, net, sc, s);
-        launch_rle_events(d_jobs.as<RleJob>(), npt, net, sc, d_ev.as<uint8_t>(), mp_ ? d_gend.as<uint64_t>() : nullptr, nwords, s);
+        launch_rle_structure(pjobs, (int)nstreams, npt, net, sc, s);
+        launch_rle_events(pjobs, npt, net, sc, d_ev.as<uint8_t>(), mp_ ? d_gend.as<uint64_t>() : nullptr, nwords, s);
     }
     // one scan for the planner's prefixes per group of 8 positions: the event streams' E8, the raw
     // record sizes' P8 and, for the single-page planner of a wide schema, Q8 over raw + the
     // record-indexed streams' global event bytes (k_plan folds converged streams into one load)
     uint32_t nfold = 0;
-    for (uint32_t k = 0; k < nstreams; k++) nfold += hs[k].rank_col < 0 ? 1 : 0;
+    for (const PlanStream &S : hs) nfold += S.rank_col < 0 ? 1 : 0;
     // (few streams: the planner's evaluations are cheap already and the fold's extra pass over
     // the batch costs more, C2 4 streams: +0.8 ms per 100 M records; C3 199 streams: -6 ms per 10 M)
     const bool fold = plan && !mp_ && nfold >= 16 && !fold_off();
@@ -431,7 +474,7 @@ replan:
     if (fold) {
         ENS(d_Q, (groups + 1) * 8);
         ENS(d_qv, ne * 4);
-        launch_plan_fold(d_ev.as<uint8_t>(), ev_stride, d_streams.as<PlanStream>(), nstreams, d_raw.as<uint32_t>(), ne,
+        launch_plan_fold(d_ev.as<uint8_t>(), ev_stride, pstreams, nstreams, d_raw.as<uint32_t>(), ne,
                          d_qv.as<uint32_t>(), s);
     }
     launch_plan_prefix(plan ? d_ev.as<uint8_t>() : nullptr, plan ? d_E.as<uint32_t>() : nullptr, plan ? nstreams : 0, ev_stride,
@@ -449,8 +492,8 @@ replan:
     pa.n = ne; pa.final_flush = final_flush ? 1 : 0; pa.ncols = nc; pa.next_rg_size = next_rg_size;
     pa.P8 = d_P.as<uint64_t>(); pa.raw = d_raw.as<uint32_t>(); pa.cols = d_cols.as<DevCol>();
     pa.Q8 = fold ? d_Q.as<uint64_t>() : nullptr; pa.qv = fold ? d_qv.as<uint32_t>() : nullptr;
-    pa.jobs = d_jobs.as<RleJob>(); pa.lr_a = sc.lr_a; pa.lr_b = sc.lr_b; pa.lr_off = sc.lr_off; pa.lr_rle = sc.lr_rle;
-    pa.streams = d_streams.as<PlanStream>(); pa.nstreams = (int32_t)nstreams;
+    pa.jobs = pjobs; pa.lr_a = sc.lr_a; pa.lr_b = sc.lr_b; pa.lr_off = sc.lr_off; pa.lr_rle = sc.lr_rle;
+    pa.streams = pstreams; pa.nstreams = (int32_t)nstreams;
     pa.nbool = v2_ ? 0 : (int32_t)nbool; pa.bool_cols = d_bool.as<uint32_t>();
     pa.E8 = nstreams ? d_E.as<uint32_t>() : nullptr; pa.ev = nstreams ? d_ev.as<uint8_t>() : nullptr; pa.ev_stride = ev_stride;
     pa.gend = nstreams ? d_gend.as<uint64_t>() : nullptr; pa.gend_stride = nwords;
@@ -539,7 +582,7 @@ replan:
             if (v2_ && cols[c].phys == KPW_BOOLEAN) {   // RunLengthBitPackingHybridValuesWriter(1)
                 RleJob J;
                 memset(&J, 0, sizeof(J));
-                J.src.kind = 0; J.src.ptr = cbits[bool_pos[c]];
+                J.src.kind = 0; J.src.ptr = cbits_[bool_pos[c]];
                 J.src.base = cols[c].optional ? 0 : (uint64_t)C.s;   // optional: rank of C.s, set on the device
                 J.len = (uint32_t)len; J.bw = 1;
                 C.bool_job = (int32_t)ej.size();

@@ -180,6 +180,12 @@ private:
     hipEvent_t kev_[4] = {};
     std::vector<uint32_t> opt_idx_, bool_idx_;
     int run_rle(std::vector<RleJob> &jobs, uint32_t &nptiles, uint32_t &netiles, RleScratch &sc);
+    int rle_layout(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, std::vector<uint32_t> &ptj, std::vector<uint32_t> &etj);
+    void rle_bind(RleScratch &sc, const uint8_t *ptj_d, const uint8_t *etj_d);
+    // the planner's streams and RLE jobs over the first ne records (v2: clears the optional
+    // booleans' compacted bit arrays on the stream)
+    int plan_inputs(const std::vector<DevCol> &hc, uint64_t ne, uint64_t nwords, std::vector<PlanStream> &hs,
+                    std::vector<RleJob> &pj);
     // multi-page regime (engine_mp.cpp)
     bool mp_ = false;
     bool probe_ = false;                 // encode() is a probe_pages call

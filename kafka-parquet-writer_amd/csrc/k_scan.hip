@@ -187,7 +187,9 @@ LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s)
     if (need > sc->bytes) {
         // earlier scans of this handle may still use the old buffer on `s`
         if (sc->p) dev_free_after(sc->p, s);
-        sc->bytes = need * 2;
+        // (at least 16 MiB: one cleared buffer serves every scan of a typical job, instead of a
+        // clear at each first larger scan)
+        sc->bytes = std::max<size_t>(need * 2, 16u << 20);
         sc->p = dev_alloc(sc->bytes);
         if (!sc->p || hipMemsetAsync(sc->p, 0, sc->bytes, s) != hipSuccess) {
             sc->bytes = 0; sc->failed = true; return LbView{nullptr, 0};
