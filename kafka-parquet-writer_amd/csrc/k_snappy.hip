@@ -687,17 +687,21 @@ void launch_snappy(const SnappyArgs &a, hipStream_t s)
         // that hands back (rounds, long copies) to k_snappy_v, then k_snappy_s_rest, unbudgeted
         static const uint32_t vbudget = [] { const char *e = getenv("KPW_SNAPPY_VBUDGET"); return e ? (uint32_t)atoi(e) : 256u; }();
         static const uint32_t sbudget = [] { const char *e = getenv("KPW_SNAPPY_SBUDGET"); return e ? (uint32_t)atoi(e) : 128u; }();
+        // A launch of few fragments (a page-size probe's cut pages) is latency-bound: one wave
+        // per fragment takes ~40 us per 64 KiB where a segment-parallel workgroup takes ~10, so
+        // they all go to the segment kernel first (the same bytes either way)
+        const bool few = a.nfrags <= 64;
         SnappyArgs v = a;
         v.v_budget = vbudget;
-        hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, v);
-        if (vbudget && sbudget) {   // the batched LDS kernel on the incompressible ones, also with a budget
+        if (!few) hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, v);
+        if (!few && vbudget && sbudget) {   // the batched LDS kernel on the incompressible ones, also with a budget
             SnappyArgs r = a;
             r.s_budget = sbudget;
             hipLaunchKernelGGL(k_snappy_s_rest, dim3(a.nfrags), dim3(64), 0, s, r);
         }
         SnappyArgs g = a;   // (the fragment counter is 0: zeroed once, left at 0 by every launch)
         g.order = nullptr;
-        g.seg_only_marked = vbudget ? 1 : 0;
+        g.seg_only_marked = (vbudget && !few) ? 1 : 0;
         hipLaunchKernelGGL(k_snappy_seg, dim3(a.seg_grid), dim3(1024), 0, s, g);
         SnappyArgs b = a;
         b.order = nullptr;
