@@ -45,6 +45,9 @@ struct Walker {
     uint32_t pend_bytes, pend_rle;
     uint32_t grp;       // groups in the current bit-packed run
     uint32_t state;     // 0 walking, 1 converged, 2 no more events in the batch
+#ifdef KPW_PLAN_PROF
+    uint32_t steps;     // profiling build: walk iterations
+#endif
 };
 
 __device__ __forceinline__ int32_t java_f2i(float f)
@@ -105,6 +108,9 @@ template <class Src>
 __device__ uint64_t walker_query(Walker &w, int64_t r, const Src &src, uint64_t n, const EvView &Eg)
 {
     while (w.state == 0) {
+#ifdef KPW_PLAN_PROF
+        w.steps++;
+#endif
         if (w.pend_pos < 0) {
             const int64_t p = w.p;
             if (p + 8 > (int64_t)n) { w.state = 2; break; }
@@ -621,38 +627,69 @@ __device__ __forceinline__ void walker_init(Walker &w, int64_t p)
 // v2 BOOLEAN column c: RLE bytes its value stream emitted since the page start (walker wb,
 // started by bool_walker_init at the page's first record); stream position = value rank for an
 // optional column
-__device__ __forceinline__ void bool_walker_init(const PageCutArgs &a, int c, Walker &wb, int64_t q)
+// A column's inputs to the multi-page checks, loaded once per kernel (each check used to reload
+// the descriptor fields from global memory ahead of the data loads: one more dependent latency
+// per check, r04 bulk multi-page ~2 us per check)
+struct MpColInfo {
+    const uint64_t *pres;    // null: REQUIRED
+    const uint32_t *pcnt;
+    const uint64_t *sp;      // BYTE_ARRAY size prefix
+    const uint64_t *gdl;     // definition-level stream: run-end bits, events (kdl < 0: none)
+    EvView edl;
+    const uint64_t *bbits;   // v2 BOOLEAN value stream: bits, run-end bits, events, length (kb < 0: none)
+    const uint64_t *gb;
+    EvView eb;
+    uint64_t blen;
+    int32_t phys, vsize, kdl, kb;
+};
+__device__ __forceinline__ MpColInfo mp_col_info(const PageCutArgs &a, int c)
 {
-    const DevCol &col = a.cols[c];
-    walker_init(wb, col.optional ? (int64_t)pc_at(col, (uint64_t)q) : q);
+    const DevCol col = a.cols[c];
+    MpColInfo I;
+    I.pres = col.optional ? col.pres : nullptr;
+    I.pcnt = col.pcnt;
+    I.sp = col.phys == 6 ? a.sp[c] : nullptr;
+    I.phys = col.phys; I.vsize = col.vsize;
+    I.kdl = a.col_stream[c];
+    I.gdl = nullptr; I.gb = nullptr; I.bbits = nullptr; I.blen = 0;
+    I.edl = EvView{nullptr, nullptr}; I.eb = EvView{nullptr, nullptr};
+    if (I.kdl >= 0) { I.gdl = a.gend + (uint64_t)I.kdl * a.gend_stride; I.edl = ev_view(a, I.kdl); }
+    I.kb = a.col_bstream ? a.col_bstream[c] : -1;
+    if (I.kb >= 0) {
+        const PlanStream S = a.streams[I.kb];
+        I.bbits = S.bits; I.blen = S.len;
+        I.gb = a.gend + (uint64_t)I.kb * a.gend_stride; I.eb = ev_view(a, I.kb);
+    }
+    return I;
 }
-__device__ __forceinline__ uint64_t col_bool_rle(const PageCutArgs &a, int c, Walker &wb, int64_t r)
+__device__ __forceinline__ uint64_t mp_rank(const MpColInfo &I, int64_t r)
 {
-    const int k = a.col_bstream[c];
-    const DevCol &col = a.cols[c];
-    const PlanStream &S = a.streams[k];
-    const int64_t pos = col.optional ? (int64_t)pc_at(col, (uint64_t)r) : r;
-    return walker_query(wb, pos, SrcDirect{S.bits, a.gend + (uint64_t)k * a.gend_stride}, S.len, ev_view(a, k));
+    return I.pres ? pc_at_p(I.pres, I.pcnt, (uint64_t)r) : (uint64_t)r;
+}
+// v2 BOOLEAN column: RLE bytes its value stream emitted since the page start (walker wb,
+// started by bool_walker_init at the page's first record); stream position = value rank for an
+// optional column
+__device__ __forceinline__ void bool_walker_init(const MpColInfo &I, Walker &wb, int64_t q) { walker_init(wb, (int64_t)mp_rank(I, q)); }
+__device__ __forceinline__ uint64_t col_bool_rle(const MpColInfo &I, Walker &wb, int64_t r)
+{
+    return walker_query(wb, (int64_t)mp_rank(I, r), SrcDirect{I.bbits, I.gb}, I.blen, I.eb);
 }
 // rl(0) + dl + data buffered sizes of column c over the page [q, r):
 // dl = RunLengthBitPackingHybridEncoder bytes emitted since q (walker), data =
 // FallbackValuesWriter.rawDataByteSize / PlainValuesWriter size / boolean bit count (v1) or
 // boolean RLE bytes (v2, walker wb).
-__device__ __forceinline__ uint64_t col_data_bytes(const PageCutArgs &a, int c, Walker &wb, int64_t q, int64_t r)
+__device__ __forceinline__ uint64_t col_data_bytes(const PageCutArgs &a, const MpColInfo &I, Walker &wb, int64_t q, int64_t r)
 {
-    const DevCol &col = a.cols[c];
-    if (col.phys == 0 && a.v2) return col_bool_rle(a, c, wb, r);
-    const uint64_t cnt = col.optional ? pc_at(col, (uint64_t)r) - pc_at(col, (uint64_t)q) : (uint64_t)(r - q);
-    if (col.phys == 0) return (cnt + 7) / 8;
-    if (col.phys == 6) return a.sp[c][r] - a.sp[c][q];
-    return cnt * (uint64_t)col.vsize;
+    if (I.phys == 0 && a.v2) return col_bool_rle(I, wb, r);
+    if (I.phys == 6) return I.sp[r] - I.sp[q];
+    const uint64_t cnt = mp_rank(I, r) - mp_rank(I, q);
+    if (I.phys == 0) return (cnt + 7) / 8;
+    return cnt * (uint64_t)I.vsize;
 }
-__device__ __forceinline__ uint64_t col_dl_bytes(const PageCutArgs &a, int c, Walker &w, int64_t r)
+__device__ __forceinline__ uint64_t col_dl_bytes(const PageCutArgs &a, const MpColInfo &I, Walker &w, int64_t r)
 {
-    const int k = a.col_stream[c];
-    if (k < 0) return 0;
-    const DevCol &col = a.cols[c];
-    return walker_query(w, r, SrcDirect{col.pres, a.gend + (uint64_t)k * a.gend_stride}, a.n, ev_view(a, k));
+    if (I.kdl < 0) return 0;
+    return walker_query(w, r, SrcDirect{I.pres, I.gdl}, a.n, I.edl);
 }
 
 // ColumnWriterV1.accountForValueWritten (estimateNextSizeCheck = true), one thread per
@@ -664,23 +701,38 @@ __global__ void __launch_bounds__(64) k_page_cuts(PageCutArgs a)
 {
     const int c = blockIdx.x * 64 + threadIdx.x;
     if (c >= a.ncols) return;
+    const MpColInfo I = mp_col_info(a, c);
     Walker w, wb;
     int64_t q = a.s;
     walker_init(w, q);
     int32_t next = 100;
     uint32_t nc = 0;
+#ifdef KPW_PLAN_PROF
+    uint32_t pp_checks = 0, pp_steps = 0;
+    const uint64_t pp_t0 = wall_clock64();
+    w.steps = 0;
+#endif
     for (;;) {
+#ifdef KPW_PLAN_PROF
+        pp_checks++;
+#endif
         const int64_t x = q + (int64_t)next;
         if (x >= a.h) break;
         const int32_t vc = next + 1;
-        const uint64_t mem = col_dl_bytes(a, c, w, x + 1) + col_data_bytes(a, c, wb, q, x + 1);
+        const uint64_t mem = col_dl_bytes(a, I, w, x + 1) + col_data_bytes(a, I, wb, q, x + 1);
         if (mem > (uint64_t)a.page_size) {
             if (nc < a.cap) a.cuts[(uint64_t)c * a.cap + nc] = x + 1;
             else atomicOr(a.overflow, 1);
             nc++;
             next = vc / 2;
             q = x + 1;
+#ifdef KPW_PLAN_PROF
+            pp_steps += w.steps;
+#endif
             walker_init(w, q);
+#ifdef KPW_PLAN_PROF
+            w.steps = 0;
+#endif
         } else {
             float t = __fmul_rn((float)vc, (float)a.page_size);
             t = __fdiv_rn(t, (float)mem);
@@ -689,6 +741,10 @@ __global__ void __launch_bounds__(64) k_page_cuts(PageCutArgs a)
         }
     }
     a.ncuts[c] = nc < a.cap ? nc : a.cap;
+#ifdef KPW_PLAN_PROF
+    printf("[page_cuts] s %lld h %lld col %d cuts %u checks %u walk steps %u ticks %llu\n", (long long)a.s, (long long)a.h, c, nc,
+           pp_checks, pp_steps + w.steps, (unsigned long long)(wall_clock64() - pp_t0));
+#endif
 }
 
 // ColumnWriteStoreV2.sizeCheck (PARQUET_2_0), one wave for the whole store, lanes own columns:
@@ -701,14 +757,16 @@ __global__ void __launch_bounds__(64) k_page_cuts(PageCutArgs a)
 __global__ void __launch_bounds__(64) k_page_cuts_v2(PageCutArgs a)
 {
     __shared__ Walker Wd[MAX_COLS], Wb[MAX_COLS];
+    __shared__ MpColInfo CI[MAX_COLS];
     __shared__ int64_t Q[MAX_COLS];
     __shared__ uint32_t NC[MAX_COLS];
     const int lane = threadIdx.x;
     for (int c = lane; c < a.ncols; c += 64) {
+        CI[c] = mp_col_info(a, c);
         Q[c] = a.s;
         NC[c] = 0;
         walker_init(Wd[c], a.s);
-        if (a.col_bstream[c] >= 0) bool_walker_init(a, c, Wb[c], a.s);
+        if (CI[c].kb >= 0) bool_walker_init(CI[c], Wb[c], a.s);
     }
     const int64_t ps = a.page_size;
     const int64_t tol = (int64_t)__fmul_rn((float)ps, 0.1f);
@@ -718,7 +776,8 @@ __global__ void __launch_bounds__(64) k_page_cuts_v2(PageCutArgs a)
         int64_t mn = INT64_MAX;
         for (int c = lane; c < a.ncols; c += 64) {
             const int64_t q = Q[c];
-            const int64_t used = (int64_t)(col_dl_bytes(a, c, Wd[c], x1) + col_data_bytes(a, c, Wb[c], q, x1));
+            const MpColInfo &I = CI[c];
+            const int64_t used = (int64_t)(col_dl_bytes(a, I, Wd[c], x1) + col_data_bytes(a, I, Wb[c], q, x1));
             const int64_t rows = x1 - q;
             int64_t rem = ps - used;
             if (rem <= tol) {   // ColumnWriterV2.writePage(rowCount)
@@ -727,7 +786,7 @@ __global__ void __launch_bounds__(64) k_page_cuts_v2(PageCutArgs a)
                 NC[c]++;
                 Q[c] = x1;
                 walker_init(Wd[c], x1);
-                if (a.col_bstream[c] >= 0) bool_walker_init(a, c, Wb[c], x1);
+                if (I.kb >= 0) bool_walker_init(I, Wb[c], x1);
                 rem = ps;
             }
             const int64_t fill = used == 0 ? 10000 : ((int64_t)(float)rows / used) * rem;
@@ -751,9 +810,11 @@ __global__ void __launch_bounds__(64) k_page_cuts_v2(PageCutArgs a)
 // columns; r only grows, so each column's page cursor and walker advance monotonically.
 struct MpCol {
     Walker w, wb;       // definition levels; v2 boolean values
+    MpColInfo I;
     int64_t q;
+    int64_t next_cut;   // the column's next page end (INT64_MAX: none)
     uint64_t pb;
-    uint32_t ci, pad;
+    uint32_t ci, nc;
 };
 
 __device__ uint64_t mp_mem(const PageCutArgs &a, MpCol *S, int64_t r)
@@ -761,32 +822,131 @@ __device__ uint64_t mp_mem(const PageCutArgs &a, MpCol *S, int64_t r)
     uint64_t part = 0;
     for (int c = threadIdx.x; c < a.ncols; c += 64) {
         MpCol &m = S[c];
-        const uint32_t nc = a.ncuts[c];
-        while (m.ci < nc && a.cuts[(uint64_t)c * a.cap + m.ci] <= r) {
+        while (m.next_cut <= r) {
             m.pb += a.pbytes[a.pb_off[c] + m.ci];
-            m.q = a.cuts[(uint64_t)c * a.cap + m.ci];
+            m.q = m.next_cut;
             m.ci++;
+            m.next_cut = m.ci < m.nc ? a.cuts[(uint64_t)c * a.cap + m.ci] : INT64_MAX;
             walker_init(m.w, m.q);
-            if (a.v2 && a.col_bstream[c] >= 0) bool_walker_init(a, c, m.wb, m.q);
+            if (a.v2 && m.I.kb >= 0) bool_walker_init(m.I, m.wb, m.q);
         }
-        part += m.pb + col_dl_bytes(a, c, m.w, r) + col_data_bytes(a, c, m.wb, m.q, r);
+        part += m.pb + col_dl_bytes(a, m.I, m.w, r) + col_data_bytes(a, m.I, m.wb, m.q, r);
     }
     return wave_sum(part);
+}
+
+// A walker's value at r with a bounded walk (<= 16 windows of 4096 positions; false: over budget)
+template <class Src>
+__device__ __forceinline__ bool walker_query_capped(Walker &w, int64_t r, const Src &src, uint64_t n, const EvView &Eg, uint64_t &val)
+{
+    for (int k = 0; k < 16; k++) {
+        const int64_t t = (w.state == 0 && r - w.p > 4096) ? w.p + 4096 : r;
+        val = walker_query(w, t, src, n, Eg);
+        if (t == r) return true;
+        if (w.state != 0) { val = walker_query(w, r, src, n, Eg); return true; }
+    }
+    return false;
+}
+
+// memSize at record r evaluated by one lane alone (v1), for the clamp points ahead of the
+// sequential cursor S (read only): each column's pages between the cursor and r, and its
+// definition-level walker from the open page's start (the cursor's walker when it is the same
+// page).  false: a walk over its budget (the point is then left to the sequential evaluation).
+__device__ bool mp_mem_point(const PageCutArgs &a, const MpCol *S, int64_t r, uint64_t &M)
+{
+    uint64_t tot = 0;
+    for (int c = 0; c < a.ncols; c++) {
+        const MpCol &m = S[c];
+        uint32_t ci = m.ci;
+        int64_t q = m.q, nxt = m.next_cut;
+        uint64_t pb = m.pb;
+        while (nxt <= r) {
+            pb += a.pbytes[a.pb_off[c] + ci];
+            q = nxt;
+            ci++;
+            nxt = ci < m.nc ? a.cuts[(uint64_t)c * a.cap + ci] : INT64_MAX;
+        }
+        uint64_t dl = 0;
+        if (m.I.kdl >= 0) {
+            Walker w;
+            if (q == m.q) w = m.w; else walker_init(w, q);
+            if (!walker_query_capped(w, r, SrcDirect{m.I.pres, m.I.gdl}, a.n, m.I.edl, dl)) return false;
+        }
+        Walker wb;   // (v1: unused)
+        tot += pb + dl + col_data_bytes(a, m.I, wb, q, r);
+    }
+    M = tot;
+    return true;
 }
 
 __global__ void __launch_bounds__(64) k_plan_mp(PageCutArgs a)
 {
     __shared__ MpCol S[MAX_COLS];
     for (int c = threadIdx.x; c < a.ncols; c += 64) {
-        walker_init(S[c].w, a.s);
-        if (a.v2 && a.col_bstream[c] >= 0) bool_walker_init(a, c, S[c].wb, a.s);
-        S[c].q = a.s; S[c].pb = 0; S[c].ci = 0;
+        MpCol &m = S[c];
+        m.I = mp_col_info(a, c);
+        walker_init(m.w, a.s);
+        if (a.v2 && m.I.kb >= 0) bool_walker_init(m.I, m.wb, a.s);
+        m.q = a.s; m.pb = 0; m.ci = 0;
+        m.nc = a.ncuts[c];
+        m.next_cut = m.nc ? a.cuts[(uint64_t)c * a.cap] : INT64_MAX;
     }
     __syncthreads();
     const int64_t T = a.next_rg_size;
     const int64_t s = a.s;
     int64_t rc = 100, cut = -1;
+#ifdef KPW_PLAN_PROF
+    uint32_t pp_checks = 0;
+    const uint64_t pp_t0 = wall_clock64();
+#endif
+    const int lane = threadIdx.x;
+    bool clamp = false;   // the previous decision took the recordCount + 10000 clamp
     while (s + rc <= a.h) {
+        if (clamp && !a.v2) {
+            // (as k_plan) the next 64 clamp-step points at once, lane j for point j: its memSize
+            // and parquet-mr's decision there; the first point past the horizon, that cuts, that
+            // leaves the clamp path or whose walk ran over budget ends the batch
+            __syncthreads();   // the cursor's state, written by every lane, is read by each
+            const int64_t rcv = rc + 10000 * (int64_t)lane;
+            const bool past = s + rcv > a.h;
+            bool ok = true, cut_j = false;
+            int64_t nc = rcv + 10000;
+            if (!past) {
+                uint64_t Mu = 0;
+                ok = mp_mem_point(a, S, s + rcv, Mu);
+                if (ok) {
+                    const int64_t M = (int64_t)Mu;
+                    const int64_t rs = M / rcv;
+                    cut_j = M > T - 2 * rs;
+                    if (!cut_j) {
+                        const float qf = __fdiv_rn((float)T, (float)rs);
+                        const int64_t est = jadd(rcv, java_f2l(qf)) / 2;
+                        const int64_t lo = est > 100 ? est : 100;
+                        const int64_t hi = jadd(rcv, 10000);
+                        nc = lo < hi ? lo : hi;
+                        if (nc < rcv + 1) nc = rcv + 1;
+                    }
+                }
+            }
+#ifdef KPW_PLAN_PROF
+            pp_checks++;
+#endif
+            const uint64_t stop = __ballot(past || !ok || cut_j || nc != rcv + 10000);
+            if (!stop) { rc += 10000 * 64; continue; }
+            const int js = __builtin_ctzll(stop);   // uniform
+            const int64_t rcs = rc + 10000 * (int64_t)js;
+            if (s + rcs > a.h) { rc = rcs; continue; }   // leaves the loop
+            clamp = false;
+            if (!__builtin_amdgcn_readlane((int)ok, js)) { rc = rcs; continue; }   // the sequential check, at rcs
+            if (__builtin_amdgcn_readlane((int)cut_j, js)) { cut = s + rcs; break; }
+            const uint32_t nlo = __builtin_amdgcn_readlane((uint32_t)nc, js);
+            const uint32_t nhi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)nc >> 32), js);
+            rc = (int64_t)(((uint64_t)nhi << 32) | nlo);
+            continue;
+        }
+#ifdef KPW_PLAN_PROF
+        pp_checks++;
+#endif
         const int64_t M = (int64_t)mp_mem(a, S, s + rc);
         const int64_t rs = M / rc;
         if (M > T - 2 * rs) { cut = s + rc; break; }
@@ -796,11 +956,17 @@ __global__ void __launch_bounds__(64) k_plan_mp(PageCutArgs a)
         const int64_t hi = jadd(rc, 10000);
         int64_t nc = lo < hi ? lo : hi;
         if (nc < rc + 1) nc = rc + 1;
+        clamp = nc == rc + 10000;
         rc = nc;
     }
     int64_t open_buf = 0;
     if (cut < 0 && a.h == (int64_t)a.n && s < a.h) open_buf = (int64_t)mp_mem(a, S, a.h);
     if (threadIdx.x == 0) { a.out[0] = cut; a.out[1] = open_buf; }
+#ifdef KPW_PLAN_PROF
+    if (threadIdx.x == 0)
+        printf("[plan_mp] s %lld h %lld cut %lld checks %u ticks %llu\n", (long long)a.s, (long long)a.h, (long long)cut, pp_checks,
+               (unsigned long long)(wall_clock64() - pp_t0));
+#endif
 }
 
 void launch_str_sizes(const DevCol *cols, int c, uint64_t n, uint32_t *sz, hipStream_t s)
