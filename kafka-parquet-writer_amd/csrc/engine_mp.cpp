@@ -619,7 +619,11 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     }
     uint64_t acc_len = 0;
     const uint64_t per_rec = std::max<uint64_t>(1, Ptot / ne);
+    // first horizon: 2 x the raw records of a row group, or 1.25 x the last row group this engine
+    // cut (flushed pages count compressed, so a row group holds more than T of raw bytes; a short
+    // horizon costs a second speculative encode, C2 1 MiB pages: 4.3 M -> 8.5 M for a 6.7 M cut)
     int64_t guess = std::max<int64_t>(1000, (int64_t)(2 * (uint64_t)T / per_rec));
+    if (mp_last_rg_ > 0) guess = std::max<int64_t>(guess, mp_last_rg_ + mp_last_rg_ / 4 + 200);
     int64_t s0 = 0;
     std::vector<std::vector<int64_t>> cuts;
     MpRun run;
@@ -688,6 +692,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
             rs = append(s0, r);
             if (rs) return rs;
             guess = std::max<int64_t>(1000, (r - s0) + (r - s0) / 4 + 200);
+            mp_last_rg_ = r - s0;
             s0 = r;
             if (max_cuts > 0 && (int32_t)out.rgs.size() >= max_cuts) break;   // re-planned by the caller
             continue;

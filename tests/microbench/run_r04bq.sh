@@ -3,5 +3,5 @@
 OUT=gpurun_out/r04bq
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "not fullsize" > $OUT/pytest.log 2>&1 || exit $?
-KPW_GPU_LIB=tests/microbench/build/libvar/libkpw_pmp.so timeout -k 10 300 python3 tests/microbench/bulk_mp_leg.py 20000000 1 > $OUT/bp.log 2>&1 || exit $?
+true
 timeout -k 10 300 python3 tests/microbench/bulk_mp_leg.py 100000000 2 > $OUT/bm.log 2>&1 || exit $?
