@@ -77,16 +77,18 @@ uint64_t stage_flush_bytes()
     return v;
 }
 // Eager jobs: a fill buffer holding at least this many appended bytes is submitted early when
-// an encode worker is idle and nothing is queued (KPW_EAGER_MB, default 512; a negative value
+// an encode worker is idle and nothing is queued (KPW_EAGER_MB, default 384; a negative value
 // turns it off).  The GPU then starts on the data already in HBM instead of waiting for a full
 // job, and close() finds less left to encode; jobs stay at the full size while the workers are
-// busy.  C2 writer path 33.5 -> 35.8 GB/s, C5 28.4 -> 31.6 (384 / 640 / 768 MiB measured lower;
-// DESIGN.md §6).
+// busy.  C2 writer path 33.5 -> 35.8 GB/s, C5 28.4 -> 31.6 with 512 MiB in r02; with round 4's
+// fewer dispatches and syncs per job 384 MiB measured better (alternating on one box: C2 5 runs
+// 42.1-44.5 against 35.7-43.5 GB/s with 512, C3 42.6-45.8 against 42.2, C4 21.2-21.3 against
+// 20.7-20.9, C5 unchanged; 256 MiB lower).
 uint64_t eager_job_bytes()
 {
     static const uint64_t b = [] {
         const char *e = getenv("KPW_EAGER_MB");
-        const long long v = e ? atoll(e) : 512;
+        const long long v = e ? atoll(e) : 384;
         return v > 0 ? (uint64_t)v << 20 : 0ull;
     }();
     return b;
