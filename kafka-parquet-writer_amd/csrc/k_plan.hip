@@ -222,6 +222,9 @@ struct LWalker {
     uint32_t state;     // 0 walking, 1 converged, 2 no long runs left (closed form)
 };
 __device__ __forceinline__ uint64_t bp_bytes(uint64_t G) { return G + (G + 62) / 63; }
+#ifndef LW_BATCH
+#define LW_BATCH 8u   // long runs per load round of a walker
+#endif
 
 __device__ __forceinline__ void lw_init(LWalker &w, const PlanSt &S, int64_t p)
 {
@@ -256,17 +259,17 @@ __device__ uint64_t lw_query(LWalker &w, int64_t r, const PlanSt &S, const EvVie
         if (w.cur >= S.nlong) { w.state = 2; break; }
         // 8 long runs per round: their loads issue together (one latency per 8 runs; C3 walks
         // ~150 runs before the parses meet)
-        const uint32_t nb = S.nlong - w.cur < 8 ? S.nlong - w.cur : 8;
-        uint32_t A[8], B[8], Fl[8];
+        const uint32_t nb = S.nlong - w.cur < LW_BATCH ? S.nlong - w.cur : LW_BATCH;
+        uint32_t A[LW_BATCH], B[LW_BATCH], Fl[LW_BATCH];
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < (int)LW_BATCH; i++) {
             const bool v = (uint32_t)i < nb;
             A[i] = v ? S.lra[w.cur + i] : 0;
             B[i] = v ? S.lrb[w.cur + i] : 0;
             Fl[i] = v ? S.lrle[w.cur + i] : 0;
         }
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < (int)LW_BATCH; i++) {
             if ((uint32_t)i >= nb) break;
             const int64_t b = B[i];
             int64_t a = A[i];
