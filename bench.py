@@ -21,8 +21,9 @@ opens fresh writers, so nothing an encoder learns (K7's longest-first fragment o
 between steps.
 
 Secondary keys: `resident_encode` (kpw_encoder_encode on a batch already in HBM, the r01
-headline), `c4` (the C4 writer line, 2 steps) and `bulk_multipage` (C2 bulk writes with 1 MiB
-pages inside 128 MiB row groups, 2 steps), `per_record` / `per_record_multipage` (the
+headline), `c4` (the C4 writer line, 2 steps), `bulk_multipage` (C2 bulk writes with 1 MiB
+pages inside 128 MiB row groups, 2 steps), `c5` (BASELINE config 5 at its shape: 8 concurrent
+writers of 15.625 M Rec8 records each, 2 steps), `per_record` / `per_record_multipage` (the
 reference's write + getDataSize loop at 128 MiB / 1 MiB pages, the oracle's same loops in
 `cpu_baseline`), `roofline` (the dominant kernel, timed with HIP events on the encoder's stream inside
 the timed writer steps; algorithmic bytes per launch), `roofline.pipeline_frac` (sum of
@@ -351,6 +352,49 @@ def writer_leg(kpw, kind, seed, n, device, steps, warmup, page_size=128 * MiB, s
                 workload=sschema.message_name.split(".")[-1] + ", SNAPPY, 128 MiB row groups, pageSize %d" % page_size)
 
 
+def c5_leg(kpw, device, steps, warmup):
+    """Secondary writer line for BASELINE config 5 at its stated shape: the 8
+    partitions of the 64-partition topic this GPU owns (seeds 0xC0FFEE05 + p), one concurrent
+    kpw_writer per partition on its own thread (KafkaProtoParquetWriter.java:175-179), 125 M Rec8
+    records per GPU (15.625 M per partition), SNAPPY, 128 MiB row groups, 500 k poll batches;
+    one step = all 8 files closed.  Same drop-in and timing as the headline."""
+    import synth
+    kind, n, wseed, wdesc = WORKLOADS["c5"]
+    sschema = synth.SCHEMAS[kind]
+    schema = kpw.Schema(sschema.message_name, sschema.columns, sschema.proto_class)
+    props = kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=kpw.SNAPPY, page_size=128 * MiB)
+    per = n // C5_PARTS_PER_GPU
+    parts = [synth.generate(kind, wseed + p, per, alloc=kpw.pinned_empty) for p in range(C5_PARTS_PER_GPU)]
+    nb = sum(int(o[-1]) for _, o in parts)
+
+    def step():
+        res, errs = [None] * len(parts), []
+
+        def one(k):
+            try:
+                res[k] = write_file(kpw, schema, props, parts[k][0], parts[k][1], device)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        ts = [threading.Thread(target=one, args=(k,)) for k in range(len(parts))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        return sum(size for size, _ in res)
+
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    file_bytes = sum(step() for _ in range(steps))
+    dt = time.perf_counter() - t0
+    return dict(value=round(nb * steps / dt / 1e9, 4), unit="GB/s", records_per_s=round(steps * per * len(parts) / dt, 1),
+                ms_per_step=round(dt / steps * 1e3, 3), steps=steps, warmup=warmup, records_per_step=per * len(parts),
+                bytes_per_step=nb, file_bytes_per_step=int(file_bytes / steps), writers=len(parts),
+                records_per_writer=per, workload=wdesc + ", 128 MiB row groups, 500 k poll batches")
+
+
 def cpu_baseline_per_record(sschema, kind, seed, n, max_file_size, page_size):
     """CPU-baseline leg of the per-record loop: the oracle's kpwo_write + kpwo_data_size per
     record on the same records as per_record_leg, one thread (one WorkerThread)."""
@@ -464,7 +508,7 @@ def main():
     ap.add_argument("--per-record-page-kb", type=int, default=128 * 1024,
                     help="pageSize of the per-record leg (reference default = blockSize, KafkaProtoParquetWriter.java:474)")
     ap.add_argument("--secondary-steps", type=int, default=2,
-                    help="timed steps of the secondary writer legs at N=1 (c4 and bulk_multipage; 0 = skip)")
+                    help="timed steps of the secondary writer legs at N=1 (c4, bulk_multipage and c5; 0 = skip)")
     ap.add_argument("--per-record-mp-page-kb", type=int, default=1024,
                     help="pageSize of a second per-record leg with page cuts inside row groups (pageSize(...), "
                          "KafkaProtoParquetWriter.java:656-659; 0 = skip)")
@@ -586,13 +630,14 @@ def main():
         if args.per_record_mp_page_kb:   # pageSize < blockSize: page cuts inside row groups (size probes)
             per_record_mp = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_records, local_rank,
                                            args.per_record_max_file_mb * MiB, args.per_record_mp_page_kb * 1024)
-    c4_leg = bulk_mp = None
+    c4_leg = bulk_mp = c5 = None
     if args.secondary_steps and world == 1 and args.workload == "c2":
         # the config where encode, not PCIe, sets the pace (C4), and bulk writes with 1 MiB pages
         c4k, c4n, c4seed, _ = WORKLOADS["c4"]
         c4_leg = writer_leg(kpw, c4k, c4seed, c4n, local_rank, args.secondary_steps, 1)
         bulk_mp = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, page_size=MiB,
                              sets=[s[0] for s in sets])
+        c5 = c5_leg(kpw, local_rank, args.secondary_steps, 1)
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         threads = args.cpu_threads or host_threads()
@@ -633,6 +678,7 @@ def main():
         "per_record_multipage": per_record_mp,
         "c4": c4_leg,
         "bulk_multipage": bulk_mp,
+        "c5": c5,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

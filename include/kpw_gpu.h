@@ -57,7 +57,8 @@ int kpw_writer_write(kpw_writer *w, const uint8_t *data, const uint64_t *offsets
 /* kpw_writer_write for a consumer that polls into a ring of >= 2 kpw_host_alloc batches
  * (north_star: polled batches in pinned staging, moved to HBM by hipMemcpyAsync on a side
  * stream): the call returns once the batch's DMA is queued, and the DMA may still read `data`
- * until the NEXT kpw_writer_* call on this handle returns (the next async write waits for it
+ * until the NEXT kpw_writer_* call on this handle returns (any entry point, getters and
+ * kpw_writer_free included, waits for it before returning; the next async write waits for it
  * then, with its own DMA already queued behind it, so the copy stream never idles between
  * poll batches).  `offsets` may be reused at once.  Same records, file and errors as
  * kpw_writer_write; memory outside kpw_host_alloc is copied before the call returns. */

@@ -63,6 +63,11 @@ Engine::~Engine()
     const auto t0 = std::chrono::steady_clock::now();
     for (auto &e : ev_) if (e) (void)hipEventDestroy(e);
     for (auto &e : kev_) if (e) (void)hipEventDestroy(e);
+    for (int k = 0; k < UP_RING; k++)
+        if (up_ev_[k]) {
+            if (up_used_[k]) (void)hipEventSynchronize(up_ev_[k]);
+            (void)hipEventDestroy(up_ev_[k]);
+        }
     if (stream) (void)hipStreamSynchronize(stream);
     seg_scratch_free(seg_);
     if (stream) (void)hipStreamDestroy(stream);
@@ -144,6 +149,7 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto &e : ev_) CK(hipEventCreate(&e));
     for (auto &e : kev_) CK(hipEventCreate(&e));
+    for (auto &e : up_ev_) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const size_t nc = cols.size();
     col_vals.resize(nc); col_shash.resize(nc); col_spfx.resize(nc); col_soff.resize(nc); col_slen.resize(nc); col_pres.resize(nc); col_vbits.resize(nc); col_pcnt.resize(nc);
     col_cbits.resize(bool_idx_.size());
@@ -168,7 +174,13 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
 // ordering explicit.
 int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::vector<uint8_t *> &dev)
 {
-    static thread_local std::vector<uint8_t> host;
+    const int k = up_k_;
+    up_k_ = (up_k_ + 1) % UP_RING;
+    if (up_used_[k]) {   // the copy that last read this slot has completed (at once in practice)
+        up_used_[k] = false;
+        CK(hipEventSynchronize(up_ev_[k]));
+    }
+    std::vector<uint8_t> &host = up_host_[k];
     size_t tot = 0;
     for (const HostPart &q : parts) tot += (q.bytes + 255) & ~(size_t)255;
     ENS(buf, std::max<size_t>(tot, 256));
@@ -181,6 +193,8 @@ int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::v
         at += (q.bytes + 255) & ~(size_t)255;
     }
     CK(xh2d(buf.p, host.data(), tot, stream));
+    CK(hipEventRecord(up_ev_[k], stream));
+    up_used_[k] = true;
     return KPW_OK;
 }
 

@@ -178,6 +178,14 @@ private:
         d_tile_sfx, d_tile_sfx_off, d_chunk_sfx;
     hipEvent_t ev_[9] = {};
     hipEvent_t kev_[4] = {};
+    // upload_parts' pageable host staging: a ring of buffers, each reused only after the event
+    // recorded behind its copy has completed (correct whether or not hipMemcpyAsync has consumed
+    // a pageable source by the time it returns)
+    static constexpr int UP_RING = 4;
+    std::vector<uint8_t> up_host_[UP_RING];
+    hipEvent_t up_ev_[UP_RING] = {};
+    bool up_used_[UP_RING] = {};
+    int up_k_ = 0;
     std::vector<uint32_t> opt_idx_, bool_idx_;
     int run_rle(std::vector<RleJob> &jobs, uint32_t &nptiles, uint32_t &netiles, RleScratch &sc);
     int rle_layout(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, std::vector<uint32_t> &ptj, std::vector<uint32_t> &etj);

@@ -222,9 +222,7 @@ struct LWalker {
     uint32_t state;     // 0 walking, 1 converged, 2 no long runs left (closed form)
 };
 __device__ __forceinline__ uint64_t bp_bytes(uint64_t G) { return G + (G + 62) / 63; }
-#ifndef LW_BATCH
-#define LW_BATCH 8u   // long runs per load round of a walker
-#endif
+constexpr uint32_t LW_BATCH = 8;   // long runs per load round of a walker (16 measured slower)
 
 __device__ __forceinline__ void lw_init(LWalker &w, const PlanSt &S, int64_t p)
 {

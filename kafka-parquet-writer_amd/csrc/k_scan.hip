@@ -164,17 +164,18 @@ uint64_t *scan_tmp(SegScratch *sc, uint64_t words, hipStream_t s)
     return (uint64_t *)sc->tmp;
 }
 
-// look-back timeouts counted on the scratch (kpw_lookback.h)
-// Status words of one single-pass launch (nwords: ntiles x scans; w == nullptr: allocation
-// failed, sc->failed set).  Grown buffers start zeroed; the epoch wraps after 2^15 - 1
-// launches with a clear.
+// Look-back timeouts counted since the previous call (kpw_lookback.h), read and cleared: the
+// count lives in its own word (SegScratch::fails), which the status words' growth and
+// epoch-wrap clears never touch, so a timeout early in an encode is still seen at its end and
+// does not fail the handle's later encodes.
 int lb_failures(SegScratch *sc, hipStream_t s)
 {
-    if (!sc->p) return 0;
+    if (!sc->fails) return 0;
     uint32_t n = 0;
-    if (hipMemcpyAsync(&n, (const uint64_t *)sc->p + 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(&n, sc->fails, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -1;
+    if (n && (hipMemsetAsync(sc->fails, 0, 4, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)) return -1;
     return (int)n;
 }
 
@@ -184,6 +185,12 @@ int lb_failures(SegScratch *sc, hipStream_t s)
 LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s)
 {
     const size_t need = 64 + (size_t)nwords * 8;
+    if (!sc->fails) {
+        sc->fails = (uint32_t *)dev_alloc(64);
+        if (!sc->fails || hipMemsetAsync(sc->fails, 0, 64, s) != hipSuccess) {
+            sc->failed = true; return LbView{nullptr, 0, nullptr};
+        }
+    }
     if (need > sc->bytes) {
         // earlier scans of this handle may still use the old buffer on `s`
         if (sc->p) dev_free_after(sc->p, s);
@@ -192,15 +199,15 @@ LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s)
         sc->bytes = std::max<size_t>(need * 2, 16u << 20);
         sc->p = dev_alloc(sc->bytes);
         if (!sc->p || hipMemsetAsync(sc->p, 0, sc->bytes, s) != hipSuccess) {
-            sc->bytes = 0; sc->failed = true; return LbView{nullptr, 0};
+            sc->bytes = 0; sc->failed = true; return LbView{nullptr, 0, nullptr};
         }
         sc->epoch = 0;
     }
     if (++sc->epoch >= (1u << 15)) {
-        if (hipMemsetAsync(sc->p, 0, sc->bytes, s) != hipSuccess) { sc->failed = true; return LbView{nullptr, 0}; }
+        if (hipMemsetAsync(sc->p, 0, sc->bytes, s) != hipSuccess) { sc->failed = true; return LbView{nullptr, 0, nullptr}; }
         sc->epoch = 1;
     }
-    return LbView{(uint64_t *)sc->p, sc->epoch};
+    return LbView{(uint64_t *)sc->p, sc->epoch, sc->fails};
 }
 
 template <class F>
@@ -330,7 +337,9 @@ void seg_scratch_free(SegScratch &sc)
 {
     dev_free(sc.p);
     dev_free(sc.tmp);
+    dev_free(sc.fails);
     sc.p = sc.tmp = nullptr;
+    sc.fails = nullptr;
     sc.bytes = sc.tmp_bytes = 0;
 }
 

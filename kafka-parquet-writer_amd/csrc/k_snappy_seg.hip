@@ -57,12 +57,6 @@ constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the wh
 #endif
 
 constexpr uint32_t SG_NOMATCH = 0xffff;  // cand[]: the table entry's 4 bytes differ (positions < 65521)
-#ifdef SG_FP16
-// SG_FP16: the rounds compare 16-bit fingerprints of the 4-byte keys (half the key array each
-// round re-reads); a fingerprint match is confirmed on the fragment's bytes where the parse
-// takes it, so cand[] may hold a false candidate but no decision does
-__device__ __forceinline__ uint32_t sg_fp(uint32_t x) { return (x ^ (x >> 16)) & 0xffffu; }
-#endif
 
 enum : uint32_t { MS = 0, MP = 1, MT = 2 };
 struct PS {
@@ -249,11 +243,7 @@ __device__ __forceinline__ uint32_t put_lit_tag(sgg_u8 *o, uint32_t op, uint32_t
 // at rec[r * SG_T + t], so a wave's loads and stores cover contiguous 1 KiB / 512 B spans.
 struct SgScratch {
     uint4 sig4[8 * SG_T];         // positions sorted by (hash, position), 8 entries per piece
-#ifdef SG_FP16
-    uint4 key4[8 * SG_T];         // a 16-bit fingerprint of the 4 bytes at each sorted entry's position
-#else
     uint4 key4[16 * SG_T];        // the 4 bytes at each sorted entry's position
-#endif
     uint64_t bflag[SG_T];         // bit j of word t: sorted entry 64t+j starts a hash bucket
     uint64_t rec[SG_T * SG_RECS]; // copies found by the last parse, per segment
     uint32_t job[2 * SG_T][4];    // long literals: src, dst, len
@@ -359,9 +349,6 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
             if (ipe - 1 >= sk) o.own |= 1ull << (ipe - 1 - sk); else o.lfl = true;
             c = S.a.cand[ipe];
             o.own |= 1ull << (ipe - sk);
-#ifdef SG_FP16
-            if (c != SG_NOMATCH && in.ld32(c) != in.ld32(ipe)) c = SG_NOMATCH;   // a fingerprint's false match
-#endif
             if (c == SG_NOMATCH) { st = PS{MS, ipe + 1, 32, ipe}; continue; }
             base = ipe; lit = false;
         } else {
@@ -390,20 +377,6 @@ __device__ __forceinline__ ParseOut sg_parse(const SgShared &S, SgScratch &G, co
 #pragma unroll
             for (int k = (int)SG_PB - 1; k >= 0; k--)
                 if (v[k] && cc[k] != SG_NOMATCH) hit = k;
-#ifdef SG_FP16
-            // a fingerprint's false match is a miss: the next matching probe is the hit
-            for (uint32_t fpm = 0; hit >= 0;) {
-                uint32_t qh = q[0], ch = cc[0];
-#pragma unroll
-                for (int k = 1; k < (int)SG_PB; k++) if (hit == k) { qh = q[k]; ch = cc[k]; }
-                if (in.ld32(ch) == in.ld32(qh)) break;
-                fpm |= 1u << hit;
-                hit = -1;
-#pragma unroll
-                for (int k = (int)SG_PB - 1; k >= 0; k--)
-                    if (v[k] && cc[k] != SG_NOMATCH && !((fpm >> k) & 1)) hit = k;
-            }
-#endif
 #pragma unroll
             for (int k = 0; k < (int)SG_PB; k++)
                 if (v[k] && (hit < 0 || k <= hit)) o.own |= 1ull << (q[k] - sk);
@@ -566,11 +539,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 for (int u = 0; u < 16; u++) asm volatile("" : "+v"(idx[u]));   // one wait for the batch
 #pragma unroll
                 for (int u = 0; u < 16; u++)
-#ifdef SG_NOSTORE
-                    if (h[u] != 0xffffffffu && idx[u] == 0x12345678u) sig[sig_slot((idx[u] >> ((h[u] & 1) * 16)) & 0xffffu)] = (uint16_t)((g0 + u) * 64 + lane);
-#else
                     if (h[u] != 0xffffffffu) sig[sig_slot((idx[u] >> ((h[u] & 1) * 16)) & 0xffffu)] = (uint16_t)((g0 + u) * 64 + lane);
-#endif
             }
         }
         __threadfence_block();
@@ -605,13 +574,8 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                     prevp = pp[e];
                     kk[e] = lds_ld32(S, pp[e]);
                 }
-#ifdef SG_FP16
-                kp[q * SG_T] = sg_u32x4{sg_fp(kk[0]) | (sg_fp(kk[1]) << 16), sg_fp(kk[2]) | (sg_fp(kk[3]) << 16),
-                                        sg_fp(kk[4]) | (sg_fp(kk[5]) << 16), sg_fp(kk[6]) | (sg_fp(kk[7]) << 16)};
-#else
                 kp[(2 * q) * SG_T] = sg_u32x4{kk[0], kk[1], kk[2], kk[3]};
                 kp[(2 * q + 1) * SG_T] = sg_u32x4{kk[4], kk[5], kk[6], kk[7]};
-#endif
             }
             }
             G.bflag[t] = bf;
@@ -686,39 +650,6 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                 uint32_t km = (!same && m) ? in.ld32(m) : key0;
 #pragma unroll
                 for (int q = 0; q < (int)SG_SEG / 2; q++) asm volatile("" : "+v"(sg2[q]));   // re-extract, do not keep 64 values live
-#ifdef SG_FP16
-                if (!same) {
-                    // fingerprints: 2 chunks of 4 pieces (8 entries per piece)
-                    sgg_cu4 *kp = (sgg_cu4 *)(G.key4 + t);
-                    asm volatile("" : "+v"(kp));
-                    uint32_t fkm = sg_fp(km);
-                    const uint32_t fk0 = sg_fp(key0);
-                    sg_u32x4 kb[2][4];
-#pragma unroll
-                    for (int i = 0; i < 4; i++) kb[0][i] = kp[i * SG_T];
-#pragma unroll
-                    for (int c4 = 0; c4 < 2; c4++) {
-                        if (c4 < 1) {
-#pragma unroll
-                            for (int i = 0; i < 4; i++) kb[1][i] = kp[(4 + i) * SG_T];
-                        }
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const sg_u32x4 k4 = kb[c4][i];
-                            const uint32_t kw[4] = {k4.x, k4.y, k4.z, k4.w};
-#pragma unroll
-                            for (int e = 0; e < 8; e++) {
-                                const int j = (c4 * 4 + i) * 8 + e;
-                                const uint32_t fe = (kw[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-                                const uint32_t p = (sg2[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-                                if ((bf >> j) & 1) { m = 0; fkm = fk0; }
-                                if (i0 + j < npos) S.a.cand[p] = (uint16_t)(fkm == fe ? m : SG_NOMATCH);
-                                if ((insm >> j) & 1) { m = p; fkm = fe; }
-                            }
-                        }
-                    }
-                }
-#else
                 if (!same) {
                     // keys in 4 chunks of 4 pieces, the next chunk's loads in flight while one is
                     // used (the base is re-derived every round: hoisted per-piece addresses spill)
@@ -748,7 +679,6 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
                         }
                     }
                 }
-#endif
             }
             PMARK(15);
             __syncthreads();

@@ -16,16 +16,17 @@
 // tile does).  A ticket counter would not need that, but one atomic per tile on a single
 // address serialised the launch (r04: the element-tile kernels over ~50 k tiles took 0.7 ms
 // where the multi-launch scans took 0.1).  The spin is bounded: a tile that waits past the
-// bound counts a failure in w[1] (the engine fails the encode on it, lb_failures) and goes on
-// with a wrong value rather than hang the GPU.
+// bound counts a failure in *fails (the engine fails the encode on it, lb_failures) and goes
+// on with a wrong value rather than hang the GPU.
 #pragma once
 #include "kpw_device.h"
 
 namespace kpw {
 
 struct LbView {
-    uint64_t *w;      // w[1] (low u32): look-back timeouts; status words from w[8]
+    uint64_t *w;      // status words from w[8]
     uint32_t epoch;
+    uint32_t *fails;  // look-back timeouts (SegScratch::fails)
 };
 constexpr uint32_t LB_ST_AGG = 1, LB_ST_INC = 2;
 
@@ -56,7 +57,7 @@ __device__ __forceinline__ T lb_lookback(const LbView &L, uint32_t sbase, uint32
                 if ((uint32_t)((wv >> 2) & 0x7fff) == L.epoch && (wv & 3) != 0) { ok = true; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (!ok) { atomicAdd((uint32_t *)(L.w + 1), 1u); wv = LB_ST_INC; }   // counted; value 0, terminal
+            if (!ok) { atomicAdd(L.fails, 1u); wv = LB_ST_INC; }   // counted; value 0, terminal
         }
         const bool term = !valid || (wv & 3) == LB_ST_INC;
         const uint64_t tm = __ballot(term);

@@ -938,8 +938,6 @@ static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
         const int st = E.encode(B.d, W.offs + s0, (uint64_t)(lim - s0), j.kind == JOB_FINAL, T, nullptr, out);
         E.max_cuts = 0;
         if (st) return jfail(st, E.error());
-        if (s0 == 0 && lb_failures(&W.scan.sc, s) != 0)   // the offsets scan (kpw_lookback.h)
-            return jfail(KPW_ERR_DEVICE, "offsets scan look-back timed out");
         W.njobs++;   // page buffer sets alternate per encode
         if (out.invalid_record >= 0) {
             // records from the invalid one on are never written (KafkaProtoParquetWriter.java:270-276)
@@ -1817,10 +1815,41 @@ extern "C" int64_t kpw_writer_data_size(kpw_writer *w)
     }
 }
 
-extern "C" int64_t kpw_writer_num_records(const kpw_writer *w) { return w ? w->num_records : -1; }
-extern "C" int64_t kpw_writer_creation_time_ms(const kpw_writer *w) { return w ? w->created_ms : -1; }
-extern "C" int64_t kpw_writer_failed_record(const kpw_writer *w) { return w ? w->failed_record : -1; }
-extern "C" const char *kpw_writer_last_error(const kpw_writer *w) { return w ? w->err.c_str() : "null handle"; }
+// The getters are entry points too: the batch of an earlier kpw_writer_write_async is free
+// once any kpw_writer_* call returns (kpw_gpu.h), so each releases it first (nothing to wait
+// for when no DMA is pending).  The handle is const in the C-ABI only as a promise about the
+// file it describes; its pipeline state is the library's.
+static void release_from_getter(const kpw_writer *w)
+{
+    try {
+        (void)release_batches(const_cast<kpw_writer *>(w));   // a failed DMA is recorded (wfail)
+    } catch (...) {
+    }
+}
+extern "C" int64_t kpw_writer_num_records(const kpw_writer *w)
+{
+    if (!w) return -1;
+    release_from_getter(w);
+    return w->num_records;
+}
+extern "C" int64_t kpw_writer_creation_time_ms(const kpw_writer *w)
+{
+    if (!w) return -1;
+    release_from_getter(w);
+    return w->created_ms;
+}
+extern "C" int64_t kpw_writer_failed_record(const kpw_writer *w)
+{
+    if (!w) return -1;
+    release_from_getter(w);
+    return w->failed_record;
+}
+extern "C" const char *kpw_writer_last_error(const kpw_writer *w)
+{
+    if (!w) return "null handle";
+    release_from_getter(w);
+    return w->err.c_str();
+}
 
 // close() (ParquetFile.java:65-68): flush everything staged (after an invalid record: only
 // the records before it), then the footer.  Idempotent.
@@ -1875,7 +1904,11 @@ extern "C" int kpw_writer_file_bytes(const kpw_writer *w, const uint8_t **bytes,
     return KPW_OK;
 }
 
-extern "C" void kpw_writer_free(kpw_writer *w) { delete w; }
+extern "C" void kpw_writer_free(kpw_writer *w)
+{
+    if (w) release_from_getter(w);   // no DMA may still read a caller's batch once the handle is gone
+    delete w;
+}
 
 extern "C" int kpw_writer_stats(kpw_writer *w, double *out, int cap)
 {

@@ -60,3 +60,27 @@ def test_async_then_sync_calls_release_the_batch():
     assert st == 0
     ow.close()
     assert pf.file_bytes() == ow.file_bytes()
+
+
+@pytest.mark.parametrize("getter", ["num_records", "creation_time", "failed_record", "last_error"])
+def test_async_then_getter_releases_the_batch(getter):
+    """Every kpw_writer_* entry point releases an async write's batch: a consumer
+    that calls getNumWrittenRecords() (or another getter) after kpw_writer_write_async and then
+    refills the slot must not corrupt the file."""
+    import kpw
+    n = 600_000
+    data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE0C, n)
+    third = n // 3
+    buf = kpw.pinned_empty(int(offs[third]))
+    buf[:] = data[:int(offs[third])]
+    props = kpw.ParquetProperties(block_size=2 * MiB, compression_codec_name=kpw.SNAPPY)
+    pf = kpw.ParquetFile(None, kpw.Schema(synth.REC8.message_name, synth.REC8.columns, synth.REC8.proto_class), props)
+    pf.write_batch_async(buf, offs[:third + 1])
+    L, h = pf._L, pf._h
+    {"num_records": L.kpw_writer_num_records, "creation_time": L.kpw_writer_creation_time_ms,
+     "failed_record": L.kpw_writer_failed_record, "last_error": L.kpw_writer_last_error}[getter](h)
+    buf[:] = 0x5A   # released by the getter
+    pf.write_batch((data[int(offs[third]):], offs[third:] - offs[third]))
+    pf.close()
+    want = oracle.encode_file(synth.REC8, data, offs, oracle.make_props(block_size=2 * MiB, codec=1))
+    assert pf.file_bytes() == want, pqwalk.first_difference(pf.file_bytes(), want)

@@ -58,3 +58,50 @@ def test_full_size_writer_matches_oracle_per_row_group(kind, n, seed):
     import pyarrow.parquet as pq
     md = pq.ParquetFile(io.BytesIO(fb)).metadata
     assert md.num_rows == n and md.num_columns == len(schema.columns)
+
+
+def _c5_partition(p, n, out, errs):
+    """One Kafka partition's writer, as bench.py's c5 leg drives it: pinned poll batches of
+    500 k records handed over with kpw_writer_write_async (absolute offsets into the batch
+    array), then close()."""
+    import kpw
+    try:
+        data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE05 + p, n, alloc=kpw.pinned_empty)
+        pf = kpw.ParquetFile(None, kpw.Schema(synth.REC8.message_name, synth.REC8.columns, synth.REC8.proto_class),
+                             kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=kpw.SNAPPY))
+        L, h = pf._L, pf._h
+        for a in range(0, n, 500_000):
+            b = min(n, a + 500_000)
+            pf._check(L.kpw_writer_write_async(h, data.ctypes.data, offs.ctypes.data + 8 * a, b - a), "write")
+        pf.close()
+        assert pf.get_num_written_records() == n
+        out[p] = (pf.file_bytes(), data, offs)
+        pf.__del__()
+    except Exception as e:  # noqa: BLE001
+        errs.append((p, e))
+
+
+def test_c5_concurrent_writers_full_size():
+    """C5 as BASELINE config 5 / SURVEY §8(d) define it on one GPU: 8 partitions of the
+    64-partition topic (seeds 0xC0FFEE05 + p), one concurrent kpw_writer per partition on its
+    own thread (KafkaProtoParquetWriter.java:175-179: threadCount WorkerThreads, each owning one
+    ParquetFile), 125 M / 8 = 15.625 M Rec8 records each, SNAPPY, 128 MiB row groups, 500 k
+    poll batches: 8 writers x 2 encode workers on one device with eager jobs and open-row-group
+    carries.  Every file is checked row group by row group against the oracle."""
+    import threading
+    parts = 8
+    n = max(1000, int(125_000_000 // parts * SCALE))
+    out, errs = {}, []
+    ts = [threading.Thread(target=_c5_partition, args=(p, n, out, errs)) for p in range(parts)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    props = oracle.make_props(block_size=128 * MiB, page_size=128 * MiB, codec=1, enable_dictionary=True)
+    for p in range(parts):
+        fb, data, offs = out.pop(p)
+        assert fb[:4] == b"PAR1" and fb[-4:] == b"PAR1"
+        errs = check_row_groups(synth.REC8, data, offs, fb, props)
+        assert not errs, (p, errs[:10])
+        del fb, data, offs
