@@ -1071,6 +1071,10 @@ static int submit(kpw_writer *w, int kind, int64_t n_exact)
     }
     {
         std::lock_guard<std::mutex> g(w->mu);
+        if (trace_on())
+            fprintf(stderr, "[kpw] submit job %llu kind=%d new records=%lld (%.0f MiB) at %.1f ms, %d in flight, %d queued\n",
+                    (unsigned long long)w->next_seq, kind, (long long)F.ends.size(), (F.len - F.gap) / 1048576.0,
+                    now_ms() - w->t_open, w->inflight, (int)w->q.size());
         w->q.push_back(Job{f, kind, next, n_exact, w->next_seq++});
         w->cv.notify_all();
     }
