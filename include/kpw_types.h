@@ -40,7 +40,7 @@ enum kpw_physical_type {
 };
 
 /* parquet-format CompressionCodec. */
-enum kpw_codec { KPW_UNCOMPRESSED = 0, KPW_SNAPPY = 1 };
+enum kpw_codec { KPW_UNCOMPRESSED = 0, KPW_SNAPPY = 1, KPW_GZIP = 2 };   /* parquet-format CompressionCodec values */
 
 /* parquet-format Encoding. */
 enum kpw_encoding {

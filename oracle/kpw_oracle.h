@@ -67,6 +67,12 @@ int64_t kpwo_delta_encode(const uint64_t *vals, uint64_t n, int is_long, uint8_t
 /* snappy::RawCompress, pinned algorithm (see oracle_snappy.c header). */
 int64_t kpwo_snappy_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap);
 uint64_t kpwo_snappy_max_compressed_length(uint64_t n);
+/* GZIP (oracle_deflate.c): zlib 1.2.11 level-6 raw deflate in java.util.zip.GZIPOutputStream
+ * framing, one member per page; -1 if it does not fit `cap` */
+int64_t kpwo_deflate_raw(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap);
+int64_t kpwo_gzip_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap);
+uint64_t kpwo_gzip_bound(uint64_t n);
+uint32_t kpwo_crc32(uint32_t crc, const uint8_t *p, uint64_t n);
 
 #ifdef __cplusplus
 }

@@ -30,7 +30,7 @@ class PropsC(ctypes.Structure):
                 ("dfs_block_size", ctypes.c_int64), ("max_padding_size", ctypes.c_int64)]
 
 
-UNCOMPRESSED, SNAPPY = 0, 1
+UNCOMPRESSED, SNAPPY, GZIP = 0, 1, 2
 MiB = 1024 * 1024
 
 
@@ -88,6 +88,11 @@ def lib():
                                         ctypes.c_uint64]
         L.kpwo_snappy_compress.restype = ctypes.c_int64
         L.kpwo_snappy_compress.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        for fn in (L.kpwo_gzip_compress, L.kpwo_deflate_raw):
+            fn.restype = ctypes.c_int64
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        L.kpwo_gzip_bound.restype = ctypes.c_uint64
+        L.kpwo_gzip_bound.argtypes = [ctypes.c_uint64]
         L.kpwo_snappy_max_compressed_length.restype = ctypes.c_uint64
         L.kpwo_snappy_max_compressed_length.argtypes = [ctypes.c_uint64]
         _lib = L
@@ -197,4 +202,26 @@ def snappy_compress(data: bytes):
     n = L.kpwo_snappy_compress(data, len(data), out, cap)
     if n < 0:
         raise OracleError(-1, "snappy")
+    return out.raw[:n]
+
+
+def gzip_compress(data: bytes):
+    """One page as CompressionCodecName.GZIP writes it (oracle_deflate.c)."""
+    L = lib()
+    cap = L.kpwo_gzip_bound(len(data))
+    out = ctypes.create_string_buffer(int(cap))
+    n = L.kpwo_gzip_compress(data, len(data), out, cap)
+    if n < 0:
+        raise OracleError(-1, "gzip")
+    return out.raw[:n]
+
+
+def deflate_raw(data: bytes):
+    """zlib 1.2.11 level-6 raw deflate (windowBits -15, memLevel 8) of `data` (oracle_deflate.c)."""
+    L = lib()
+    cap = L.kpwo_gzip_bound(len(data))
+    out = ctypes.create_string_buffer(int(cap))
+    n = L.kpwo_deflate_raw(data, len(data), out, cap)
+    if n < 0:
+        raise OracleError(-1, "deflate")
     return out.raw[:n]

@@ -1041,6 +1041,13 @@ static void page_compress(kpwo_writer *w, const buf_t *in, buf_t *out)
         if (need > w->ctmp_cap) { w->ctmp = (uint8_t *)xrealloc(w->ctmp, need); w->ctmp_cap = need; }
         int64_t c = kpwo_snappy_compress(in->p, in->n, w->ctmp, w->ctmp_cap);
         buf_put(out, w->ctmp, (uint64_t)c);
+    } else if (w->props.codec == KPW_GZIP) {
+        /* GzipCodec without native hadoop: one java.util.zip.GZIPOutputStream member per page,
+         * also for an empty page (oracle_deflate.c) */
+        uint64_t need = kpwo_gzip_bound(in->n);
+        if (need > w->ctmp_cap) { w->ctmp = (uint8_t *)xrealloc(w->ctmp, need); w->ctmp_cap = need; }
+        int64_t c = kpwo_gzip_compress(in->p, in->n, w->ctmp, w->ctmp_cap);
+        buf_put(out, w->ctmp, (uint64_t)c);
     } else {
         buf_put(out, in->p, in->n);
     }
@@ -1578,7 +1585,7 @@ kpwo_writer *kpwo_open(const kpw_schema *schema, const kpw_props *props, int *st
     int st = KPW_OK;
     if (!schema || !props || schema->num_columns <= 0 || !schema->columns || !schema->message_name) { st = KPW_ERR_INVALID_ARG; goto fail; }
     if ((props->writer_version != 1 && props->writer_version != 2) ||
-        (props->codec != KPW_UNCOMPRESSED && props->codec != KPW_SNAPPY) ||
+        (props->codec != KPW_UNCOMPRESSED && props->codec != KPW_SNAPPY && props->codec != KPW_GZIP) ||
         props->block_size <= 0 || props->page_size <= 0 || props->dictionary_page_size <= 0) { st = KPW_ERR_UNSUPPORTED; goto fail; }
     kpwo_writer *w = (kpwo_writer *)xmalloc(sizeof(*w));
     memset(w, 0, sizeof(*w));

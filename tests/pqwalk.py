@@ -105,6 +105,9 @@ def decompress_pages(buf, codec_name="snappy"):
         elif codec_name == "snappy":
             raw = pg["body"][:lv] + pa.decompress(pg["body"][lv:], decompressed_size=h[2] - lv, codec="snappy",
                                                   asbytes=True)
+        elif codec_name == "gzip":   # one gzip member per page (Python's gzip module: header, CRC, ISIZE checked)
+            import gzip
+            raw = pg["body"][:lv] + gzip.decompress(pg["body"][lv:])
         else:
             raw = pg["body"]
         assert len(raw) == h[2]

@@ -50,6 +50,41 @@ def test_snappy_roundtrip_pyarrow(n):
         assert pa.decompress(c, decompressed_size=n, codec="snappy", asbytes=True) == data
 
 
+def _zlib_gzip_member(data):
+    """What GzipCodec without native hadoop writes per page: java.util.zip.GZIPOutputStream
+    (Java 8) = header 1f 8b 08 00, MTIME 0, XFL 0, OS 0 + zlib level-6 raw deflate (here: Python's
+    zlib, the same zlib 1.2.11 algorithm) + CRC-32 + ISIZE."""
+    import zlib
+    c = zlib.compressobj(6, zlib.DEFLATED, -15, 8, zlib.Z_DEFAULT_STRATEGY)
+    body = c.compress(data) + c.flush()
+    return bytes([0x1F, 0x8B, 8, 0, 0, 0, 0, 0, 0, 0]) + body + struct.pack("<II", zlib.crc32(data), len(data) & 0xFFFFFFFF)
+
+
+def _deflate_inputs():
+    rng = np.random.default_rng(11)
+    out = [b"", b"a", b"ab", b"abc", b"aaaa", bytes(1), bytes(300), bytes(70000)]
+    out.append(rng.integers(0, 256, 150_000, dtype=np.uint8).tobytes())          # stored blocks
+    out.append(rng.integers(0, 3, 250_000, dtype=np.uint8).tobytes())            # long chains, window slides
+    out.append((b"kafka-parquet-writer gzip page " * 9000)[:200_000])           # long matches
+    out.append(b"".join(struct.pack("<q", 1_700_000_000_000 + i + int(v)) for i, v in
+                        enumerate(rng.integers(0, 1000, 40_000))))                # PLAIN int64
+    js = b"".join(b'{"id":%d,"event":"%s","value":%d}' % (i, b"click" if v & 1 else b"view", v % 99991)
+                  for i, v in enumerate(rng.integers(0, 1 << 30, 12_000)))
+    out.append(js)                                                               # lazy matches, dynamic trees
+    out.append(bytes(rng.integers(0, 256, 40_000, dtype=np.uint8)) + bytes(40_000) + js[:50_000])   # mixed blocks
+    return out
+
+
+@pytest.mark.parametrize("i", range(14))
+def test_deflate_matches_zlib(i):
+    """The oracle's deflate (a restatement of zlib 1.2.11 level 6) is byte-identical to the zlib
+    Python links, and each page member round-trips through the gzip module."""
+    import gzip
+    data = _deflate_inputs()[i]
+    assert oracle.gzip_compress(data) == _zlib_gzip_member(data)
+    assert gzip.decompress(oracle.gzip_compress(data)) == data
+
+
 def _readback(schema, recs, fb):
     tbl = pq.read_table(io.BytesIO(fb))
     assert tbl.num_rows == len(recs)
@@ -62,8 +97,11 @@ CASES = [
 ]
 
 
+CODEC_NAMES = {oracle.UNCOMPRESSED: "none", oracle.SNAPPY: "snappy", oracle.GZIP: "gzip"}
+
+
 @pytest.mark.parametrize("kind,param,n", CASES)
-@pytest.mark.parametrize("codec", [oracle.UNCOMPRESSED, oracle.SNAPPY])
+@pytest.mark.parametrize("codec", [oracle.UNCOMPRESSED, oracle.SNAPPY, oracle.GZIP])
 @pytest.mark.parametrize("page_size,block_size", [(128 * MiB, 128 * MiB), (MiB, 128 * MiB), (8192, 64 * 1024)])
 @pytest.mark.parametrize("dictionary", [True, False])
 def test_oracle_readback(kind, param, n, codec, page_size, block_size, dictionary):
@@ -72,15 +110,17 @@ def test_oracle_readback(kind, param, n, codec, page_size, block_size, dictionar
     props = oracle.make_props(block_size=block_size, page_size=page_size, codec=codec, enable_dictionary=dictionary)
     fb = oracle.encode_file(schema, data, offs, props)
     _readback(schema, synth.records(data, offs), fb)
-    # every page decodes with an independent Snappy, header sizes consistent
-    pqwalk.decompress_pages(fb, "snappy" if codec == oracle.SNAPPY else "none")
+    # every page decodes with an independent Snappy / gzip, header sizes consistent
+    for pg, raw in pqwalk.decompress_pages(fb, CODEC_NAMES[codec]):
+        if codec == oracle.GZIP:   # and is exactly zlib's member of the uncompressed page
+            assert pg["body"] == _zlib_gzip_member(raw)
 
 
 V2_CASES = [(synth.KIND_SAMPLE, 30, 3000), (synth.KIND_REC8, 0, 4000), (synth.KIND_HIGHCARD, 0, 1500)]
 
 
 @pytest.mark.parametrize("kind,param,n", V2_CASES)
-@pytest.mark.parametrize("codec", [oracle.UNCOMPRESSED, oracle.SNAPPY])
+@pytest.mark.parametrize("codec", [oracle.UNCOMPRESSED, oracle.SNAPPY, oracle.GZIP])
 @pytest.mark.parametrize("page_size,block_size", [(128 * MiB, 128 * MiB), (8192, 64 * 1024)])
 @pytest.mark.parametrize("dictionary", [True, False])
 def test_oracle_v2_readback(kind, param, n, codec, page_size, block_size, dictionary):
@@ -92,7 +132,7 @@ def test_oracle_v2_readback(kind, param, n, codec, page_size, block_size, dictio
                               writer_version=2)
     fb = oracle.encode_file(schema, data, offs, props)
     _readback(schema, synth.records(data, offs), fb)
-    pqwalk.decompress_pages(fb, "snappy" if codec == oracle.SNAPPY else "none")
+    pqwalk.decompress_pages(fb, CODEC_NAMES[codec])
     assert {p["header"][1] for p in pqwalk.pages(fb)} <= {2, 3}   # dictionary + DataPageV2 only
 
 
