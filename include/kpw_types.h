@@ -88,7 +88,9 @@ typedef struct kpw_props {
     int32_t page_size;             /* page size threshold */
     int32_t dictionary_page_size;  /* max dictionary byte size before PLAIN fallback */
     int32_t enable_dictionary;     /* 0/1 (effective) */
-    int32_t codec;                 /* enum kpw_codec */
+    int32_t codec;                 /* enum kpw_codec: CompressionCodecName UNCOMPRESSED / SNAPPY / GZIP
+                                      (GZIP = GzipCodec without native hadoop: one
+                                      java.util.zip.GZIPOutputStream member per page) */
     int32_t writer_version;        /* 1 = PARQUET_1_0 (the only version the reference reaches);
                                       2 = PARQUET_2_0 (DataPageV2, RLE_DICTIONARY, DELTA_BINARY_PACKED /
                                       DELTA_BYTE_ARRAY fallback) behind this explicit flag */

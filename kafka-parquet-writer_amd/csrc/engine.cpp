@@ -111,7 +111,7 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     // The reference can never turn the dictionary off (ParquetFile.java:48-50).
     if (pr->writer_version == 2 && !pr->enable_dictionary)
         return fail(KPW_ERR_UNSUPPORTED, "PARQUET_2_0 requires the dictionary on (the only setting the reference produces)");
-    if (pr->codec != KPW_UNCOMPRESSED && pr->codec != KPW_SNAPPY) return fail(KPW_ERR_UNSUPPORTED, "codec");
+    if (pr->codec != KPW_UNCOMPRESSED && pr->codec != KPW_SNAPPY && pr->codec != KPW_GZIP) return fail(KPW_ERR_UNSUPPORTED, "codec");
     if (pr->block_size <= 0 || pr->page_size <= 0 || pr->dictionary_page_size <= 0) return fail(KPW_ERR_INVALID_ARG, "sizes");
     props = *pr;
     v2_ = pr->writer_version == 2;
@@ -198,13 +198,22 @@ int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::v
     return KPW_OK;
 }
 
+// KPW_COPY_TRACE=1: every small host <-> device copy of the engine (size) on stderr
+static bool copy_trace()
+{
+    static const bool v = [] { const char *e = getenv("KPW_COPY_TRACE"); return e && e[0] == '1'; }();
+    return v;
+}
+
 hipError_t Engine::xh2d(void *dst, const void *src, size_t bytes, hipStream_t s)
 {
+    if (copy_trace() && bytes) fprintf(stderr, "[kpw] copy h2d %zu B\n", bytes);
     return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
 }
 
 hipError_t Engine::xd2h(void *dst, const void *src, size_t bytes, hipStream_t s)
 {
+    if (copy_trace() && bytes) fprintf(stderr, "[kpw] copy d2h %zu B\n", bytes);
     return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s) : hipSuccess;
 }
 
@@ -910,6 +919,22 @@ replan:
         }
         pages_dev_ = d_comp.as<uint8_t>();
         pages_len_ = ctot;
+    } else if (props.codec == KPW_GZIP) {
+        uint64_t cap = 4096;
+        for (int p = 0; p < 2 * nch; p++) cap += ppre[p] + dfl_member_bound(plen[p]);
+        ENS(d_comp, cap);
+        CK(hipEventRecord(kev_[2], s));
+        if (int st = gzip_pages(d_body.as<uint8_t>(), body_tot, d_poff, v2_ ? d_ppre : nullptr, poff, plen,
+                                std::vector<char>(2 * nch, 1), d_pcoff, d_pclen, pt + 1, pt + 3, s))
+            return st;
+        CK(hipEventRecord(kev_[3], s));
+        CK(xd2h(ptab.data(), pt, (4 + 5 * P2) * 8, s));   // compressed total, overflow, offsets, lengths
+        CK(xsync(s));
+        if (ptab[3]) return fail(KPW_ERR_DEVICE, "gzip member overflowed its scratch slot");
+        pcoff.assign(ptab.begin() + 4 + 3 * P2, ptab.begin() + 4 + 4 * P2);
+        pclen.assign(ptab.begin() + 4 + 4 * P2, ptab.begin() + 4 + 5 * P2);
+        pages_dev_ = d_comp.as<uint8_t>();
+        pages_len_ = ptab[1];
     } else {   // uncompressed: a (v2) page body starts at its level prefix
         pcoff.resize(2 * nch);
         pclen.resize(2 * nch);
@@ -975,7 +1000,7 @@ replan:
     CK(hipEventElapsedTime(&stage_ms[7], ev_[0], ev_[7]));
     CK(hipEventElapsedTime(&stage_ms[8], kev_[0], kev_[1]));
     stage_ms[9] = 0;
-    if (props.codec == KPW_SNAPPY) CK(hipEventElapsedTime(&stage_ms[9], kev_[2], kev_[3]));
+    if (props.codec == KPW_SNAPPY || props.codec == KPW_GZIP) CK(hipEventElapsedTime(&stage_ms[9], kev_[2], kev_[3]));
 
     // ---------------------------------------------------------------- results
     for (int ci = 0; ci < nch; ci++) {
@@ -1078,6 +1103,52 @@ int Engine::copy_pages(uint64_t off, uint64_t len, void *host)
 {
     if (!pages_dev_ || off + len > pages_len_) return fail(KPW_ERR_INVALID_ARG, "copy_pages range");
     CK(hipMemcpy(host, pages_dev_ + off, len, hipMemcpyDeviceToHost));
+    return KPW_OK;
+}
+
+// GZIP (CompressionCodecName.GZIP, ParquetFile.java:45): k_deflate.hip on the listed page slots.
+// Per input byte the match finder keeps a chain distance (2 B), two match results (8 B) and a
+// symbol slot (4 B); each member is built in its own scratch slot, then the pages are packed.
+int Engine::gzip_pages(const uint8_t *body, uint64_t body_len, const uint64_t *d_poff, const uint64_t *d_ppre,
+                       const std::vector<uint64_t> &poff, const std::vector<uint64_t> &plen, const std::vector<char> &on,
+                       uint64_t *d_pcoff, uint64_t *d_pclen, uint64_t *tot, uint64_t *overflow, hipStream_t s)
+{
+    const uint32_t nslots = (uint32_t)plen.size();
+    std::vector<DflPage> pages;
+    std::vector<DflTile> tiles;
+    std::vector<int32_t> slot_page(nslots, -1);
+    uint64_t gz = 0;
+    for (uint32_t p = 0; p < nslots; p++) {
+        // a dictionary page slot (even) with no bytes has no page; a data page always has one
+        // (an empty v2 values section still gets its 20-byte member)
+        if (!on[p] || (!(p & 1) && plen[p] == 0)) continue;
+        slot_page[p] = (int32_t)pages.size();
+        const uint64_t cap = (dfl_member_bound(plen[p]) + 255) & ~255ull;
+        pages.push_back(DflPage{poff[p], plen[p], gz, cap});
+        for (uint64_t t = 0; t * 32768 < plen[p]; t++) tiles.push_back(DflTile{(uint32_t)(pages.size() - 1), (uint32_t)t});
+        gz += cap;
+    }
+    const uint32_t np = (uint32_t)pages.size(), nt = (uint32_t)tiles.size();
+    ENS(d_dfl_pdist, std::max<uint64_t>(body_len, 1) * 2 + 64);
+    ENS(d_dfl_m128, std::max<uint64_t>(body_len, 1) * 4 + 64);
+    ENS(d_dfl_m32, std::max<uint64_t>(body_len, 1) * 4 + 64);
+    ENS(d_dfl_sym, std::max<uint64_t>(body_len, 1) * 4 + 64);
+    ENS(d_dfl_gz, std::max<uint64_t>(gz, 256));
+    ENS(d_dfl_glen, std::max<uint32_t>(np, 1) * 8);
+    std::vector<uint8_t *> tp;
+    if (int st = upload_parts(d_dfl_tab, {{pages.data(), pages.size() * sizeof(DflPage)}, {tiles.data(), tiles.size() * sizeof(DflTile)},
+                                          {slot_page.data(), slot_page.size() * 4}}, tp))
+        return st;
+    DflArgs a{};
+    a.in = body; a.pages = (const DflPage *)tp[0]; a.tiles = (const DflTile *)tp[1];
+    a.pdist = d_dfl_pdist.as<uint16_t>(); a.m128 = d_dfl_m128.as<uint32_t>(); a.m32 = d_dfl_m32.as<uint32_t>();
+    a.sym = d_dfl_sym.as<uint32_t>(); a.gz = d_dfl_gz.as<uint8_t>(); a.glen = d_dfl_glen.as<uint64_t>();
+    a.nslots = nslots; a.slot_page = (const int32_t *)tp[2];
+    a.page_off = d_poff; a.page_pre = d_ppre; a.page_coff = d_pcoff; a.page_clen = d_pclen;
+    a.out = d_comp.as<uint8_t>(); a.tot = tot; a.overflow = overflow;
+    CK(hipMemsetAsync(overflow, 0, 8, s));
+    launch_deflate(a, np, nt, s);
+    CK(hipGetLastError());
     return KPW_OK;
 }
 

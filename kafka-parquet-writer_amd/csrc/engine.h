@@ -165,6 +165,12 @@ private:
     DevBuf d_sblob, d_sprof;
     DevBuf d_seg_scratch, d_seg_counter;   // k_snappy_seg (one scratch block per CU)
     int seg_args(SnappyArgs &sa);          // fills sa.seg_* (KPW_SNAPPY_SEG=0: sequential kernels only)
+    // K7 for GZIP: members of the page slots with `on[p]` into d_comp (offsets / lengths in
+    // d_pcoff / d_pclen, total at tot[0]); the caller reads them back as for Snappy
+    int gzip_pages(const uint8_t *body, uint64_t body_len, const uint64_t *d_poff, const uint64_t *d_ppre,
+                   const std::vector<uint64_t> &poff, const std::vector<uint64_t> &plen, const std::vector<char> &on,
+                   uint64_t *d_pcoff, uint64_t *d_pclen, uint64_t *tot, uint64_t *overflow, hipStream_t s);
+    DevBuf d_dfl_tab, d_dfl_pdist, d_dfl_m128, d_dfl_m32, d_dfl_sym, d_dfl_gz, d_dfl_glen;
     DevBuf d_body_alt, d_comp_alt;
     std::vector<double> sn_cost_;       // K7 mean fragment duration per (column, page kind), previous batch
     std::unordered_map<uint64_t, double> sn_fcost_;   // per (kind, fragment index)

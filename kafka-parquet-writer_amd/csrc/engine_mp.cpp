@@ -402,6 +402,24 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         pclen.assign(ptab.begin() + 4 + 4 * P2, ptab.begin() + 4 + 5 * P2);
         pages_dev_ = d_comp.as<uint8_t>();
         pages_len_ = ctot;
+    } else if (props.codec == KPW_GZIP) {
+        // a probe (k7_from) compresses only the data pages cut since its previous probe
+        std::vector<char> on(2 * npg, 1);
+        if (k7_from)
+            for (int p = 0; p < 2 * npg; p++) on[p] = (p & 1) && k7_on[p >> 1];
+        uint64_t cap = 4096;
+        for (int p = 0; p < 2 * npg; p++) cap += ppre[p] + dfl_member_bound(plen[p]);
+        ENS(d_comp, cap);
+        if (int rs = gzip_pages(d_body.as<uint8_t>(), body_tot, d_poff, v2_ ? d_ppre : nullptr, poff, plen, on, d_pcoff,
+                                d_pclen, pt + 1, pt + 3, st))
+            return rs;
+        CK(xd2h(ptab.data(), pt, (4 + 5 * P2) * 8, st));   // compressed total, overflow, offsets, lengths
+        CK(xsync(st));
+        if (ptab[3]) return fail(KPW_ERR_DEVICE, "gzip member overflowed its scratch slot");
+        pcoff.assign(ptab.begin() + 4 + 3 * P2, ptab.begin() + 4 + 4 * P2);
+        pclen.assign(ptab.begin() + 4 + 4 * P2, ptab.begin() + 4 + 5 * P2);
+        pages_dev_ = d_comp.as<uint8_t>();
+        pages_len_ = ptab[1];
     } else {   // uncompressed: a (v2) page body starts at its level prefix
         for (int p = 0; p < 2 * npg; p++) { pcoff[p] = poff[p] - ppre[p]; pclen[p] = plen[p] + ppre[p]; }
         pages_dev_ = d_body.as<uint8_t>();

@@ -146,6 +146,35 @@ constexpr uint32_t SNAPPY_FRAG = 65536;
 // output window, plus one window of slack for the final partial flush
 constexpr uint32_t SNAPPY_FRAG_CAP = ((32 + SNAPPY_FRAG + SNAPPY_FRAG / 6 + 255) / 256) * 256 + 256;
 void launch_snappy(const SnappyArgs &a, hipStream_t s);
+
+// K7 for GZIP (k_deflate.hip): one gzip member per listed page slot
+struct DflPage {
+    uint64_t off, len;   // page bytes in `in`
+    uint64_t slot, cap;  // its member's scratch slot in `gz` and the slot's size
+};
+struct DflTile {
+    uint32_t page, tile;  // listed page, 32 KiB tile of it
+};
+struct DflArgs {
+    const uint8_t *in;
+    const DflPage *pages;        // listed pages
+    const DflTile *tiles;
+    uint16_t *pdist;             // per input byte: distance to the previous same-hash position (0: none)
+    uint32_t *m128, *m32;        // per input byte: longest_match, length | distance << 9
+    uint32_t *sym;               // per input byte: symbol slots of the open block
+    uint8_t *gz;                 // member scratch
+    uint64_t *glen;              // per listed page: member length (~0: did not fit)
+    uint32_t nslots;             // page slots
+    const int32_t *slot_page;    // page slot -> listed page (-1: not compressed)
+    const uint64_t *page_off, *page_pre;   // per slot (page_pre: v2 level prefix, or nullptr)
+    uint64_t *page_coff, *page_clen;       // per slot: compressed offset / length
+    uint8_t *out;                // packed pages
+    uint64_t *tot;               // [0] total bytes
+    uint64_t *overflow;          // set to 1 when a member overflowed its slot (not expected: the slot is deflateBound)
+};
+void launch_deflate(const DflArgs &a, uint32_t npages_listed, uint32_t ntiles, hipStream_t s);
+// worst-case gzip member of n bytes (zlib's deflateBound for these parameters + framing)
+inline uint64_t dfl_member_bound(uint64_t n) { return n + (n >> 12) + (n >> 14) + (n >> 25) + 13 + 18 + 64; }
 size_t snappy_seg_scratch_bytes(uint32_t grid);
 constexpr uint32_t SEG_ABORTED = 0xfffffffeu;   // frag_len: k_snappy_seg handed the fragment on
 constexpr uint32_t SEG_TODO = 0xfffffffdu;      // frag_len: k_snappy_v ran past its budget (k_snappy_seg's work)

@@ -548,6 +548,8 @@ static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, s
         base = w->carry_store.as<uint8_t>();
         dst.carry_in_store = true;
     }
+    if (c && trace_on()) fprintf(stderr, "[kpw] carry %llu B (%zu records) %s\n", (unsigned long long)c, i1 - i0,
+                                 dst.carry_in_store ? "to the carry store" : "into the gap");
     if (c && hipMemcpyAsync(base + at, src.d + b0, c, hipMemcpyDeviceToDevice, s) != hipSuccess) return KPW_ERR_DEVICE;
     dst.carry.resize(i1 - i0 + 1);
     for (size_t i = i0; i <= i1; i++) dst.carry[i - i0] = hb[i] - b0 + at;

@@ -6,9 +6,9 @@ behaviour, backed by the HIP C-ABI library ``libkpw_gpu.so`` (include/kpw_gpu.h)
 is no CPU fallback: constructing a ParquetFile without the library raises.
 """
 from ._lib import (KpwError, InvalidProtoError, load_library, library_path, Schema, Column,
-                   UNCOMPRESSED, SNAPPY)
+                   UNCOMPRESSED, SNAPPY, GZIP)
 from .parquet_file import ParquetFile, ParquetProperties, pinned_empty
 from .encoder import Encoder, DeviceBuffer
 
 __all__ = ["ParquetFile", "ParquetProperties", "Encoder", "DeviceBuffer", "Schema", "Column", "KpwError", "InvalidProtoError",
-           "load_library", "library_path", "UNCOMPRESSED", "SNAPPY", "pinned_empty"]
+           "load_library", "library_path", "UNCOMPRESSED", "SNAPPY", "GZIP", "pinned_empty"]

@@ -5,7 +5,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
 
-UNCOMPRESSED, SNAPPY = 0, 1
+UNCOMPRESSED, SNAPPY, GZIP = 0, 1, 2   # CompressionCodecName values the reference passes through (ParquetFile.java:45)
 KPW_OK, KPW_ERR_INVALID_PROTO = 0, -3
 STATUS_NAMES = {0: "OK", -1: "INVALID_ARG", -2: "UNSUPPORTED", -3: "INVALID_PROTO", -4: "IO", -5: "DEVICE",
                 -6: "NOMEM", -7: "STATE", -8: "LIMIT"}

@@ -26,7 +26,7 @@ import datetime
 
 import numpy as np
 
-from ._lib import (KpwError, InvalidProtoError, load_library, make_schema, _PropsC, UNCOMPRESSED, SNAPPY,
+from ._lib import (KpwError, InvalidProtoError, load_library, make_schema, _PropsC, UNCOMPRESSED, SNAPPY, GZIP,
                    KPW_ERR_INVALID_PROTO)
 
 MiB = 1024 * 1024

@@ -28,7 +28,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("name,kind,param,n", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("codec", [0, 1], ids=["uncompressed", "snappy"])
+@pytest.mark.parametrize("codec", [0, 1, 2], ids=["uncompressed", "snappy", "gzip"])
 @pytest.mark.parametrize("block_size", [128 * MiB, 64 * 1024], ids=["rg128M", "rg64K"])
 def test_pages_match_oracle(name, kind, param, n, codec, block_size):
     schema = synth.SCHEMAS[kind]
@@ -38,7 +38,7 @@ def test_pages_match_oracle(name, kind, param, n, codec, block_size):
 
 
 @pytest.mark.parametrize("name,kind,param,n", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("codec", [0, 1], ids=["uncompressed", "snappy"])
+@pytest.mark.parametrize("codec", [0, 1, 2], ids=["uncompressed", "snappy", "gzip"])
 @pytest.mark.parametrize("block_size", [128 * MiB, 64 * 1024], ids=["rg128M", "rg64K"])
 def test_v2_pages_match_oracle(name, kind, param, n, codec, block_size):
     """A10 / PARQUET_2_0: DataPageV2 headers, unprefixed levels in front of the compressed
@@ -221,7 +221,7 @@ def test_tiny_batches(n):
 
 
 @pytest.mark.parametrize("kind", [synth.KIND_SAMPLE, synth.KIND_REC8])
-@pytest.mark.parametrize("codec", [0, 1])
+@pytest.mark.parametrize("codec", [0, 1, 2], ids=["uncompressed", "snappy", "gzip"])
 @pytest.mark.parametrize("n,batches", [(20000, 3), (300000, 2)], ids=["model", "bulk"])
 def test_writer_file_identical(kind, codec, n, batches):
     """The ParquetFile drop-in writes the same file bytes as the oracle, across several
@@ -505,3 +505,42 @@ def test_writer_record_length_widths():
     env = dict(os.environ, KPW_MODEL_MAX_BATCH="8", KPW_STAGE_FLUSH_MB="1", KPW_EAGER_MB="-1")
     r = subprocess.run([sys.executable, "-c", _LEN_CHILD, paths], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "lengths ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+@pytest.mark.parametrize("pattern", ["random", "zeros", "period3", "text", "mixed"])
+def test_gzip_patterns(pattern):
+    """K7 GZIP on byte patterns that exercise zlib's corner cases: stored blocks (incompressible),
+    maximal matches and long chains (zeros, short periods), lazy matches and dynamic trees (text),
+    window slides and blocks of 16383 symbols (every page here is > 64 KiB)."""
+    rng = np.random.default_rng(7)
+    n = 60000
+    if pattern == "random":
+        vals = [rng.integers(0, 256, 40, dtype=np.uint8).tobytes() for _ in range(n)]
+    elif pattern == "zeros":
+        vals = [bytes(24) for _ in range(n)]
+    elif pattern == "period3":
+        vals = [b"abc" * 11 for _ in range(n)]
+    elif pattern == "text":
+        words = [b"kafka", b"parquet", b"writer", b"gzip", b"deflate", b"page", b"row", b"group"]
+        vals = [b" ".join(words[int(k)] for k in rng.integers(0, 8, 6)) for _ in range(n)]
+    else:
+        vals = [rng.integers(0, 256, 40, dtype=np.uint8).tobytes() if i % 3 == 0 else b"x" * (i % 50) for i in range(n)]
+    # one required bytes field (1) carries the pattern bytes
+    recs = [b"\x0a" + protoutil_varint(len(v)) + v for v in vals]
+    from types import SimpleNamespace
+    s = SimpleNamespace(message_name="test.Bytes", columns=[("payload", 1, synth.BYTES, synth.REQUIRED)],
+                        proto_class="test.Bytes")
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum([len(r) for r in recs], out=offs[1:])
+    data = np.frombuffer(b"".join(recs), dtype=np.uint8)
+    errs = gh.compare_pages(s, data, offs, codec=2, dictionary=False)
+    assert not errs, "\n".join(errs[:12])
+
+
+def protoutil_varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
