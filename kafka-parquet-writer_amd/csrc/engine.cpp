@@ -172,7 +172,7 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
 // 7-10 % (every SDMA copy between two kernels of the stream is a cross-engine wait), so they
 // stay plain pageable copies; the readbacks are synchronous, xsync keeps the call sites'
 // ordering explicit.
-int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::vector<uint8_t *> &dev)
+int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::vector<uint8_t *> &dev, size_t tail_room)
 {
     const int k = up_k_;
     up_k_ = (up_k_ + 1) % UP_RING;
@@ -183,7 +183,7 @@ int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::v
     std::vector<uint8_t> &host = up_host_[k];
     size_t tot = 0;
     for (const HostPart &q : parts) tot += (q.bytes + 255) & ~(size_t)255;
-    ENS(buf, std::max<size_t>(tot, 256));
+    ENS(buf, std::max<size_t>(tot + tail_room, 256));
     host.resize(tot);
     dev.clear();
     size_t at = 0;
@@ -219,19 +219,21 @@ hipError_t Engine::xd2h(void *dst, const void *src, size_t bytes, hipStream_t s)
 
 hipError_t Engine::xsync(hipStream_t s) { return hipStreamSynchronize(s); }
 
-// Lays out tiles for the given jobs (ptj / etj: tile -> job) and sizes the scratch.
-int Engine::rle_layout(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, std::vector<uint32_t> &ptj, std::vector<uint32_t> &etj)
+// Lays out tiles for the given jobs (first tile and tile count per job) and sizes the scratch.
+int Engine::rle_layout(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net)
 {
     npt = net = 0;
+    uint32_t nlt = 0;
     uint64_t e0 = 0;
-    ptj.clear();
-    etj.clear();
     for (size_t j = 0; j < jobs.size(); j++) {
         RleJob &J = jobs[j];
         const uint64_t len = J.len;
         J.tile0 = npt;
         J.ntiles = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
         npt += J.ntiles;
+        J.ltile0 = nlt;
+        J.nltiles = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_L_H - 1) / KPW_TILE_L_H);
+        nlt += J.nltiles;
         const uint64_t cap = len / 8 + 2;
         J.etile0 = net;
         J.netiles = (uint32_t)((cap + 255) / 256);
@@ -240,24 +242,26 @@ int Engine::rle_layout(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, 
         e0 += (uint64_t)J.netiles * 256;
         J.n_long = J.n_rle = 0;
         J.total_bytes = J.total_groups = J.final_gap_off = J.final_gap_groups = J.final_gap_start = 0;
-        ptj.insert(ptj.end(), J.ntiles, (uint32_t)j);
-        etj.insert(etj.end(), J.netiles, (uint32_t)j);
     }
-    ENS(r_last, npt * 8); ENS(r_prev, npt * 8); ENS(r_lrcnt, npt * 4); ENS(r_lroff, npt * 4);
+    r_nlt_ = nlt;
+    ENS(r_last, nlt * 8); ENS(r_prev, nlt * 8); ENS(r_lrcnt, nlt * 4); ENS(r_lroff, nlt * 4);
     ENS(r_lra, e0 * 4); ENS(r_lrb, e0 * 4); ENS(r_lrf, e0); ENS(r_rg, e0 * 4);
     ENS(r_rb, e0 * 4); ENS(r_rboff, e0 * 8); ENS(r_rgoff, e0 * 8);
+    ENS(r_ptj, std::max<uint64_t>(1, npt) * 4); ENS(r_etj, std::max<uint64_t>(1, net) * 4); ENS(r_ltj, std::max<uint64_t>(1, nlt) * 4);
     return KPW_OK;
 }
 
-// The scratch of the jobs laid out last, with their uploaded tile maps.
-void Engine::rle_bind(RleScratch &sc, const uint8_t *ptj_d, const uint8_t *etj_d)
+// The scratch of the jobs laid out last.
+void Engine::rle_bind(RleScratch &sc)
 {
-    sc.ptile_job = (uint32_t *)ptj_d;
+    sc.ptile_job = r_ptj.as<uint32_t>();
+    sc.ltile_job = r_ltj.as<uint32_t>();
+    sc.n_ltiles = r_nlt_;
     sc.last_brk = r_last.as<int64_t>();
     sc.prev_brk = r_prev.as<int64_t>();
     sc.lr_cnt = r_lrcnt.as<uint32_t>();
     sc.lr_off = r_lroff.as<uint32_t>();
-    sc.etile_job = (uint32_t *)etj_d;
+    sc.etile_job = r_etj.as<uint32_t>();
     sc.lr_a = r_lra.as<uint32_t>();
     sc.lr_b = r_lrb.as<uint32_t>();
     sc.lr_rle = nullptr;   // kept by the planning jobs only (set by the caller)
@@ -268,15 +272,50 @@ void Engine::rle_bind(RleScratch &sc, const uint8_t *ptj_d, const uint8_t *etj_d
     sc.seg = &seg_;
 }
 
-// Lays out tiles for the given jobs, uploads them (d_jobs: the job table first) and binds the scratch.
+// The position / element / long-run tile -> job maps of the jobs laid out last, expanded on the device from
+// their uploaded table (k_maps.hip), and the scratch bound.
+int Engine::rle_maps(const RleJob *jobs_d, uint32_t njobs, RleScratch &sc)
+{
+    static_assert(sizeof(RleJob) % 4 == 0, "job words");
+    TileMapArgs ta{};
+    ta.nm = 3;
+    ta.m[0] = TileMapSpec{&jobs_d->tile0, &jobs_d->ntiles, (uint32_t)(sizeof(RleJob) / 4), njobs, r_ptj.as<uint32_t>()};
+    ta.m[1] = TileMapSpec{&jobs_d->etile0, &jobs_d->netiles, (uint32_t)(sizeof(RleJob) / 4), njobs, r_etj.as<uint32_t>()};
+    ta.m[2] = TileMapSpec{&jobs_d->ltile0, &jobs_d->nltiles, (uint32_t)(sizeof(RleJob) / 4), njobs, r_ltj.as<uint32_t>()};
+    launch_tile_maps(ta, stream);
+    CK(hipGetLastError());
+    rle_bind(sc);
+    return KPW_OK;
+}
+
+// Lays out tiles for the given jobs, uploads the job table (d_jobs), expands its maps and binds
+// the scratch.
 int Engine::run_rle(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, RleScratch &sc)
 {
-    static thread_local std::vector<uint32_t> ptj, etj;
-    if (int st = rle_layout(jobs, npt, net, ptj, etj)) return st;
+    if (int st = rle_layout(jobs, npt, net)) return st;
     std::vector<uint8_t *> dp;
-    if (int st = upload_parts(d_jobs, {{jobs.data(), jobs.size() * sizeof(RleJob)}, {ptj.data(), npt * 4}, {etj.data(), net * 4}}, dp))
-        return st;
-    rle_bind(sc, dp[1], dp[2]);
+    if (int st = upload_parts(d_jobs, {{jobs.data(), jobs.size() * sizeof(RleJob)}}, dp)) return st;
+    return rle_maps(d_jobs.as<RleJob>(), (uint32_t)jobs.size(), sc);
+}
+
+// Host side of the dictionary insertion order (k_dict_order): the dictionary chunks in chunk
+// order and, per round k, the tiles of rounds < k (chunks with more than k' tiles, k' < k).
+int Engine::dict_order(const std::vector<uint32_t> &count, const std::vector<uint8_t> &is_dict, uint32_t &ndict_tiles,
+                       std::vector<uint32_t> &list, std::vector<uint32_t> &roff)
+{
+    list.clear();
+    uint32_t maxnt = 0;
+    for (size_t ci = 0; ci < count.size(); ci++)
+        if (is_dict[ci]) { list.push_back((uint32_t)ci); maxnt = std::max(maxnt, count[ci]); }
+    std::vector<uint32_t> hist(maxnt + 1, 0);
+    for (uint32_t ci : list) hist[count[ci]]++;
+    roff.assign(maxnt + 1, 0);
+    uint32_t more = (uint32_t)list.size() - hist[0];   // chunks with more than k tiles, k = 0
+    for (uint32_t k = 0; k < maxnt; k++) {
+        roff[k + 1] = roff[k] + more;
+        more -= hist[k + 1];
+    }
+    ndict_tiles = roff[maxnt];
     return KPW_OK;
 }
 
@@ -402,19 +441,20 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     std::vector<PlanStream> hs;
     std::vector<RleJob> pj;
     uint32_t npt = 0, net = 0;
-    static thread_local std::vector<uint32_t> pptj, petj;
     static const uint64_t kNoErr = ~0ull;
     std::vector<HostPart> parts{{hc.data(), nc * sizeof(DevCol)}, {&kNoErr, 8}};
     if (pre) {
         if (int st = plan_inputs(hc, n, nwords, hs, pj)) return st;
-        if (int st = rle_layout(pj, npt, net, pptj, petj)) return st;
+        if (int st = rle_layout(pj, npt, net)) return st;
         parts.push_back({pj.data(), pj.size() * sizeof(RleJob)});
-        parts.push_back({pptj.data(), (size_t)npt * 4});
-        parts.push_back({petj.data(), (size_t)net * 4});
         parts.push_back({hs.data(), hs.size() * sizeof(PlanStream)});
     }
     std::vector<uint8_t *> cp;
     if (int st = upload_parts(d_cols, parts, cp)) return st;
+    RleScratch sc{};
+    if (pre) {
+        if (int st = rle_maps((const RleJob *)cp[2], nstreams, sc)) return st;
+    }
     unsigned long long *const d_err = (unsigned long long *)cp[1];
     ENS(d_raw, n * 4);
     DecodeArgs da;
@@ -449,14 +489,13 @@ replan:
         CK(xsync(s));
         return KPW_OK;
     }
-    RleScratch sc{};
     const uint64_t ev_stride = (ne + 1 + 7) & ~7ull;   // event bytes per stream (positions 0..ne, 8-aligned)
     const bool pre_ok = pre && ne == n;   // the uploaded inputs are this plan's
     RleJob *pjobs = pre_ok ? (RleJob *)cp[2] : nullptr;   // (d_jobs is set, and may move, in run_rle)
-    PlanStream *pstreams = pre_ok ? (PlanStream *)cp[5] : nullptr;
+    PlanStream *pstreams = pre_ok ? (PlanStream *)cp[3] : nullptr;
     if (plan) {
         if (pre_ok) {
-            rle_bind(sc, cp[3], cp[4]);
+            rle_bind(sc);   // (maps expanded after the upload)
         } else {
             if (int st = plan_inputs(hc, ne, nwords, hs, pj)) return st;
             ENS(d_streams, nstreams * sizeof(PlanStream));
@@ -564,7 +603,9 @@ replan:
     // ---------------------------------------------------------------- chunk descriptors
     const int nch = nrg * nc;
     std::vector<ChunkDesc> ch(nch);
-    std::vector<uint32_t> ctj, cfirst(nch), ccount(nch);
+    std::vector<uint32_t> cfirst(nch), ccount(nch);
+    std::vector<uint8_t> cdict(nch);
+    uint32_t nct = 0;
     std::vector<RleJob> ej;
     std::vector<DeltaJob> dj;          // v2 DELTA streams (INT32/INT64: 1, BYTE_ARRAY: prefix + suffix lengths)
     std::vector<uint32_t> dblk_job;    // job of each DELTA block tile
@@ -629,12 +670,12 @@ replan:
                 }
             }
             const uint32_t nt = (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
-            cfirst[ci] = (uint32_t)ctj.size();
+            cfirst[ci] = nct;
             ccount[ci] = nt;
-            ctj.insert(ctj.end(), nt, (uint32_t)ci);
+            cdict[ci] = C.is_dict;
+            nct += nt;
         }
     }
-    const uint32_t nct = (uint32_t)ctj.size();
     // Dictionary hash tables.  Full size: >= 2x the most entries the dictionary can hold before
     // its fallback (dictionaryByteSize > dictPageSize: entries of >= 4 / 8 bytes), so probe
     // chains stay short until the fallback; a table that fills anyway means more entries than
@@ -668,14 +709,10 @@ replan:
     // Dictionary insertion order: tile k of every dictionary chunk before tile k+1 of any, so
     // each chunk is scanned roughly in record order and a chunk that crosses the 1 MiB
     // fallback threshold stops after a few tiles instead of inserting all of its values.
-    std::vector<uint32_t> dorder;
-    {
-        uint32_t maxnt = 0;
-        for (int ci = 0; ci < nch; ci++) if (ch[ci].is_dict) maxnt = std::max(maxnt, ccount[ci]);
-        for (uint32_t k = 0; k < maxnt; k++)
-            for (int ci = 0; ci < nch; ci++)
-                if (ch[ci].is_dict && k < ccount[ci]) dorder.push_back(cfirst[ci] + k);
-    }
+    // (expanded on the device, k_dict_order, from the dictionary chunks and per-round offsets)
+    static thread_local std::vector<uint32_t> dlist, droff;
+    uint32_t ndict_tiles = 0;
+    dict_order(ccount, cdict, ndict_tiles, dlist, droff);
     // chunk descriptors, then 4 words of string-statistics metadata per chunk (one readback)
     static_assert(sizeof(ChunkDesc) % 8 == 0, "metadata words follow the descriptors");
     ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
@@ -693,20 +730,31 @@ replan:
     uint64_t *const d_pcoff = d_ppre + P2, *const d_pclen = d_pcoff + P2;
     uint32_t *const d_coll = (uint32_t *)(pt + 2);
     for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
-    // one upload: descriptors (+ room for their statistics metadata), then chunk tile -> chunk,
-    // first tile and tile count per chunk, dictionary insertion order
-    static thread_local std::vector<uint8_t> chbuf;
-    chbuf.assign((size_t)nch * (sizeof(ChunkDesc) + 32), 0);
-    memcpy(chbuf.data(), ch.data(), (size_t)nch * sizeof(ChunkDesc));
+    // one upload: descriptors, first tile and tile count per chunk, the dictionary chunks and
+    // their per-round tile offsets; the chunk tile -> chunk map and the dictionary insertion order
+    // are expanded from them on the device, the descriptors' statistics metadata zeroed there
+    const size_t desc_bytes = (size_t)nch * sizeof(ChunkDesc);
     std::vector<uint8_t *> ctp;
-    if (int st = upload_parts(d_chunks, {{chbuf.data(), chbuf.size()}, {ctj.data(), (size_t)nct * 4}, {cfirst.data(), (size_t)nch * 4},
-                                         {ccount.data(), (size_t)nch * 4}, {dorder.data(), dorder.size() * 4}}, ctp))
+    if (int st = upload_parts(d_chunks, {{cfirst.data(), (size_t)nch * 4}, {ccount.data(), (size_t)nch * 4},
+                                         {dlist.data(), dlist.size() * 4}, {droff.data(), droff.size() * 4},
+                                         {ch.data(), desc_bytes}}, ctp, (size_t)nch * 32))
         return st;
-    ctp.erase(ctp.begin());   // (the descriptors: d_chunks.p)
+    ChunkDesc *const d_ch = (ChunkDesc *)ctp[4];   // descriptors, then their metadata words
+    CK(hipMemsetAsync(ctp[4] + desc_bytes, 0, (size_t)nch * 32, s));
+    ENS(d_ctj, std::max<uint64_t>(1, nct) * 4); ENS(d_dorder, std::max<uint64_t>(1, ndict_tiles) * 4);
+    {
+        TileMapArgs ta{};
+        ta.nm = 1;
+        ta.m[0] = TileMapSpec{(const uint32_t *)ctp[0], (const uint32_t *)ctp[1], 1u, (uint32_t)nch, d_ctj.as<uint32_t>()};
+        launch_tile_maps(ta, s);
+        launch_dict_order((const uint32_t *)ctp[2], (uint32_t)dlist.size(), (const uint32_t *)ctp[0], (const uint32_t *)ctp[1],
+                          (const uint32_t *)ctp[3], (uint32_t)droff.size() - 1, d_dorder.as<uint32_t>(), s);
+        CK(hipGetLastError());
+    }
     ChunkArgs a{};
-    a.ch = d_chunks.as<ChunkDesc>(); a.nchunks = nch; a.nctiles = nct; a.cols = d_cols.as<DevCol>(); a.data = d_data;
-    a.ctile_chunk = (uint32_t *)ctp[0]; a.ctile_first = (uint32_t *)ctp[1];
-    a.ctile_count = (uint32_t *)ctp[2]; a.tile_raw = d_tile_raw.as<uint64_t>();
+    a.ch = d_ch; a.nchunks = nch; a.nctiles = nct; a.cols = d_cols.as<DevCol>(); a.data = d_data;
+    a.ctile_chunk = d_ctj.as<uint32_t>(); a.ctile_first = (uint32_t *)ctp[0];
+    a.ctile_count = (uint32_t *)ctp[1]; a.tile_raw = d_tile_raw.as<uint64_t>();
     a.tile_raw_off = d_tile_raw_off.as<uint64_t>(); a.tile_smin = d_tile_smin.as<uint64_t>();
     a.tile_smax = d_tile_smax.as<uint64_t>(); a.tile_cnt = d_tile_cnt.as<uint32_t>(); a.tile_sz = d_tile_sz.as<uint64_t>();
     a.ht = d_ht.as<HtSlot>();
@@ -714,7 +762,7 @@ replan:
     a.max_dict_bytes = (uint32_t)props.dictionary_page_size;
     a.data_end = d_off + n;
     a.collision = d_coll;
-    a.dict_order = (uint32_t *)ctp[3]; a.ndict_tiles = (uint32_t)dorder.size();
+    a.dict_order = d_dorder.as<uint32_t>(); a.ndict_tiles = ndict_tiles;
     a.v2 = v2_ ? 1 : 0;
     a.seg = &seg_;
     // v2 DELTA streams: dense inputs share the chunks' rank-indexed id space (ids_off)
@@ -750,7 +798,7 @@ replan:
     // A hint-sized table that overflowed (flag word 1) re-runs the phase at full size.
     for (bool exact = false, first = true;; first = false) {
         a.exact_strings = exact ? 1 : 0;
-        if (!first) CK(xh2d(d_chunks.p, ch.data(), nch * sizeof(ChunkDesc), s));   // a re-run starts from the host's
+        if (!first) CK(xh2d(d_ch, ch.data(), nch * sizeof(ChunkDesc), s));   // a re-run starts from the host's
         if (v2_ && !dj.empty()) CK(xh2d(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), s));
         // ------------------------------------------------------------ K6 + K2
         a.ht_clear = d_ht.as<HtSlot>(); a.ht_clear_n = ht_off;   // K6 empties the hash tables and the flags
@@ -947,12 +995,12 @@ replan:
     // ---------------------------------------------------------------- metadata
     // binary min/max bytes: gather (offset, len) pairs, then the bytes into one blob
     std::vector<uint64_t> smeta(4 * nch, 0);
-    uint64_t *const d_smeta = (uint64_t *)(d_chunks.as<ChunkDesc>() + nch);
-    launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta, nullptr, s);
+    uint64_t *const d_smeta = (uint64_t *)(d_ch + nch);
+    launch_stats_gather(d_ch, nch, d_cols.as<DevCol>(), d_data, d_smeta, nullptr, s);
     {   // descriptors + metadata in one copy
         static thread_local std::vector<uint8_t> md;
         md.resize(nch * (sizeof(ChunkDesc) + 32));
-        CK(xd2h(md.data(), d_chunks.p, md.size(), s));
+        CK(xd2h(md.data(), d_ch, md.size(), s));
         CK(xsync(s));
         memcpy(ch.data(), md.data(), nch * sizeof(ChunkDesc));
         for (auto &C : ch) chunk_stats_derive(C);
@@ -982,7 +1030,7 @@ replan:
         if (blob_len) {
             std::vector<uint8_t> blob(blob_len);
             ENS(d_sblob, blob_len);
-            launch_stats_gather(d_chunks.as<ChunkDesc>(), nch, d_cols.as<DevCol>(), d_data, d_smeta,
+            launch_stats_gather(d_ch, nch, d_cols.as<DevCol>(), d_data, d_smeta,
                                 d_sblob.as<uint8_t>(), s);
             CK(xd2h(blob.data(), d_sblob.p, blob_len, s));
             CK(xsync(s));

@@ -155,7 +155,9 @@ private:
     // planning
     DevBuf d_ev, d_E, d_gend, d_plan;
     // rle scratch (shared by planning and encoding)
-    DevBuf r_last, r_prev, r_lrcnt, r_lroff, r_lra, r_lrb, r_lrf, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;   // d_jobs: jobs + tile maps
+    DevBuf r_last, r_prev, r_lrcnt, r_lroff, r_lra, r_lrb, r_lrf, r_rg, r_rb, r_rboff, r_rgoff, d_jobs;   // d_jobs: the job table
+    DevBuf r_ptj, r_etj, r_ltj, d_ctj, mp_dtj, d_dorder;
+    uint32_t r_nlt_ = 0;                     // long-run tiles of the RLE jobs laid out last   // tile -> job maps and the dictionary order (built by k_maps)
     // chunks
     DevBuf d_chunks, d_ctile, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
         d_tile_cnt, d_tile_sz, d_ht, d_ids, d_ent_rec, d_ent_boff, d_ptab,   // d_ptab: page table (engine.cpp)
@@ -194,8 +196,11 @@ private:
     int up_k_ = 0;
     std::vector<uint32_t> opt_idx_, bool_idx_;
     int run_rle(std::vector<RleJob> &jobs, uint32_t &nptiles, uint32_t &netiles, RleScratch &sc);
-    int rle_layout(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net, std::vector<uint32_t> &ptj, std::vector<uint32_t> &etj);
-    void rle_bind(RleScratch &sc, const uint8_t *ptj_d, const uint8_t *etj_d);
+    int rle_layout(std::vector<RleJob> &jobs, uint32_t &npt, uint32_t &net);
+    void rle_bind(RleScratch &sc);
+    int rle_maps(const RleJob *jobs_d, uint32_t njobs, RleScratch &sc);
+    int dict_order(const std::vector<uint32_t> &count, const std::vector<uint8_t> &is_dict, uint32_t &ndict_tiles,
+                   std::vector<uint32_t> &list, std::vector<uint32_t> &roff);
     // the planner's streams and RLE jobs over the first ne records (v2: clears the optional
     // booleans' compacted bit arrays on the stream)
     int plan_inputs(const std::vector<DevCol> &hc, uint64_t ne, uint64_t nwords, std::vector<PlanStream> &hs,
@@ -227,7 +232,8 @@ private:
     // Several host tables in one H2D copy into `buf` (256-byte aligned parts): their device
     // addresses in `dev`.  One copy instead of one per table (each is a blit kernel).
     struct HostPart { const void *p; size_t bytes; };
-    int upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::vector<uint8_t *> &dev);
+    // tail_room: bytes reserved on the device after the last part (not copied)
+    int upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::vector<uint8_t *> &dev, size_t tail_room = 0);
     hipError_t xh2d(void *dst, const void *src, size_t bytes, hipStream_t s);
     hipError_t xd2h(void *dst, const void *src, size_t bytes, hipStream_t s);
     hipError_t xsync(hipStream_t s);

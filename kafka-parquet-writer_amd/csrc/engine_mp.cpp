@@ -113,7 +113,9 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     std::vector<int> bool_pos(nc, -1);
     for (size_t i = 0; i < bool_idx_.size(); i++) bool_pos[bool_idx_[i]] = (int)i;
     uint64_t ht_off = 0, ids_off = 0;
-    std::vector<uint32_t> dtj, dfirst(nc), dcount(nc), ptj, pfirst, pcount;
+    std::vector<uint32_t> dfirst(nc), dcount(nc), pfirst, pcount;
+    std::vector<uint8_t> ddict(nc);
+    uint32_t npt = 0, ndt = 0;
     std::vector<char> k7_on;           // per page: its data page is compressed (k7_from)
     // dictionary insertion rounds of at least ~1024 tiles over all dictionary chunks: a probe of
     // one column inserts its prefix in 4x fewer launches (each a latency-bound ~50 us), a bulk
@@ -146,9 +148,10 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         D.owner = -1;
         D.first_page = (int32_t)pg.size();
         const uint32_t nt = on ? (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H) : 0u;
-        dfirst[c] = (uint32_t)dtj.size();
+        dfirst[c] = ndt;
         dcount[c] = nt;
-        dtj.insert(dtj.end(), nt, (uint32_t)c);
+        ddict[c] = D.is_dict;
+        ndt += nt;
         if (!on) { D.npages = 0; continue; }
         int64_t q = s;
         for (size_t i = 0; i <= cuts[c].size(); i++) {
@@ -206,9 +209,9 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
                 }
             }
             const uint32_t pt = (uint32_t)std::max<uint64_t>(1, ((uint64_t)(pe - q) + KPW_TILE_P_H - 1) / KPW_TILE_P_H);
-            pfirst.push_back((uint32_t)ptj.size());
+            pfirst.push_back(npt);
             pcount.push_back(pt);
-            ptj.insert(ptj.end(), pt, (uint32_t)pg.size());
+            npt += pt;
             pg.push_back(P);
             k7_on.push_back(!k7_from || (i >= (*k7_from)[c] && i < cuts[c].size()));
             q = pe;
@@ -216,17 +219,13 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         D.npages = (int32_t)pg.size() - D.first_page;
     }
     const int npg = (int)pg.size();
-    const uint32_t npt = (uint32_t)ptj.size(), ndt = (uint32_t)dtj.size();
-    std::vector<uint32_t> dorder, rlen;   // tile k of every chunk before tile k + 1; per round its slice
-    {
-        uint32_t maxnt = 0;
-        for (int c = 0; c < nc; c++) if (dch[c].is_dict) maxnt = std::max(maxnt, dcount[c]);
-        for (uint32_t k = 0; k < maxnt; k++) {
-            if (k % round_tiles == 0) rlen.push_back(0);
-            for (int c = 0; c < nc; c++)
-                if (dch[c].is_dict && k < dcount[c]) { dorder.push_back(dfirst[c] + k); rlen.back()++; }
-        }
-    }
+    // dictionary insertion order (tile k of every chunk before tile k + 1, expanded on the device)
+    // and per round of round_tiles its slice
+    std::vector<uint32_t> dlist, droff, rlen;
+    uint32_t ndict_tiles = 0;
+    dict_order(dcount, ddict, ndict_tiles, dlist, droff);
+    const uint32_t maxnt = (uint32_t)droff.size() - 1;
+    for (uint32_t k = 0; k < maxnt; k += round_tiles) rlen.push_back(droff[std::min(maxnt, k + round_tiles)] - droff[k]);
     // page descriptors use the engine's chunk buffers; dictionary descriptors their own
     // chunk descriptors, then 4 words of string-statistics metadata per chunk (one readback)
     static_assert(sizeof(ChunkDesc) % 8 == 0, "metadata words follow the descriptors");
@@ -269,16 +268,30 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         dla.blk_sz = d_blk_sz.as<uint64_t>(); dla.blk_off = d_blk_off.as<uint64_t>(); dla.btot = d_btot.as<uint64_t>();
         dla.seg = &seg_;
     }
-    std::vector<uint8_t *> tp;   // page tiles, dictionary tiles and the insertion order in one copy
-    if (int rs = upload_parts(d_ctile, {{ptj.data(), (size_t)npt * 4}, {pfirst.data(), (size_t)npg * 4}, {pcount.data(), (size_t)npg * 4},
-                                        {dtj.data(), (size_t)ndt * 4}, {dfirst.data(), (size_t)nc * 4}, {dcount.data(), (size_t)nc * 4},
-                                        {dorder.data(), dorder.size() * 4}}, tp))
+    // first tile and tile count per page and per dictionary chunk, the dictionary chunks and their
+    // per-round offsets in one copy; the tile maps and the insertion order expanded from them
+    std::vector<uint8_t *> tp;
+    if (int rs = upload_parts(d_ctile, {{pfirst.data(), (size_t)npg * 4}, {pcount.data(), (size_t)npg * 4},
+                                        {dfirst.data(), (size_t)nc * 4}, {dcount.data(), (size_t)nc * 4},
+                                        {dlist.data(), dlist.size() * 4}, {droff.data(), droff.size() * 4}}, tp))
         return rs;
+    ENS(d_ctj, std::max<uint64_t>(1, npt) * 4); ENS(mp_dtj, std::max<uint64_t>(1, ndt) * 4);
+    ENS(d_dorder, std::max<uint64_t>(1, ndict_tiles) * 4);
+    {
+        TileMapArgs ta{};
+        ta.nm = 2;
+        ta.m[0] = TileMapSpec{(const uint32_t *)tp[0], (const uint32_t *)tp[1], 1u, (uint32_t)npg, d_ctj.as<uint32_t>()};
+        ta.m[1] = TileMapSpec{(const uint32_t *)tp[2], (const uint32_t *)tp[3], 1u, (uint32_t)nc, mp_dtj.as<uint32_t>()};
+        launch_tile_maps(ta, st);
+        launch_dict_order((const uint32_t *)tp[4], (uint32_t)dlist.size(), (const uint32_t *)tp[2], (const uint32_t *)tp[3],
+                          (const uint32_t *)tp[5], maxnt, d_dorder.as<uint32_t>(), st);
+        CK(hipGetLastError());
+    }
 
     ChunkArgs ap{};
     ap.ch = d_chunks.as<ChunkDesc>(); ap.nchunks = npg; ap.nctiles = npt; ap.cols = d_cols.as<DevCol>(); ap.data = d_data;
-    ap.ctile_chunk = (uint32_t *)tp[0]; ap.ctile_first = (uint32_t *)tp[1];
-    ap.ctile_count = (uint32_t *)tp[2]; ap.tile_raw = d_tile_raw.as<uint64_t>();
+    ap.ctile_chunk = d_ctj.as<uint32_t>(); ap.ctile_first = (uint32_t *)tp[0];
+    ap.ctile_count = (uint32_t *)tp[1]; ap.tile_raw = d_tile_raw.as<uint64_t>();
     ap.tile_raw_off = d_tile_raw_off.as<uint64_t>(); ap.tile_smin = d_tile_smin.as<uint64_t>();
     ap.tile_smax = d_tile_smax.as<uint64_t>(); ap.tile_cnt = d_tile_cnt.as<uint32_t>(); ap.tile_sz = d_tile_sz.as<uint64_t>();
     ap.ht = d_ht.as<HtSlot>();
@@ -292,12 +305,12 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     if (v2_) { ap.djobs = dla.jobs; ap.djobs_w = dla.jobs; ap.chunk_sfx = d_chunk_sfx.as<uint64_t>(); }
     ChunkArgs ad = ap;
     ad.ch = mp_dch.as<ChunkDesc>(); ad.nchunks = nc; ad.nctiles = ndt;
-    ad.ctile_chunk = (uint32_t *)tp[3]; ad.ctile_first = (uint32_t *)tp[4];
-    ad.ctile_count = (uint32_t *)tp[5]; ad.tile_raw = mp_dtile_raw.as<uint64_t>(); ad.tile_raw_off = nullptr;
+    ad.ctile_chunk = mp_dtj.as<uint32_t>(); ad.ctile_first = (uint32_t *)tp[2];
+    ad.ctile_count = (uint32_t *)tp[3]; ad.tile_raw = mp_dtile_raw.as<uint64_t>(); ad.tile_raw_off = nullptr;
     ad.tile_smin = mp_dtile_smin.as<uint64_t>(); ad.tile_smax = mp_dtile_smax.as<uint64_t>();
     ad.tile_cnt = mp_dtile_cnt.as<uint32_t>(); ad.tile_sz = mp_dtile_sz.as<uint64_t>();
     ad.max_dict_bytes = 0xFFFFFFFFu;   // the dictPageSize limit is applied per page (k_mp_dict_decide)
-    ad.dict_order = (uint32_t *)tp[6]; ad.ndict_tiles = (uint32_t)dorder.size();
+    ad.dict_order = d_dorder.as<uint32_t>(); ad.ndict_tiles = ndict_tiles;
     ad.mp_round_tiles = round_tiles; ad.mp_nrounds = (uint32_t)rlen.size(); ad.mp_round_len = rlen.data();
     ad.mp_dict_limit = (uint32_t)props.dictionary_page_size;
 

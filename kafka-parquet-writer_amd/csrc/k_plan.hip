@@ -200,7 +200,7 @@ struct PlanSt {
     const uint64_t *rpres;   // rank-indexed stream: the presence bits and counts of its column
     const uint32_t *rpcnt;
     const uint32_t *lra, *lrb;   // the stream's long runs (K3 structure of the planning jobs)
-    const uint32_t *lroff;       // per position tile of the stream: its first long run ending there
+    const uint32_t *lroff;       // per long-run tile of the stream: its first long run ending there
     const uint8_t *lrle;         // per long run: the global parse took it as an RLE run
     uint32_t nlong, ntiles;
     int64_t len;
@@ -228,7 +228,7 @@ __device__ __forceinline__ void lw_init(LWalker &w, const PlanSt &S, int64_t p)
 {
     w.gs = p; w.eacc = 0; w.conv_pos = -1; w.delta = 0; w.state = 0;
     // first long run ending after p: a binary search among the runs ending in p's tile
-    const uint32_t t = (uint32_t)((uint64_t)p / KPW_TILE_P);
+    const uint32_t t = (uint32_t)((uint64_t)p / KPW_TILE_L);
     uint32_t lo = t < S.ntiles ? S.lroff[t] : S.nlong;
     uint32_t hi = t + 1 < S.ntiles ? S.lroff[t + 1] : S.nlong;
     while (lo < hi) {
@@ -424,9 +424,9 @@ __global__ void __launch_bounds__(PLAN_T) k_plan(PlanArgs a)
         PlanSt t;
         t.rpres = nullptr; t.rpcnt = nullptr;
         if (S.rank_col >= 0) { t.rpres = a.cols[S.rank_col].pres; t.rpcnt = a.cols[S.rank_col].pcnt; }
-        t.lra = a.lr_a + J.e0; t.lrb = a.lr_b + J.e0; t.lroff = a.lr_off + J.tile0;
+        t.lra = a.lr_a + J.e0; t.lrb = a.lr_b + J.e0; t.lroff = a.lr_off + J.ltile0;
         t.lrle = a.lr_rle + J.e0;
-        t.nlong = J.n_long; t.ntiles = J.ntiles; t.len = J.len;
+        t.nlong = J.n_long; t.ntiles = J.nltiles; t.len = J.len;
         St[k] = t;
     }
     for (int k = tid; k < a.nbool; k += PLAN_T) {

@@ -50,128 +50,131 @@ __device__ __forceinline__ uint32_t run_map(uint32_t a, uint32_t b)
     return m;
 }
 
-// values p0 .. p0+7 of a stream (0 past len): one bitmask word pair or eight independent
-// loads, instead of a chain of guarded single loads
-__device__ __forceinline__ void src_get8(const ValSrc &s, int64_t p0, int64_t len, uint32_t v[8])
+// ------------------------------------------------------------------ long runs
+// Over the long-run tiles (KPW_TILE_L = 16384 positions: 64 per thread, so a bit stream's tile
+// is one 2 KiB slice of its bitmask): the last value break per tile, a segmented max-scan of
+// those (the break before each tile), the long runs ending in each tile counted, a sum-scan of
+// the counts, then the runs written as (a, b); the job's last tile stores n_long.  Each thread
+// works on the 64-bit break mask of its positions, so the long-run ends are bit operations
+// (a break whose previous break is >= 8 positions back) rather than a loop over positions.
+// (Round 5: 8 positions per thread and 2048 per tile before: C3's 199 planning streams were
+// ~75 k blocks per launch, each mostly block-scan overhead.  r04: one launch with both scans as
+// in-kernel look-backs measured 2x slower here: every tile has full work, and its look-back
+// round trips are exposed; the element-tile kernels below keep theirs, since most of their
+// tiles are past the job's runs and exit at once.)
+
+// The break mask of a thread's 64 positions [p0, p0 + 64), p0 = wb + 64 * lane (wb: the wave's
+// first position, uniform): bit k set iff p0 + k < len and the value there starts a new run
+// (position 0, or a value unlike the one before it).  Bits: the lane's own 64 bits (lanes read
+// consecutive words).  u32 values: the wave loads its 4096 positions row by row (row k =
+// positions wb + 64k .. + 63, one coalesced load per lane), a row's breaks are one ballot, and
+// lane k keeps row k's.
+__device__ __forceinline__ uint64_t brk_mask64(const ValSrc &s, int64_t wb, int64_t len)
 {
-    if (p0 + 8 <= len) {
-        if (s.kind == 0) {
-            const uint64_t b = s.base + (uint64_t)p0;
-            const uint64_t *w = (const uint64_t *)s.ptr;
-            const uint32_t sh = (uint32_t)(b & 63);
-            uint64_t bits = w[b >> 6] >> sh;
-            if (sh > 56) bits |= w[(b >> 6) + 1] << (64 - sh);
-#pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = (uint32_t)((bits >> k) & 1ull);
-        } else {
-            const uint32_t *q = (const uint32_t *)s.ptr + s.base + (uint64_t)p0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = q[k];
-        }
-        return;
+    const uint32_t lane = threadIdx.x & 63;
+    if (wb >= len) return 0;   // (uniform per wave)
+    const int64_t p0 = wb + 64 * (int64_t)lane;
+    if (s.kind == 0) {
+        if (p0 >= len) return 0;
+        const uint64_t *w = (const uint64_t *)s.ptr;
+        const uint64_t b = s.base + (uint64_t)p0;
+        const uint32_t sh = (uint32_t)(b & 63);
+        uint64_t cur = w[b >> 6] >> sh;
+        if (sh) cur |= w[(b >> 6) + 1] << (64 - sh);
+        uint64_t before;   // the value before p0, in bit 0; at position 0 its complement (a break)
+        if (p0 == 0) before = ~cur & 1ull;
+        else before = (w[(b - 1) >> 6] >> ((b - 1) & 63)) & 1ull;
+        uint64_t m = cur ^ ((cur << 1) | before);
+        if (len - p0 < 64) m &= (1ull << (len - p0)) - 1;
+        return m;
     }
+    const uint32_t *q = (const uint32_t *)s.ptr + s.base;
+    uint32_t carry = wb > 0 ? q[wb - 1] : 0u;   // the value before the current row
+    uint64_t mine = 0;
+    for (uint32_t k0 = 0; k0 < 64; k0 += 8) {
+        uint32_t v[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = p0 + k < len ? src_get(s, (uint64_t)(p0 + k)) : 0u;
+        for (uint32_t j = 0; j < 8; j++) {
+            const int64_t pos = wb + 64 * (int64_t)(k0 + j) + lane;
+            v[j] = pos < len ? q[pos] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const int64_t pos = wb + 64 * (int64_t)(k0 + j) + lane;
+            uint32_t pv = (uint32_t)__shfl_up((int)v[j], 1);
+            if (lane == 0) pv = carry;
+            carry = (uint32_t)__shfl((int)v[j], 63);
+            const uint64_t row = __ballot(pos < len && (pos == 0 || v[j] != pv));
+            if (lane == k0 + j) mine = row;
+        }
+    }
+    return mine;
 }
 
-// ------------------------------------------------------------------ long runs
-// Over the position tiles: the last value break per tile, a segmented max-scan of those (the
-// break before each tile), the long runs ending in each tile counted, a sum-scan of the counts,
-// then the runs written as (a, b); the job's last tile stores n_long.  (r04: one launch with
-// both scans as in-kernel look-backs measured 2x slower here: every tile has full work, and
-// its look-back round trips are exposed; the element-tile kernels below keep theirs, since
-// most of their tiles are past the job's runs and exit at once.)
+__device__ __forceinline__ int64_t hi_bit_pos(uint64_t m, int64_t p0) { return p0 + 63 - (int64_t)__clzll((long long)m); }
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_bounds(const RleJob *jobs, const uint32_t *ptile_job, int64_t *last_brk)
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_bounds(const RleJob *jobs, const uint32_t *ltile_job, int64_t *last_brk)
 {
     __shared__ int64_t lds[KPW_BLOCK];
     const uint32_t t = blockIdx.x;
-    const RleJob &J = jobs[ptile_job[t]];
+    const RleJob &J = jobs[ltile_job[t]];
     const ValSrc src = job_src(J);
     const int64_t len = J.len;
-    const int64_t p0 = (int64_t)(t - J.tile0) * KPW_TILE_P + threadIdx.x * 8;
-    int64_t last = -1;
-    if (p0 < len) {
-        uint32_t prev = p0 > 0 ? src_get(src, p0 - 1) : 0;
-        uint32_t vv[8];
-        src_get8(src, p0, len, vv);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int64_t i = p0 + k;
-            if (i >= len) break;
-            const uint32_t v = vv[k];
-            if (i == 0 || v != prev) last = i;
-            prev = v;
-        }
-    }
+    const int64_t wb = (int64_t)(t - J.ltile0) * KPW_TILE_L + (int64_t)(threadIdx.x >> 6) * 4096;
+    const uint64_t m = brk_mask64(src, wb, len);
+    int64_t last = m ? hi_bit_pos(m, wb + 64 * (int64_t)(threadIdx.x & 63)) : -1;
     last = block_reduce<int64_t, OpMaxI64>(last, lds);
     if (threadIdx.x == 0) last_brk[t] = last;
 }
 
 // write = 0: long runs per tile into cnt[t]; write = 1: the runs at their offsets off[t]
-__global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const uint32_t *ptile_job, const int64_t *prev_brk,
+__global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const uint32_t *ltile_job, const int64_t *prev_brk,
                                                             uint32_t *cnt, const uint32_t *off, uint32_t *lr_a, uint32_t *lr_b,
                                                             int write)
 {
     __shared__ int64_t ldsi[KPW_BLOCK];
     __shared__ uint32_t ldsu[KPW_BLOCK];
     const uint32_t t = blockIdx.x;
-    RleJob &J = jobs[ptile_job[t]];
+    RleJob &J = jobs[ltile_job[t]];
     const ValSrc src = job_src(J);
     const int64_t len = J.len;
-    const int64_t p0 = (int64_t)(t - J.tile0) * KPW_TILE_P + threadIdx.x * 8;
-    uint32_t brk = 0;
-    int64_t local_last = -1;
-    if (p0 < len) {
-        uint32_t prev = p0 > 0 ? src_get(src, p0 - 1) : 0;
-        uint32_t vv[8];
-        src_get8(src, p0, len, vv);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int64_t i = p0 + k;
-            if (i >= len) break;
-            const uint32_t v = vv[k];
-            if (i == 0 || v != prev) { brk |= 1u << k; local_last = i; }
-            prev = v;
-        }
-    }
+    const int64_t wb = (int64_t)(t - J.ltile0) * KPW_TILE_L + (int64_t)(threadIdx.x >> 6) * 4096;
+    const int64_t p0 = wb + 64 * (int64_t)(threadIdx.x & 63);
+    const uint64_t m = brk_mask64(src, wb, len);
     int64_t tot_i;
-    int64_t incoming = block_scan_excl<int64_t, OpMaxI64>(local_last, ldsi, &tot_i);
-    const int64_t pb = (t == J.tile0) ? -1 : prev_brk[t];
+    int64_t incoming = block_scan_excl<int64_t, OpMaxI64>(m ? hi_bit_pos(m, p0) : -1, ldsi, &tot_i);
+    const int64_t pb = (t == J.ltile0) ? -1 : prev_brk[t];
     if (pb > incoming) incoming = pb;
 
-    // pass: count (and optionally write) long runs ending in this thread's positions
-    uint32_t c = 0;
-    for (int pass = 0; pass < (write ? 2 : 1); pass++) {
-        uint64_t base = 0;
-        if (pass == 1) {
-            uint32_t tot;
-            const uint32_t ex = block_scan_excl<uint32_t, OpSum32>(c, ldsu, &tot);
-            if (t == J.tile0 + J.ntiles - 1 && threadIdx.x == 0) J.n_long = off[t] + tot;
-            base = J.e0 + off[t] + ex;
-        }
-        int64_t prev = incoming;
-        uint32_t k2 = 0;
-        for (int k = 0; k < 8; k++) {
-            const int64_t i = p0 + k;
-            if (i >= len) break;
-            if ((brk >> k) & 1) {
-                if (i > 0 && i - prev >= 8) {
-                    if (pass == 1) { lr_a[base + k2] = (uint32_t)prev; lr_b[base + k2] = (uint32_t)i; }
-                    k2++;
-                }
-                prev = i;
-            }
-            if (i == len - 1 && len - prev >= 8) {  // final run of the stream
-                if (pass == 1) { lr_a[base + k2] = (uint32_t)prev; lr_b[base + k2] = (uint32_t)len; }
-                k2++;
-            }
-        }
-        c = k2;
+    // long-run ends: breaks whose previous break is >= 8 positions back (inside the mask for all
+    // but the lowest break; the lowest one's previous break is `incoming`; position 0 never ends
+    // one: 0 - (-1) < 8)
+    uint64_t le = m & ~((m << 1) | (m << 2) | (m << 3) | (m << 4) | (m << 5) | (m << 6) | (m << 7));
+    if (m) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        if (p0 + (int64_t)l - incoming < 8) le &= ~(1ull << l);
     }
-    if (!write) {
-        const uint32_t s = block_reduce<uint32_t, OpSum32>(c, ldsu);
-        if (threadIdx.x == 0) cnt[t] = s;
+    // the final run of the stream ends at len, in the thread holding position len - 1
+    const bool has_last = p0 < len && len - 1 < p0 + 64;
+    const int64_t lastb = m ? hi_bit_pos(m, p0) : incoming;
+    const bool fin = has_last && len - lastb >= 8;
+    const uint32_t c = (uint32_t)__popcll(le) + (fin ? 1u : 0u);
+    if (write) {
+        uint32_t tot;
+        const uint32_t ex = block_scan_excl<uint32_t, OpSum32>(c, ldsu, &tot);
+        if (t == J.ltile0 + J.nltiles - 1 && threadIdx.x == 0) J.n_long = off[t] + tot;
+        uint64_t o = J.e0 + off[t] + ex;
+        for (uint64_t r = le; r; r &= r - 1) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(r);
+            const uint64_t lower = m & ((1ull << i) - 1);
+            lr_a[o] = (uint32_t)(lower ? hi_bit_pos(lower, p0) : incoming);
+            lr_b[o] = (uint32_t)(p0 + i);
+            o++;
+        }
+        if (fin) { lr_a[o] = (uint32_t)lastb; lr_b[o] = (uint32_t)len; }
+    } else {
+        const uint32_t sum = block_reduce<uint32_t, OpSum32>(c, ldsu);
+        if (threadIdx.x == 0) cnt[t] = sum;
     }
 }
 
@@ -398,12 +401,13 @@ void launch_rle_structure(RleJob *jobs_d, int njobs, uint32_t n_ptiles, uint32_t
                           hipStream_t s)
 {
     if (!njobs || !n_ptiles) return;
-    hipLaunchKernelGGL(k_rle_bounds, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, sc.last_brk);
-    seg_tile_scan<int64_t, OpMaxI64>(sc.last_brk, sc.prev_brk, sc.ptile_job, n_ptiles, nullptr, sc.seg, s);
-    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, (const int64_t *)sc.prev_brk,
+    const uint32_t nlt = sc.n_ltiles;
+    hipLaunchKernelGGL(k_rle_bounds, dim3(nlt), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ltile_job, sc.last_brk);
+    seg_tile_scan<int64_t, OpMaxI64>(sc.last_brk, sc.prev_brk, sc.ltile_job, nlt, nullptr, sc.seg, s);
+    hipLaunchKernelGGL(k_rle_longruns, dim3(nlt), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ltile_job, (const int64_t *)sc.prev_brk,
                        sc.lr_cnt, (const uint32_t *)sc.lr_off, sc.lr_a, sc.lr_b, 0);
-    seg_tile_scan<uint32_t, OpSum32>(sc.lr_cnt, sc.lr_off, sc.ptile_job, n_ptiles, nullptr, sc.seg, s);
-    hipLaunchKernelGGL(k_rle_longruns, dim3(n_ptiles), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ptile_job, (const int64_t *)sc.prev_brk,
+    seg_tile_scan<uint32_t, OpSum32>(sc.lr_cnt, sc.lr_off, sc.ltile_job, nlt, nullptr, sc.seg, s);
+    hipLaunchKernelGGL(k_rle_longruns, dim3(nlt), dim3(KPW_BLOCK), 0, s, jobs_d, sc.ltile_job, (const int64_t *)sc.prev_brk,
                        sc.lr_cnt, (const uint32_t *)sc.lr_off, sc.lr_a, sc.lr_b, 1);
     LbView L = lb_prepare(sc.seg, 2ull * n_etiles, s);
     if (!L.w) return;

@@ -6,6 +6,7 @@
 #define KPW_BLOCK 256           // threads per block for the streaming kernels (4 waves)
 #define KPW_TILE_P 2048         // positions per position-tile (256 threads x 8)
 #define KPW_TILE_E 256          // elements per element-tile (1 per thread)
+#define KPW_TILE_L 16384        // positions per long-run tile (256 threads x 64: one break mask each)
 
 namespace kpw {
 

@@ -9,6 +9,7 @@ namespace kpw {
 constexpr int MAX_COLS = 256;
 constexpr int FMAP_SIZE = 1024;
 constexpr uint64_t KPW_TILE_P_H = 2048;   // host copy of KPW_TILE_P
+constexpr uint64_t KPW_TILE_L_H = 16384;  // host copy of KPW_TILE_L
 
 // One schema column as the device sees it (decode outputs live in these buffers).
 struct DevCol {
@@ -69,6 +70,7 @@ struct RleJob {
     uint32_t bw;           // bit width (device may set it)
     uint32_t tile0, ntiles;        // position tiles [tile0, tile0+ntiles)
     uint32_t etile0, netiles;      // element tiles (long runs / RLE runs)
+    uint32_t ltile0, nltiles;      // long-run tiles [ltile0, ltile0+nltiles) (KPW_TILE_L positions each)
     uint64_t e0;                   // base index into element arrays (capacity netiles*KPW_TILE_E)
     uint64_t out_off;              // encode: output byte offset; plan: event array base (positions)
     // results (device written)
@@ -82,8 +84,10 @@ struct RleJob {
 
 struct RleScratch {
     uint32_t *ptile_job;           // position tile -> job
-    int64_t *last_brk, *prev_brk;  // per position tile: its last value break / the one before it
-    uint32_t *lr_cnt, *lr_off;     // per position tile: long runs ending in it / their offset
+    uint32_t *ltile_job;           // long-run tile -> job
+    uint32_t n_ltiles;
+    int64_t *last_brk, *prev_brk;  // per long-run tile: its last value break / the one before it
+    uint32_t *lr_cnt, *lr_off;     // per long-run tile: long runs ending in it / their offset
     uint32_t *etile_job;           // element tile -> job
     uint32_t *lr_a, *lr_b;         // long runs (a, b)
     uint8_t *lr_rle;               // per long run: the parse took it as an RLE run (planning; null: not kept)
@@ -248,6 +252,23 @@ void launch_rle_write(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, cons
                       uint8_t *out, hipStream_t s);
 void launch_rle_events(RleJob *jobs_d, uint32_t n_ptiles, uint32_t n_etiles, const RleScratch &sc,
                        uint8_t *ev, uint64_t *gend, uint64_t gend_stride, hipStream_t s);
+
+// k_maps.hip: tile -> job maps expanded from the job tables' (first tile, tile count) words
+// (job j's words at first[j * stride], count[j * stride]); up to 4 maps per launch
+struct TileMapSpec {
+    const uint32_t *first, *count;
+    uint32_t stride, n;            // words between jobs; jobs
+    uint32_t *map;
+};
+struct TileMapArgs {
+    TileMapSpec m[4];
+    uint32_t nm;
+};
+void launch_tile_maps(const TileMapArgs &a, hipStream_t s);
+// dictionary insertion order: tile k of every listed chunk (list order) before tile k + 1 of
+// any; round_off[k] = tiles of rounds < k
+void launch_dict_order(const uint32_t *list, uint32_t nl, const uint32_t *first, const uint32_t *count,
+                       const uint32_t *round_off, uint32_t nrounds, uint32_t *out, hipStream_t s);
 
 void launch_plan(const PlanArgs &a, hipStream_t s);
 void launch_plan_fold(const uint8_t *ev, uint64_t ev_stride, const PlanStream *streams, uint32_t nstreams, const uint32_t *raw,
