@@ -167,11 +167,20 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
 
 #define ENS(buf, bytes) do { if ((buf).ensure(bytes)) return fail(KPW_ERR_NOMEM, "device allocation failed: " #buf); } while (0)
 
+// KPW_COPY_TRACE=1: every small host <-> device copy of the engine (size) on stderr
+static bool copy_trace()
+{
+    static const bool v = [] { const char *e = getenv("KPW_COPY_TRACE"); return e && e[0] == '1'; }();
+    return v;
+}
+
 // The engine's small host tables and readbacks.  Measured (r04, C2 writer A/B on one box):
 // staging them through a pinned arena so they run on SDMA instead of one blit kernel each cost
 // 7-10 % (every SDMA copy between two kernels of the stream is a cross-engine wait), so they
 // stay plain pageable copies; the readbacks are synchronous, xsync keeps the call sites'
-// ordering explicit.
+// ordering explicit.  Re-measured in r05 (profiles/r05h_small_copies.md) with every upload and
+// readback as a hipMemcpyDeviceToDeviceNoCU copy through pinned staging: C2 140 -> 152-154 ms
+// per step, C3 284-297 -> 296-303.
 int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::vector<uint8_t *> &dev, size_t tail_room)
 {
     const int k = up_k_;
@@ -196,13 +205,6 @@ int Engine::upload_parts(DevBuf &buf, const std::vector<HostPart> &parts, std::v
     CK(hipEventRecord(up_ev_[k], stream));
     up_used_[k] = true;
     return KPW_OK;
-}
-
-// KPW_COPY_TRACE=1: every small host <-> device copy of the engine (size) on stderr
-static bool copy_trace()
-{
-    static const bool v = [] { const char *e = getenv("KPW_COPY_TRACE"); return e && e[0] == '1'; }();
-    return v;
 }
 
 hipError_t Engine::xh2d(void *dst, const void *src, size_t bytes, hipStream_t s)
@@ -716,7 +718,7 @@ replan:
     // chunk descriptors, then 4 words of string-statistics metadata per chunk (one readback)
     static_assert(sizeof(ChunkDesc) % 8 == 0, "metadata words follow the descriptors");
     ENS(d_tile_raw, nct * 8); ENS(d_tile_raw_off, nct * 8); ENS(d_tile_smin, nct * 8); ENS(d_tile_smax, nct * 8);
-    ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8);
+    ENS(d_tile_cnt, nct * 4); ENS(d_tile_sz, nct * 8); ENS(d_fmask, (uint64_t)nct * KPW_BLOCK_H);
     ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
     ENS(d_ids, std::max<uint64_t>(1, ids_off) * 4); ENS(d_ent_rec, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
@@ -759,6 +761,7 @@ replan:
     a.tile_smax = d_tile_smax.as<uint64_t>(); a.tile_cnt = d_tile_cnt.as<uint32_t>(); a.tile_sz = d_tile_sz.as<uint64_t>();
     a.ht = d_ht.as<HtSlot>();
     a.ids = d_ids.as<uint32_t>(); a.ent_rec = d_ent_rec.as<uint64_t>(); a.ent_boff = d_ent_boff.as<uint64_t>();
+    a.fmask = d_fmask.as<uint8_t>();
     a.max_dict_bytes = (uint32_t)props.dictionary_page_size;
     a.data_end = d_off + n;
     a.collision = d_coll;

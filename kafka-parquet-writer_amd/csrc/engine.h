@@ -159,6 +159,7 @@ private:
     DevBuf r_ptj, r_etj, r_ltj, d_ctj, mp_dtj, d_dorder;
     uint32_t r_nlt_ = 0;                     // long-run tiles of the RLE jobs laid out last   // tile -> job maps and the dictionary order (built by k_maps)
     // chunks
+    DevBuf d_fmask;   // k_dict_firsts: first occurrences per chunk tile and thread (u8)
     DevBuf d_chunks, d_ctile, d_tile_raw, d_tile_raw_off, d_tile_smin, d_tile_smax,
         d_tile_cnt, d_tile_sz, d_ht, d_ids, d_ent_rec, d_ent_boff, d_ptab,   // d_ptab: page table (engine.cpp)
         d_body;

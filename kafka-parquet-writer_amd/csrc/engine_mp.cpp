@@ -234,7 +234,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ENS(d_tile_cnt, npt * 4); ENS(d_tile_sz, npt * 8);
     ENS(mp_dch, nc * sizeof(ChunkDesc));
     ENS(mp_dtile_raw, ndt * 8); ENS(mp_dtile_smin, ndt * 8); ENS(mp_dtile_smax, ndt * 8); ENS(mp_dtile_cnt, ndt * 4);
-    ENS(mp_dtile_sz, ndt * 8);
+    ENS(mp_dtile_sz, ndt * 8); ENS(d_fmask, (uint64_t)std::max(npt, ndt) * KPW_BLOCK_H);
     ENS(d_ht, std::max<uint64_t>(1, ht_off) * sizeof(HtSlot));
     ENS(d_ids, std::max<uint64_t>(1, ids_off) * 4); ENS(d_ent_rec, std::max<uint64_t>(1, ids_off) * 8);
     ENS(d_ent_boff, std::max<uint64_t>(1, ids_off) * 8);
@@ -296,6 +296,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ap.tile_smax = d_tile_smax.as<uint64_t>(); ap.tile_cnt = d_tile_cnt.as<uint32_t>(); ap.tile_sz = d_tile_sz.as<uint64_t>();
     ap.ht = d_ht.as<HtSlot>();
     ap.ids = d_ids.as<uint32_t>(); ap.ent_rec = d_ent_rec.as<uint64_t>(); ap.ent_boff = d_ent_boff.as<uint64_t>();
+    ap.fmask = d_fmask.as<uint8_t>();
     ap.max_dict_bytes = (uint32_t)props.dictionary_page_size;
     ap.data_end = d_off + n; ap.collision = d_coll;
     ap.page_pre = d_ppre;

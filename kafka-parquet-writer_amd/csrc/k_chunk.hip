@@ -453,7 +453,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
                                                            const uint32_t *slotof, uint32_t *tile_cnt, uint64_t *tile_sz,
                                                            const uint32_t *tile_cnt_off, const uint64_t *tile_sz_off,
                                                            uint64_t *ent_rec, uint64_t *ent_boff, int write, RleJob *jobs,
-                                                           uint32_t max_dict_bytes, uint32_t *retry)
+                                                           uint32_t max_dict_bytes, uint32_t *retry, uint8_t *fmask)
 {
     __shared__ uint64_t lds[KPW_BLOCK];
     __shared__ uint32_t ldu[KPW_BLOCK];
@@ -473,29 +473,36 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
     uint64_t sz = 0;
     uint32_t firsts = 0;  // bitmask over the 8 records
     uint32_t esz[8];
-    if (active) {
-        for (int k = 0; k < 8; k++) {
-            esz[k] = 0;
-            const uint64_t r = T.rec(k);
-            if (r >= T.e) break;
-            if (!present_at(col, r)) continue;
-            const uint64_t rank = T.rank(col, r);
-            const uint32_t slot = slotof[C.ids_off + rank];
-            if (ht[C.ht_off + slot].min == (uint32_t)rank) {
-                firsts |= 1u << k;
-                cnt++;
-                esz[k] = col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize;
-                sz += esz[k];
+    if (!write) {
+        // the count pass finds the first occurrences (a slot and a table load per value) and keeps
+        // them per thread in fmask, so the write pass loads nothing per value but that byte
+        if (active) {
+            for (int k = 0; k < 8; k++) {
+                const uint64_t r = T.rec(k);
+                if (r >= T.e) break;
+                if (!present_at(col, r)) continue;
+                const uint64_t rank = T.rank(col, r);
+                const uint32_t slot = slotof[C.ids_off + rank];
+                if (ht[C.ht_off + slot].min == (uint32_t)rank) {
+                    firsts |= 1u << k;
+                    cnt++;
+                    sz += col.phys == 6 ? 4 + col.slen[r] : (uint32_t)col.vsize;
+                }
             }
         }
-    }
-    if (!write) {
+        fmask[(uint64_t)t * KPW_BLOCK + threadIdx.x] = (uint8_t)firsts;
         const uint32_t sc = block_reduce<uint32_t, OpSum32>(cnt, ldu);
         const uint64_t ss = block_reduce<uint64_t, OpSum64>(sz, lds);
         if (threadIdx.x == 0) { tile_cnt[t] = sc; tile_sz[t] = ss; }
         return;
     }
     if (!active) return;   // block-uniform
+    firsts = fmask[(uint64_t)t * KPW_BLOCK + threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        esz[k] = 0;
+        if ((firsts >> k) & 1) esz[k] = col.phys == 6 ? 4 + col.slen[T.rec(k)] : (uint32_t)col.vsize;
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t lt = (1ull << lane) - 1;
     uint32_t lpre[8];
@@ -980,12 +987,12 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
     }
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
                        a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 0, jobs, a.max_dict_bytes,
-                       a.collision + 1);
+                       a.collision + 1, a.fmask);
     seg_tile_scan_u32(a.tile_cnt, a.tile_cnt, a.ctile_chunk, a.nctiles, a.seg, s);
     seg_tile_scan_u64(a.tile_sz, a.tile_sz, a.ctile_chunk, a.nctiles, a.seg, s);
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,
                        a.ht, a.ids, a.tile_cnt, a.tile_sz, a.tile_cnt, a.tile_sz, a.ent_rec, a.ent_boff, 1, jobs, a.max_dict_bytes,
-                       a.collision + 1);
+                       a.collision + 1, a.fmask);
     hipLaunchKernelGGL(k_dict_ids, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first, a.ht, a.ids,
                        a.data, a.ent_rec, a.data_end, a.collision);
     // BYTE_ARRAY statistics need the dictionary outcome (entries stand in for the values);

@@ -42,6 +42,7 @@ struct ChunkArgs {
     uint64_t body_tail;            // page writers: the body's end (k_chunk_prep clears 512 bytes from there)
     uint32_t *ids;
     uint64_t *ent_rec, *ent_boff;
+    uint8_t *fmask;                // per chunk tile and thread: its first occurrences (k_dict_firsts' count pass)
     uint32_t max_dict_bytes;
     int32_t exact_strings;         // 1: BYTE_ARRAY dictionary keys compared byte-for-byte (collision retry)
     const uint64_t *data_end;      // device pointer to offsets[n] (end of the record bytes)

@@ -10,6 +10,7 @@ constexpr int MAX_COLS = 256;
 constexpr int FMAP_SIZE = 1024;
 constexpr uint64_t KPW_TILE_P_H = 2048;   // host copy of KPW_TILE_P
 constexpr uint64_t KPW_TILE_L_H = 16384;  // host copy of KPW_TILE_L
+constexpr uint64_t KPW_BLOCK_H = 256;     // host copy of KPW_BLOCK
 
 // One schema column as the device sees it (decode outputs live in these buffers).
 struct DevCol {

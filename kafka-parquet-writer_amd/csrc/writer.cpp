@@ -670,13 +670,9 @@ static int append_job(kpw_writer *w, Worker &W, BatchOut &out, int set)
                 return KPW_ERR_DEVICE;
             ds = w->d2h_stream;
         }
-        // KPW_ASM_NOCU=1 (A/B): the file bytes as a copy without compute units (the pinned chunks
-        // are device-addressable), i.e. on SDMA instead of a blit kernel on every CU
-        static const bool nocu = [] { const char *e = getenv("KPW_ASM_NOCU"); return e && e[0] == '1'; }();
-        const hipMemcpyKind dk = nocu ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost;
         uint64_t at = 0;
         for (const auto &sp : spans) {
-            if (hipMemcpyAsync(sp.first, W.d_asm_out.as<uint8_t>() + at, sp.second, dk, ds) != hipSuccess)
+            if (hipMemcpyAsync(sp.first, W.d_asm_out.as<uint8_t>() + at, sp.second, hipMemcpyDeviceToHost, ds) != hipSuccess)
                 return KPW_ERR_DEVICE;
             at += sp.second;
         }
