@@ -680,6 +680,13 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         acc_len += pages_len_;
         return KPW_OK;
     };
+    // Non-final batches planned as a whole (no HDFS alignment): every row group's cut first (the
+    // speculative passes), then the cuts and the carry go to the caller (on_plan: the next job
+    // starts on the other worker), then each row group's exact pass.  Interleaved, the next job
+    // waited for every exact pass of this one.
+    const bool defer = !final_flush && max_cuts <= 0;
+    struct PlannedRg { int64_t s, e; std::vector<std::vector<int64_t>> cuts; };
+    std::vector<PlannedRg> planned;
     while (s0 < (int64_t)ne) {
         int64_t h = std::min<int64_t>((int64_t)ne, s0 + guess);
         int64_t po[2] = {-1, 0};
@@ -719,10 +726,14 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         if (po[0] >= 0) {
             const int64_t r = po[0];
             for (auto &v : cuts) v.erase(std::remove_if(v.begin(), v.end(), [r](int64_t x) { return x > r; }), v.end());
-            int rs = mp_pipeline(d_data, d_off, n, hc, s0, r, cuts, run);
-            if (rs) return rs;
-            rs = append(s0, r);
-            if (rs) return rs;
+            if (defer) {
+                planned.push_back(PlannedRg{s0, r, cuts});
+            } else {
+                int rs = mp_pipeline(d_data, d_off, n, hc, s0, r, cuts, run);
+                if (rs) return rs;
+                rs = append(s0, r);
+                if (rs) return rs;
+            }
             guess = std::max<int64_t>(1000, (r - s0) + (r - s0) / 4 + 200);
             mp_last_rg_ = r - s0;
             s0 = r;
@@ -743,6 +754,13 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     out.open_records = (int64_t)ne - s0;
     if (final_flush) out.open_buffered = 0;
     if (on_plan) on_plan(out);
+    for (const PlannedRg &g : planned) {   // (defer) the exact passes
+        int rs = mp_pipeline(d_data, d_off, n, hc, g.s, g.e, g.cuts, run);
+        if (rs) return rs;
+        rs = append(g.s, g.e);
+        if (rs) return rs;
+    }
+    CK(xsync(st));
     out.d_pages = mp_acc.as<uint8_t>();
     out.pages_len = acc_len;
     pages_dev_ = mp_acc.as<uint8_t>();
