@@ -18,6 +18,17 @@
  * on the data).
  *
  *   gcc -O2 -I../../include snappy_seg_proto.c ../../oracle/oracle_snappy.c -o /tmp/segp && /tmp/segp
+ *   /tmp/segp -f pages.bin   (pages from dump_any.py): per page rounds, and a rounds histogram
+ *
+ * Options (environment):
+ *   GPUF=1   every lookup reads the previous round's inserted set, as k_snappy_seg does (default:
+ *            a lane's lookups inside its own segment see its live insertions of this parse)
+ *   MODE=4   in-round forwarding, bounded: after the Jacobi parse, every lane whose entry differs
+ *            from the forwarded exit of its left neighbours re-parses once in the same round
+ *   MODE=1/2 in-round forwarding, unbounded (Gauss-Seidel: lanes re-parse left to right until
+ *            consistent; 2 also lets them see the left lanes' live insertions): one round, but
+ *            the re-parses form a chain ("maxchain" = its longest run per round)
+ *   TRACE=1  per round: lanes whose exit changed, entries changed, first inconsistent lane
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -29,6 +40,7 @@ int64_t kpwo_snappy_compress(const uint8_t *in, uint64_t n, uint8_t *out, uint64
 #define SEG 64
 #define MAXSEG 1024
 #define MAXIT 64
+static int GPUF = 0;
 static int HOPCAP = 1 << 30;
 
 enum { M_S = 0, M_P = 1, M_T = 2 };
@@ -81,7 +93,7 @@ static void lane_parse(const Frag *F, uint32_t k, St st, Lane *L)
     const uint32_t sk = k * SEG, sk1 = sk + SEG;
     L->own = 0; L->flag_left = 0; L->found = 0; L->aborted = 0; L->nm = 0; L->lookups = 0; L->hops = 0;
 #define INSERT(q) do { uint32_t q_ = (q); if (q_ >= sk) L->own |= 1ull << (q_ - sk); else L->flag_left = 1; } while (0)
-#define INS(q) ((q) >= sk ? (int)((L->own >> ((q) - sk)) & 1) : bit(F->iprev, (q)))
+#define INS(q) ((q) >= sk && !GPUF ? (int)((L->own >> ((q) - sk)) & 1) : bit(F->iprev, (q)))
     while (st.mode != M_T && st.ip < sk1) {
         uint32_t base, ne;
         uint32_t c;
@@ -150,7 +162,8 @@ static int st_eq(St a, St b)
 
 static Lane lanes[MAXSEG];
 static St entry[MAXSEG];
-static uint64_t stat_lookups, stat_hops, stat_cost;
+static uint64_t stat_lookups, stat_hops, stat_cost, stat_reparse, stat_chain;
+static int MODE = 0; static int TRACE = 0;
 
 /* returns output length, or -1 when the rounds do not converge; *rounds = rounds run */
 static long seg_fragment(const uint8_t *in, uint32_t n, uint8_t *out, int *rounds)
@@ -183,7 +196,49 @@ static long seg_fragment(const uint8_t *in, uint32_t n, uint8_t *out, int *round
             for (int i = 0; i < lanes[k].nm; i++) c += lanes[k].m[i].len / 16;
             if (c > mx) mx = c;
         }
-        stat_cost += mx;
+        if (MODE == 4) {   /* one extra Jacobi parse of the mismatched segments, same cand */
+            static St ent2[MAXSEG];
+            int32_t j = -1;
+            const St init0 = {M_S, 1, 32, 0};
+            for (uint32_t k = 1; k < nseg; k++) {
+                if (lanes[k - 1].found) j = (int32_t)k - 1;
+                ent2[k] = j >= 0 ? ff(lanes[j].exit, k * SEG, F.ip_limit) : ff(init0, k * SEG, F.ip_limit);
+            }
+            for (uint32_t k = 1; k < nseg; k++)
+                if (!st_eq(entry[k], ent2[k])) { entry[k] = ent2[k]; lane_parse(&F, k, entry[k], &lanes[k]); stat_reparse++; }
+        }
+        if (MODE >= 1 && MODE <= 2) {
+            int chain = 0, maxchain = 0;
+            for (uint32_t k = 1; k < nseg; k++) {
+                if (!st_eq(entry[k], lanes[k - 1].exit)) {
+                    entry[k] = lanes[k - 1].exit;
+                    if (MODE == 2) {   /* live I of the segments to the left */
+                        memset(bm2, 0, sizeof bm2);
+                        for (uint32_t q = 0; q < k; q++) { bm2[q] |= lanes[q].own; if (lanes[q].flag_left && q) bm2[q - 1] |= 1ull << 63; }
+                        for (uint32_t q = k; q < 1024; q++) bm2[q] = bm[q];
+                        F.iprev = bm2;
+                    }
+                    lane_parse(&F, k, entry[k], &lanes[k]);
+                    F.iprev = bm;
+                    chain++; stat_reparse++;
+                    if (chain > maxchain) maxchain = chain;
+                } else chain = 0;
+            }
+            stat_chain += maxchain;
+        }
+        if (TRACE) {
+            static St pex[MAXSEG]; static uint64_t pown[MAXSEG]; static St pent[MAXSEG];
+            int ch = 0, che = 0;
+            for (uint32_t k = 0; k < nseg; k++) {
+                if (it > 0 && (!st_eq(pex[k], lanes[k].exit) || pown[k] != lanes[k].own)) ch++;
+                if (it > 0 && !st_eq(pent[k], entry[k])) che++;
+                pex[k] = lanes[k].exit; pown[k] = lanes[k].own; pent[k] = entry[k];
+            }
+            int bad = 0; for (uint32_t k = 1; k < nseg; k++) if (!st_eq(entry[k], lanes[k-1].exit)) bad++;
+            /* first inconsistent segment */
+            int front = -1; for (uint32_t k = 1; k < nseg; k++) if (!st_eq(entry[k], lanes[k-1].exit)) { front = k; break; }
+            fprintf(stderr, "  it %d changed %d entry-changed %d entry-mismatch %d front %d\n", it, ch, che, bad, front);
+        }
         memset(bm2, 0, sizeof bm2);
         for (uint32_t k = 0; k < nseg; k++) {
             bm2[k] |= lanes[k].own;
@@ -276,13 +331,14 @@ static int file_mode(const char *path)
     }
     printf("frags %ld mismatches %d nonconverged %ld; rounds histogram:", frags, bad, fail);
     for (int i = 0; i <= MAXIT; i++) if (hist[i]) printf(" %d:%ld", i, hist[i]);
-    printf("\ncost/frag (max-lane decisions summed over rounds) %.1f\n", (double)stat_cost / frags);
+    printf("\ncost/frag %.1f reparses/frag %.1f maxchain-sum/frag %.1f\n", (double)stat_cost / frags, (double)stat_reparse/frags, (double)stat_chain/frags);
     return bad != 0;
 }
 
 int main(int argc, char **argv)
 {
     if (getenv("HOPCAP")) HOPCAP = atoi(getenv("HOPCAP"));
+    if (getenv("MODE")) MODE = atoi(getenv("MODE")); if (getenv("TRACE")) TRACE = atoi(getenv("TRACE")); if (getenv("GPUF")) GPUF = atoi(getenv("GPUF"));
     if (argc > 2 && !strcmp(argv[1], "-f")) return file_mode(argv[2]);
     const char *kinds[] = {"ts", "price", "user_id", "random", "zeros", "key16", "json", "defl", "mixed", "sparse"};
     static uint8_t page[65536 + 4096], o1[200000], o2[200000];
