@@ -23,9 +23,9 @@ between steps.
 Secondary keys: `resident_encode` (kpw_encoder_encode on a batch already in HBM, the r01
 headline), `c4` (the C4 writer line, 2 steps), `bulk_multipage` (C2 bulk writes with 1 MiB
 pages inside 128 MiB row groups, 2 steps), `c5` (BASELINE config 5 at its shape: 8 concurrent
-writers of 15.625 M Rec8 records each, 2 steps), `per_record` / `per_record_multipage` (the
-reference's write + getDataSize loop at 128 MiB / 1 MiB pages, the oracle's same loops in
-`cpu_baseline`), `roofline` (the dominant kernel, timed with HIP events on the encoder's stream inside
+writers of 15.625 M Rec8 records each, 2 steps), `per_record` / `per_record_multipage` /
+`per_record_64k` (the reference's write + getDataSize loop at 128 MiB / 1 MiB / 64 KiB pages, the
+oracle's same loops in `cpu_baseline`), `roofline` (the dominant kernel, timed with HIP events on the encoder's stream inside
 the timed writer steps; algorithmic bytes per launch), `roofline.pipeline_frac` (sum of
 algorithmic bytes over sum of device time of every encode stage, §8d), a measured device copy
 ceiling, and `cpu_baseline` (the CPU oracle — a C restatement of parquet-mr 1.10.1 — doing the
@@ -512,6 +512,9 @@ def main():
     ap.add_argument("--per-record-mp-page-kb", type=int, default=1024,
                     help="pageSize of a second per-record leg with page cuts inside row groups (pageSize(...), "
                          "KafkaProtoParquetWriter.java:656-659; 0 = skip)")
+    ap.add_argument("--per-record-64k-records", type=int, default=1_000_000,
+                    help="records of a third per-record leg with 64 KiB pages in 128 MiB row groups, GPU and oracle "
+                         "(VERDICT r4: per_record_64k; 0 = skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -630,6 +633,10 @@ def main():
         if args.per_record_mp_page_kb:   # pageSize < blockSize: page cuts inside row groups (size probes)
             per_record_mp = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_records, local_rank,
                                            args.per_record_max_file_mb * MiB, args.per_record_mp_page_kb * 1024)
+    per_record_64k = None
+    if args.per_record_64k_records and world == 1:   # 64 KiB pages: a size probe every ~2-3 k records
+        per_record_64k = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_64k_records, local_rank,
+                                        args.per_record_max_file_mb * MiB, 64 * 1024)
     c4_leg = bulk_mp = c5 = None
     if args.secondary_steps and world == 1 and args.workload == "c2":
         # the config where encode, not PCIe, sets the pace (C4), and bulk writes with 1 MiB pages
@@ -654,6 +661,10 @@ def main():
                                                                   args.per_record_max_file_mb * MiB,
                                                                   args.per_record_mp_page_kb * 1024)
             per_record_mp["oracle_records_per_s"] = cpu["per_record_multipage"]["records_per_s"]
+        if per_record_64k:
+            cpu["per_record_64k"] = cpu_baseline_per_record(sschema, kind, wseed, args.per_record_64k_records,
+                                                            args.per_record_max_file_mb * MiB, 64 * 1024)
+            per_record_64k["oracle_records_per_s"] = cpu["per_record_64k"]["records_per_s"]
     out = {
         "metric": "Parquet encode GB/s + records/sec (whole node) at 1/2/4/8 MI355X vs CPU writer",
         "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -676,6 +687,7 @@ def main():
         "stage_roofline": stage_roof,
         "per_record": per_record,
         "per_record_multipage": per_record_mp,
+        "per_record_64k": per_record_64k,
         "c4": c4_leg,
         "bulk_multipage": bulk_mp,
         "c5": c5,
