@@ -21,6 +21,8 @@
 // and plans every row group of a batch in one pass.
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "engine.h"
 #include "filewriter.h"
@@ -603,6 +605,24 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
     return KPW_OK;
 }
 
+// The speculative horizon's hint across engines: the records of the last row group any engine
+// cut for the same schema and properties.  A writer opens two fresh engines per file, and a first
+// horizon from the raw bytes alone (2 x blockSize) falls short where flushed pages count
+// compressed (C2 Rec8 1 MiB pages: 4.3 M against 6.5 M records per row group), costing each
+// engine's first job a second speculative pass.  Only the horizon depends on it, never a byte.
+static std::mutex g_horizon_mu;
+static std::unordered_map<uint64_t, int64_t> g_horizon;
+
+static uint64_t horizon_key(const std::vector<ColInfo> &cols, const kpw_props &p)
+{
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    for (const ColInfo &c : cols) { mix((uint64_t)c.field_number); mix((uint64_t)c.phys); mix((uint64_t)c.optional); mix((uint64_t)c.dict); }
+    mix((uint64_t)p.block_size); mix((uint64_t)p.page_size); mix((uint64_t)p.dictionary_page_size); mix((uint64_t)p.codec);
+    mix((uint64_t)p.writer_version);
+    return h;
+}
+
 int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                       const std::vector<DevCol> &hc, uint64_t gend_stride, uint64_t ev_stride, BatchOut &out)
 {
@@ -655,6 +675,12 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     // cut (flushed pages count compressed, so a row group holds more than T of raw bytes; a short
     // horizon costs a second speculative encode, C2 1 MiB pages: 4.3 M -> 8.5 M for a 6.7 M cut)
     int64_t guess = std::max<int64_t>(1000, (int64_t)(2 * (uint64_t)T / per_rec));
+    const uint64_t hkey = horizon_key(cols, props);
+    if (mp_last_rg_ <= 0) {
+        std::lock_guard<std::mutex> g(g_horizon_mu);
+        auto it = g_horizon.find(hkey);
+        if (it != g_horizon.end()) mp_last_rg_ = it->second;
+    }
     if (mp_last_rg_ > 0) guess = std::max<int64_t>(guess, mp_last_rg_ + mp_last_rg_ / 4 + 200);
     int64_t s0 = 0;
     std::vector<std::vector<int64_t>> cuts;
@@ -736,6 +762,10 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
             }
             guess = std::max<int64_t>(1000, (r - s0) + (r - s0) / 4 + 200);
             mp_last_rg_ = r - s0;
+            {
+                std::lock_guard<std::mutex> g(g_horizon_mu);
+                g_horizon[hkey] = mp_last_rg_;
+            }
             s0 = r;
             if (max_cuts > 0 && (int32_t)out.rgs.size() >= max_cuts) break;   // re-planned by the caller
             continue;
