@@ -1167,28 +1167,51 @@ int Engine::gzip_pages(const uint8_t *body, uint64_t body_len, const uint64_t *d
     const uint32_t nslots = (uint32_t)plen.size();
     std::vector<DflPage> pages;
     std::vector<DflTile> tiles;
+    std::vector<DflSeg> segs;
+    std::vector<DflBlk> blks;
+    std::vector<uint32_t> page_seg0, page_blk0, page_tile0;
     std::vector<int32_t> slot_page(nslots, -1);
     uint64_t gz = 0;
     for (uint32_t p = 0; p < nslots; p++) {
         // a dictionary page slot (even) with no bytes has no page; a data page always has one
         // (an empty v2 values section still gets its 20-byte member)
         if (!on[p] || (!(p & 1) && plen[p] == 0)) continue;
-        slot_page[p] = (int32_t)pages.size();
-        const uint64_t cap = (dfl_member_bound(plen[p]) + 255) & ~255ull;
+        const uint32_t pg = (uint32_t)pages.size();
+        slot_page[p] = (int32_t)pg;
+        const uint64_t cap = (dfl_member_bound(plen[p]) + 16 + 255) & ~255ull;   // (the stream starts at slot + 16)
         pages.push_back(DflPage{poff[p], plen[p], gz, cap});
-        for (uint64_t t = 0; t * 32768 < plen[p]; t++) tiles.push_back(DflTile{(uint32_t)(pages.size() - 1), (uint32_t)t});
+        page_tile0.push_back((uint32_t)tiles.size());
+        for (uint64_t t = 0; t * 32768 < plen[p]; t++) tiles.push_back(DflTile{pg, (uint32_t)t});
+        page_seg0.push_back((uint32_t)segs.size());
+        const uint64_t ns = std::max<uint64_t>(1, (plen[p] + DFL_SEG - 1) / DFL_SEG);
+        for (uint64_t k = 0; k < ns; k++) segs.push_back(DflSeg{pg, (uint32_t)k});
+        page_blk0.push_back((uint32_t)blks.size());
+        const uint64_t nb = (plen[p] + 1) / DFL_BLK + 2;   // blocks of 16383 symbols, at most one per byte (+ the final)
+        for (uint64_t j = 0; j < nb; j++) blks.push_back(DflBlk{pg, (uint32_t)j});
         gz += cap;
     }
+    page_tile0.push_back((uint32_t)tiles.size());
+    page_seg0.push_back((uint32_t)segs.size());
+    page_blk0.push_back((uint32_t)blks.size());
     const uint32_t np = (uint32_t)pages.size(), nt = (uint32_t)tiles.size();
+    const uint32_t nsegs = (uint32_t)segs.size(), nblks = (uint32_t)blks.size();
     ENS(d_dfl_pdist, std::max<uint64_t>(body_len, 1) * 2 + 64);
     ENS(d_dfl_m128, std::max<uint64_t>(body_len, 1) * 4 + 64);
     ENS(d_dfl_m32, std::max<uint64_t>(body_len, 1) * 4 + 64);
     ENS(d_dfl_sym, std::max<uint64_t>(body_len, 1) * 4 + 64);
+    ENS(d_dfl_dsym, (body_len + np + 64) * 4);
+    ENS(d_dfl_dpos, (body_len + np + 64) * 4);
     ENS(d_dfl_gz, std::max<uint64_t>(gz, 256));
     ENS(d_dfl_glen, std::max<uint32_t>(np, 1) * 8);
+    ENS(d_dfl_seg, std::max<uint64_t>(nsegs, 1) * (2 * sizeof(DflSt) + 12));
+    ENS(d_dfl_page, std::max<uint64_t>(np, 1) * 12 + std::max<uint64_t>(nt, 1) * 4 + 64);
+    ENS(d_dfl_blk, std::max<uint64_t>(nblks, 1) * 20);
     std::vector<uint8_t *> tp;
     if (int st = upload_parts(d_dfl_tab, {{pages.data(), pages.size() * sizeof(DflPage)}, {tiles.data(), tiles.size() * sizeof(DflTile)},
-                                          {slot_page.data(), slot_page.size() * 4}}, tp))
+                                          {slot_page.data(), slot_page.size() * 4}, {segs.data(), segs.size() * sizeof(DflSeg)},
+                                          {blks.data(), blks.size() * sizeof(DflBlk)}, {page_seg0.data(), page_seg0.size() * 4},
+                                          {page_blk0.data(), page_blk0.size() * 4}, {page_tile0.data(), page_tile0.size() * 4}},
+                              tp))
         return st;
     DflArgs a{};
     a.in = body; a.pages = (const DflPage *)tp[0]; a.tiles = (const DflTile *)tp[1];
@@ -1197,8 +1220,47 @@ int Engine::gzip_pages(const uint8_t *body, uint64_t body_len, const uint64_t *d
     a.nslots = nslots; a.slot_page = (const int32_t *)tp[2];
     a.page_off = d_poff; a.page_pre = d_ppre; a.page_coff = d_pcoff; a.page_clen = d_pclen;
     a.out = d_comp.as<uint8_t>(); a.tot = tot; a.overflow = overflow;
+    a.segs = (const DflSeg *)tp[3]; a.nsegs = nsegs; a.blks = (const DflBlk *)tp[4]; a.nblks = nblks;
+    a.page_seg0 = (const uint32_t *)tp[5]; a.page_blk0 = (const uint32_t *)tp[6]; a.page_tile0 = (const uint32_t *)tp[7];
+    {   // per segment: entry and exit states, dirty flag, symbol count and offset
+        uint8_t *q = d_dfl_seg.as<uint8_t>();
+        a.seg_entry = (DflSt *)q; q += (size_t)nsegs * sizeof(DflSt);
+        a.seg_exit = (DflSt *)q; q += (size_t)nsegs * sizeof(DflSt);
+        a.seg_dirty = (uint32_t *)q; q += (size_t)nsegs * 4;
+        a.seg_cnt = (uint32_t *)q; q += (size_t)nsegs * 4;
+        a.seg_sym0 = (uint32_t *)q;
+    }
+    {   // per page: symbols, blocks, CRC; per tile: CRC; the round flag
+        uint32_t *q = d_dfl_page.as<uint32_t>();
+        a.page_T = q; q += np; a.page_nblk = q; q += np; a.page_crc = q; q += np;
+        a.tile_crc = q; q += nt;
+        a.flag = q;
+    }
+    {   // per block: bits (or stored bytes), offset, kind
+        uint8_t *q = d_dfl_blk.as<uint8_t>();
+        a.blk_bits = (uint64_t *)q; q += (size_t)nblks * 8;
+        a.blk_off = (uint64_t *)q; q += (size_t)nblks * 8;
+        a.blk_kind = (uint32_t *)q;
+    }
+    a.dsym = d_dfl_dsym.as<uint32_t>(); a.dpos = d_dfl_dpos.as<uint32_t>();
     CK(hipMemsetAsync(overflow, 0, 8, s));
-    launch_deflate(a, np, nt, s);
+    launch_deflate_prep(a, nt, s);
+    CK(hipGetLastError());
+    // parse rounds until no segment's entry changes (the converged prefix grows by at least one
+    // segment per round, so this ends; every dumped page took 2)
+    for (uint32_t round = 0;; round++) {
+        CK(hipMemsetAsync(a.flag, 0, 4, s));
+        launch_deflate_round(a, s);
+        CK(hipGetLastError());
+        uint32_t changed = 0;
+        CK(xd2h(&changed, a.flag, 4, s));
+        CK(xsync(s));
+        if (!changed) break;
+        if (round > nsegs + 1) return fail(KPW_ERR_DEVICE, "gzip parse did not converge");
+    }
+    launch_deflate_finish(a, np, s);
+    CK(hipMemsetAsync(d_dfl_gz.p, 0, std::max<uint64_t>(gz, 256), s));   // the emit pass ors bits into zeroed words
+    launch_deflate_emit(a, np, s);
     CK(hipGetLastError());
     return KPW_OK;
 }

@@ -173,7 +173,8 @@ private:
     int gzip_pages(const uint8_t *body, uint64_t body_len, const uint64_t *d_poff, const uint64_t *d_ppre,
                    const std::vector<uint64_t> &poff, const std::vector<uint64_t> &plen, const std::vector<char> &on,
                    uint64_t *d_pcoff, uint64_t *d_pclen, uint64_t *tot, uint64_t *overflow, hipStream_t s);
-    DevBuf d_dfl_tab, d_dfl_pdist, d_dfl_m128, d_dfl_m32, d_dfl_sym, d_dfl_gz, d_dfl_glen;
+    DevBuf d_dfl_tab, d_dfl_pdist, d_dfl_m128, d_dfl_m32, d_dfl_sym, d_dfl_gz, d_dfl_glen, d_dfl_dsym, d_dfl_dpos,
+        d_dfl_seg, d_dfl_page, d_dfl_blk;
     DevBuf d_body_alt, d_comp_alt;
     std::vector<double> sn_cost_;       // K7 mean fragment duration per (column, page kind), previous batch
     std::unordered_map<uint64_t, double> sn_fcost_;   // per (kind, fragment index)

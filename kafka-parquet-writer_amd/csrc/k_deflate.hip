@@ -9,15 +9,26 @@
 // evaluation and the insert loop after a match both insert every position), so a position's
 // chain = the earlier positions with the same 3-byte hash, and longest_match(p) depends only on
 // p and on whether the previous match was >= good_length (chain 128 or 32 candidates); the
-// previous match length only filters the result (a candidate counts iff it beats it).  So:
+// previous match length only filters the result (a candidate counts iff it beats it).  What is
+// left of the loop is a small state machine over positions, parsed segment-parallel, and the
+// blocks of 16383 symbols are independent once their symbols and bit offsets are known:
 //   k_dfl_prev   per 32 KiB tile of a page, one wave: the previous position with the same hash
 //                (64 positions per step: hash peers by ballots, a 32 K-entry head table in LDS);
 //   k_dfl_match  per position, in parallel: the chain walk of longest_match for 128 and for 32
 //                candidates (first longest, nice_length 128 stops) -> (length, distance);
-//   k_dfl_page   per page, one wave: the lazy parse itself (window slides tracked for the
-//                stored-block rule), trees.c's block decisions and Huffman trees per 16383
-//                symbols, the bit stream, CRC-32 and the gzip framing;
-//   k_dfl_sizes / k_dfl_copy   compressed page sizes and offsets, pages packed in order.
+//   k_dfl_tcrc   per tile, one wave: its CRC-32 (pieces combined in GF(2));
+//   k_dfl_parse / k_dfl_fix   per 2048-position segment, one thread: the lazy parse from an
+//                entry state, rounds until every entry is its left neighbour's exit (the host
+//                reads a flag between rounds; 2 rounds on every dumped C2 / C3 / C4 page);
+//   k_dfl_pscan / k_dfl_gather   symbol offsets per segment, counts and blocks per page, the
+//                symbols dense;
+//   k_dfl_bsize / k_dfl_boff / k_dfl_bemit   per block, one workgroup: frequencies, trees.c's
+//                trees and stored / static / dynamic choice, its bit count; per page the blocks'
+//                bit offsets; then every block writes its bits at its offset;
+//   k_dfl_sizes / k_dfl_copy   members framed (java.util.zip.GZIPOutputStream header, CRC-32,
+//                ISIZE) and packed in page order.
+// (Round 5 before this: one lane per page ran the parse and the bit stream, ~minutes for a
+// 128 MiB page, the reference's default page size.)
 #include "kpw_chunk.h"
 #include "kpw_device.h"
 
@@ -161,13 +172,8 @@ struct DflTrees {
     uint8_t dist_code[512], length_code[256];
     int16_t base_length[LENGTH_CODES], base_dist[D_CODES];
     int heap_len, heap_max;
-    int l_max, d_max, bl_max;
+    int l_max, d_max, bl_max, max_bl;
     uint64_t opt_len, static_len;
-    // bit writer
-    uint64_t bi_buf;
-    int bi_valid;
-    uint64_t op;          // output bytes written (from the page's deflate start)
-    uint32_t last_lit;
 };
 
 __constant__ int8_t c_extra_lbits[LENGTH_CODES] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
@@ -231,16 +237,6 @@ __device__ void static_init(DflTrees &S)
 }
 
 __device__ __forceinline__ uint32_t d_code(const DflTrees &S, uint32_t dist) { return dist < 256 ? S.dist_code[dist] : S.dist_code[256 + (dist >> 7)]; }
-
-__device__ void init_block(DflTrees &S)
-{
-    for (int n = 0; n < L_CODES; n++) S.dyn_ltree[n].fc = 0;
-    for (int n = 0; n < D_CODES; n++) S.dyn_dtree[n].fc = 0;
-    for (int n = 0; n < BL_CODES; n++) S.bl_tree[n].fc = 0;
-    S.dyn_ltree[END_BLOCK].fc = 1;
-    S.opt_len = S.static_len = 0;
-    S.last_lit = 0;
-}
 
 __device__ __forceinline__ bool smaller(const CtData *tree, int n, int m, const uint8_t *depth)
 {
@@ -373,282 +369,554 @@ __device__ void scan_tree(DflTrees &S, CtData *tree, int max_code)
     }
 }
 
-__device__ __forceinline__ void put_byte(DflTrees &S, uint8_t *out, uint64_t cap, uint8_t b)
+// CRC-32 (IEEE reflected, java.util.zip.CRC32) of pieces combined in GF(2): the CRC of A || B is
+// crc(A) * x^(8 |B|) + crc(B) modulo the polynomial (reflected bit order: x^0 is bit 31)
+constexpr uint32_t CRC_POLY = 0xedb88320u;
+__device__ uint32_t gf2_mulmod(uint32_t a, uint32_t b)
 {
-    if (S.op < cap) out[S.op] = b;
-    S.op++;
-}
-__device__ __forceinline__ void send_bits(DflTrees &S, uint8_t *out, uint64_t cap, uint32_t value, int length)
-{
-    S.bi_buf |= (uint64_t)value << S.bi_valid;
-    S.bi_valid += length;
-    while (S.bi_valid >= 16) {
-        put_byte(S, out, cap, (uint8_t)S.bi_buf);
-        put_byte(S, out, cap, (uint8_t)(S.bi_buf >> 8));
-        S.bi_buf >>= 16;
-        S.bi_valid -= 16;
-    }
-}
-__device__ void bi_windup(DflTrees &S, uint8_t *out, uint64_t cap)
-{
-    if (S.bi_valid > 8) { put_byte(S, out, cap, (uint8_t)S.bi_buf); put_byte(S, out, cap, (uint8_t)(S.bi_buf >> 8)); }
-    else if (S.bi_valid > 0) put_byte(S, out, cap, (uint8_t)S.bi_buf);
-    S.bi_buf = 0;
-    S.bi_valid = 0;
-}
-
-__device__ void send_tree(DflTrees &S, uint8_t *out, uint64_t cap, const CtData *tree, int max_code)
-{
-    int n, prevlen = -1, curlen, nextlen = tree[0].dl, count = 0, max_count = 7, min_count = 4;
-    if (nextlen == 0) max_count = 138, min_count = 3;
-    for (n = 0; n <= max_code; n++) {
-        curlen = nextlen;
-        nextlen = tree[n + 1].dl;
-        if (++count < max_count && curlen == nextlen) continue;
-        else if (count < min_count) {
-            do { send_bits(S, out, cap, S.bl_tree[curlen].fc, S.bl_tree[curlen].dl); } while (--count != 0);
-        } else if (curlen != 0) {
-            if (curlen != prevlen) { send_bits(S, out, cap, S.bl_tree[curlen].fc, S.bl_tree[curlen].dl); count--; }
-            send_bits(S, out, cap, S.bl_tree[REP_3_6].fc, S.bl_tree[REP_3_6].dl);
-            send_bits(S, out, cap, (uint32_t)count - 3, 2);
-        } else if (count <= 10) {
-            send_bits(S, out, cap, S.bl_tree[REPZ_3_10].fc, S.bl_tree[REPZ_3_10].dl);
-            send_bits(S, out, cap, (uint32_t)count - 3, 3);
-        } else {
-            send_bits(S, out, cap, S.bl_tree[REPZ_11_138].fc, S.bl_tree[REPZ_11_138].dl);
-            send_bits(S, out, cap, (uint32_t)count - 11, 7);
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
         }
-        count = 0;
-        prevlen = curlen;
-        if (nextlen == 0) max_count = 138, min_count = 3;
-        else if (curlen == nextlen) max_count = 6, min_count = 3;
-        else max_count = 7, min_count = 4;
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ CRC_POLY : b >> 1;
     }
+    return p;
 }
-
-// symbols of the current block: lit (dist 0) or (length - 3, distance) packed lc | dist << 8
-__device__ void compress_block(DflTrees &S, uint8_t *out, uint64_t cap, const uint32_t *sym, const CtData *ltree,
-                               const CtData *dtree)
+// x^(8 n) modulo the polynomial: square-and-multiply over x^(2^k), k from 3
+__device__ uint32_t gf2_x8n(uint64_t n)
 {
-    for (uint32_t lx = 0; lx < S.last_lit; lx++) {
-        const uint32_t sv = sym[lx];
-        uint32_t dist = sv >> 8;
-        int lc = (int)(sv & 0xff);
-        if (dist == 0) {
-            send_bits(S, out, cap, ltree[lc].fc, ltree[lc].dl);
-        } else {
-            uint32_t code = S.length_code[lc];
-            send_bits(S, out, cap, ltree[code + LITERALS + 1].fc, ltree[code + LITERALS + 1].dl);
-            int extra = c_extra_lbits[code];
-            if (extra != 0) { lc -= S.base_length[code]; send_bits(S, out, cap, (uint32_t)lc, extra); }
-            dist--;
-            code = d_code(S, dist);
-            send_bits(S, out, cap, dtree[code].fc, dtree[code].dl);
-            extra = c_extra_dbits[code];
-            if (extra != 0) { dist -= (uint32_t)S.base_dist[code]; send_bits(S, out, cap, dist, extra); }
-        }
+    uint32_t p = 1u << 31;         // x^0
+    uint32_t sq = 1u << 30;        // x^1
+    for (int k = 0; k < 3; k++) sq = gf2_mulmod(sq, sq);   // x^8
+    while (n) {
+        if (n & 1) p = gf2_mulmod(sq, p);
+        n >>= 1;
+        if (n) sq = gf2_mulmod(sq, sq);
     }
-    send_bits(S, out, cap, ltree[END_BLOCK].fc, ltree[END_BLOCK].dl);
+    return p;
 }
-
-// _tr_flush_block (zlib 1.2.11, level > 0); buf: the block's bytes when they are still in
-// zlib's window (block_start >= 0), else nullptr
-__device__ void flush_block(DflTrees &S, uint8_t *out, uint64_t cap, const uint32_t *sym, const uint8_t *buf,
-                            uint64_t stored_len, int last)
-{
-    S.l_max = build_tree(S, S.dyn_ltree, 0);
-    S.d_max = build_tree(S, S.dyn_dtree, 1);
-    scan_tree(S, S.dyn_ltree, S.l_max);
-    scan_tree(S, S.dyn_dtree, S.d_max);
-    S.bl_max = build_tree(S, S.bl_tree, 2);
-    int max_blindex;
-    for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
-        if (S.bl_tree[c_bl_order[max_blindex]].dl != 0) break;
-    S.opt_len += 3 * ((uint64_t)max_blindex + 1) + 5 + 5 + 4;
-    uint64_t opt_lenb = (S.opt_len + 3 + 7) >> 3;
-    const uint64_t static_lenb = (S.static_len + 3 + 7) >> 3;
-    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
-    if (stored_len + 4 <= opt_lenb && buf) {
-        send_bits(S, out, cap, (0u << 1) + (uint32_t)last, 3);
-        bi_windup(S, out, cap);
-        put_byte(S, out, cap, (uint8_t)stored_len);
-        put_byte(S, out, cap, (uint8_t)(stored_len >> 8));
-        put_byte(S, out, cap, (uint8_t)~stored_len);
-        put_byte(S, out, cap, (uint8_t)(~stored_len >> 8));
-        for (uint64_t i = 0; i < stored_len; i++) put_byte(S, out, cap, buf[i]);
-    } else if (static_lenb == opt_lenb) {
-        send_bits(S, out, cap, (1u << 1) + (uint32_t)last, 3);
-        compress_block(S, out, cap, sym, S.static_ltree, S.static_dtree);
-    } else {
-        send_bits(S, out, cap, (2u << 1) + (uint32_t)last, 3);
-        const int lcodes = S.l_max + 1, dcodes = S.d_max + 1, blcodes = max_blindex + 1;
-        send_bits(S, out, cap, (uint32_t)lcodes - 257, 5);
-        send_bits(S, out, cap, (uint32_t)dcodes - 1, 5);
-        send_bits(S, out, cap, (uint32_t)blcodes - 4, 4);
-        for (int rank = 0; rank < blcodes; rank++) send_bits(S, out, cap, S.bl_tree[c_bl_order[rank]].dl, 3);
-        send_tree(S, out, cap, S.dyn_ltree, lcodes - 1);
-        send_tree(S, out, cap, S.dyn_dtree, dcodes - 1);
-        compress_block(S, out, cap, sym, S.dyn_ltree, S.dyn_dtree);
-    }
-    init_block(S);
-    if (last) bi_windup(S, out, cap);
-}
-
-// CRC-32 (IEEE reflected), java.util.zip.CRC32; zlib's crc32_combine for the lanes' pieces
-__device__ uint32_t gf2_times(const uint32_t *mat, uint32_t vec)
-{
-    uint32_t sum = 0;
-    while (vec) {
-        if (vec & 1) sum ^= *mat;
-        vec >>= 1;
-        mat++;
-    }
-    return sum;
-}
-__device__ void gf2_square(uint32_t *square, const uint32_t *mat)
-{
-    for (int n = 0; n < 32; n++) square[n] = gf2_times(mat, mat[n]);
-}
-__device__ uint32_t crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2)
-{
-    uint32_t even[32], odd[32];
-    if (len2 == 0) return crc1;
-    odd[0] = 0xedb88320u;
-    uint32_t row = 1;
-    for (int n = 1; n < 32; n++) { odd[n] = row; row <<= 1; }
-    gf2_square(even, odd);
-    gf2_square(odd, even);
-    do {
-        gf2_square(even, odd);
-        if (len2 & 1) crc1 = gf2_times(even, crc1);
-        len2 >>= 1;
-        if (len2 == 0) break;
-        gf2_square(odd, even);
-        if (len2 & 1) crc1 = gf2_times(odd, crc1);
-        len2 >>= 1;
-    } while (len2 != 0);
-    return crc1 ^ crc2;
-}
+__device__ __forceinline__ uint32_t crc32_combine(uint32_t crc1, uint32_t crc2, uint32_t shift) { return gf2_mulmod(shift, crc1) ^ crc2; }
 
 }  // namespace
 
-// One wave per page.  Thread 0 runs deflate_slow over the precomputed matches (the symbols of
-// the open block in the page's symbol slots), trees.c per block and the bit stream; then the
-// wave computes the CRC-32 in 64 pieces and writes the framing.  Output: the page's gzip member
-// at a.gz + P.slot (capacity P.cap), its length in a.glen[page index].
-__global__ void __launch_bounds__(64) k_dfl_page(DflArgs a)
+// ------------------------------------------------------------------ the parse, segment-parallel
+// deflate_slow's loop over the precomputed matches is a small state machine: at each loop top p
+// the state is (p, match_length, match_start, match_available), and a step emits at most one
+// symbol (the literal before p, or the previous match) and moves p by 1 or to the match's end.
+// Neither the window slides nor the block flushes change it.  So every DFL_SEG-position segment
+// is parsed by one thread from an entry state (a fresh state at its start in the first round),
+// its exit is the first loop top past its end, and rounds re-parse the segments whose entry
+// differs from their left neighbour's exit until none does: that fixed point is the sequential
+// parse (induction over segments).  Symbols go to the slot of their loop top (bit 31: present;
+// literal c: c, match: (length - 3) | distance << 8); a segment owns the slots of its range and
+// clears the ones it passes without a symbol.  CPU model: tests/microbench/deflate_seg_proto.c
+// (every dumped C2 / C3 / C4 page converges in at most 2 rounds).
+constexpr uint32_t SYM_ON = 1u << 31;
+
+__global__ void __launch_bounds__(256) k_dfl_seg_init(DflArgs a)
 {
-    __shared__ DflTrees S;
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= a.nsegs) return;
+    a.seg_entry[k] = DflSt{a.segs[k].seg * DFL_SEG, 0, D_MIN_MATCH - 1, 0};
+    a.seg_dirty[k] = 1;
+}
+
+__global__ void __launch_bounds__(256) k_dfl_parse(DflArgs a)
+{
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= a.nsegs || !a.seg_dirty[k]) return;
+    const DflSeg G = a.segs[k];
+    const DflPage P = a.pages[G.page];
+    const uint64_t n = P.len;
+    const uint32_t begin = G.seg * DFL_SEG;
+    const uint32_t end = (uint64_t)begin + DFL_SEG < n ? begin + DFL_SEG : (uint32_t)n;
+    const uint8_t *in = a.in + P.off;
+    const uint16_t *pdist = a.pdist + P.off;
+    const uint32_t *m128 = a.m128 + P.off, *m32 = a.m32 + P.off;
+    uint32_t *sym = a.sym + P.off;
+    const DflSt e = a.seg_entry[k];
+    for (uint32_t q = begin; q < e.p && q < end; q++) sym[q] = 0;   // inside the previous segment's last match
+    uint32_t p = e.p, match_length = e.ml, match_start = e.ms, cnt = 0;
+    bool match_available = e.ma != 0;
+    while (p < end) {
+        uint32_t hash_head = 0;   // NIL
+        if (n - p >= D_MIN_MATCH) {
+            const uint32_t d = pdist[p];
+            if (d) hash_head = p - d;
+        }
+        const uint32_t prev_length = match_length, prev_match = match_start;
+        match_length = D_MIN_MATCH - 1;
+        if (hash_head != 0 && prev_length < D_LAZY) {
+            const uint32_t r = prev_length >= D_GOOD ? m32[p] : m128[p];
+            const uint32_t rl = r & 0x1ff;
+            if (r && rl > prev_length) {
+                match_length = rl;
+                match_start = p - (r >> 9);
+            } else {
+                match_length = prev_length;   // longest_match returns best_len unchanged
+            }
+            if (match_length == D_MIN_MATCH && p - match_start > D_TOO_FAR) match_length = D_MIN_MATCH - 1;
+        }
+        if (prev_length >= D_MIN_MATCH && match_length <= prev_length) {
+            sym[p] = SYM_ON | ((p - 1 - prev_match) << 8) | (prev_length - D_MIN_MATCH);
+            cnt++;
+            const uint32_t np = p + prev_length - 1;
+            for (uint32_t q = p + 1; q < np && q < end; q++) sym[q] = 0;
+            p = np;
+            match_available = false;
+            match_length = D_MIN_MATCH - 1;
+        } else if (match_available) {
+            sym[p] = SYM_ON | in[p - 1];
+            cnt++;
+            p++;
+        } else {
+            sym[p] = 0;
+            match_available = true;
+            p++;
+        }
+    }
+    a.seg_exit[k] = DflSt{p, match_length >= D_MIN_MATCH ? match_start : 0u, match_length, match_available ? 1u : 0u};
+    a.seg_cnt[k] = cnt;
+}
+
+__global__ void __launch_bounds__(256) k_dfl_fix(DflArgs a)
+{
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= a.nsegs) return;
+    if (a.segs[k].seg == 0) { a.seg_dirty[k] = 0; return; }   // a page's first entry is exact
+    const DflSt x = a.seg_exit[k - 1], e = a.seg_entry[k];
+    const bool same = x.p == e.p && x.ml == e.ml && x.ma == e.ma && (x.ml < D_MIN_MATCH || x.ms == e.ms);
+    a.seg_dirty[k] = same ? 0u : 1u;
+    if (!same) {
+        a.seg_entry[k] = x;
+        atomicOr(a.flag, 1u);
+    }
+}
+
+// ------------------------------------------------------------------ CRC per 32 KiB tile
+// one wave per tile: 64 pieces of 512 bytes (table in LDS), combined with x^4096
+__global__ void __launch_bounds__(64) k_dfl_tcrc(DflArgs a)
+{
     __shared__ uint32_t crc_t[256];
     __shared__ uint32_t lcrc[64];
-    const DflPage P = a.pages[blockIdx.x];
+    const DflTile T = a.tiles[blockIdx.x];
+    const DflPage P = a.pages[T.page];
     const uint32_t lane = threadIdx.x;
-    const uint8_t *in = a.in + P.off;
-    uint8_t *gz = a.gz + P.slot;
     for (uint32_t i = lane; i < 256; i += 64) {
         uint32_t c = i;
-        for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? CRC_POLY ^ (c >> 1) : c >> 1;
         crc_t[i] = c;
     }
-    if (lane == 0) {
-        static_init(S);
-        init_block(S);
-        S.bi_buf = 0;
-        S.bi_valid = 0;
-        S.op = 0;
-        const uint64_t n = P.len, cap = P.cap - 18;
-        uint8_t *out = gz + 10;
-        uint32_t *sym = a.sym + P.off;   // a block's symbols: at most one per input byte
-        uint64_t p = 0, base = 0, block_start = 0;
-        uint32_t prev_length, match_length = D_MIN_MATCH - 1, prev_match = 0, match_start = 0;
-        bool match_available = false;
-        auto tally = [&](uint32_t v, uint32_t lc, uint32_t dist) -> bool {
-            sym[S.last_lit++] = lc | (dist << 8);
-            if (dist == 0) S.dyn_ltree[lc].fc++;
-            else {
-                S.dyn_ltree[S.length_code[lc] + LITERALS + 1].fc++;
-                S.dyn_dtree[d_code(S, dist - 1)].fc++;
-            }
-            (void)v;
-            return S.last_lit == D_LIT_BUFSIZE - 1;
-        };
-        auto flush = [&](int last) {
-            const bool in_window = block_start >= base;   // zlib: block_start >= 0 after the slides
-            flush_block(S, out, cap, sym, in_window ? in + block_start : nullptr, p - block_start, last);
-            block_start = p;
-        };
-        for (;;) {
-            uint64_t wend = base + 2 * D_WSIZE < n ? base + 2 * D_WSIZE : n;
-            uint64_t lookahead = wend - p;
-            if (lookahead < D_MIN_LOOKAHEAD) {   // fill_window: slide once the window is nearly full
-                if (p - base >= D_WSIZE + D_MAX_DIST) base += D_WSIZE;
-                wend = base + 2 * D_WSIZE < n ? base + 2 * D_WSIZE : n;
-                lookahead = wend - p;
-                if (lookahead == 0) break;
-            }
-            uint64_t hash_head = 0;   // NIL
-            if (lookahead >= D_MIN_MATCH) {
-                const uint32_t d = a.pdist[P.off + p];
-                if (d) hash_head = p - d;
-            }
-            prev_length = match_length, prev_match = match_start;
-            match_length = D_MIN_MATCH - 1;
-            if (hash_head != 0 && prev_length < D_LAZY && p - hash_head <= D_MAX_DIST) {
-                const uint32_t r = prev_length >= D_GOOD ? a.m32[P.off + p] : a.m128[P.off + p];
-                const uint32_t rl = r & 0x1ff;
-                if (r && rl > prev_length) {
-                    match_length = rl;
-                    match_start = (uint32_t)(p - (r >> 9));
-                } else {
-                    match_length = prev_length;   // longest_match returns best_len unchanged
-                }
-                if (match_length == D_MIN_MATCH && p - match_start > D_TOO_FAR) match_length = D_MIN_MATCH - 1;
-            }
-            if (prev_length >= D_MIN_MATCH && match_length <= prev_length) {
-                const bool bf = tally(0, prev_length - D_MIN_MATCH, (uint32_t)(p - 1 - prev_match));
-                p += prev_length - 1;
-                match_available = false;
-                match_length = D_MIN_MATCH - 1;
-                if (bf) flush(0);
-            } else if (match_available) {
-                const bool bf = tally(0, in[p - 1], 0);
-                if (bf) flush(0);
-                p++;
-            } else {
-                match_available = true;
-                p++;
-            }
-        }
-        if (match_available) (void)tally(0, in[p - 1], 0);
-        flush(1);
-        a.glen[blockIdx.x] = S.op <= cap ? S.op : ~0ull;
-    }
     __syncthreads();
-    // CRC-32 of the page: 64 contiguous pieces, combined in order
-    const uint64_t per = (P.len + 63) / 64, b0 = lane * per < P.len ? lane * per : P.len;
-    const uint64_t b1 = b0 + per < P.len ? b0 + per : P.len;
+    const uint64_t ts = (uint64_t)T.tile * D_WSIZE, te = ts + D_WSIZE < P.len ? ts + D_WSIZE : P.len;
+    const uint8_t *in = a.in + P.off;
+    const uint64_t b0 = ts + (uint64_t)lane * 512 < te ? ts + (uint64_t)lane * 512 : te;
+    const uint64_t b1 = b0 + 512 < te ? b0 + 512 : te;
     uint32_t c = 0xffffffffu;
     for (uint64_t i = b0; i < b1; i++) c = crc_t[(c ^ in[i]) & 0xff] ^ (c >> 8);
     lcrc[lane] = ~c;
     __syncthreads();
     if (lane == 0) {
+        const uint32_t x512 = gf2_x8n(512);
         uint32_t crc = 0;
         for (uint32_t k = 0; k < 64; k++) {
-            const uint64_t s0 = k * per < P.len ? k * per : P.len;
-            const uint64_t s1 = s0 + per < P.len ? s0 + per : P.len;
-            crc = crc32_combine(crc, lcrc[k], s1 - s0);
+            const uint64_t s0 = ts + (uint64_t)k * 512 < te ? ts + (uint64_t)k * 512 : te;
+            const uint64_t s1 = s0 + 512 < te ? s0 + 512 : te;
+            if (s1 == s0) break;
+            crc = crc32_combine(crc, lcrc[k], s1 - s0 == 512 ? x512 : gf2_x8n(s1 - s0));
         }
-        const uint64_t dl = a.glen[blockIdx.x];
-        if (dl != ~0ull) {
-            const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0};
-            for (int i = 0; i < 10; i++) gz[i] = hdr[i];
-            uint8_t *t = gz + 10 + dl;
-            const uint32_t isz = (uint32_t)P.len;
-            for (int i = 0; i < 4; i++) t[i] = (uint8_t)(crc >> (8 * i));
-            for (int i = 0; i < 4; i++) t[4 + i] = (uint8_t)(isz >> (8 * i));
-            a.glen[blockIdx.x] = dl + 18;
+        a.tile_crc[blockIdx.x] = crc;
+    }
+}
+
+// ------------------------------------------------------------------ per page: symbol offsets
+// One workgroup per page: the segments' symbol offsets (exclusive), the symbol count (+ the
+// final literal zlib tallies after the loop when a match was still pending), the block count
+// (blocks of 16383 symbols; a flush after a full block tallied inside the loop leaves an empty
+// final block), and the page CRC from its tiles'.
+__global__ void __launch_bounds__(KPW_BLOCK) k_dfl_pscan(DflArgs a)
+{
+    __shared__ uint32_t lds[KPW_BLOCK];
+    const uint32_t pg = blockIdx.x;
+    const DflPage P = a.pages[pg];
+    const uint32_t s0 = a.page_seg0[pg], ns = a.page_seg0[pg + 1] - s0;
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < ns; i0 += KPW_BLOCK) {
+        const uint32_t i = i0 + threadIdx.x;
+        const uint32_t c = i < ns ? a.seg_cnt[s0 + i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_scan_excl<uint32_t, OpSum32>(c, lds, &tot);
+        if (i < ns) a.seg_sym0[s0 + i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        const bool fin = P.len > 0 && a.seg_exit[s0 + ns - 1].ma != 0;
+        const uint32_t T = carry + (fin ? 1u : 0u);
+        if (fin) {
+            const uint64_t base = P.off + pg;
+            a.dsym[base + carry] = a.in[P.off + P.len - 1];
+            a.dpos[base + carry] = (uint32_t)P.len;
+        }
+        uint32_t nb = 1;
+        if (T) {
+            nb = (T + DFL_BLK - 1) / DFL_BLK;
+            if (T % DFL_BLK == 0 && !fin) nb++;
+        }
+        a.page_T[pg] = T;
+        a.page_nblk[pg] = nb;
+        const uint32_t t0 = a.page_tile0[pg], t1 = a.page_tile0[pg + 1];
+        const uint32_t xt = gf2_x8n(D_WSIZE);
+        uint32_t crc = 0;
+        for (uint32_t t = t0; t < t1; t++) {
+            const uint64_t ts = (uint64_t)(t - t0) * D_WSIZE;
+            const uint64_t len = P.len - ts < D_WSIZE ? P.len - ts : D_WSIZE;
+            crc = crc32_combine(crc, a.tile_crc[t], len == D_WSIZE ? xt : gf2_x8n(len));
+        }
+        a.page_crc[pg] = crc;
+    }
+}
+
+// One workgroup per segment: its present symbols, dense at the page's base + its offset.
+__global__ void __launch_bounds__(KPW_BLOCK) k_dfl_gather(DflArgs a)
+{
+    __shared__ uint32_t lds[KPW_BLOCK];
+    const uint32_t k = blockIdx.x;
+    const DflSeg G = a.segs[k];
+    const DflPage P = a.pages[G.page];
+    const uint32_t begin = G.seg * DFL_SEG;
+    const uint32_t end = (uint64_t)begin + DFL_SEG < P.len ? begin + DFL_SEG : (uint32_t)P.len;
+    const uint32_t q0 = begin + threadIdx.x * 8;
+    uint32_t v[8], c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        v[i] = q0 + i < end ? a.sym[P.off + q0 + i] : 0u;
+        c += v[i] >> 31;
+    }
+    uint32_t tot;
+    uint32_t at = a.seg_sym0[k] + block_scan_excl<uint32_t, OpSum32>(c, lds, &tot);
+    const uint64_t base = P.off + G.page;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (v[i] >> 31) {
+            a.dsym[base + at] = v[i] & ~SYM_ON;
+            a.dpos[base + at] = q0 + i;
+            at++;
+        }
+}
+
+// ------------------------------------------------------------------ blocks
+// One workgroup per deflate block: the frequencies (LDS atomics), trees.c on thread 0 (the same
+// decisions as _tr_flush_block: stored when its bytes are still in zlib's window and no longer,
+// static when no longer than dynamic), then the block's bits.  Size pass (emit = false): the
+// bit count; emit pass: the bits at the block's offset in the page's stream (zeroed first;
+// words shared with a neighbour are or-ed atomically, the others stored).
+struct DflBlockLds {
+    DflTrees S;
+    uint32_t lfreq[L_CODES], dfreq[D_CODES];
+    uint32_t kind, hbits, stored_len, block_start;
+    uint64_t scan[KPW_BLOCK];
+};
+
+// bits of one symbol under the trees (v: lc | dist << 8)
+__device__ __forceinline__ uint32_t sym_bits(const DflTrees &S, const CtData *lt, const CtData *dt, uint32_t v)
+{
+    const uint32_t dist = v >> 8, lc = v & 0xff;
+    if (dist == 0) return lt[lc].dl;
+    const uint32_t code = S.length_code[lc], dc = d_code(S, dist - 1);
+    return lt[code + LITERALS + 1].dl + c_extra_lbits[code] + dt[dc].dl + c_extra_dbits[dc];
+}
+
+// a bit writer at an absolute bit position of a 64-bit-word stream; `lo` / `hi`: the bit range
+// this writer owns alone (words inside it are stored, the others or-ed)
+struct BitW {
+    uint64_t *w;
+    uint64_t pos;    // absolute bit of acc's bit 0 (a multiple of 64)
+    uint64_t acc;
+    uint32_t nb;
+    uint64_t lo, hi;
+    __device__ void start(uint64_t *words, uint64_t at, uint64_t own_lo, uint64_t own_hi)
+    {
+        w = words; pos = at & ~63ull; nb = (uint32_t)(at & 63); acc = 0; lo = own_lo; hi = own_hi;
+    }
+    __device__ void word(uint64_t idx, uint64_t v)
+    {
+        const uint64_t b = idx * 64;
+        if (b >= lo && b + 64 <= hi) w[idx] = v;
+        else if (v) atomicOr((unsigned long long *)&w[idx], (unsigned long long)v);
+    }
+    __device__ void put(uint32_t v, uint32_t len)
+    {
+        if (!len) return;
+        acc |= (uint64_t)v << nb;
+        if (nb + len >= 64) {
+            word(pos >> 6, acc);
+            acc = nb ? (uint64_t)v >> (64 - nb) : 0;
+            pos += 64;
+            nb = nb + len - 64;
+        } else {
+            nb += len;
         }
     }
+    __device__ void flush()
+    {
+        if (nb) word(pos >> 6, acc);
+    }
+};
+
+// symbol end (the position after its bytes) and its loop top
+__device__ __forceinline__ uint64_t sym_end(uint32_t v, uint32_t pos) { return (v >> 8) ? (uint64_t)pos - 1 + (v & 0xff) + D_MIN_MATCH : pos; }
+
+__device__ void dfl_block(const DflArgs &a, DflBlockLds &L, bool emit)
+{
+    DflTrees &S = L.S;
+    const uint32_t b = blockIdx.x;
+    const DflBlk B = a.blks[b];
+    const uint32_t pg = B.page;
+    const DflPage P = a.pages[pg];
+    const uint32_t nblk = a.page_nblk[pg];
+    if (B.j >= nblk) {
+        if (!emit && threadIdx.x == 0) { a.blk_bits[b] = 0; a.blk_kind[b] = 0xffu; }
+        return;   // block-uniform
+    }
+    if (emit && a.glen[pg] == ~0ull) return;   // the member would not fit its slot (reported by k_dfl_sizes)
+    const uint32_t T = a.page_T[pg];
+    const uint32_t s_lo = B.j * DFL_BLK, s_hi = s_lo + DFL_BLK < T ? s_lo + DFL_BLK : T;
+    const bool last = B.j == nblk - 1;
+    const uint64_t base = P.off + pg;
+    const uint32_t *dsym = a.dsym + base, *dpos = a.dpos + base;
+    if (threadIdx.x == 0) static_init(S);
+    for (uint32_t i = threadIdx.x; i < L_CODES; i += KPW_BLOCK) L.lfreq[i] = 0;
+    for (uint32_t i = threadIdx.x; i < D_CODES; i += KPW_BLOCK) L.dfreq[i] = 0;
+    __syncthreads();
+    for (uint32_t i = s_lo + threadIdx.x; i < s_hi; i += KPW_BLOCK) {
+        const uint32_t v = dsym[i], dist = v >> 8, lc = v & 0xff;
+        if (dist == 0) atomicAdd(&L.lfreq[lc], 1u);
+        else {
+            atomicAdd(&L.lfreq[S.length_code[lc] + LITERALS + 1], 1u);
+            atomicAdd(&L.dfreq[d_code(S, dist - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < L_CODES; i++) S.dyn_ltree[i].fc = (uint16_t)L.lfreq[i];
+        for (int i = 0; i < D_CODES; i++) S.dyn_dtree[i].fc = (uint16_t)L.dfreq[i];
+        for (int i = 0; i < BL_CODES; i++) S.bl_tree[i].fc = 0;
+        S.dyn_ltree[END_BLOCK].fc++;
+        S.opt_len = S.static_len = 0;
+        S.l_max = build_tree(S, S.dyn_ltree, 0);
+        S.d_max = build_tree(S, S.dyn_dtree, 1);
+        scan_tree(S, S.dyn_ltree, S.l_max);
+        scan_tree(S, S.dyn_dtree, S.d_max);
+        S.bl_max = build_tree(S, S.bl_tree, 2);
+        int max_blindex;
+        for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
+            if (S.bl_tree[c_bl_order[max_blindex]].dl != 0) break;
+        S.opt_len += 3 * ((uint64_t)max_blindex + 1) + 5 + 5 + 4;
+        uint64_t opt_lenb = (S.opt_len + 3 + 7) >> 3;
+        const uint64_t static_lenb = (S.static_len + 3 + 7) >> 3;
+        if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+        // the block's bytes: from the previous flush to this one (after its last symbol; the
+        // final flush at the page end); zlib's window base then: one 32 KiB slide at every loop
+        // top that found strstart >= base + WSIZE + MAX_DIST
+        const uint64_t start = s_lo ? sym_end(dsym[s_lo - 1], dpos[s_lo - 1]) : 0;
+        const uint64_t flush_at = last ? P.len : sym_end(dsym[s_hi - 1], dpos[s_hi - 1]);
+        const uint64_t top = last ? P.len : dpos[s_hi - 1];
+        const uint64_t wbase = top >= D_WSIZE + D_MAX_DIST ? D_WSIZE * ((top - (D_WSIZE + D_MAX_DIST)) / D_WSIZE + 1) : 0;
+        const uint64_t stored_len = flush_at - start;
+        L.block_start = (uint32_t)start;
+        L.stored_len = (uint32_t)stored_len;
+        if (stored_len + 4 <= opt_lenb && start >= wbase) L.kind = 0;
+        else if (static_lenb == opt_lenb) L.kind = 1;
+        else L.kind = 2;
+        L.hbits = 3;
+        if (L.kind == 2) {   // header: counts, the bit-length code lengths, both trees run-length coded
+            uint32_t h = 3 + 5 + 5 + 4 + 3 * (uint32_t)(max_blindex + 1);
+            const CtData *trees[2] = {S.dyn_ltree, S.dyn_dtree};
+            const int maxc[2] = {S.l_max, S.d_max};
+            for (int t = 0; t < 2; t++) {   // send_tree's bits, counted
+                const CtData *tree = trees[t];
+                int prevlen = -1, curlen, nextlen = tree[0].dl, count = 0, max_count = 7, min_count = 4;
+                if (nextlen == 0) max_count = 138, min_count = 3;
+                for (int q = 0; q <= maxc[t]; q++) {
+                    curlen = nextlen;
+                    nextlen = q + 1 <= maxc[t] ? tree[q + 1].dl : 0xffff;
+                    if (++count < max_count && curlen == nextlen) continue;
+                    else if (count < min_count) h += (uint32_t)count * S.bl_tree[curlen].dl;
+                    else if (curlen != 0) {
+                        if (curlen != prevlen) { h += S.bl_tree[curlen].dl; count--; }
+                        h += S.bl_tree[REP_3_6].dl + 2;
+                    } else if (count <= 10) h += S.bl_tree[REPZ_3_10].dl + 3;
+                    else h += S.bl_tree[REPZ_11_138].dl + 7;
+                    count = 0;
+                    prevlen = curlen;
+                    if (nextlen == 0) max_count = 138, min_count = 3;
+                    else if (curlen == nextlen) max_count = 6, min_count = 3;
+                    else max_count = 7, min_count = 4;
+                }
+            }
+            L.hbits = h;
+            S.max_bl = max_blindex;
+        }
+    }
+    __syncthreads();
+    const uint32_t kind = L.kind;
+    uint64_t *words = (uint64_t *)(a.gz + P.slot + 16);
+    if (kind == 0) {   // stored: 3 header bits, then byte-aligned LEN, NLEN and the bytes
+        if (!emit) {
+            if (threadIdx.x == 0) { a.blk_bits[b] = L.stored_len; a.blk_kind[b] = 0; }
+            return;
+        }
+        const uint64_t o = a.blk_off[b];
+        const uint64_t at = (o + 3 + 7) >> 3;                 // first byte after the header's pad
+        const uint64_t nbytes = 4 + (uint64_t)L.stored_len;
+        if (threadIdx.x == 0) {
+            BitW w;
+            w.start(words, o, 0, 0);   // (shared words only)
+            w.put(last ? 1u : 0u, 3);
+            w.flush();
+        }
+        const uint8_t *src = a.in + P.off + L.block_start;
+        const uint16_t len = (uint16_t)L.stored_len;
+        auto byte_at = [&](uint64_t i) -> uint8_t {   // i-th byte of LEN, NLEN, data
+            if (i == 0) return (uint8_t)len;
+            if (i == 1) return (uint8_t)(len >> 8);
+            if (i == 2) return (uint8_t)~len;
+            if (i == 3) return (uint8_t)(~len >> 8);
+            return src[i - 4];
+        };
+        const uint64_t w0 = at >> 3, w1 = (at + nbytes + 7) >> 3;
+        for (uint64_t wi = w0 + threadIdx.x; wi < w1; wi += KPW_BLOCK) {
+            uint64_t v = 0;
+            bool whole = true;
+            for (int k = 0; k < 8; k++) {
+                const uint64_t byte = wi * 8 + k;
+                if (byte < at || byte >= at + nbytes) { whole = false; continue; }
+                v |= (uint64_t)byte_at(byte - at) << (8 * k);
+            }
+            if (whole) words[wi] = v;
+            else if (v) atomicOr((unsigned long long *)&words[wi], (unsigned long long)v);
+        }
+        return;
+    }
+    const CtData *lt = kind == 1 ? S.static_ltree : S.dyn_ltree;
+    const CtData *dt = kind == 1 ? S.static_dtree : S.dyn_dtree;
+    // this thread's symbols and their bits
+    const uint32_t nsym = s_hi - s_lo, per = (nsym + KPW_BLOCK - 1) / KPW_BLOCK;
+    const uint32_t i0 = s_lo + threadIdx.x * per < s_hi ? s_lo + threadIdx.x * per : s_hi;
+    const uint32_t i1 = i0 + per < s_hi ? i0 + per : s_hi;
+    uint64_t mine = 0;
+    for (uint32_t i = i0; i < i1; i++) mine += sym_bits(S, lt, dt, dsym[i]);
+    uint64_t tot;
+    const uint64_t ex = block_scan_excl<uint64_t, OpSum64>(mine, L.scan, &tot);
+    const uint32_t eob = lt[END_BLOCK].dl;
+    if (!emit) {
+        if (threadIdx.x == 0) { a.blk_bits[b] = L.hbits + tot + eob; a.blk_kind[b] = kind; }
+        return;
+    }
+    const uint64_t o = a.blk_off[b];
+    if (threadIdx.x == 0) {   // header (and the end-of-block code)
+        BitW w;
+        w.start(words, o, 0, 0);
+        w.put(((kind == 1 ? 1u : 2u) << 1) + (last ? 1u : 0u), 3);
+        if (kind == 2) {
+            const int lcodes = S.l_max + 1, dcodes = S.d_max + 1, blcodes = S.max_bl + 1;
+            w.put((uint32_t)lcodes - 257, 5);
+            w.put((uint32_t)dcodes - 1, 5);
+            w.put((uint32_t)blcodes - 4, 4);
+            for (int rank = 0; rank < blcodes; rank++) w.put(S.bl_tree[c_bl_order[rank]].dl, 3);
+            const CtData *trees[2] = {S.dyn_ltree, S.dyn_dtree};
+            const int maxc[2] = {lcodes - 1, dcodes - 1};
+            for (int t = 0; t < 2; t++) {   // send_tree
+                const CtData *tree = trees[t];
+                int prevlen = -1, curlen, nextlen = tree[0].dl, count = 0, max_count = 7, min_count = 4;
+                if (nextlen == 0) max_count = 138, min_count = 3;
+                for (int q = 0; q <= maxc[t]; q++) {
+                    curlen = nextlen;
+                    nextlen = q + 1 <= maxc[t] ? tree[q + 1].dl : 0xffff;
+                    if (++count < max_count && curlen == nextlen) continue;
+                    else if (count < min_count) {
+                        do { w.put(S.bl_tree[curlen].fc, S.bl_tree[curlen].dl); } while (--count != 0);
+                    } else if (curlen != 0) {
+                        if (curlen != prevlen) { w.put(S.bl_tree[curlen].fc, S.bl_tree[curlen].dl); count--; }
+                        w.put(S.bl_tree[REP_3_6].fc, S.bl_tree[REP_3_6].dl);
+                        w.put((uint32_t)count - 3, 2);
+                    } else if (count <= 10) {
+                        w.put(S.bl_tree[REPZ_3_10].fc, S.bl_tree[REPZ_3_10].dl);
+                        w.put((uint32_t)count - 3, 3);
+                    } else {
+                        w.put(S.bl_tree[REPZ_11_138].fc, S.bl_tree[REPZ_11_138].dl);
+                        w.put((uint32_t)count - 11, 7);
+                    }
+                    count = 0;
+                    prevlen = curlen;
+                    if (nextlen == 0) max_count = 138, min_count = 3;
+                    else if (curlen == nextlen) max_count = 6, min_count = 3;
+                    else max_count = 7, min_count = 4;
+                }
+            }
+        }
+        w.flush();
+        BitW e;
+        e.start(words, o + L.hbits + tot, 0, 0);
+        e.put(lt[END_BLOCK].fc, eob);
+        e.flush();
+    }
+    {   // the symbols
+        const uint64_t s0 = o + L.hbits + ex;
+        BitW w;
+        w.start(words, s0, s0, s0 + mine);
+        for (uint32_t i = i0; i < i1; i++) {
+            const uint32_t v = dsym[i];
+            uint32_t dist = v >> 8;
+            int lc = (int)(v & 0xff);
+            if (dist == 0) {
+                w.put(lt[lc].fc, lt[lc].dl);
+            } else {
+                uint32_t code = S.length_code[lc];
+                w.put(lt[code + LITERALS + 1].fc, lt[code + LITERALS + 1].dl);
+                int extra = c_extra_lbits[code];
+                if (extra) w.put((uint32_t)(lc - S.base_length[code]), (uint32_t)extra);
+                dist--;
+                code = d_code(S, dist);
+                w.put(dt[code].fc, dt[code].dl);
+                extra = c_extra_dbits[code];
+                if (extra) w.put(dist - (uint32_t)S.base_dist[code], (uint32_t)extra);
+            }
+        }
+        w.flush();
+    }
+}
+
+__global__ void __launch_bounds__(KPW_BLOCK) k_dfl_bsize(DflArgs a)
+{
+    __shared__ DflBlockLds L;
+    dfl_block(a, L, false);
+}
+__global__ void __launch_bounds__(KPW_BLOCK) k_dfl_bemit(DflArgs a)
+{
+    __shared__ DflBlockLds L;
+    dfl_block(a, L, true);
+}
+
+// One thread per page: every block's bit offset (a stored block pads its header to a byte), the
+// stream's bytes after the final pad, the member length (10 header + stream + 8 trailer bytes).
+__global__ void __launch_bounds__(64) k_dfl_boff(DflArgs a, uint32_t npages)
+{
+    const uint32_t pg = blockIdx.x * 64 + threadIdx.x;
+    if (pg >= npages) return;
+    const DflPage P = a.pages[pg];
+    const uint32_t b0 = a.page_blk0[pg], nb = a.page_nblk[pg];
+    uint64_t off = 0;
+    for (uint32_t j = 0; j < nb; j++) {
+        a.blk_off[b0 + j] = off;
+        if (a.blk_kind[b0 + j] == 0) off = ((off + 3 + 7) & ~7ull) + 32 + 8 * a.blk_bits[b0 + j];
+        else off += a.blk_bits[b0 + j];
+    }
+    const uint64_t g = 10 + ((off + 7) >> 3) + 8;
+    a.glen[pg] = g <= P.cap - 16 ? g : ~0ull;
 }
 
 // page slot p: clen = [v2 level prefix] + its gzip member (pages not listed: the prefix only);
@@ -688,21 +956,54 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dfl_copy(DflArgs a)
     if (pre) block_copy(dst, a.in + a.page_off[p] - pre, (uint32_t)pre, threadIdx.x, KPW_BLOCK);
     const int32_t k = a.slot_page[p];
     if (k < 0 || a.glen[k] == ~0ull) return;
-    const uint64_t g = a.glen[k];
-    const uint8_t *src = a.gz + a.pages[k].slot;
-    for (uint64_t o = 0; o < g; o += 1u << 20) {
-        const uint32_t m = (uint32_t)(g - o < (1u << 20) ? g - o : (1u << 20));
-        block_copy(dst + pre + o, src + o, m, threadIdx.x, KPW_BLOCK);
+    const uint64_t g = a.glen[k], dl = g - 18;
+    const uint8_t *src = a.gz + a.pages[k].slot + 16;
+    uint8_t *m = dst + pre;
+    if (threadIdx.x < 10) {   // java.util.zip.GZIPOutputStream's header
+        const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0};
+        m[threadIdx.x] = hdr[threadIdx.x];
+    } else if (threadIdx.x < 18) {   // CRC-32 and ISIZE, little-endian
+        const uint32_t i = threadIdx.x - 10;
+        const uint32_t v = i < 4 ? a.page_crc[k] : (uint32_t)a.pages[k].len;
+        m[10 + dl + i] = (uint8_t)(v >> (8 * (i & 3)));
+    }
+    for (uint64_t o = 0; o < dl; o += 1u << 20) {
+        const uint32_t c = (uint32_t)(dl - o < (1u << 20) ? dl - o : (1u << 20));
+        block_copy(m + 10 + o, src + o, c, threadIdx.x, KPW_BLOCK);
     }
 }
 
-void launch_deflate(const DflArgs &a, uint32_t npages_listed, uint32_t ntiles, hipStream_t s)
+void launch_deflate_prep(const DflArgs &a, uint32_t ntiles, hipStream_t s)
 {
     if (ntiles) {
         hipLaunchKernelGGL(k_dfl_prev, dim3(ntiles), dim3(64), 0, s, a);
         hipLaunchKernelGGL(k_dfl_match, dim3(ntiles * (D_WSIZE / 256)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_dfl_tcrc, dim3(ntiles), dim3(64), 0, s, a);
     }
-    if (npages_listed) hipLaunchKernelGGL(k_dfl_page, dim3(npages_listed), dim3(64), 0, s, a);
+    if (a.nsegs) hipLaunchKernelGGL(k_dfl_seg_init, dim3((a.nsegs + 255) / 256), dim3(256), 0, s, a);
+}
+
+void launch_deflate_round(const DflArgs &a, hipStream_t s)
+{
+    if (!a.nsegs) return;
+    hipLaunchKernelGGL(k_dfl_parse, dim3((a.nsegs + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_dfl_fix, dim3((a.nsegs + 255) / 256), dim3(256), 0, s, a);
+}
+
+// after the last round: symbol offsets, dense symbols, block sizes and offsets
+void launch_deflate_finish(const DflArgs &a, uint32_t npages, hipStream_t s)
+{
+    if (!npages) return;
+    hipLaunchKernelGGL(k_dfl_pscan, dim3(npages), dim3(KPW_BLOCK), 0, s, a);
+    if (a.nsegs) hipLaunchKernelGGL(k_dfl_gather, dim3(a.nsegs), dim3(KPW_BLOCK), 0, s, a);
+    if (a.nblks) hipLaunchKernelGGL(k_dfl_bsize, dim3(a.nblks), dim3(KPW_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(k_dfl_boff, dim3((npages + 63) / 64), dim3(64), 0, s, a, npages);
+}
+
+// (the member scratch zeroed by the caller) the bit streams, sizes and offsets, the packed pages
+void launch_deflate_emit(const DflArgs &a, uint32_t npages, hipStream_t s)
+{
+    if (npages && a.nblks) hipLaunchKernelGGL(k_dfl_bemit, dim3(a.nblks), dim3(KPW_BLOCK), 0, s, a);
     hipLaunchKernelGGL(k_dfl_sizes, dim3(1), dim3(KPW_BLOCK), 0, s, a);
     if (a.nslots) hipLaunchKernelGGL(k_dfl_copy, dim3(a.nslots), dim3(KPW_BLOCK), 0, s, a);
 }

@@ -156,14 +156,25 @@ struct DflPage {
 struct DflTile {
     uint32_t page, tile;  // listed page, 32 KiB tile of it
 };
+struct DflSeg {
+    uint32_t page, seg;   // listed page, DFL_SEG-position segment of it
+};
+struct DflBlk {
+    uint32_t page, j;     // listed page, deflate block j of it (blocks past the page's count: idle)
+};
+struct DflSt {
+    uint32_t p, ms, ml, ma;   // deflate_slow loop-top state: strstart, match_start, match_length, match_available
+};
+constexpr uint32_t DFL_SEG = 2048;       // positions per parse segment (one thread each)
+constexpr uint32_t DFL_BLK = 16383;      // symbols per deflate block (zlib's lit_bufsize - 1 at level 6)
 struct DflArgs {
     const uint8_t *in;
     const DflPage *pages;        // listed pages
     const DflTile *tiles;
     uint16_t *pdist;             // per input byte: distance to the previous same-hash position (0: none)
     uint32_t *m128, *m32;        // per input byte: longest_match, length | distance << 9
-    uint32_t *sym;               // per input byte: symbol slots of the open block
-    uint8_t *gz;                 // member scratch
+    uint32_t *sym;               // per input byte: the symbol the parse emits at that loop top (bit 31: present)
+    uint8_t *gz;                 // member scratch (per page: the deflate stream at slot + 16)
     uint64_t *glen;              // per listed page: member length (~0: did not fit)
     uint32_t nslots;             // page slots
     const int32_t *slot_page;    // page slot -> listed page (-1: not compressed)
@@ -172,8 +183,24 @@ struct DflArgs {
     uint8_t *out;                // packed pages
     uint64_t *tot;               // [0] total bytes
     uint64_t *overflow;          // set to 1 when a member overflowed its slot (not expected: the slot is deflateBound)
+    // the segment-parallel parse and the block-parallel bit stream (k_deflate.hip)
+    const DflSeg *segs;
+    uint32_t nsegs, nblks;
+    const DflBlk *blks;
+    const uint32_t *page_seg0, *page_blk0, *page_tile0;   // per listed page (+1 entry): first segment / block / tile
+    DflSt *seg_entry, *seg_exit;
+    uint32_t *seg_dirty, *seg_cnt, *seg_sym0;
+    uint32_t *flag;              // a parse round changed an entry
+    uint32_t *dsym, *dpos;       // per listed page, from P.off + page index: dense symbols and their loop tops
+    uint32_t *page_T, *page_nblk, *page_crc, *tile_crc;
+    uint64_t *blk_bits, *blk_off;
+    uint32_t *blk_kind;          // 0 stored, 1 static, 2 dynamic (0xff: past the page's blocks)
 };
-void launch_deflate(const DflArgs &a, uint32_t npages_listed, uint32_t ntiles, hipStream_t s);
+// phases (the host runs the parse rounds until no entry changes, reading `flag` between them)
+void launch_deflate_prep(const DflArgs &a, uint32_t ntiles, hipStream_t s);
+void launch_deflate_round(const DflArgs &a, hipStream_t s);
+void launch_deflate_finish(const DflArgs &a, uint32_t npages_listed, hipStream_t s);
+void launch_deflate_emit(const DflArgs &a, uint32_t npages_listed, hipStream_t s);
 // worst-case gzip member of n bytes (zlib's deflateBound for these parameters + framing)
 inline uint64_t dfl_member_bound(uint64_t n) { return n + (n >> 12) + (n >> 14) + (n >> 25) + 13 + 18 + 64; }
 size_t snappy_seg_scratch_bytes(uint32_t grid);

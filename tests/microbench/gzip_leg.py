@@ -7,10 +7,13 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-for p in ("", "synth", "kafka-parquet-writer_amd"):
+for p in ("", "synth", "kafka-parquet-writer_amd", "oracle", "tests"):
     sys.path.insert(0, os.path.join(ROOT, p))
 import kpw  # noqa: E402
 import synth  # noqa: E402
+
+import oracle  # noqa: E402  (the checker)
+import pqwalk  # noqa: E402
 
 n = int(sys.argv[1])
 page = int(sys.argv[2]) if len(sys.argv) > 2 else 128 << 20
@@ -26,3 +29,10 @@ for rep in range(2):
     dt = time.perf_counter() - t0
     print("gzip writer: %d records (%d bytes), page %d: %.3f s, %.1f MB/s, file %d bytes"
           % (n, int(offs[-1]), page, dt, offs[-1] / dt / 1e6, len(pf.file_bytes())), flush=True)
+fb = pf.file_bytes()
+t0 = time.perf_counter()
+ob = oracle.encode_file(s, data, offs, oracle.make_props(block_size=128 << 20, page_size=page, codec=2))
+print("oracle (one core): %.3f s; files identical: %s" % (time.perf_counter() - t0, fb == ob), flush=True)
+if fb != ob:
+    print(pqwalk.first_difference(fb, ob), flush=True)
+    sys.exit(1)
