@@ -23,7 +23,8 @@ between steps.
 Secondary keys: `resident_encode` (kpw_encoder_encode on a batch already in HBM, the r01
 headline), `c4` (the C4 writer line, 2 steps), `bulk_multipage` (C2 bulk writes with 1 MiB
 pages inside 128 MiB row groups, 2 steps), `c5` (BASELINE config 5 at its shape: 8 concurrent
-writers of 15.625 M Rec8 records each, 2 steps), `per_record` / `per_record_multipage` /
+writers of 15.625 M Rec8 records each, 2 steps), `gzip` (the C2 writer line with
+CompressionCodecName.GZIP, 2 steps), `per_record` / `per_record_multipage` /
 `per_record_64k` (the reference's write + getDataSize loop at 128 MiB / 1 MiB / 64 KiB pages, the
 oracle's same loops in `cpu_baseline`), `roofline` (the dominant kernel, timed with HIP events on the encoder's stream inside
 the timed writer steps; algorithmic bytes per launch), `roofline.pipeline_frac` (sum of
@@ -325,7 +326,7 @@ def per_record_leg(kpw, schema, sschema, kind, seed, n, device, max_file_size, p
                 reference_sizing_hint_records_per_s=300000)
 
 
-def writer_leg(kpw, kind, seed, n, device, steps, warmup, page_size=128 * MiB, sets=None):
+def writer_leg(kpw, kind, seed, n, device, steps, warmup, page_size=128 * MiB, sets=None, codec=None):
     """Secondary writer-path line (same drop-in and timing as the headline, fewer steps): another
     workload (C4) or another page size (pageSize(...) < blockSize, KafkaProtoParquetWriter.java:656-659
     -> ParquetFile.java:47: bulk writes with page cuts inside row groups)."""
@@ -334,7 +335,8 @@ def writer_leg(kpw, kind, seed, n, device, steps, warmup, page_size=128 * MiB, s
     schema = kpw.Schema(sschema.message_name, sschema.columns, sschema.proto_class)
     if sets is None:
         sets = [synth.generate(kind, seed + 0x1000 * k, n, alloc=kpw.pinned_empty) for k in range(2)]
-    props = kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=kpw.SNAPPY, page_size=page_size)
+    codec = kpw.SNAPPY if codec is None else codec
+    props = kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=codec, page_size=page_size)
     for i in range(warmup):
         write_file(kpw, schema, props, sets[i % 2][0], sets[i % 2][1], device)
     t0 = time.perf_counter()
@@ -349,7 +351,8 @@ def writer_leg(kpw, kind, seed, n, device, steps, warmup, page_size=128 * MiB, s
     return dict(value=round(nb / dt / 1e9, 4), unit="GB/s", records_per_s=round(steps * (len(sets[0][1]) - 1) / dt, 1),
                 ms_per_step=round(dt / steps * 1e3, 3), steps=steps, warmup=warmup, records_per_step=len(sets[0][1]) - 1,
                 bytes_per_step=int(nb / steps), file_bytes_per_step=int(file_bytes / steps), page_size=page_size,
-                workload=sschema.message_name.split(".")[-1] + ", SNAPPY, 128 MiB row groups, pageSize %d" % page_size)
+                workload=sschema.message_name.split(".")[-1] + ", %s, 128 MiB row groups, pageSize %d"
+                % ("GZIP" if codec == kpw.GZIP else "SNAPPY", page_size))
 
 
 def c5_leg(kpw, device, steps, warmup):
@@ -508,7 +511,7 @@ def main():
     ap.add_argument("--per-record-page-kb", type=int, default=128 * 1024,
                     help="pageSize of the per-record leg (reference default = blockSize, KafkaProtoParquetWriter.java:474)")
     ap.add_argument("--secondary-steps", type=int, default=2,
-                    help="timed steps of the secondary writer legs at N=1 (c4, bulk_multipage and c5; 0 = skip)")
+                    help="timed steps of the secondary writer legs at N=1 (c4, bulk_multipage, c5 and gzip; 0 = skip)")
     ap.add_argument("--per-record-mp-page-kb", type=int, default=1024,
                     help="pageSize of a second per-record leg with page cuts inside row groups (pageSize(...), "
                          "KafkaProtoParquetWriter.java:656-659; 0 = skip)")
@@ -637,7 +640,7 @@ def main():
     if args.per_record_64k_records and world == 1:   # 64 KiB pages: a size probe every ~2-3 k records
         per_record_64k = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_64k_records, local_rank,
                                         args.per_record_max_file_mb * MiB, 64 * 1024)
-    c4_leg = bulk_mp = c5 = None
+    c4_leg = bulk_mp = c5 = gz = None
     if args.secondary_steps and world == 1 and args.workload == "c2":
         # the config where encode, not PCIe, sets the pace (C4), and bulk writes with 1 MiB pages
         c4k, c4n, c4seed, _ = WORKLOADS["c4"]
@@ -645,6 +648,8 @@ def main():
         bulk_mp = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, page_size=MiB,
                              sets=[s[0] for s in sets])
         c5 = c5_leg(kpw, local_rank, args.secondary_steps, 1)
+        # the same C2 records with CompressionCodecName.GZIP (no BASELINE config; K7' k_deflate.hip)
+        gz = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, sets=[s[0] for s in sets], codec=kpw.GZIP)
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         threads = args.cpu_threads or host_threads()
@@ -691,6 +696,7 @@ def main():
         "c4": c4_leg,
         "bulk_multipage": bulk_mp,
         "c5": c5,
+        "gzip": gz,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
