@@ -1,6 +1,6 @@
 """Full-size parity of the bench workloads through the ParquetFile drop-in (kpw_writer_*):
 C2 (100 M Rec8), C3 (10 M Wide), C4 (20 M HighCard), SNAPPY, 128 MiB row groups, the bench's
-seeds (VERDICT r03 "missing 2").  The single-threaded oracle would take minutes
+seeds (VERDICT r03 "missing 2"), and C2's records with GZIP (round 5).  The single-threaded oracle would take minutes
 for a whole file, but every row group is independent in parquet-mr: after a flush
 InternalParquetRecordWriter resets recordCount and checks again at 100 records, and column
 chunks depend only on the row group's records.  So each row group of the GPU file is checked
@@ -24,10 +24,10 @@ MiB = 1024 * 1024
 SCALE = float(os.environ.get("KPW_FULL_SCALE", "1.0"))
 
 
-def _writer_file(schema, data, offs, batch):
+def _writer_file(schema, data, offs, batch, codec=1):
     import kpw
     pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class),
-                         kpw.ParquetProperties(compression_codec_name=kpw.SNAPPY))
+                         kpw.ParquetProperties(compression_codec_name=codec))
     n = len(offs) - 1
     for a in range(0, n, batch):
         b = min(n, a + batch)
@@ -38,18 +38,19 @@ def _writer_file(schema, data, offs, batch):
     return fb
 
 
-@pytest.mark.parametrize("kind,n,seed", [
-    (synth.KIND_REC8, 100_000_000, 0xC0FFEE02),    # C2
-    (synth.KIND_WIDE, 10_000_000, 0xC0FFEE03),     # C3
-    (synth.KIND_HIGHCARD, 20_000_000, 0xC0FFEE04),  # C4
-], ids=["c2", "c3", "c4"])
-def test_full_size_writer_matches_oracle_per_row_group(kind, n, seed):
+@pytest.mark.parametrize("kind,n,seed,codec", [
+    (synth.KIND_REC8, 100_000_000, 0xC0FFEE02, 1),    # C2
+    (synth.KIND_WIDE, 10_000_000, 0xC0FFEE03, 1),     # C3
+    (synth.KIND_HIGHCARD, 20_000_000, 0xC0FFEE04, 1),  # C4
+    (synth.KIND_REC8, 100_000_000, 0xC0FFEE02, 2),    # C2 records with GZIP (the bench's gzip key)
+], ids=["c2", "c3", "c4", "c2_gzip"])
+def test_full_size_writer_matches_oracle_per_row_group(kind, n, seed, codec):
     n = max(1000, int(n * SCALE))
     schema = synth.SCHEMAS[kind]
     data, offs = synth.generate(kind, seed, n)
-    fb = _writer_file(schema, data, offs, 500_000)   # the bench's poll() batch size
+    fb = _writer_file(schema, data, offs, 500_000, codec)   # the bench's poll() batch size
     assert fb[:4] == b"PAR1" and fb[-4:] == b"PAR1"
-    props = oracle.make_props(block_size=128 * MiB, page_size=128 * MiB, codec=1, enable_dictionary=True)
+    props = oracle.make_props(block_size=128 * MiB, page_size=128 * MiB, codec=codec, enable_dictionary=True)
     errs = check_row_groups(schema, data, offs, fb, props)
     assert not errs, errs[:10]
     # the file also reads back in an independent reader with the right shape
