@@ -69,6 +69,7 @@ struct BatchOut {
 // multi-page regime: one encode of [s, e) -> per column its pages (dictionary page first)
 struct MpRun {
     std::vector<std::vector<PageOut>> cols;
+    std::vector<ChunkDesc> pg, dch;   // the run's page and dictionary descriptors as the device left them
 };
 
 // While alive, DevBuf::ensure on this thread orders the release of a replaced block after the
@@ -134,6 +135,11 @@ public:
     // > 0: plan at most this many row groups per encode (the rest stays unconsumed, also on a
     // final flush).  HDFS block alignment re-plans after each row group with the next limit.
     int32_t max_cuts = 0;
+    // Multi-page, non-final: after a row-group cut whose remaining records are less than a row
+    // group's raw bytes, stop (they are the next job's carry, which plans them again) instead of
+    // encoding them to look for a cut; open_buffered is then -1 (unknown).  The writer's
+    // write-path jobs only: getDataSize plans the open row group when it needs the size.
+    bool lazy_open = false;
     std::vector<ColInfo> cols;
     kpw_props props{};
     std::string message_name, proto_class;
@@ -226,9 +232,12 @@ private:
     // k7_from (probe): per column the first cut page to compress; the dictionary page, the open
     // page and the cut pages before k7_from[c] are not compressed (their compressed sizes in
     // `run` are then meaningless)
+    // spec (splice, v1): `run` is only each column's page after its last cut (cuts[c] < e) plus
+    // its dictionary page, encoded with the dictionary `spec` (the speculative pass over a range
+    // starting at s) left on the device: the pages before are spec's, byte for byte
     int mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s, int64_t e,
                     const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask = nullptr,
-                    const std::vector<uint32_t> *k7_from = nullptr);
+                    const std::vector<uint32_t> *k7_from = nullptr, const MpRun *spec = nullptr);
     int grow_keep(DevBuf &b, size_t bytes, size_t keep);
     // the engine's small host <-> device transfers (engine.cpp: why they stay pageable copies)
     // Several host tables in one H2D copy into `buf` (256-byte aligned parts): their device

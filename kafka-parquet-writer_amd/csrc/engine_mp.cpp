@@ -20,6 +20,7 @@
 // The single-page regime (pageSize >= blockSize, the reference default) stays in engine.cpp
 // and plans every row group of a batch in one pass.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -103,8 +104,9 @@ int Engine::mp_cuts(PageCutArgs &a, int64_t s, int64_t h, std::vector<std::vecto
 // pages_dev_ (PageOut offsets), grouped per column: optional dictionary page, data pages.
 int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, const std::vector<DevCol> &hc, int64_t s,
                         int64_t e, const std::vector<std::vector<int64_t>> &cuts, MpRun &run, const std::vector<char> *mask,
-                        const std::vector<uint32_t> *k7_from)
+                        const std::vector<uint32_t> *k7_from, const MpRun *spec)
 {
+    if (spec && (v2_ || mask || k7_from)) return fail(KPW_ERR_STATE, "multi-page splice: v1 bulk passes only");
     hipStream_t st = stream;
     const int nc = (int)cols.size();
     run.cols.assign(nc, {});
@@ -134,8 +136,22 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         D.is_dict = cols[c].dict && on ? 1 : 0;
         D.smin = ~0ull; D.smax = 0;
         D.ids_off = ids_off; D.ent_off = ids_off;
-        if (on) ids_off += len;
-        if (D.is_dict) {
+        if (on && !spec) ids_off += len;
+        if (D.is_dict && spec) {
+            // the speculative pass's dictionary (ids, entries, tables) stays where it is; the
+            // chunk's pages before its last cut are spec's pages, decided as they were there
+            const ChunkDesc &S = spec->dch[c];
+            D.ht_off = S.ht_off; D.ht_cap = S.ht_cap; D.ht_plim = S.ht_plim;
+            D.ids_off = S.ids_off; D.ent_off = S.ent_off;
+            D.dict_n = S.dict_all;
+            const size_t kept = cuts[c].size();
+            if (kept) {
+                const ChunkDesc &P0 = spec->pg[S.first_page];
+                D.tail_mode = P0.fallback ? 2u : 1u;
+                for (size_t i = 0; i < kept; i++)
+                    if (!spec->pg[S.first_page + i].fallback) D.tail_dict_n = spec->pg[S.first_page + i].dict_n;
+            }
+        } else if (D.is_dict) {
             // Insertion runs in rounds of round_tiles tiles per chunk and a chunk stops after
             // the round in which its dictionary passed dictPageSize (pages before the fallback
             // page keep their ids: every value before the crossing is inserted).  So a table
@@ -155,8 +171,9 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         ddict[c] = D.is_dict;
         ndt += nt;
         if (!on) { D.npages = 0; continue; }
-        int64_t q = s;
-        for (size_t i = 0; i <= cuts[c].size(); i++) {
+        // (splice: only the page after the last cut)
+        int64_t q = spec && !cuts[c].empty() ? cuts[c].back() : s;
+        for (size_t i = spec ? cuts[c].size() : 0; i <= cuts[c].size(); i++) {
             const int64_t pe = i < cuts[c].size() ? std::min<int64_t>(cuts[c][i], e) : e;
             if (pe <= q) continue;
             ChunkDesc P;
@@ -334,7 +351,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             if (v2_) launch_v2_bool_jobs(ap, d_jobs.as<RleJob>(), st);   // optional booleans: page rank base + length
         }
         launch_mp_pages_init(ap.ch, npg, ad.ch, ap.cols, d_jobs.as<RleJob>(), st);
-        launch_dict(ad, d_jobs.as<RleJob>(), st);            // K2 per column chunk
+        if (!spec) launch_dict(ad, d_jobs.as<RleJob>(), st);   // K2 per column chunk (splice: spec's)
         launch_page_str_stats(ap, st);
         launch_mp_dict_decide(ap.ch, npg, ad.ch, ap.cols, ap.ent_rec, ap.ent_boff, (uint32_t)props.dictionary_page_size,
                               d_jobs.as<RleJob>(), st);
@@ -559,6 +576,8 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         }
         out.push_back(q);
     }
+    run.pg = std::move(pg);
+    run.dch = std::move(dch);
     return KPW_OK;
 }
 
@@ -612,6 +631,20 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
 // engine's first job a second speculative pass.  Only the horizon depends on it, never a byte.
 static std::mutex g_horizon_mu;
 static std::unordered_map<uint64_t, int64_t> g_horizon;
+
+// KPW_MP_LAZY=0: Engine::lazy_open is ignored (A/B)
+static bool lazy_on()
+{
+    static const bool on = [] { const char *e = getenv("KPW_MP_LAZY"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
+// KPW_MP_SPLICE=0: every exact pass re-encodes the whole row group (A/B of the splice)
+static bool splice_on()
+{
+    static const bool on = [] { const char *e = getenv("KPW_MP_SPLICE"); return !(e && e[0] == '0'); }();
+    return on;
+}
 
 static uint64_t horizon_key(const std::vector<ColInfo> &cols, const kpw_props &p)
 {
@@ -706,6 +739,68 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         acc_len += pages_len_;
         return KPW_OK;
     };
+    // Splice: the kept pages of the speculative `run` (per column its data pages before the last
+    // cut <= e, contiguous in pages_dev_) go to the output first, then the exact pass over the
+    // last pages (which reuses the device buffers) and its pages.
+    auto append_splice = [&](int64_t s, int64_t e) -> int {
+        MpRun sp = std::move(run);
+        std::vector<uint64_t> ko0(nc, 0), kofs(nc, 0);
+        uint64_t kept_total = 0;
+        for (int c = 0; c < nc; c++) {
+            kofs[c] = kept_total;
+            const size_t k = cuts[c].size();
+            if (!k) continue;
+            size_t first = 0;
+            while (first < sp.cols[c].size() && sp.cols[c][first].page_type == KPW_DICTIONARY_PAGE) first++;
+            if (first + k + 1 > sp.cols[c].size()) return fail(KPW_ERR_DEVICE, "multi-page splice: page list mismatch");
+            const PageOut &a0 = sp.cols[c][first], &a1 = sp.cols[c][first + k - 1];
+            ko0[c] = a0.offset;
+            kept_total += a1.offset + (uint64_t)a1.compressed_size - a0.offset;
+        }
+        if (grow_keep(mp_acc, acc_len + kept_total + 64 + 4096, acc_len)) return KPW_ERR_NOMEM;
+        const uint64_t kept_base = acc_len;
+        for (int c = 0; c < nc; c++) {
+            const uint64_t l = (c + 1 < nc ? kofs[c + 1] : kept_total) - kofs[c];
+            if (l) CK(hipMemcpyAsync(mp_acc.as<uint8_t>() + kept_base + kofs[c], pages_dev_ + ko0[c], l, hipMemcpyDeviceToDevice, st));
+        }
+        acc_len += kept_total;
+        int rs = mp_pipeline(d_data, d_off, n, hc, s, e, cuts, run, nullptr, nullptr, &sp);
+        if (rs) return rs;
+        if (grow_keep(mp_acc, acc_len + pages_len_ + 64 + 4096, acc_len)) return KPW_ERR_NOMEM;
+        if (pages_len_) CK(hipMemcpyAsync(mp_acc.as<uint8_t>() + acc_len, pages_dev_, pages_len_, hipMemcpyDeviceToDevice, st));
+        out.rgs.push_back(RowGroupOut{s, e - s, (int32_t)out.chunks.size()});
+        for (int c = 0; c < nc; c++) {
+            ChunkOut co;
+            co.column = c;
+            co.first_page = (int32_t)out.pages.size();
+            co.num_values = e - s;
+            co.has_dictionary = 0;
+            size_t t = 0;   // the exact pass: [dictionary page] last page
+            for (; t < run.cols[c].size() && run.cols[c][t].page_type == KPW_DICTIONARY_PAGE; t++) {
+                PageOut p = run.cols[c][t];
+                co.has_dictionary = 1;
+                p.offset += acc_len;
+                out.pages.push_back(p);
+            }
+            const size_t k = cuts[c].size();
+            size_t first = 0;
+            while (first < sp.cols[c].size() && sp.cols[c][first].page_type == KPW_DICTIONARY_PAGE) first++;
+            for (size_t i = 0; i < k; i++) {
+                PageOut p = sp.cols[c][first + i];
+                p.offset = p.offset - ko0[c] + kept_base + kofs[c];
+                out.pages.push_back(p);
+            }
+            for (; t < run.cols[c].size(); t++) {
+                PageOut p = run.cols[c][t];
+                p.offset += acc_len;
+                out.pages.push_back(p);
+            }
+            co.num_pages = (int32_t)out.pages.size() - co.first_page;
+            out.chunks.push_back(co);
+        }
+        acc_len += pages_len_;
+        return KPW_OK;
+    };
     // Non-final batches planned as a whole (no HDFS alignment): every row group's cut first (the
     // speculative passes), then the cuts and the carry go to the caller (on_plan: the next job
     // starts on the other worker), then each row group's exact pass.  Interleaved, the next job
@@ -713,14 +808,25 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     const bool defer = !final_flush && max_cuts <= 0;
     struct PlannedRg { int64_t s, e; std::vector<std::vector<int64_t>> cuts; };
     std::vector<PlannedRg> planned;
+    PlannedRg late{-1, -1, {}};   // lazy_open: the last row group's splice, after on_plan
+    int n_spliced = 0;
+    // KPW_TRACE=1: wall time per phase (page cuts, speculative encodes, row-group checks, splices,
+    // full exact passes); the phases end in host syncs, so the clock brackets their device work
+    const bool tr = getenv("KPW_TRACE") && getenv("KPW_TRACE")[0] == '1';
+    double tph[5] = {0, 0, 0, 0, 0};
+    auto tnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double tm = tr ? tnow() : 0.0;
+    auto lap = [&](int k) { if (tr) { const double t = tnow(); tph[k] += t - tm; tm = t; } };
     while (s0 < (int64_t)ne) {
         int64_t h = std::min<int64_t>((int64_t)ne, s0 + guess);
         int64_t po[2] = {-1, 0};
         for (;;) {
             int rs = mp_cuts(a, s0, h, cuts);
             if (rs) return rs;
+            lap(0);
             rs = mp_pipeline(d_data, d_off, n, hc, s0, h, cuts, run);
             if (rs) return rs;
+            lap(1);
             // header + compressed bytes of every cut page (the open page per column is last),
             // column c's at pb_off[c] (compact: the cut capacity per column is (h - s) / 2 + 2,
             // and a strided table of that size cost a 100+ MB host fill and H2D per row group)
@@ -746,19 +852,39 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
             CK(hipGetLastError());
             CK(xd2h(po, a.out, 16, st));
             CK(xsync(st));
+            lap(2);
             if (po[0] >= 0 || h == (int64_t)ne) break;
             h = std::min<int64_t>((int64_t)ne, s0 + 2 * (h - s0));
         }
         if (po[0] >= 0) {
             const int64_t r = po[0];
             for (auto &v : cuts) v.erase(std::remove_if(v.begin(), v.end(), [r](int64_t x) { return x > r; }), v.end());
-            if (defer) {
+            // Splice (v1): every page before a column's last cut <= r is the speculative pass's,
+            // byte for byte (its cut, ids, bit width and fallback / first-page decisions do not
+            // depend on where the row group ends), so the exact pass encodes only each column's
+            // last page and dictionary page.  A column cut exactly at r (its dictionary page would
+            // have no page to ride with) and the v2 DELTA streams take the whole exact pass.
+            bool splice = splice_on() && !v2_ && planned.empty();
+            for (int c = 0; c < nc && splice; c++) splice = cuts[c].empty() || cuts[c].back() < r;
+            // lazy_open: the records after r are the next job's carry (it plans them from r, so a
+            // cut among them is found there); this row group's splice then runs after on_plan
+            const bool last = lazy_open && lazy_on() && !final_flush && max_cuts <= 0 &&
+                              (uint64_t)((int64_t)ne - r) * per_rec < (uint64_t)T;
+            if (splice && last) {
+                late = PlannedRg{s0, r, {}};
+            } else if (splice) {
+                int rs = append_splice(s0, r);
+                if (rs) return rs;
+                n_spliced++;
+                lap(3);
+            } else if (defer) {
                 planned.push_back(PlannedRg{s0, r, cuts});
             } else {
                 int rs = mp_pipeline(d_data, d_off, n, hc, s0, r, cuts, run);
                 if (rs) return rs;
                 rs = append(s0, r);
                 if (rs) return rs;
+                lap(4);
             }
             guess = std::max<int64_t>(1000, (r - s0) + (r - s0) / 4 + 200);
             mp_last_rg_ = r - s0;
@@ -768,6 +894,10 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
             }
             s0 = r;
             if (max_cuts > 0 && (int32_t)out.rgs.size() >= max_cuts) break;   // re-planned by the caller
+            if (last) {
+                out.open_buffered = -1;
+                break;
+            }
             continue;
         }
         if (final_flush) {   // [s0, ne) was just encoded with its final pages
@@ -784,13 +914,25 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     out.open_records = (int64_t)ne - s0;
     if (final_flush) out.open_buffered = 0;
     if (on_plan) on_plan(out);
+    lap(2);
+    if (late.s >= 0) {   // (the speculative run and cuts of this row group are still in place)
+        int rs = append_splice(late.s, late.e);
+        if (rs) return rs;
+        n_spliced++;
+        lap(3);
+    }
     for (const PlannedRg &g : planned) {   // (defer) the exact passes
         int rs = mp_pipeline(d_data, d_off, n, hc, g.s, g.e, g.cuts, run);
         if (rs) return rs;
         rs = append(g.s, g.e);
         if (rs) return rs;
+        lap(4);
     }
     CK(xsync(st));
+    lap(4);
+    if (tr)
+        fprintf(stderr, "[kpw] multi-page encode: %zu row groups, %d spliced; ms: page cuts %.2f, speculative %.2f, checks %.2f, "
+                        "splices %.2f, exact %.2f\n", out.rgs.size(), n_spliced, tph[0], tph[1], tph[2], tph[3], tph[4]);
     out.d_pages = mp_acc.as<uint8_t>();
     out.pages_len = acc_len;
     pages_dev_ = mp_acc.as<uint8_t>();

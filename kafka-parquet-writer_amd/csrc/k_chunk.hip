@@ -1111,6 +1111,27 @@ __global__ void k_mp_satisfy(ChunkDesc *pg, ChunkDesc *dch, int ndch, const DevC
     if (!D.is_dict) return;
     const DevCol &col = cols[D.col];
     ChunkDesc &P0 = pg[D.first_page];
+    D.dict_all = D.dict_n;
+    if (D.tail_mode == 2) {   // the kept pages are PLAIN: so is the chunk's last page, and no dictionary page
+        for (int p = D.first_page; p < D.first_page + D.npages; p++) pg[p].fallback = 1;
+        D.fallback = 1;
+        P0.dictpage_len = 0;
+        return;
+    }
+    if (D.tail_mode == 1) {   // the kept first page passed isCompressionSatisfying
+        int last = -1;
+        for (int p = D.first_page; p < D.first_page + D.npages; p++) if (!pg[p].fallback) last = p;
+        const uint32_t dn = last >= 0 ? pg[last].dict_n : D.tail_dict_n;
+        if (dn > 0) {
+            D.dict_n = dn;
+            D.fallback = 0;
+            P0.dictpage_len = ent_cum(col, D, ent_rec, ent_boff, dn);
+        } else {
+            D.fallback = 1;
+            P0.dictpage_len = 0;
+        }
+        return;
+    }
     if (!P0.fallback) {
         const uint64_t val = 1 + jobs[P0.id_job].total_bytes;
         if (!(val + P0.dict_bytes < P0.raw_bytes))

@@ -221,6 +221,13 @@ struct ChunkDesc {
     int32_t owner;                 // page: dictionary descriptor index (-1 single-page regime)
     int32_t first_page, npages;    // dictionary descriptor: its pages
     int32_t rl0_len;               // v2: bytes of the width-0 repetition-level stream (layout)
+    // multi-page splice (engine_mp.cpp): an exact pass that re-encodes only each column's last
+    // page reuses the speculative pass's dictionary descriptor
+    uint32_t dict_all;             // dictionary descriptor: K2's entries (k_mp_satisfy then narrows dict_n)
+    uint32_t tail_mode;            // 0: the chunk's first page is in this run; 1: kept first page, dictionary
+                                   // satisfying; 2: kept first page, every page of the chunk PLAIN
+    uint32_t tail_dict_n;          // mode 1: dict_n of the last kept dictionary-encoded page (0: none)
+    uint32_t pad_tail;
 };
 
 // One DELTA_BINARY_PACKED stream (k_delta.hip).

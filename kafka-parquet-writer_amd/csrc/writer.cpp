@@ -189,6 +189,8 @@ struct Job {
     int buf, kind, next;
     int64_t n_exact;                   // EXACT: records [0, n_exact) of the buffer form complete row groups
     uint64_t seq;                      // submission order (= file order)
+    bool lazy;                         // PLANNED from the write path: the open row group's buffered
+                                       // size may be left unknown (Engine::lazy_open)
 };
 
 }  // namespace
@@ -829,8 +831,10 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
         // EXACT jobs are encoded non-final: the GPU planner must cut the same single row group
         // the host size model cut (checked below), so every such row group cross-checks the model
         E.on_plan = on_plan;
+        E.lazy_open = j.lazy;
         const int st = E.encode(B.d, W.offs, (uint64_t)n_enc, j.kind == JOB_FINAL, E.props.block_size, nullptr, out);
         E.on_plan = nullptr;
+        E.lazy_open = false;
         if (st) return plan_fail(st, E.error());
     } else {
         on_plan(out);
@@ -1040,7 +1044,7 @@ static void worker_main(kpw_writer *w, int x)
 }
 
 // Hand the fill buffer to the workers and start filling the next one.
-static int submit(kpw_writer *w, int kind, int64_t n_exact)
+static int submit(kpw_writer *w, int kind, int64_t n_exact, bool exact_open = false)
 {
     if (int st = flush_slot(w)) return st;
     StageBuf &F = w->buf[w->fill];
@@ -1077,7 +1081,7 @@ static int submit(kpw_writer *w, int kind, int64_t n_exact)
             fprintf(stderr, "[kpw] submit job %llu kind=%d new records=%lld (%.0f MiB) at %.1f ms, %d in flight, %d queued\n",
                     (unsigned long long)w->next_seq, kind, (long long)F.ends.size(), (F.len - F.gap) / 1048576.0,
                     now_ms() - w->t_open, w->inflight, (int)w->q.size());
-        w->q.push_back(Job{f, kind, next, n_exact, w->next_seq++});
+        w->q.push_back(Job{f, kind, next, n_exact, w->next_seq++, kind == JOB_PLANNED && !exact_open});
         w->cv.notify_all();
     }
     if (kind == JOB_PLANNED) w->dirty = false;
@@ -1812,9 +1816,14 @@ extern "C" int64_t kpw_writer_data_size(kpw_writer *w)
             }
             return w->last_rg_end + w->model.buffered();
         }
-        if (w->dirty && submit(w, JOB_PLANNED, 0)) return -1;   // encode what is staged (completed row groups flushed)
+        if (w->dirty && submit(w, JOB_PLANNED, 0, true)) return -1;   // encode what is staged (completed row groups flushed)
         if (drain(w)) return -1;
         if (observe_failure(w)) return -1;
+        if (w->open_buffered < 0) {   // the last job left the open row group to the next one: plan it now
+            if (submit(w, JOB_PLANNED, 0, true)) return -1;
+            if (drain(w)) return -1;
+            if (observe_failure(w)) return -1;
+        }
         return w->last_rg_end + w->open_buffered;
     } catch (...) {
         return -1;

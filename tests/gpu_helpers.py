@@ -22,14 +22,14 @@ def to_device(data, offsets):
 
 
 def gpu_encoder_pages(schema, data, offsets, codec=0, block_size=128 * MiB, page_size=128 * MiB, dictionary=True,
-                      writer_version=1, enc=None):
+                      writer_version=1, enc=None, dict_page_size=MiB):
     """Returns (row_groups, [(rg, col, [page dicts with 'body'])]) from the HIP encoder
     (a fresh one, or `enc` to reuse an encoder across batches)."""
     import kpw
     if enc is None:
         enc = kpw.Encoder(kpw.Schema(schema.message_name, schema.columns, schema.proto_class), codec=codec,
                           block_size=block_size, page_size=page_size, enable_dictionary=dictionary,
-                          writer_version=writer_version)
+                          writer_version=writer_version, dictionary_page_size=dict_page_size)
     d, o = to_device(data, offsets)
     info = enc.encode(d.ptr, o.ptr, len(offsets) - 1, final=True)
     blob = enc.pages_bytes()
@@ -68,7 +68,7 @@ def oracle_row_groups(fb):
 def oracle_props(**kw):
     return oracle.make_props(block_size=kw.get("block_size", 128 * MiB), page_size=kw.get("page_size", 128 * MiB),
                              codec=kw.get("codec", 0), enable_dictionary=kw.get("dictionary", True),
-                             writer_version=kw.get("writer_version", 1))
+                             writer_version=kw.get("writer_version", 1), dictionary_page_size=kw.get("dict_page_size", MiB))
 
 
 def compare_pages(schema, data, offsets, **kw):

@@ -24,10 +24,10 @@ MiB = 1024 * 1024
 SCALE = float(os.environ.get("KPW_FULL_SCALE", "1.0"))
 
 
-def _writer_file(schema, data, offs, batch, codec=1):
+def _writer_file(schema, data, offs, batch, codec=1, page_size=128 * MiB):
     import kpw
     pf = kpw.ParquetFile(None, kpw.Schema(schema.message_name, schema.columns, schema.proto_class),
-                         kpw.ParquetProperties(compression_codec_name=codec))
+                         kpw.ParquetProperties(compression_codec_name=codec, page_size=page_size))
     n = len(offs) - 1
     for a in range(0, n, batch):
         b = min(n, a + batch)
@@ -59,6 +59,18 @@ def test_full_size_writer_matches_oracle_per_row_group(kind, n, seed, codec):
     import pyarrow.parquet as pq
     md = pq.ParquetFile(io.BytesIO(fb)).metadata
     assert md.num_rows == n and md.num_columns == len(schema.columns)
+
+
+def test_full_size_multipage_writer_matches_oracle_per_row_group():
+    """bench.py's bulk_multipage leg at full size: C2's 100 M Rec8 records with 1 MiB pages
+    (row groups cut by the speculative passes, exact passes spliced, write-path jobs leaving
+    their open row group to the next job), every row group against the oracle."""
+    n = max(1000, int(100_000_000 * SCALE))
+    data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE02, n)
+    fb = _writer_file(synth.REC8, data, offs, 500_000, 1, page_size=MiB)
+    props = oracle.make_props(block_size=128 * MiB, page_size=MiB, codec=1, enable_dictionary=True)
+    errs = check_row_groups(synth.REC8, data, offs, fb, props)
+    assert not errs, errs[:10]
 
 
 def _c5_partition(p, n, out, errs):

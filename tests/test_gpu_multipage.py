@@ -5,6 +5,7 @@ dictPageSize, isCompressionSatisfying on the first page only, and row groups cut
 check that counts flushed pages by their header + compressed bytes.  Every page byte-identical
 to the CPU oracle (oracle/oracle_core.c colw_account / check_block_size)."""
 import io
+import os
 
 import pyarrow.parquet as pq
 import pytest
@@ -60,6 +61,51 @@ def test_multipage_fallback_mid_chunk():
     fb = oracle.encode_file(synth.SAMPLE, data, offs, oracle.make_props(codec=1, page_size=64 * KiB))
     encs = [p["header"][5][2] for p in pqwalk.pages(fb) if p["col"] == 0 and p["header"][1] == 0]
     assert encs[0] == 2 and encs[-1] == 0, encs   # PLAIN_DICTIONARY first, PLAIN after the fallback
+
+
+# (codec, row-group size, dictPageSize in KiB): for _pairs_records(60000) and 16 KiB pages the
+# oracle's query column crosses dictPageSize in every row group's first page (4), a middle page
+# (24, 70, 160, 240, 256), the last page (258, 404), just after the row-group end (inside the
+# speculative pass's range: 262, 408), or never within a row group (400, 412)
+SPLICE_CASES = [(0, 160, 4), (0, 160, 24), (0, 160, 160), (0, 160, 240), (0, 160, 256), (0, 160, 258), (0, 160, 262),
+                (0, 160, 400), (1, 160, 4), (1, 160, 70), (1, 160, 404), (1, 160, 408), (1, 160, 412), (2, 64, 4),
+                (2, 64, 100), (2, 64, 150), (2, 64, 200)]
+
+
+@pytest.mark.parametrize("codec,rg_kib,dict_kib", SPLICE_CASES, ids=["c%d_rg%dK_d%dK" % c for c in SPLICE_CASES])
+def test_multipage_splice_dictionary_crossing(codec, rg_kib, dict_kib):
+    # many row groups cut inside one batch, so every exact pass but the last is a splice
+    # (engine_mp.cpp: only each column's last page and its dictionary page re-encoded): the
+    # dictionary crosses dictPageSize in the first page (every page PLAIN), in a middle page,
+    # in the last page of the row group, after its end (the last page keeps its ids), or never
+    data, offs = _pairs_records(60000)
+    kw = dict(codec=codec, block_size=rg_kib * KiB, page_size=16 * KiB, dict_page_size=dict_kib * KiB)
+    fb = oracle.encode_file(synth.SAMPLE, data, offs, gh.oracle_props(**kw))
+    assert len(gh.oracle_row_groups(fb)) >= 3
+    errs = gh.compare_to_file(synth.SAMPLE, data, offs, fb, **kw)[0]
+    assert not errs, "\n".join(errs[:12])
+
+
+@pytest.mark.parametrize("name,kind,param,n", CASES, ids=[c[0] for c in CASES])
+def test_multipage_splice_gzip(name, kind, param, n):
+    # the splice with GZIP members (kept pages copied, the last page and dictionary page deflated)
+    schema = synth.SCHEMAS[kind]
+    data, offs = synth.generate(kind, 0xC0FFEE44 + kind, n, param=param)
+    errs = gh.compare_pages(schema, data, offs, codec=2, block_size=128 * KiB, page_size=4 * KiB)
+    assert not errs, "\n".join(errs[:12])
+
+
+@pytest.mark.parametrize("mode", ["file", "data_size"])
+def test_multipage_lazy_open_jobs(mode):
+    # write-path jobs of ~6 MB (KPW_EAGER_MB=4, in a child process: the knob is read once) stop
+    # after their last row-group cut and carry the rest to the next job without planning it
+    # (Engine::lazy_open); getDataSize after a batch then plans the open row group on demand
+    import subprocess
+    import sys
+    env = dict(os.environ, KPW_EAGER_MB="4")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "lazy_open_child.py"), mode, "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "LAZY_OPEN_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
 
 
 @pytest.mark.parametrize("page_size", [64, 300])
