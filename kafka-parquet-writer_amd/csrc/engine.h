@@ -140,6 +140,8 @@ public:
     // encoding them to look for a cut; open_buffered is then -1 (unknown).  The writer's
     // write-path jobs only: getDataSize plans the open row group when it needs the size.
     bool lazy_open = false;
+    // Multi-page: records of the last row group an engine of this schema and properties cut (0: none yet)
+    int64_t rg_records_hint() const;
     std::vector<ColInfo> cols;
     kpw_props props{};
     std::string message_name, proto_class;

@@ -656,6 +656,13 @@ static uint64_t horizon_key(const std::vector<ColInfo> &cols, const kpw_props &p
     return h;
 }
 
+int64_t Engine::rg_records_hint() const
+{
+    std::lock_guard<std::mutex> g(g_horizon_mu);
+    auto it = g_horizon.find(horizon_key(cols, props));
+    return it == g_horizon.end() ? 0 : it->second;
+}
+
 int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                       const std::vector<DevCol> &hc, uint64_t gend_stride, uint64_t ev_stride, BatchOut &out)
 {
@@ -866,10 +873,10 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
             // have no page to ride with) and the v2 DELTA streams take the whole exact pass.
             bool splice = splice_on() && !v2_ && planned.empty();
             for (int c = 0; c < nc && splice; c++) splice = cuts[c].empty() || cuts[c].back() < r;
-            // lazy_open: the records after r are the next job's carry (it plans them from r, so a
-            // cut among them is found there); this row group's splice then runs after on_plan
-            const bool last = lazy_open && lazy_on() && !final_flush && max_cuts <= 0 &&
-                              (uint64_t)((int64_t)ne - r) * per_rec < (uint64_t)T;
+            // lazy_open: fewer records after r than this row group holds are the next job's carry
+            // (it plans them from r, so a cut among them is found there); this row group's
+            // splice then runs after on_plan
+            const bool last = lazy_open && lazy_on() && !final_flush && max_cuts <= 0 && (int64_t)ne - r < r - s0;
             if (splice && last) {
                 late = PlannedRg{s0, r, {}};
             } else if (splice) {

@@ -94,6 +94,17 @@ uint64_t eager_job_bytes()
     return b;
 }
 
+// Multi-page writers (pageSize < blockSize) submit eager jobs while the workers are busy too, as
+// long as fewer than this many jobs are queued (KPW_MP_EAGER_QUEUE, default 3; 0: as single-page).
+// A multi-page job's row-group cuts need its speculative encodes, so jobs run one after another
+// up to their cuts; jobs grown to the full stage size (1 GiB) carry open row groups larger than
+// the buffers' gap (a rebuild per carry) and bigger page buffers.
+int mp_eager_queue()
+{
+    static const int v = [] { const char *e = getenv("KPW_MP_EAGER_QUEUE"); return e ? atoi(e) : 3; }();
+    return v;
+}
+
 // Writes of more records than this leave the per-record size model (bulk path).
 uint64_t model_max_batch()
 {
@@ -456,20 +467,6 @@ static int grow_fill(kpw_writer *w, uint64_t bytes)
 }
 
 // Record boundaries of a buffer's records: carried then appended ([n+1] absolute offsets).
-static size_t nbounds(const StageBuf &B) { return (B.carry.empty() ? 1 : B.carry.size()) + B.ends.size(); }
-static void boundaries(const StageBuf &B, uint64_t *hb)
-{
-    size_t k = 0;
-    if (B.carry.empty()) hb[k++] = B.gap;
-    else { memcpy(hb, B.carry.data(), B.carry.size() * 8); k = B.carry.size(); }
-    if (!B.ends.empty()) memcpy(hb + k, B.ends.data(), B.ends.size() * 8);
-}
-static void boundaries(const StageBuf &B, std::vector<uint64_t> &hb)
-{
-    hb.resize(nbounds(B));
-    boundaries(B, hb.data());
-}
-
 // fn(a, b) over [0, n) split over up to 4 host threads (for large n)
 template <class Fn>
 static void par_for(uint64_t n, Fn fn)
@@ -483,6 +480,24 @@ static void par_for(uint64_t n, Fn fn)
     for (unsigned i = 1; i < t; i++) th[i] = std::thread(fn, std::min(n, per * i), std::min(n, per * (i + 1)));
     fn(0, std::min(n, per));
     for (unsigned i = 1; i < t; i++) th[i].join();
+}
+
+static size_t nbounds(const StageBuf &B) { return (B.carry.empty() ? 1 : B.carry.size()) + B.ends.size(); }
+// (a job's worker runs this between the previous job's cuts and its own start: 7 M records are
+// 56 MB into pinned memory, ~5 ms on one thread, so the appended part is copied on up to 4)
+static void boundaries(const StageBuf &B, uint64_t *hb)
+{
+    size_t k = 0;
+    if (B.carry.empty()) hb[k++] = B.gap;
+    else { memcpy(hb, B.carry.data(), B.carry.size() * 8); k = B.carry.size(); }
+    const uint64_t *src = B.ends.data();
+    uint64_t *dst = hb + k;
+    par_for(B.ends.size(), [=](uint64_t a, uint64_t b) { memcpy(dst + a, src + a, (b - a) * 8); });
+}
+static void boundaries(const StageBuf &B, std::vector<uint64_t> &hb)
+{
+    hb.resize(nbounds(B));
+    boundaries(B, hb.data());
 }
 
 // ---------------------------------------------------------------- workers
@@ -1534,6 +1549,26 @@ static int write_bulk(kpw_writer *w, const uint8_t *data, const uint64_t *offset
 // never has to grow (grow_fill drains the pipeline and copies the buffer: C3's 690 MB poll
 // batches did that on every second batch).  Batches that fit are appended whole, as before
 // (jobs end at the first batch that reaches the job size).
+// Multi-page writers: appended records per eager job, about one row group's (the last one an
+// engine of this schema and properties cut, +2 %), so a job cuts one row group and carries a few
+// records; a byte or batch-granular size lets the carry grow by the difference every job until it
+// outgrows the buffers' gap.  0: no target (single-page, no row group cut yet, or turned off).
+static uint64_t mp_job_records(kpw_writer *w)
+{
+    if (mp_eager_queue() <= 0 || !eager_job_bytes() || !w->eng.multi_page()) return 0;
+    const int64_t R = w->eng.rg_records_hint();
+    return R > 0 ? (uint64_t)((double)R * 1.02) : 0;
+}
+
+// An eager job may be submitted now: an encode worker is idle and nothing is queued (multi-page:
+// fewer than mp_eager_queue() jobs are queued).
+static bool eager_go(kpw_writer *w)
+{
+    std::lock_guard<std::mutex> g(w->mu);
+    if (mp_eager_queue() > 0 && w->eng.multi_page()) return (int)w->q.size() < mp_eager_queue();
+    return w->q.empty() && w->inflight < w->nworkers;
+}
+
 static int write_bulk_split(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n)
 {
     while (n) {
@@ -1542,6 +1577,16 @@ static int write_bulk_split(kpw_writer *w, const uint8_t *data, const uint64_t *
         const uint64_t room = F.cap > F.len + 64 ? F.cap - F.len - 64 : 0;
         // largest k with offsets[k] - offsets[0] <= room
         uint64_t k = (uint64_t)(std::upper_bound(offsets, offsets + n + 1, offsets[0] + room) - offsets) - 1;
+        const uint64_t ke = mp_job_records(w);
+        if (ke && F.ends.size() < ke && F.ends.size() + std::min(k, n) > ke) {   // the job's row group ends in this batch
+            const uint64_t m = ke - F.ends.size();
+            if (int st = write_bulk(w, data, offsets, m)) return st;
+            offsets += m;
+            n -= m;
+            if (eager_go(w))
+                if (int st = submit(w, JOB_PLANNED, 0)) return st;
+            continue;
+        }
         if (k >= n) return write_bulk(w, data, offsets, n);
         if (k == 0 && used == 0) k = 1;   // one record larger than a job: the buffer grows
         if (k)
@@ -1738,14 +1783,9 @@ static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offse
     if (!w->model_on) {
         const uint64_t used = F.len - F.gap;
         if (used >= stage_flush_bytes()) return submit(w, JOB_PLANNED, 0);
-        if (eager_job_bytes() && used >= eager_job_bytes()) {
-            bool idle;
-            {
-                std::lock_guard<std::mutex> g(w->mu);
-                idle = w->q.empty() && w->inflight < w->nworkers;
-            }
-            if (idle) return submit(w, JOB_PLANNED, 0);
-        }
+        const uint64_t ke = mp_job_records(w);
+        if (ke ? F.ends.size() >= ke : eager_job_bytes() && used >= eager_job_bytes())
+            if (eager_go(w)) return submit(w, JOB_PLANNED, 0);
     }
     return KPW_OK;
 }
