@@ -55,9 +55,6 @@ constexpr uint32_t SG_LITCOPY = 128;     // longer literals are copied by the wh
 #ifndef SG_SW
 #define SG_SW 4u                 // sort scatter: waves (each owns the hashes h % SG_SW)
 #endif
-#ifndef SG_RADIX
-#define SG_RADIX 0               // sort: 1 = two stable 7-bit digit passes with wave ballots (A/B), 0 = counting sort, LDS atomics
-#endif
 
 constexpr uint32_t SG_NOMATCH = 0xffff;  // cand[]: the table entry's 4 bytes differ (positions < 65521)
 
@@ -493,76 +490,6 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         }
         __syncthreads();
         PMARK(8);
-        uint64_t bf = 0;
-#if SG_RADIX
-        // Stable LSD radix sort of the positions by hash, two 7-bit digits, no returning atomics
-        // (the counting sort's scatter was bound by them, ~2.8 cycles per active lane): wave w
-        // takes a contiguous chunk of the entries; per 64 of them a digit's lanes find each
-        // other with 7 ballots, the lowest one bumps the wave's counter of that digit (the
-        // lanes of one instruction touch distinct counters: plain LDS read-modify-writes), and
-        // a scan in (digit, wave) order gives every wave its output range per digit.  Pass 0
-        // reads the hashes from the staged fragment and writes hash << 16 | position (into the
-        // key array, written later); pass 1 writes the sorted positions and their hashes (into
-        // the copy records, used later), from which the bucket starts follow.
-        {
-            uint32_t *wcnt = S.a.su.cnt;   // [wave * 128 + digit] (a wave's lanes hit 32 banks)
-            const uint32_t C = ((npos + SG_W - 1) / SG_W + 63) & ~63u;
-            const uint32_t b_lo = w * C, b_hi = (w + 1) * C < npos ? (w + 1) * C : npos;
-            __attribute__((address_space(1))) uint32_t *ping = (__attribute__((address_space(1))) uint32_t *)G.key4;
-            sgg_u16 *sig = (sgg_u16 *)G.sig4;
-            const uint64_t lt = (1ull << lane) - 1;
-#pragma unroll 1
-            for (uint32_t pass = 0; pass < 2; pass++) {
-                const uint32_t dsh = 16 + 7 * pass;
-                for (uint32_t i = t; i < 128 * SG_W; i += SG_T) wcnt[i] = 0;
-                __syncthreads();
-#pragma unroll 1
-                for (uint32_t ph = 0; ph < 2; ph++) {   // 0 count, 1 scatter
-#pragma unroll 2
-                    for (uint32_t b0 = b_lo; b0 < b_hi; b0 += 64) {
-                        const uint32_t i = b0 + lane;
-                        const bool v = i < b_hi;
-                        uint32_t e = 0;
-                        if (v) e = pass ? ping[i] : (sg_hash(lds_ld32(S, i + 1), shift) << 16) | (i + 1);
-                        const uint32_t d = (e >> dsh) & 127u;
-                        uint64_t m = __ballot(v);
-#pragma unroll
-                        for (int k = 0; k < 7; k++) {
-                            const uint64_t bk = __ballot((d >> k) & 1u);
-                            m &= ((d >> k) & 1u) ? bk : ~bk;
-                        }
-                        const bool lead = v && !(m & lt);
-                        uint32_t *cp = &wcnt[w * 128 + d];
-                        if (ph == 0) {
-                            if (lead) *cp += (uint32_t)__popcll(m);
-                        } else {
-                            const uint32_t base = v ? *cp : 0u;
-                            if (v) {
-                                const uint32_t dst = base + (uint32_t)__popcll(m & lt);
-                                if (pass == 0) ping[dst] = e;
-                                else sig[sig_slot(dst)] = (uint16_t)e;
-                            }
-                            if (lead) *cp = base + (uint32_t)__popcll(m);
-                        }
-                    }
-                    __syncthreads();
-                    if (ph == 0) {   // exclusive scan of the counters in (digit, wave) order
-                        const uint32_t k0 = 2 * t, k1 = 2 * t + 1;   // (digit k / SG_W, wave k % SG_W)
-                        const uint32_t a0 = (k0 % SG_W) * 128 + k0 / SG_W, a1 = (k1 % SG_W) * 128 + k1 / SG_W;
-                        const uint32_t c0 = wcnt[a0], c1 = wcnt[a1];
-                        uint32_t tot;
-                        const uint32_t ex = sg_scan_excl(c0 + c1, S, &tot);
-                        wcnt[a0] = ex;
-                        wcnt[a1] = ex + c0;
-                        __syncthreads();
-                    }
-                }
-                __threadfence_block();
-                __syncthreads();
-            }
-        }
-        PMARK(11);
-#else
 #pragma unroll 8
         for (uint32_t j = 0; j < SG_SEG; j++) {
             const uint32_t p = j * SG_T + t;
@@ -570,6 +497,7 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         }
         __syncthreads();
         PMARK(9);
+        uint64_t bf = 0;
         {   // exclusive scan of the counters: thread t owns counter words [t*wpt, t*wpt + wpt)
             const uint32_t words = tsize / 2, wpt = (words + SG_T - 1) / SG_T, w0 = t * wpt;
             uint32_t loc = 0;
@@ -617,31 +545,11 @@ __device__ __forceinline__ void k_snappy_seg_t(const SnappyArgs &a)
         __threadfence_block();
         __syncthreads();
         PMARK(11);
-#endif
         // order check, bucket-start bits -> global (every round reads its 64 entries and bits)
         int bad = 0;
         {
             const uint32_t i0 = t * SG_SEG;
-#if SG_RADIX
-            {   // bucket starts: entry i starts one when its hash differs from entry i - 1's
-                sgg_cu4 *hp = (sgg_cu4 *)(G.sig4 + t * 8);
-                uint32_t hprev = i0 > 0 && i0 <= npos ? sg_hash(lds_ld32(S, ((sgg_cu16 *)G.sig4)[i0 - 1]), shift) : 0xffffffffu;
-                bf = 0;
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const sg_u32x4 pv = hp[q];
-#pragma unroll
-                    for (int e = 0; e < 8; e++) {
-                        const uint32_t j = q * 8 + e;
-                        const uint32_t hh = sg_hash(lds_ld32(S, (pv[e >> 1] >> ((e & 1) * 16)) & 0xffffu), shift);
-                        if (i0 + j < npos && hh != hprev) bf |= 1ull << j;
-                        hprev = hh;
-                    }
-                }
-            }
-#else
             bf = S.ibits[t];
-#endif
             uint32_t prevp = (i0 > 0 && i0 <= npos) ? ((sgg_cu16 *)G.sig4)[sig_slot(i0 - 1)] : 0;
             // with the check, the 4 bytes at every sorted entry's position, from the staged
             // fragment: the rounds compare a position with its candidate there, so the parse's
