@@ -701,6 +701,8 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     a.gend_stride = gend_stride;
     a.sp = mp_spp.as<const uint64_t *>(); a.next_rg_size = T;
     a.col_bstream = mp_bstream.as<int32_t>(); a.streams = d_streams.as<PlanStream>(); a.v2 = v2_ ? 1 : 0;
+    static const int str_spec = [] { const char *e = getenv("KPW_PAGE_CUT_SPEC"); return e && e[0] == '0' ? 0 : 1; }();
+    a.str_spec = str_spec;
     if (opt_idx_.empty() && !(v2_ && !bool_idx_.empty())) { a.E8 = nullptr; a.ev = nullptr; a.gend = nullptr; }   // no planner streams
 
     if (probe_) {   // probe_pages: the open row group's prefix [0, ne); its page cuts from the GPU planner

@@ -698,11 +698,85 @@ __device__ __forceinline__ uint64_t col_dl_bytes(const PageCutArgs &a, const MpC
 // record x the page holds vc = x - q + 1 values; a check (vc > next) cuts when memSize >
 // pageSize (next = vc / 2, count restarts), else next = (int)(vc + (float)vc * pageSize /
 // memSize) / 2 + 1 in Java float arithmetic.
+// the non-cutting branch of the page check: next = (int)(vc + (float)vc * pageSize / memSize) / 2 + 1
+__device__ __forceinline__ int32_t pc_next(int32_t vc, int64_t page_size, uint64_t mem)
+{
+    float t = __fmul_rn((float)vc, (float)page_size);
+    t = __fdiv_rn(t, (float)mem);
+    return java_f2i(__fadd_rn((float)vc, t)) / 2 + 1;
+}
+__device__ __forceinline__ int64_t shfl64(int64_t v, int k)
+{
+    const int lo = __shfl((int)(uint32_t)v, k, 64), hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), k, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// A REQUIRED BYTE_ARRAY column's checks (memSize = sp[x + 1] - sp[q], one dependent load each;
+// ~1900 per C2 row group at 1 MiB pages) in speculative batches: lane k follows the chain k
+// checks ahead with memSize predicted from the page's bytes per value so far and loads sp at
+// its check, all lanes in one round trip; the chain then takes the loaded values as long as
+// the predicted positions are the actual ones (lane 0's always is: at least one check per trip)
+constexpr int PC_SPEC = 8;
+__device__ void page_cuts_str(const PageCutArgs &a, const MpColInfo &I, int c)
+{
+    const int lane = (int)threadIdx.x;
+    int64_t q = a.s;
+    int32_t next = 100;
+    uint32_t nc = 0;
+    uint64_t sq = I.sp[q];
+    double bpv;   // bytes per value of the open page (prediction only)
+    {
+        const int64_t r = a.h < q + 4096 ? a.h : q + 4096;
+        bpv = r > q ? (double)(I.sp[r] - sq) / (double)(r - q) : 1.0;
+    }
+    for (;;) {
+        int64_t xk = -1;
+        if (lane < PC_SPEC) {
+            int64_t pq = q;
+            int32_t pn = next;
+            for (int j = 0;; j++) {
+                const int64_t x = pq + (int64_t)pn;
+                if (x >= a.h) break;
+                if (j == lane) { xk = x; break; }
+                const int32_t vc = pn + 1;
+                const uint64_t memp = (uint64_t)(bpv * (double)vc) + 1;
+                if (memp > (uint64_t)a.page_size) { pq = x + 1; pn = vc / 2; }
+                else pn = pc_next(vc, a.page_size, memp);
+            }
+        }
+        const uint64_t val = xk >= 0 ? I.sp[xk + 1] : 0;
+        bool done = false;
+        for (int k = 0; k < PC_SPEC; k++) {
+            const int64_t x = q + (int64_t)next;
+            if (x >= a.h) { done = true; break; }
+            if (shfl64(xk, k) != x) break;
+            const uint64_t mem = (uint64_t)shfl64((int64_t)val, k) - sq;
+            const int32_t vc = next + 1;
+            if (mem > (uint64_t)a.page_size) {
+                if (lane == 0) {
+                    if (nc < a.cap) a.cuts[(uint64_t)c * a.cap + nc] = x + 1;
+                    else atomicOr(a.overflow, 1);
+                }
+                nc++;
+                next = vc / 2;
+                q = x + 1;
+                sq += mem;
+            } else {
+                next = pc_next(vc, a.page_size, mem);
+            }
+            if (mem) bpv = (double)mem / (double)vc;
+        }
+        if (done) break;
+    }
+    if (lane == 0) a.ncuts[c] = nc < a.cap ? nc : a.cap;
+}
+
 __global__ void __launch_bounds__(64) k_page_cuts(PageCutArgs a)
 {
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    if (c >= a.ncols) return;
+    const int c = blockIdx.x;   // one wave per column: a column's chain waits only for its own loads
     const MpColInfo I = mp_col_info(a, c);
+    if (I.phys == 6 && I.kdl < 0 && a.str_spec) { page_cuts_str(a, I, c); return; }
+    if (threadIdx.x) return;
     Walker w, wb;
     int64_t q = a.s;
     walker_init(w, q);
@@ -977,7 +1051,7 @@ void launch_str_sizes(const DevCol *cols, int c, uint64_t n, uint32_t *sz, hipSt
 void launch_page_cuts(const PageCutArgs &a, hipStream_t s)
 {
     if (a.v2) hipLaunchKernelGGL(k_page_cuts_v2, dim3(1), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(k_page_cuts, dim3((a.ncols + 63) / 64), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_page_cuts, dim3(a.ncols), dim3(64), 0, s, a);
 }
 void launch_plan_mp(const PageCutArgs &a, hipStream_t s)
 {

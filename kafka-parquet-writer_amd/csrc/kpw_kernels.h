@@ -175,7 +175,7 @@ struct PageCutArgs {
     const int32_t *col_bstream;    // per column: its boolean value stream (E/gend index) or -1
     const PlanStream *streams;     // the planner streams (bits / length of the boolean ones)
     int32_t v2;
-    int32_t pad2;
+    int32_t str_spec;              // k_page_cuts: speculative batches for REQUIRED BYTE_ARRAY columns (KPW_PAGE_CUT_SPEC=0: off)
 };
 void launch_str_sizes(const DevCol *cols, int c, uint64_t n, uint32_t *sz, hipStream_t s);
 void launch_page_cuts(const PageCutArgs &a, hipStream_t s);   // v1 per column, v2 per store
