@@ -380,6 +380,7 @@ int Engine::plan_inputs(const std::vector<DevCol> &hc, uint64_t ne, uint64_t nwo
 int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
                    hipStream_t user_stream, BatchOut &out)
 {
+    t_encode_in_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
     const int st = encode_impl(d_data, d_off, n, final_flush, next_rg_size, user_stream, out);
     if (st) return st;
     // the single-pass scans count a look-back that waited past its bound (kpw_lookback.h):

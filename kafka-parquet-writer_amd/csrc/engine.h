@@ -217,7 +217,8 @@ private:
                     std::vector<RleJob> &pj);
     // multi-page regime (engine_mp.cpp)
     bool mp_ = false;
-    int64_t mp_last_rg_ = 0;           // records of the last row group the multi-page path cut (horizon hint)
+    int64_t mp_last_rg_ = 0;
+    double t_encode_in_ = 0.0;             // steady clock (ms) at the last encode() entry (KPW_TRACE)           // records of the last row group the multi-page path cut (horizon hint)
     bool probe_ = false;                 // encode() is a probe_pages call
     std::vector<int32_t> probe_npages_;
     const std::vector<char> *probe_mask_ = nullptr;

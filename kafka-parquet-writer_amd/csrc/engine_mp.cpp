@@ -825,6 +825,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     double tph[5] = {0, 0, 0, 0, 0};
     auto tnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double tm = tr ? tnow() : 0.0;
+    const double t_pre = tr ? tm - t_encode_in_ : 0.0;   // decode, planner inputs, size prefixes
     auto lap = [&](int k) { if (tr) { const double t = tnow(); tph[k] += t - tm; tm = t; } };
     while (s0 < (int64_t)ne) {
         int64_t h = std::min<int64_t>((int64_t)ne, s0 + guess);
@@ -940,8 +941,8 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
     CK(xsync(st));
     lap(4);
     if (tr)
-        fprintf(stderr, "[kpw] multi-page encode: %zu row groups, %d spliced; ms: page cuts %.2f, speculative %.2f, checks %.2f, "
-                        "splices %.2f, exact %.2f\n", out.rgs.size(), n_spliced, tph[0], tph[1], tph[2], tph[3], tph[4]);
+        fprintf(stderr, "[kpw] multi-page encode: %zu row groups, %d spliced; ms: decode + inputs %.2f, page cuts %.2f, speculative %.2f, "
+                        "checks %.2f, splices %.2f, exact %.2f\n", out.rgs.size(), n_spliced, t_pre, tph[0], tph[1], tph[2], tph[3], tph[4]);
     out.d_pages = mp_acc.as<uint8_t>();
     out.pages_len = acc_len;
     pages_dev_ = mp_acc.as<uint8_t>();

@@ -194,6 +194,11 @@ struct StageBuf {
     int64_t first_new_global = 0;      // file record index of the first appended record
     int state = BUF_FREE;
     hipEvent_t copied = nullptr;       // recorded on the copy stream after the last append
+    // the appended records' lengths, narrowed ahead of the job by a waiting worker (prep_lengths):
+    // they do not depend on the carried records, which are known only at the previous job's cuts
+    PinnedBuf lp;
+    int lp_width = 0;                  // bytes per length
+    int lp_state = 0;                  // 0 not prepared, 1 being prepared, 2 ready (under kpw_writer::mu)
 };
 
 struct Job {
@@ -361,8 +366,8 @@ static int acquire_fill(kpw_writer *w)
     {
         std::unique_lock<std::mutex> lk(w->mu);
         for (;;) {
-            for (int i = 0; i < kpw_writer::kBufs; i++)
-                if (w->buf[i].state == BUF_FREE) { k = i; break; }
+            for (int i = 0; i < kpw_writer::kBufs; i++)   // (not while a worker still reads its lengths)
+                if (w->buf[i].state == BUF_FREE && w->buf[i].lp_state != 1) { k = i; break; }
             if (k >= 0 || w->fatal_st) break;
             w->cv.wait(lk);
         }
@@ -387,6 +392,7 @@ static int acquire_fill(kpw_writer *w)
     b.carry_in_store = false;
     b.ends.clear();
     b.ncarry_expected = 0;
+    b.lp_state = 0;
     b.first_new_global = w->num_records;
     w->fill = k;
     w->fill_gen++;
@@ -492,6 +498,8 @@ static void boundaries(const StageBuf &B, uint64_t *hb)
     else { memcpy(hb, B.carry.data(), B.carry.size() * 8); k = B.carry.size(); }
     const uint64_t *src = B.ends.data();
     uint64_t *dst = hb + k;
+    static const bool par = [] { const char *e = getenv("KPW_PAR_BOUNDS"); return !(e && e[0] == '0'); }();   // (A/B)
+    if (!par) { memcpy(dst, src, B.ends.size() * 8); return; }
     par_for(B.ends.size(), [=](uint64_t a, uint64_t b) { memcpy(dst + a, src + a, (b - a) * 8); });
 }
 static void boundaries(const StageBuf &B, std::vector<uint64_t> &hb)
@@ -540,8 +548,8 @@ static bool gap_adapt()
 
 // Place records [hb[i0], hb[i1]) of buffer `src` in front of buffer `dst`'s appended records
 // (on stream s).
-static int place_carry(kpw_writer *w, const StageBuf &src, const uint64_t *hb, size_t i0, size_t i1, StageBuf &dst,
-                       hipStream_t s)
+template <class HB>
+static int place_carry(kpw_writer *w, const StageBuf &src, const HB &hb, size_t i0, size_t i1, StageBuf &dst, hipStream_t s)
 {
     const uint64_t b0 = hb[i0], c = hb[i1] - b0;
     uint64_t at;
@@ -778,6 +786,76 @@ static int upload_offsets(Worker &W, size_t count, hipStream_t s)
     }
 }
 
+// KPW_PREP_LENGTHS=0: every job narrows its record lengths itself, after its turn (A/B)
+static bool prep_on()
+{
+    static const bool on = [] { const char *e = getenv("KPW_PREP_LENGTHS"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
+// A job's record boundaries without copying them: the carried ones, then the appended ends.
+struct HostBounds {
+    const uint64_t *carry;   // carried boundaries (nc1 of them), or null: one boundary, the gap
+    size_t nc1;
+    uint64_t gap;
+    const uint64_t *ends;
+    uint64_t operator[](size_t i) const { return i < nc1 ? (carry ? carry[i] : gap) : ends[i - nc1]; }
+};
+
+// Lengths of B's appended records (ends[k] - ends[k - 1], the first from the gap) at the
+// narrowest of 1 / 2 bytes that holds them (0: wider lengths, the job's own pass handles them).
+static void prep_lengths(StageBuf &B)
+{
+    const size_t n = B.ends.size();
+    B.lp_width = 0;
+    if (!n || B.lp.ensure(n * 2 + 64)) return;
+    const uint64_t *e = B.ends.data();
+    const uint64_t g = B.gap;
+    for (int width = 1; width <= 2; width++) {
+        std::atomic<uint64_t> all_or{0};
+        auto run = [&](auto *len) {
+            par_for(n, [=, &all_or](uint64_t a, uint64_t b) {
+                uint64_t m = 0, prev = a ? e[a - 1] : g;
+                for (uint64_t i = a; i < b; i++) {
+                    const uint64_t d = e[i] - prev;
+                    prev = e[i];
+                    m |= d;
+                    len[i] = (decltype(+len[0]))d;
+                }
+                all_or.fetch_or(m, std::memory_order_relaxed);
+            });
+        };
+        if (width == 1) run((uint8_t *)B.lp.p); else run((uint16_t *)B.lp.p);
+        const uint64_t o = all_or.load();
+        if (o <= (width == 1 ? 0xffull : 0xffffull)) { B.lp_width = width; return; }
+        if (o > 0xffff) return;
+    }
+}
+
+// upload_offsets for a job whose appended records' lengths were prepared: the carried records'
+// lengths are narrowed here (a few), both parts go up in two copies.  Returns 1 when it cannot
+// (no preparation, wider lengths, a forced width): the caller takes upload_offsets.
+static int upload_offsets_prepped(Worker &W, const StageBuf &B, const HostBounds &hb, size_t count, hipStream_t s)
+{
+    const size_t nc1 = hb.nc1, nnew = count > nc1 ? count - nc1 : 0;
+    if (B.lp_width == 0 || W.len_width != 1 || nnew == 0 || nnew > B.ends.size() || hb[0] >= (1ull << 32)) return 1;
+    uint64_t o = 0;
+    for (size_t i = 1; i < nc1; i++) o |= hb[i] - hb[i - 1];
+    const int width = std::max(B.lp_width, o <= 0xff ? 1 : o <= 0xffff ? 2 : 4);
+    if (width != B.lp_width) return 1;
+    if (W.h_len.ensure(nc1 * width) || W.d_len.ensure(count * width + 64) || W.d_off.ensure((count + 1) * 8)) return KPW_ERR_NOMEM;
+    if (width == 1) { uint8_t *l = W.h_len.p; l[0] = 0; for (size_t i = 1; i < nc1; i++) l[i] = (uint8_t)(hb[i] - hb[i - 1]); }
+    else { uint16_t *l = (uint16_t *)W.h_len.p; l[0] = 0; for (size_t i = 1; i < nc1; i++) l[i] = (uint16_t)(hb[i] - hb[i - 1]); }
+    if (hipMemcpyAsync(W.d_len.p, W.h_len.p, nc1 * width, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(W.d_len.as<uint8_t>() + nc1 * width, B.lp.p, nnew * width, hipMemcpyHostToDevice, s) != hipSuccess)
+        return KPW_ERR_DEVICE;
+    launch_prefix_narrow(W.d_len.p, width, hb[0], count, W.d_off.as<uint64_t>(), &W.scan.sc, s);
+    if (W.scan.sc.failed) { W.scan.sc.failed = false; return KPW_ERR_NOMEM; }
+    if (hipGetLastError() != hipSuccess) return KPW_ERR_DEVICE;
+    W.offs = W.d_off.as<uint64_t>() + 1;   // P[k + 1] = boundary k
+    return KPW_OK;
+}
+
 static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
 {
     Worker &W = w->wk[x];
@@ -785,12 +863,18 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
     StageBuf &B = w->buf[j.buf];
     hipStream_t s = E.stream;
     bool planned = false;
+    const double t_in = trace_on() ? now_ms() : 0.0;
+    double t_planned = 0.0, t_up = 0.0;
     auto plan_fail = [&](int st, const std::string &m) {
         set_fatal(w, st, m);
         return st;
     };
     // the previous job's carried records (and a carry_store it filled) come first
     if (prev_carry && hipStreamWaitEvent(s, prev_carry, 0) != hipSuccess) return plan_fail(KPW_ERR_DEVICE, "stream wait failed");
+    {   // a worker may still be preparing this buffer's lengths (it reads B.ends)
+        std::unique_lock<std::mutex> lk(w->mu);
+        w->cv.wait(lk, [&] { return B.lp_state != 1; });
+    }
     if (int st = materialize(w, B, s)) return plan_fail(st, "stage buffer rebuild failed");
     bool after_invalid;
     {
@@ -798,11 +882,9 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
         after_invalid = w->invalid_seen;
     }
     if (after_invalid) { B.ends.clear(); B.len = B.gap; }   // records behind an invalid one are never written
-    // boundaries straight into the pinned offset buffer (also the carry bookkeeping below)
     const size_t nb = nbounds(B);
-    if (W.h_off.ensure(nb * 8)) return plan_fail(KPW_ERR_NOMEM, "offset staging allocation failed");
-    uint64_t *hb = (uint64_t *)W.h_off.p;
-    boundaries(B, hb);
+    const HostBounds hb{B.carry.empty() ? nullptr : B.carry.data(), B.carry.empty() ? (size_t)1 : B.carry.size(), B.gap,
+                        B.ends.data()};
     const int64_t nrec = (int64_t)nb - 1;
     const int64_t ncarry = B.carry.empty() ? 0 : (int64_t)B.carry.size() - 1;
     const int64_t n_enc = j.kind == JOB_EXACT ? std::min<int64_t>(j.n_exact, nrec) : nrec;
@@ -838,11 +920,19 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
         w->last_carry_ev = W.carry_ev;
         w->plan_seq = j.seq + 1;
         planned = true;
+        if (trace_on()) t_planned = now_ms();
         w->cv.notify_all();
     };
     BatchOut out;
     if (n_enc > 0) {
-        if (int st2 = upload_offsets(W, (size_t)n_enc + 1, s)) return plan_fail(st2, "H2D of offsets failed");
+        int st2 = B.lp_state == 2 && !after_invalid ? upload_offsets_prepped(W, B, hb, (size_t)n_enc + 1, s) : 1;
+        if (st2 == 1) {   // boundaries into the pinned offset buffer, lengths narrowed here
+            if (W.h_off.ensure(nb * 8)) return plan_fail(KPW_ERR_NOMEM, "offset staging allocation failed");
+            boundaries(B, (uint64_t *)W.h_off.p);
+            st2 = upload_offsets(W, (size_t)n_enc + 1, s);
+        }
+        if (st2) return plan_fail(st2, "H2D of offsets failed");
+        if (trace_on()) t_up = now_ms();
         // EXACT jobs are encoded non-final: the GPU planner must cut the same single row group
         // the host size model cut (checked below), so every such row group cross-checks the model
         E.on_plan = on_plan;
@@ -890,10 +980,11 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
     const double tq = trace_on() ? now_ms() : 0.0;
     if (int st = append_job(w, W, out, set)) return plan_fail(st, "file assembly failed: " + w->fw->error());
     if (trace_on())
-        fprintf(stderr, "[kpw] job %llu worker %d kind=%d records=%lld (carried %lld) encode %.2f ms; at %.1f: start, "
-                        "encoded %.1f, turn %.1f, appended %.1f\n",
-                (unsigned long long)j.seq, x, j.kind, (long long)n_enc, (long long)ncarry, t1 - t0, t0 - w->t_open,
-                t1 - w->t_open, tq - w->t_open, now_ms() - w->t_open);
+        fprintf(stderr, "[kpw] job %llu worker %d kind=%d records=%lld (carried %lld) encode %.2f ms; at %.1f: turn to plan "
+                        "(buffer + boundaries %.1f), start, offsets up %.1f, cuts known %.1f, encoded %.1f, turn %.1f, appended %.1f\n",
+                (unsigned long long)j.seq, x, j.kind, (long long)n_enc, (long long)ncarry, t1 - t0, t_in - w->t_open,
+                t0 - t_in, t_up ? t_up - w->t_open : 0.0, t_planned ? t_planned - w->t_open : 0.0, t1 - w->t_open,
+                tq - w->t_open, now_ms() - w->t_open);
     {
         std::lock_guard<std::mutex> g(w->mu);
         w->asm_seq = j.seq + 1;
@@ -1019,8 +1110,25 @@ static void worker_main(kpw_writer *w, int x)
         hipEvent_t prev_carry;
         {
             std::unique_lock<std::mutex> lk(w->mu);
-            // the next job starts once the previous job's cuts are known
-            w->cv.wait(lk, [w] { return (w->stop && w->q.empty()) || (!w->q.empty() && w->q.front().seq == w->plan_seq); });
+            // the next job starts once the previous job's cuts are known; meanwhile a waiting
+            // worker narrows a queued job's appended record lengths (prep_lengths)
+            for (;;) {
+                if ((w->stop && w->q.empty()) || (!w->q.empty() && w->q.front().seq == w->plan_seq)) break;
+                StageBuf *pb = nullptr;
+                if (!w->aligned && prep_on())
+                    for (const Job &qj : w->q)
+                        if (w->buf[qj.buf].lp_state == 0) { pb = &w->buf[qj.buf]; break; }
+                if (pb) {
+                    pb->lp_state = 1;
+                    lk.unlock();
+                    prep_lengths(*pb);
+                    lk.lock();
+                    pb->lp_state = 2;
+                    w->cv.notify_all();
+                    continue;
+                }
+                w->cv.wait(lk);
+            }
             if (w->q.empty()) break;   // stop requested and nothing queued
             j = w->q.front();
             w->q.pop_front();
