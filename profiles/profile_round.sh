@@ -15,7 +15,7 @@ OUT=$ROOT/gpurun_out/prof_${TAG}_${WL}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 cd "$ROOT"
-ARGS="--workload $WL --no-cpu-baseline --no-resident --per-record-records 0 --secondary-steps 0"
+ARGS="--workload $WL --no-cpu-baseline --no-resident --per-record-records 0 --per-record-64k-records 0 --secondary-steps 0"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
     python3 bench.py $ARGS --steps 3 --warmup 0 > "$OUT/fetch.log" 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
