@@ -1101,48 +1101,51 @@ __global__ void k_mp_dict_decide(ChunkDesc *pg, int npg, const ChunkDesc *dch, c
     J.bw = C.fallback ? 0 : C.bw;
 }
 
-// per chunk, after the RLE structure of the pages' id streams
-__global__ void k_mp_satisfy(ChunkDesc *pg, ChunkDesc *dch, int ndch, const DevCol *cols, const uint64_t *ent_rec,
-                             const uint64_t *ent_boff, const RleJob *jobs)
+// per chunk (one block each, threads over its pages), after the RLE structure of the pages' id streams
+__global__ void __launch_bounds__(KPW_BLOCK) k_mp_satisfy(ChunkDesc *pg, ChunkDesc *dch, int ndch, const DevCol *cols,
+                                                           const uint64_t *ent_rec, const uint64_t *ent_boff, const RleJob *jobs)
 {
-    const int d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= ndch) return;
+    __shared__ int32_t lds[KPW_BLOCK];
+    __shared__ int all_plain;
+    const int d = blockIdx.x;
     ChunkDesc &D = dch[d];
-    if (!D.is_dict) return;
+    if (!D.is_dict) return;   // block-uniform
     const DevCol &col = cols[D.col];
     ChunkDesc &P0 = pg[D.first_page];
-    D.dict_all = D.dict_n;
-    if (D.tail_mode == 2) {   // the kept pages are PLAIN: so is the chunk's last page, and no dictionary page
-        for (int p = D.first_page; p < D.first_page + D.npages; p++) pg[p].fallback = 1;
-        D.fallback = 1;
-        P0.dictpage_len = 0;
-        return;
-    }
-    if (D.tail_mode == 1) {   // the kept first page passed isCompressionSatisfying
-        int last = -1;
-        for (int p = D.first_page; p < D.first_page + D.npages; p++) if (!pg[p].fallback) last = p;
-        const uint32_t dn = last >= 0 ? pg[last].dict_n : D.tail_dict_n;
-        if (dn > 0) {
-            D.dict_n = dn;
-            D.fallback = 0;
-            P0.dictpage_len = ent_cum(col, D, ent_rec, ent_boff, dn);
-        } else {
-            D.fallback = 1;
-            P0.dictpage_len = 0;
+    const int p0 = D.first_page, p1 = D.first_page + D.npages;
+    if (threadIdx.x == 0) {
+        D.dict_all = D.dict_n;
+        // tail_mode 2: the kept pages are PLAIN, so is the chunk's last page; 0: isCompressionSatisfying
+        // on the chunk's first page (1: the kept first page passed it)
+        int ap = D.tail_mode == 2;
+        if (D.tail_mode == 0 && !P0.fallback) {
+            const uint64_t val = 1 + jobs[P0.id_job].total_bytes;
+            if (!(val + P0.dict_bytes < P0.raw_bytes)) ap = 1;
         }
+        all_plain = ap;
+    }
+    __syncthreads();
+    if (all_plain) {
+        for (int p = p0 + (int)threadIdx.x; p < p1; p += KPW_BLOCK) pg[p].fallback = 1;
+        if (threadIdx.x == 0) { D.fallback = 1; P0.dictpage_len = 0; }
         return;
     }
-    if (!P0.fallback) {
-        const uint64_t val = 1 + jobs[P0.id_job].total_bytes;
-        if (!(val + P0.dict_bytes < P0.raw_bytes))
-            for (int p = D.first_page; p < D.first_page + D.npages; p++) pg[p].fallback = 1;
-    }
+    // the last dictionary-encoded page (the fallback pages are a suffix)
     int last = -1;
-    for (int p = D.first_page; p < D.first_page + D.npages; p++) if (!pg[p].fallback) last = p;
-    if (last >= 0 && pg[last].dict_n > 0) {
-        D.dict_n = pg[last].dict_n;
+    for (int p = p0 + (int)threadIdx.x; p < p1; p += KPW_BLOCK) if (!pg[p].fallback) last = p;
+    lds[threadIdx.x] = last;
+    __syncthreads();
+    for (int o = KPW_BLOCK / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) lds[threadIdx.x] = max(lds[threadIdx.x], lds[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x) return;
+    last = lds[0];
+    const uint32_t dn = last >= 0 ? pg[last].dict_n : (D.tail_mode == 1 ? D.tail_dict_n : 0u);
+    if (dn > 0) {
+        D.dict_n = dn;
         D.fallback = 0;
-        P0.dictpage_len = ent_cum(col, D, ent_rec, ent_boff, D.dict_n);
+        P0.dictpage_len = ent_cum(col, D, ent_rec, ent_boff, dn);
     } else {
         D.fallback = 1;
         P0.dictpage_len = 0;
@@ -1174,7 +1177,7 @@ void launch_mp_dict_decide(ChunkDesc *pg, int npg, const ChunkDesc *dch, const D
 void launch_mp_satisfy(ChunkDesc *pg, ChunkDesc *dch, int ndch, const DevCol *cols, const uint64_t *ent_rec,
                        const uint64_t *ent_boff, const RleJob *jobs, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_mp_satisfy, dim3((ndch + 255) / 256), dim3(256), 0, s, pg, dch, ndch, cols, ent_rec, ent_boff, jobs);
+    if (ndch) hipLaunchKernelGGL(k_mp_satisfy, dim3(ndch), dim3(KPW_BLOCK), 0, s, pg, dch, ndch, cols, ent_rec, ent_boff, jobs);
 }
 void launch_mp_dictpage_off(const ChunkDesc *pg, ChunkDesc *dch, int ndch, hipStream_t s)
 {
