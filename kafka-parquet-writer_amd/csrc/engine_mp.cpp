@@ -127,6 +127,11 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     uint32_t ndict = 0;
     for (int c = 0; c < nc; c++) ndict += (cols[c].dict && (!mask || (*mask)[c])) ? 1 : 0;
     const uint32_t round_tiles = std::min<uint32_t>(4 * kMpRoundTiles, std::max<uint32_t>(kMpRoundTiles, 1024 / std::max<uint32_t>(1, ndict)));
+    // rounds double up to round_grow x round_tiles: the stop matters near a chunk's crossing, which
+    // the high-cardinality chunks reach in the first rounds; the later, larger rounds cost fewer
+    // latency-bound launches (a bulk row group: 23 -> 8 rounds).  The table holds one round more.
+    static const uint32_t round_grow = [] { const char *e = getenv("KPW_MP_ROUND_GROW"); const int v = e ? atoi(e) : 4; return (uint32_t)(v > 0 ? v : 1); }();
+    const uint32_t round_max = round_tiles * round_grow;
     for (int c = 0; c < nc; c++) {
         ChunkDesc &D = dch[c];
         memset(&D, 0, sizeof(D));
@@ -157,7 +162,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             // page keep their ids: every value before the crossing is inserted).  So a table
             // holds at most dictPageSize / (smallest entry) + 1 entries plus one round's values.
             const uint64_t esz = (cols[c].phys == KPW_INT64 || cols[c].phys == KPW_DOUBLE) ? 8 : 4;
-            const uint64_t maxent = (uint64_t)props.dictionary_page_size / esz + 1 + (uint64_t)round_tiles * KPW_TILE_P_H;
+            const uint64_t maxent = (uint64_t)props.dictionary_page_size / esz + 1 + (uint64_t)round_max * KPW_TILE_P_H;
             D.ht_cap = (uint32_t)next_pow2_mp(std::max<uint64_t>(16, 2 * std::min<uint64_t>(len, maxent)));
             D.ht_off = ht_off;
             ht_off += D.ht_cap + 1;
@@ -240,11 +245,14 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     const int npg = (int)pg.size();
     // dictionary insertion order (tile k of every chunk before tile k + 1, expanded on the device)
     // and per round of round_tiles its slice
-    std::vector<uint32_t> dlist, droff, rlen;
+    std::vector<uint32_t> dlist, droff, rlen, rend;
     uint32_t ndict_tiles = 0;
     dict_order(dcount, ddict, ndict_tiles, dlist, droff);
     const uint32_t maxnt = (uint32_t)droff.size() - 1;
-    for (uint32_t k = 0; k < maxnt; k += round_tiles) rlen.push_back(droff[std::min(maxnt, k + round_tiles)] - droff[k]);
+    for (uint32_t k = 0, rt = round_tiles; k < maxnt; k += rt, rt = std::min(round_max, 2 * rt)) {
+        rlen.push_back(droff[std::min(maxnt, k + rt)] - droff[k]);
+        rend.push_back(std::min(maxnt, k + rt));   // tiles per chunk through this round
+    }
     // page descriptors use the engine's chunk buffers; dictionary descriptors their own
     // chunk descriptors, then 4 words of string-statistics metadata per chunk (one readback)
     static_assert(sizeof(ChunkDesc) % 8 == 0, "metadata words follow the descriptors");
@@ -331,7 +339,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ad.tile_cnt = mp_dtile_cnt.as<uint32_t>(); ad.tile_sz = mp_dtile_sz.as<uint64_t>();
     ad.max_dict_bytes = 0xFFFFFFFFu;   // the dictPageSize limit is applied per page (k_mp_dict_decide)
     ad.dict_order = d_dorder.as<uint32_t>(); ad.ndict_tiles = ndict_tiles;
-    ad.mp_round_tiles = round_tiles; ad.mp_nrounds = (uint32_t)rlen.size(); ad.mp_round_len = rlen.data();
+    ad.mp_round_end = rend.data(); ad.mp_nrounds = (uint32_t)rlen.size(); ad.mp_round_len = rlen.data();
     ad.mp_dict_limit = (uint32_t)props.dictionary_page_size;
 
     uint32_t enpt = 0, enet = 0;

@@ -975,7 +975,7 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
             const uint32_t cnt = a.mp_round_len[j];
             if (j)
                 hipLaunchKernelGGL(k_mp_dict_stop, dim3((a.nchunks + 63) / 64), dim3(64), 0, s, a.ch, a.nchunks,
-                                   j * a.mp_round_tiles, a.mp_dict_limit);
+                                   a.mp_round_end[j - 1], a.mp_dict_limit);
             if (cnt)
                 hipLaunchKernelGGL(k_dict_insert, dim3(cnt), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order + o,
                                    a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);

@@ -56,9 +56,9 @@ struct ChunkArgs {
     uint64_t *page_pre;            // v2: uncompressed level bytes in front of each page's values
     int32_t mp;                    // multi-page regime: descriptors are pages (dictionary decided per chunk)
     // multi-page dictionary insertion in rounds (host-side, read by launch_dict): round j is
-    // dict_order[sum(len[0..j)), +len[j]) = tiles [j * round_tiles, (j + 1) * round_tiles) of
-    // every chunk; between rounds a chunk past dict_limit bytes stops (ChunkDesc::stop_tile)
-    uint32_t mp_round_tiles;
+    // dict_order[sum(len[0..j)), +len[j]) = tiles [end[j - 1], end[j]) of every chunk; between
+    // rounds a chunk past dict_limit bytes stops (ChunkDesc::stop_tile)
+    const uint32_t *mp_round_end;
     uint32_t mp_nrounds;
     const uint32_t *mp_round_len;
     uint32_t mp_dict_limit;
