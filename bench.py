@@ -222,10 +222,11 @@ def write_file(kpw, schema, props, data, offs, device, batch=POLL_BATCH):
     pf.close()
     t3 = time.perf_counter()
     res = L.kpw_writer_data_size(h), pf.pipeline_stats()   # after close: the file's length
+    t4 = time.perf_counter()
     pf.__del__()   # the writer (and its in-memory file) is released inside the step
     if os.environ.get("KPW_TRACE") == "1":
-        print("[bench] writer: open %.1f ms, writes %.1f ms, close %.1f ms, free %.1f ms" % (
-            (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (time.perf_counter() - t3) * 1e3),
+        print("[bench] writer: open %.1f ms, writes %.1f ms, close %.1f ms, stats %.1f ms, free %.1f ms" % (
+            (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (t4 - t3) * 1e3, (time.perf_counter() - t4) * 1e3),
             file=sys.stderr, flush=True)
     return res
 

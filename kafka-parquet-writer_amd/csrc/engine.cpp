@@ -70,7 +70,7 @@ Engine::~Engine()
         }
     if (stream) (void)hipStreamSynchronize(stream);
     seg_scratch_free(seg_);
-    if (stream) (void)hipStreamDestroy(stream);
+    stream_release(stream);
     if (tr)
         fprintf(stderr, "[kpw] engine free: events+stream %.1f ms\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
@@ -146,7 +146,7 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     }
     device = dev;
     CK(hipSetDevice(dev));
-    CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    CK(stream_acquire(&stream));
     for (auto &e : ev_) CK(hipEventCreate(&e));
     for (auto &e : kev_) CK(hipEventCreate(&e));
     for (auto &e : up_ev_) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -218,6 +218,44 @@ void trim_caches()
     trim(g_pin, 0, [](void *b) { (void)hipHostFree(b); });
 }
 
+// ---------------------------------------------------------------- streams
+namespace {
+std::mutex g_smu;
+std::vector<std::pair<int, hipStream_t>> g_streams;   // idle pooled streams (device, stream)
+bool stream_pool_on()
+{
+    static const bool on = [] { const char *e = getenv("KPW_STREAM_POOL"); return !(e && e[0] == '0'); }();
+    return on;
+}
+}  // namespace
+
+hipError_t stream_acquire(hipStream_t *s)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    if (stream_pool_on()) {
+        std::lock_guard<std::mutex> g(g_smu);
+        for (size_t i = g_streams.size(); i-- > 0;)
+            if (g_streams[i].first == dev) {
+                *s = g_streams[i].second;
+                g_streams.erase(g_streams.begin() + (long)i);
+                return hipSuccess;
+            }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+void stream_release(hipStream_t s)
+{
+    if (!s) return;
+    if (!stream_pool_on()) { (void)hipStreamDestroy(s); return; }
+    int dev = 0;   // (the stream's own device: an encoder handle may be freed with another one current)
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) { (void)hipStreamDestroy(s); return; }
+    std::lock_guard<std::mutex> g(g_smu);
+    if (g_streams.size() >= 256) { (void)hipStreamDestroy(s); return; }   // (bounded)
+    g_streams.push_back({dev, s});
+}
+
 }  // namespace kpw
 
 extern "C" void kpw_trim_caches(void) { kpw::trim_caches(); }

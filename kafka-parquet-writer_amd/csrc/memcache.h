@@ -27,5 +27,11 @@ void pin_free(void *p);            // nullptr ok
 size_t pin_size(const void *p);    // usable bytes of a pin_alloc block containing p (0 if none)
 bool pin_contains(const void *p, size_t n);   // [p, p+n) inside one live pin_alloc block
 void trim_caches();                // release every idle block (device pools and pinned)
+// Non-blocking HIP streams of the current device, kept across writers: hipStreamDestroy takes
+// ~2.5 ms (a writer tears down five streams per file, and the reference opens a file per
+// rotation).  stream_release takes an idle stream (its owner synchronised it) back to the pool
+// (KPW_STREAM_POOL=0: created and destroyed as before).
+hipError_t stream_acquire(hipStream_t *s);
+void stream_release(hipStream_t s);
 
 }  // namespace kpw

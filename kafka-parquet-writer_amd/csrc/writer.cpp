@@ -1254,8 +1254,8 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
     }
     wk[0].eng = &eng;
     wk[1].eng = &eng1;
-    if (hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking) != hipSuccess) return KPW_ERR_DEVICE;
-    if (hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking) != hipSuccess) return KPW_ERR_DEVICE;
+    if (stream_acquire(&copy_stream) != hipSuccess) return KPW_ERR_DEVICE;
+    if (stream_acquire(&d2h_stream) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &e : slot_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &e : fd2h_ev)
@@ -1322,8 +1322,8 @@ kpw_writer::~kpw_writer()
     if (direct_ev) (void)hipEventDestroy(direct_ev);
     for (auto &e : call_ev) if (e) (void)hipEventDestroy(e);
     if (trace_on()) tf[2] = now_ms();
-    if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
-    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    stream_release(d2h_stream);   // (synchronised above)
+    stream_release(copy_stream);
     if (trace_on()) tf[3] = now_ms();
     delete fw;
     if (trace_on()) {
@@ -2069,8 +2069,11 @@ extern "C" int kpw_writer_file_bytes(const kpw_writer *w, const uint8_t **bytes,
 
 extern "C" void kpw_writer_free(kpw_writer *w)
 {
+    const double t0 = trace_on() ? now_ms() : 0.0;
     if (w) release_from_getter(w);   // no DMA may still read a caller's batch once the handle is gone
+    const double t1 = trace_on() ? now_ms() : 0.0;
     delete w;
+    if (trace_on()) fprintf(stderr, "[kpw] writer free: release %.1f ms, delete (members included) %.1f ms\n", t1 - t0, now_ms() - t1);
 }
 
 extern "C" int kpw_writer_stats(kpw_writer *w, double *out, int cap)
