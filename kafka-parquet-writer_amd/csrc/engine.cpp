@@ -70,7 +70,7 @@ Engine::~Engine()
         }
     if (stream) (void)hipStreamSynchronize(stream);
     seg_scratch_free(seg_);
-    stream_release(stream);
+    if (stream && stream != given_stream) (void)hipStreamDestroy(stream);
     if (tr)
         fprintf(stderr, "[kpw] engine free: events+stream %.1f ms\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
@@ -146,7 +146,8 @@ int Engine::init(int dev, const kpw_schema *schema, const kpw_props *pr)
     }
     device = dev;
     CK(hipSetDevice(dev));
-    CK(stream_acquire(&stream));
+    if (given_stream) stream = given_stream;   // (a writer's stream set, released by the writer)
+    else CK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto &e : ev_) CK(hipEventCreate(&e));
     for (auto &e : kev_) CK(hipEventCreate(&e));
     for (auto &e : up_ev_) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));

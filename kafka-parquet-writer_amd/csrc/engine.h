@@ -147,6 +147,7 @@ public:
     std::string message_name, proto_class;
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t given_stream = nullptr;   // set before init: the engine's stream (the owner's to release)
     float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 K7 (k_snappy_v, k_snappy_seg, k_snappy_s_rest)
 
 private:

@@ -220,8 +220,12 @@ void trim_caches()
 
 // ---------------------------------------------------------------- streams
 namespace {
+struct StreamSet {
+    int dev, n;
+    hipStream_t s[8];
+};
 std::mutex g_smu;
-std::vector<std::pair<int, hipStream_t>> g_streams;   // idle pooled streams (device, stream)
+std::vector<StreamSet> g_sets;   // idle pooled sets
 bool stream_pool_on()
 {
     static const bool on = [] { const char *e = getenv("KPW_STREAM_POOL"); return !(e && e[0] == '0'); }();
@@ -229,31 +233,46 @@ bool stream_pool_on()
 }
 }  // namespace
 
-hipError_t stream_acquire(hipStream_t *s)
+hipError_t stream_set_acquire(int n, hipStream_t *s)
 {
+    if (n <= 0 || n > 8) return hipErrorInvalidValue;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = -1;
     if (stream_pool_on()) {
         std::lock_guard<std::mutex> g(g_smu);
-        for (size_t i = g_streams.size(); i-- > 0;)
-            if (g_streams[i].first == dev) {
-                *s = g_streams[i].second;
-                g_streams.erase(g_streams.begin() + (long)i);
+        for (size_t i = g_sets.size(); i-- > 0;)
+            if (g_sets[i].dev == dev && g_sets[i].n == n) {
+                for (int k = 0; k < n; k++) s[k] = g_sets[i].s[k];
+                g_sets.erase(g_sets.begin() + (long)i);
                 return hipSuccess;
             }
     }
-    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    for (int k = 0; k < n; k++) {
+        const hipError_t e = hipStreamCreateWithFlags(&s[k], hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            for (int j = 0; j < k; j++) (void)hipStreamDestroy(s[j]);
+            for (int j = 0; j < n; j++) s[j] = nullptr;
+            return e;
+        }
+    }
+    return hipSuccess;
 }
 
-void stream_release(hipStream_t s)
+void stream_set_release(int n, const hipStream_t *s)
 {
-    if (!s) return;
-    if (!stream_pool_on()) { (void)hipStreamDestroy(s); return; }
-    int dev = 0;   // (the stream's own device: an encoder handle may be freed with another one current)
-    if (hipStreamGetDevice(s, &dev) != hipSuccess) { (void)hipStreamDestroy(s); return; }
-    std::lock_guard<std::mutex> g(g_smu);
-    if (g_streams.size() >= 256) { (void)hipStreamDestroy(s); return; }   // (bounded)
-    g_streams.push_back({dev, s});
+    if (n <= 0 || n > 8 || !s[0]) return;
+    int dev = 0;   // (the streams' own device: the caller's current one may differ)
+    const bool keep = stream_pool_on() && hipStreamGetDevice(s[0], &dev) == hipSuccess;
+    if (keep) {
+        std::lock_guard<std::mutex> g(g_smu);
+        if (g_sets.size() < 64) {   // (bounded)
+            StreamSet t{dev, n, {}};
+            for (int k = 0; k < n; k++) t.s[k] = s[k];
+            g_sets.push_back(t);
+            return;
+        }
+    }
+    for (int k = 0; k < n; k++) if (s[k]) (void)hipStreamDestroy(s[k]);
 }
 
 }  // namespace kpw

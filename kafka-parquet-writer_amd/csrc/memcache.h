@@ -27,11 +27,14 @@ void pin_free(void *p);            // nullptr ok
 size_t pin_size(const void *p);    // usable bytes of a pin_alloc block containing p (0 if none)
 bool pin_contains(const void *p, size_t n);   // [p, p+n) inside one live pin_alloc block
 void trim_caches();                // release every idle block (device pools and pinned)
-// Non-blocking HIP streams of the current device, kept across writers: hipStreamDestroy takes
-// ~2.5 ms (a writer tears down five streams per file, and the reference opens a file per
-// rotation).  stream_release takes an idle stream (its owner synchronised it) back to the pool
-// (KPW_STREAM_POOL=0: created and destroyed as before).
-hipError_t stream_acquire(hipStream_t *s);
-void stream_release(hipStream_t s);
+// Sets of n non-blocking HIP streams of the current device, kept across writers:
+// hipStreamDestroy takes ~2.5 ms (a writer tears down four streams per file, and the reference
+// opens a file per rotation).  A set is created stream after stream and reused whole: HIP gives
+// streams hardware queues in creation order, so a set's streams sit on different queues (single
+// pooled streams mixed from different writers could share one and serialise two encode
+// workers: C4 21.3 -> 15.7 GB/s after the per-record legs).  stream_set_release takes idle
+// streams (their owner synchronised them) back (KPW_STREAM_POOL=0: created and destroyed).
+hipError_t stream_set_acquire(int n, hipStream_t *s);
+void stream_set_release(int n, const hipStream_t *s);
 
 }  // namespace kpw

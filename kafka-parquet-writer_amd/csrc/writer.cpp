@@ -237,10 +237,18 @@ struct Worker {
     std::thread th;
 };
 
+// The writer's stream set (memcache.h): eng, eng1, copy, d2h.  Declared before the engines, so
+// it is destroyed after them: the streams go back idle (every owner synchronised its own).
+struct StreamSetOwner {
+    hipStream_t s[4] = {};
+    ~StreamSetOwner() { if (s[0]) stream_set_release(4, s); }
+};
+
 struct kpw_writer {
     static constexpr int kBufs = 4;    // two encoding, one queued, one filling
     static constexpr int kSlots = 4;
     static constexpr size_t kSlotBytes = 32ull << 20;
+    StreamSetOwner sset;
     Engine eng;                        // worker 0's engine (also the caller's, for write_until_full probes)
     Engine eng1;                       // worker 1's engine
     int nworkers = 2;
@@ -1254,8 +1262,8 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
     }
     wk[0].eng = &eng;
     wk[1].eng = &eng1;
-    if (stream_acquire(&copy_stream) != hipSuccess) return KPW_ERR_DEVICE;
-    if (stream_acquire(&d2h_stream) != hipSuccess) return KPW_ERR_DEVICE;
+    copy_stream = sset.s[2];
+    d2h_stream = sset.s[3];
     for (auto &e : slot_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &e : fd2h_ev)
@@ -1322,8 +1330,7 @@ kpw_writer::~kpw_writer()
     if (direct_ev) (void)hipEventDestroy(direct_ev);
     for (auto &e : call_ev) if (e) (void)hipEventDestroy(e);
     if (trace_on()) tf[2] = now_ms();
-    stream_release(d2h_stream);   // (synchronised above)
-    stream_release(copy_stream);
+    // (the stream set goes back to the pool once the engines are gone: StreamSetOwner)
     if (trace_on()) tf[3] = now_ms();
     delete fw;
     if (trace_on()) {
@@ -1355,7 +1362,10 @@ extern "C" kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, con
 {
     try {
         kpw_writer *w = new kpw_writer();
-        int st = w->eng.init(device, schema, props);
+        int st = hipSetDevice(device) == hipSuccess && stream_set_acquire(4, w->sset.s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
+        w->eng.given_stream = w->sset.s[0];
+        w->eng1.given_stream = w->sset.s[1];
+        if (!st) st = w->eng.init(device, schema, props);
         if (!st) {
             w->fw = new FileWriter(w->eng.cols, w->eng.message_name, w->eng.proto_class, w->eng.props);
             st = w->fw->open(path);
