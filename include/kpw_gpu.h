@@ -104,7 +104,8 @@ int64_t kpw_writer_failed_record(const kpw_writer *w); /* -1 if none */
  * jobs).  [0] jobs, [1] records encoded, [2] record bytes encoded, [3] uncompressed page
  * bytes, [4] compressed page bytes, [5..14] device milliseconds per stage summed over jobs
  * (HIP events on the encoder's stream, kpw_encoder_stage_times order), [15] encode wall
- * milliseconds of the worker thread.  Returns the number of entries written (<= cap). */
+ * milliseconds of the worker thread, [16] scan look-backs that recomputed a predecessor tile
+ * instead of waiting longer (exact either way).  Returns the number of entries written (<= cap). */
 int kpw_writer_stats(kpw_writer *w, double *out, int cap);
 const char *kpw_writer_last_error(const kpw_writer *w);
 void kpw_writer_free(kpw_writer *w);

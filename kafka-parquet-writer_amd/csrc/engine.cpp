@@ -384,10 +384,11 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     t_encode_in_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
     const int st = encode_impl(d_data, d_off, n, final_flush, next_rg_size, user_stream, out);
     if (st) return st;
-    // the single-pass scans count a look-back that waited past its bound (kpw_lookback.h):
-    // their results would be wrong, so the encode fails loudly instead
+    // look-backs that waited past their bound and recomputed the predecessor (kpw_lookback.h):
+    // exact either way, counted for kpw_writer_stats
     const int lf = lb_failures(&seg_, stream);
-    if (lf != 0) return fail(KPW_ERR_DEVICE, lf < 0 ? "scan status unreadable" : "scan look-back timed out");
+    if (lf < 0) return fail(KPW_ERR_DEVICE, "scan status unreadable");
+    lb_fallbacks = (uint32_t)lf;
     return KPW_OK;
 }
 

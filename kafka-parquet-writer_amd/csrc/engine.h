@@ -149,6 +149,7 @@ public:
     hipStream_t stream = nullptr;
     hipStream_t given_stream = nullptr;   // set before init: the engine's stream (the owner's to release)
     float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 K7 (k_snappy_v, k_snappy_seg, k_snappy_s_rest)
+    uint32_t lb_fallbacks = 0;  // look-backs of the last encode that recomputed a predecessor (kpw_lookback.h)
 
 private:
     int encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,
@@ -218,8 +219,8 @@ private:
                     std::vector<RleJob> &pj);
     // multi-page regime (engine_mp.cpp)
     bool mp_ = false;
-    int64_t mp_last_rg_ = 0;
-    double t_encode_in_ = 0.0;             // steady clock (ms) at the last encode() entry (KPW_TRACE)           // records of the last row group the multi-page path cut (horizon hint)
+    int64_t mp_last_rg_ = 0;               // records of the last row group the multi-page path cut (horizon hint)
+    double t_encode_in_ = 0.0;             // steady clock (ms) at the last encode() entry (KPW_TRACE)
     bool probe_ = false;                 // encode() is a probe_pages call
     std::vector<int32_t> probe_npages_;
     const std::vector<char> *probe_mask_ = nullptr;

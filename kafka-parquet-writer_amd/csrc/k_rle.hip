@@ -183,6 +183,46 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_rle_longruns(RleJob *jobs, const 
 // composition scan, look-back 0), the RLE runs among them, placed (sum-scan, look-back 1) and
 // written as (g, b).  The job's last element tile stores n_rle.
 
+// Fallbacks of k_phase's two scans (kpw_lookback.h): tile q's composed run maps, and its RLE
+// run count, which needs the phase entering q: the scan-0 words of tiles [first, q) read
+// backwards to the nearest inclusive one (each recomputed when it is not out).
+struct PhaseFb0 {
+    const uint32_t *a, *b;   // the job's long runs (lr_a + e0, lr_b + e0)
+    uint32_t et0, nlong;
+    __device__ void operator()(uint32_t q, uint32_t &v, bool &inc) const
+    {
+        uint32_t m = OpMapCompose::id();
+        const uint64_t k0 = (uint64_t)(q - et0) * KPW_TILE_E;
+        for (uint64_t k = k0; k < k0 + KPW_TILE_E && k < nlong; k++) m = OpMapCompose::op(m, run_map(a[k], b[k]));
+        v = m;
+        inc = q == et0;
+    }
+};
+struct PhaseFb1 {
+    PhaseFb0 f0;
+    LbView L;
+    __device__ void operator()(uint32_t q, uint32_t &v, bool &inc) const
+    {
+        uint32_t pre = OpMapCompose::id();
+        for (uint32_t r = q; r-- > f0.et0;) {
+            uint32_t m;
+            bool ri;
+            lb_peek<uint32_t, EncU32>(L, r, r, f0, m, ri);
+            pre = OpMapCompose::op(m, pre);
+            if (ri) break;
+        }
+        uint32_t phi = pm_get(pre, 0), cnt = 0;
+        const uint64_t k0 = (uint64_t)(q - f0.et0) * KPW_TILE_E;
+        for (uint64_t k = k0; k < k0 + KPW_TILE_E && k < f0.nlong; k++) {
+            const uint32_t a = f0.a[k], b = f0.b[k];
+            const uint32_t g = a + ((phi - a) & 7u);
+            if (g + 8 <= b) { cnt++; phi = b & 7u; }
+        }
+        v = cnt;
+        inc = q == f0.et0;
+    }
+};
+
 __global__ void __launch_bounds__(KPW_BLOCK) k_phase(RleJob *jobs, const uint32_t *etile_job, const uint32_t *lr_a,
                                                      const uint32_t *lr_b, uint32_t *r_g, uint32_t *r_b, uint8_t *lr_rle, uint32_t nt,
                                                      LbView L)
@@ -203,14 +243,15 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_phase(RleJob *jobs, const uint32_
     if (valid) { a = lr_a[J.e0 + k]; b = lr_b[J.e0 + k]; m = run_map(a, b); }
     uint32_t tot;
     const uint32_t ex = block_scan_excl<uint32_t, OpMapCompose>(m, lds, &tot);
-    const uint32_t pre = lb_tile<uint32_t, OpMapCompose>(L, 0, u, et0, tot, u == et0, u != et0, &c0);
+    const PhaseFb0 fb0{lr_a + J.e0, lr_b + J.e0, et0, nlong};
+    const uint32_t pre = lb_tile<uint32_t, OpMapCompose>(L, 0, u, et0, tot, u == et0, u != et0, &c0, fb0);
     const uint32_t phi = pm_get(ex, pm_get(pre, 0));
     const uint32_t g = a + ((phi - a) & 7u);
     const uint32_t rle = (valid && g + 8 <= b) ? 1u : 0u;
     if (lr_rle && valid) lr_rle[J.e0 + k] = (uint8_t)rle;
     uint32_t t2;
     const uint32_t idx = block_scan_excl<uint32_t, OpSum32>(rle, lds, &t2);
-    const uint32_t off = lb_tile<uint32_t, OpSum32>(L, nt, u, et0, t2, u == et0, u != et0, &c1);
+    const uint32_t off = lb_tile<uint32_t, OpSum32>(L, nt, u, et0, t2, u == et0, u != et0, &c1, PhaseFb1{fb0, L});
     if (rle) {
         const uint64_t o = J.e0 + off + idx;
         r_g[o] = g;
@@ -227,6 +268,25 @@ __device__ __forceinline__ uint32_t rle_bytes(uint32_t L, uint32_t bw) { return 
 // One launch over the element tiles: per RLE run the bytes and groups of (gap before it + the
 // run), their offsets (two sum-scans, look-backs 0 and 1), and the job totals (the job's last
 // run, or its first tile when it has none).
+// Fallback of k_r_sizes' scans: tile q's bytes (groups = false) or groups of its RLE runs.
+struct SizesFb {
+    const uint32_t *g, *b;   // r_g + e0, r_b + e0
+    uint32_t et0, nrle, bw;
+    bool groups;
+    __device__ void operator()(uint32_t q, uint64_t &v, bool &inc) const
+    {
+        uint64_t sum = 0;
+        const uint64_t k0 = (uint64_t)(q - et0) * KPW_TILE_E;
+        for (uint64_t k = k0; k < k0 + KPW_TILE_E && k < nrle; k++) {
+            const uint32_t pe = k ? b[k - 1] : 0;
+            const uint64_t gr = (g[k] - pe) >> 3;
+            sum += groups ? gr : gap_bytes(gr, bw) + rle_bytes(b[k] - g[k], bw);
+        }
+        v = sum;
+        inc = q == et0;
+    }
+};
+
 __global__ void __launch_bounds__(KPW_BLOCK) k_r_sizes(RleJob *jobs, const uint32_t *etile_job, const uint32_t *r_g,
                                                        const uint32_t *r_b, uint64_t *r_boff, uint64_t *r_goff, uint32_t nt,
                                                        LbView L)
@@ -250,8 +310,10 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_r_sizes(RleJob *jobs, const uint3
     uint64_t t1, t2;
     const uint64_t eb = block_scan_excl<uint64_t, OpSum64>(by, lds, &t1);
     const uint64_t eg = block_scan_excl<uint64_t, OpSum64>(gr, lds, &t2);
-    const uint64_t boff = lb_tile<uint64_t, OpSum64>(L, 0, u, et0, t1, u == et0, u != et0, &c0);
-    const uint64_t goff = lb_tile<uint64_t, OpSum64>(L, nt, u, et0, t2, u == et0, u != et0, &c1);
+    const SizesFb fb{r_g + J.e0, r_b + J.e0, et0, nrle, J.bw, false};
+    const uint64_t boff = lb_tile<uint64_t, OpSum64>(L, 0, u, et0, t1, u == et0, u != et0, &c0, fb);
+    const uint64_t goff = lb_tile<uint64_t, OpSum64>(L, nt, u, et0, t2, u == et0, u != et0, &c1,
+                                                     SizesFb{fb.g, fb.b, et0, nrle, J.bw, true});
     if (valid) {
         r_boff[J.e0 + k] = boff + eb;
         r_goff[J.e0 + k] = goff + eg;

@@ -164,10 +164,9 @@ uint64_t *scan_tmp(SegScratch *sc, uint64_t words, hipStream_t s)
     return (uint64_t *)sc->tmp;
 }
 
-// Look-back timeouts counted since the previous call (kpw_lookback.h), read and cleared: the
+// Look-back fallbacks counted since the previous call (kpw_lookback.h), read and cleared: the
 // count lives in its own word (SegScratch::fails), which the status words' growth and
-// epoch-wrap clears never touch, so a timeout early in an encode is still seen at its end and
-// does not fail the handle's later encodes.
+// epoch-wrap clears never touch, so one early in an encode is still seen at its end.
 int lb_failures(SegScratch *sc, hipStream_t s)
 {
     if (!sc->fails) return 0;
@@ -188,7 +187,7 @@ LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s)
     if (!sc->fails) {
         sc->fails = (uint32_t *)dev_alloc(64);
         if (!sc->fails || hipMemsetAsync(sc->fails, 0, 64, s) != hipSuccess) {
-            sc->failed = true; return LbView{nullptr, 0, nullptr};
+            sc->failed = true; return LbView{nullptr, 0, nullptr, 0};
         }
     }
     if (need > sc->bytes) {
@@ -199,15 +198,22 @@ LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s)
         sc->bytes = std::max<size_t>(need * 2, 16u << 20);
         sc->p = dev_alloc(sc->bytes);
         if (!sc->p || hipMemsetAsync(sc->p, 0, sc->bytes, s) != hipSuccess) {
-            sc->bytes = 0; sc->failed = true; return LbView{nullptr, 0, nullptr};
+            sc->bytes = 0; sc->failed = true; return LbView{nullptr, 0, nullptr, 0};
         }
         sc->epoch = 0;
     }
     if (++sc->epoch >= (1u << 15)) {
-        if (hipMemsetAsync(sc->p, 0, sc->bytes, s) != hipSuccess) { sc->failed = true; return LbView{nullptr, 0, nullptr}; }
+        if (hipMemsetAsync(sc->p, 0, sc->bytes, s) != hipSuccess) { sc->failed = true; return LbView{nullptr, 0, nullptr, 0}; }
         sc->epoch = 1;
     }
-    return LbView{(uint64_t *)sc->p, sc->epoch, sc->fails};
+    // polls before a look-back falls back (each an agent-scope load plus a short sleep; a
+    // running predecessor publishes within microseconds).  KPW_LB_SPIN=0 falls back at once,
+    // which the tests use to exercise every fallback.
+    static const uint32_t spin = [] {
+        const char *e = getenv("KPW_LB_SPIN");
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 13);
+    }();
+    return LbView{(uint64_t *)sc->p, sc->epoch, sc->fails, spin};
 }
 
 template <class F>
@@ -281,6 +287,30 @@ __device__ __forceinline__ void seg_block_scan(T *lv, uint32_t *lh)
     }
 }
 
+// Fallback: chunk q's segmented aggregate (from its last segment head) recomputed
+// sequentially, as k_seg_scan's block scan leaves it; inclusive when the chunk has a head.
+template <typename T, typename Op>
+struct SegFb {
+    const T *in;
+    const uint32_t *seg;
+    uint32_t n;
+    __device__ void operator()(uint32_t q, T &v, bool &inc) const
+    {
+        const uint32_t b = q * SEG_CH;
+        uint32_t p = (b == 0) ? 0xffffffffu : (b - 1 < n ? seg[b - 1] : 0xfffffffeu);
+        T acc = Op::id();
+        bool head = false;
+        for (uint32_t k = b; k < b + SEG_CH; k++) {
+            const uint32_t sg = k < n ? seg[k] : 0xfffffffeu;
+            const T x = k < n ? in[k] : Op::id();
+            if (sg != p) { head = true; acc = x; } else acc = Op::op(acc, x);
+            p = sg;
+        }
+        v = acc;
+        inc = q == 0 || head;
+    }
+};
+
 template <typename T, typename Op>
 __global__ void __launch_bounds__(KPW_BLOCK) k_seg_scan(const T *in, T *out, const uint32_t *seg, uint32_t n, T *tot, uint32_t nb,
                                                         LbView L)
@@ -313,7 +343,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_seg_scan(const T *in, T *out, con
     const bool has_head = lh[KPW_BLOCK - 1] != 0;
     // the chunk's first element continues a segment of an earlier chunk: it needs a carry-in
     const bool need = b > 0 && b < n && seg[b] == seg[b - 1];
-    const T lcarry = lb_tile<T, Op>(L, 0, blk, 0, agg, blk == 0 || has_head, need, &lcarry_s);
+    const T lcarry = lb_tile<T, Op>(L, 0, blk, 0, agg, blk == 0 || has_head, need, &lcarry_s, SegFb<T, Op>{in, seg, n});
     // exclusive prefix entering my range, continuing my first segment
     T in_pre = threadIdx.x == 0 ? lcarry : lv[threadIdx.x - 1];
     const uint32_t pre_head = threadIdx.x == 0 ? 0u : lh[threadIdx.x - 1];

@@ -51,7 +51,7 @@ struct DecodeArgs {
 struct SegScratch {
     void *p = nullptr;             // single-pass scans: tile status words (kpw_lookback.h)
     size_t bytes = 0;
-    uint32_t *fails = nullptr;     // look-back timeouts since the last lb_failures (its own word:
+    uint32_t *fails = nullptr;     // look-back fallbacks since the last lb_failures (its own word:
                                    // the status words' growth and epoch-wrap clears never touch it)
     uint32_t epoch = 0;            // of the last launch (status words carry it)
     void *tmp = nullptr;           // reduce-then-scan tile sums (never the status words: any

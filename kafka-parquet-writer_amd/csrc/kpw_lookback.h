@@ -12,12 +12,17 @@
 // clear; values fit 47 bits (byte counts and positions of one encode, < 2^40).
 //
 // Tile index = blockIdx.x.  A tile waits only on lower-numbered tiles, and each XCD dispatches
-// its workgroups in index order, so the lowest unfinished tile always runs (by induction every
-// tile does).  A ticket counter would not need that, but one atomic per tile on a single
-// address serialised the launch (r04: the element-tile kernels over ~50 k tiles took 0.7 ms
-// where the multi-launch scans took 0.1).  The spin is bounded: a tile that waits past the
-// bound counts a failure in *fails (the engine fails the encode on it, lb_failures) and goes
-// on with a wrong value rather than hang the GPU.
+// its workgroups in index order, so with the kernel alone on the chip the lowest unfinished
+// tile always runs.  That fails with concurrent look-back kernels on other hardware queues:
+// kernel A's waiting tiles can fill XCD x while A's lowest unfinished tile is queued on XCD y,
+// full of kernel B's waiting tiles whose own lowest is queued on x (r05au: C5 with 8 and 16
+// hardware queues, eight writers, waited out a 2^25-spin bound).  A ticket counter avoids that
+// but one atomic per tile on a single address serialised the launch (r04: 0.7 ms where the
+// multi-launch scans took 0.1 over ~50 k tiles).  So the wait is bounded and then falls back
+// (decoupled fallback): the waiting lane recomputes the missing tile's own contribution from
+// the tile's inputs (every look-back kernel passes that function, `fb`), publishes it and goes
+// on.  Results stay exact; only the rare slow path pays, and progress no longer depends on
+// dispatch order.  Fallbacks are counted in *fails (traced by the engine).
 #pragma once
 #include "kpw_device.h"
 
@@ -26,7 +31,8 @@ namespace kpw {
 struct LbView {
     uint64_t *w;      // status words from w[8]
     uint32_t epoch;
-    uint32_t *fails;  // look-back timeouts (SegScratch::fails)
+    uint32_t *fails;  // fallbacks taken (SegScratch::fails)
+    uint32_t spin;    // polls of a predecessor's status word before the fallback (KPW_LB_SPIN)
 };
 constexpr uint32_t LB_ST_AGG = 1, LB_ST_INC = 2;
 
@@ -40,8 +46,10 @@ __device__ __forceinline__ void lb_publish(const LbView &L, uint32_t idx, uint64
 // Wave 0: the combination (in order) of tiles [first, tile) of scan `sbase` (= scan * ntiles)
 // that enters `tile`, where `first` is the first tile of its run (the job); the look-back also
 // ends at any tile that published its inclusive value.  Values travel encoded (Enc).
-template <typename T, typename Op, typename Enc>
-__device__ __forceinline__ T lb_lookback(const LbView &L, uint32_t sbase, uint32_t tile, uint32_t first)
+// fb(q, &v, &inc): tile q's status recomputed from its inputs (lane-local: no cross-lane ops),
+// v its aggregate, or its inclusive value when inc (what tile q itself would publish).
+template <typename T, typename Op, typename Enc, typename FB>
+__device__ __forceinline__ T lb_lookback(const LbView &L, uint32_t sbase, uint32_t tile, uint32_t first, const FB &fb)
 {
     const uint32_t lane = threadIdx.x & 63;
     T acc = Op::id();
@@ -52,12 +60,22 @@ __device__ __forceinline__ T lb_lookback(const LbView &L, uint32_t sbase, uint32
         uint64_t wv = 0;
         if (valid) {
             bool ok = false;
-            for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+            for (uint32_t spin = 0;; spin++) {
                 wv = __hip_atomic_load(&L.w[8 + sbase + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((uint32_t)((wv >> 2) & 0x7fff) == L.epoch && (wv & 3) != 0) { ok = true; break; }
+                if (spin >= L.spin) break;
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (!ok) { atomicAdd(L.fails, 1u); wv = LB_ST_INC; }   // counted; value 0, terminal
+            if (!ok) {
+                T v;
+                bool inc;
+                fb((uint32_t)q, v, inc);
+                wv = (Enc::enc(v) << 17) | ((uint64_t)L.epoch << 2) | (inc ? LB_ST_INC : LB_ST_AGG);
+                // (if tile q publishes too, both words are right: an AGG landing after its INC
+                // only lengthens later look-backs)
+                __hip_atomic_store(&L.w[8 + sbase + q], wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd(L.fails, 1u);
+            }
         }
         const bool term = !valid || (wv & 3) == LB_ST_INC;
         const uint64_t tm = __ballot(term);
@@ -73,6 +91,20 @@ __device__ __forceinline__ T lb_lookback(const LbView &L, uint32_t sbase, uint32
         acc = Op::op(v, acc);
         if (tm) return acc;
         base -= 64;
+    }
+}
+
+// Tile q's published status read once, recomputed by fb when it is not out (the sequential
+// prefix a fallback of a chained scan needs).
+template <typename T, typename Enc, typename FB>
+__device__ __forceinline__ void lb_peek(const LbView &L, uint32_t idx, uint32_t q, const FB &fb, T &v, bool &inc)
+{
+    const uint64_t wv = __hip_atomic_load(&L.w[8 + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)((wv >> 2) & 0x7fff) == L.epoch && (wv & 3) != 0) {
+        v = Enc::dec(wv >> 17);
+        inc = (wv & 3) == LB_ST_INC;
+    } else {
+        fb(q, v, inc);
     }
 }
 
@@ -97,9 +129,9 @@ template <> struct EncOf<int64_t> { using E = EncI64; };
 // tile's own aggregate, valid in thread 0).  `inc_now`: the tile's inclusive value does not
 // depend on earlier tiles (first of its run, or a segment head inside it), so it is published
 // at once; `need`: the tile needs its carry-in.  Returns Op::id() when !need.
-template <typename T, typename Op>
+template <typename T, typename Op, typename FB>
 __device__ __forceinline__ T lb_tile(const LbView &L, uint32_t sbase, uint32_t tile, uint32_t first, T agg, bool inc_now,
-                                     bool need, T *slot)
+                                     bool need, T *slot, const FB &fb)
 {
     using Enc = typename EncOf<T>::E;
     if (threadIdx.x == 0) {
@@ -107,7 +139,7 @@ __device__ __forceinline__ T lb_tile(const LbView &L, uint32_t sbase, uint32_t t
         lb_publish(L, sbase + tile, Enc::enc(agg), inc_now ? LB_ST_INC : LB_ST_AGG);
     }
     if (need && threadIdx.x < 64) {
-        const T c = lb_lookback<T, Op, Enc>(L, sbase, tile, first);
+        const T c = lb_lookback<T, Op, Enc>(L, sbase, tile, first, fb);
         if (threadIdx.x == 0) {
             *slot = c;
             if (!inc_now) lb_publish(L, sbase + tile, Enc::enc(Op::op(c, agg)), LB_ST_INC);

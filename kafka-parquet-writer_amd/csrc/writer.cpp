@@ -323,7 +323,7 @@ struct kpw_writer {
     double t_open = 0, t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0;
     double t_probe = 0;          // page-size probes (multi-page per-record path): wall time, count, records
     uint64_t n_probe = 0, probe_recs = 0;
-    double stats[16] = {0};            // kpw_writer_stats (job order; read after drain)
+    double stats[17] = {0};            // kpw_writer_stats (job order; read after drain)
 
     ~kpw_writer();
     int init_pipeline(const kpw_schema *schema, const kpw_props *props);
@@ -981,6 +981,7 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
         w->stats[2] += (double)(hb[n_enc] - hb[0]);
         for (int k = 0; k < 10; k++) w->stats[5 + k] += E.stage_ms[k];
         w->stats[15] += t1 - t0;
+        w->stats[16] += E.lb_fallbacks;
         W.njobs++;
     }
     if (j.kind == JOB_PLANNED) w->open_buffered = out.open_buffered;
@@ -1077,6 +1078,7 @@ static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
         w->stats[2] += (double)(hb[s0 + out.records_consumed] - hb[s0]);
         for (int k = 0; k < 10; k++) w->stats[5 + k] += E.stage_ms[k];
         w->stats[15] += t1 - t0;
+        w->stats[16] += E.lb_fallbacks;
         w->t_encode += t1 - t0;
         if (out.rgs.empty()) {   // no cut in [s0, lim): the open row group
             if (j.kind == JOB_PLANNED) w->open_buffered = out.open_buffered;
@@ -2090,7 +2092,7 @@ extern "C" int kpw_writer_stats(kpw_writer *w, double *out, int cap)
 {
     if (!w || !out || cap <= 0) return 0;
     if (release_batches(w) || drain(w)) return 0;
-    const int n = cap < 16 ? cap : 16;
+    const int n = cap < 17 ? cap : 17;
     for (int i = 0; i < n; i++) out[i] = w->stats[i];
     return n;
 }
