@@ -70,11 +70,20 @@ __device__ __forceinline__ T lb_lookback(const LbView &L, uint32_t sbase, uint32
                 T v;
                 bool inc;
                 fb((uint32_t)q, v, inc);
-                wv = (Enc::enc(v) << 17) | ((uint64_t)L.epoch << 2) | (inc ? LB_ST_INC : LB_ST_AGG);
-                // (if tile q publishes too, both words are right: an AGG landing after its INC
-                // only lengthens later look-backs)
-                __hip_atomic_store(&L.w[8 + sbase + q], wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicAdd(L.fails, 1u);
+                // An in-place scan (in == out) overwrites tile q's inputs once q has published:
+                // so the recomputation stands only if q had still published nothing after its
+                // loads completed (the fence waits for them); otherwise q's own word is used.
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+                const uint64_t w2 = __hip_atomic_load(&L.w[8 + sbase + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)((w2 >> 2) & 0x7fff) == L.epoch && (w2 & 3) != 0) {
+                    wv = w2;
+                } else {
+                    wv = (Enc::enc(v) << 17) | ((uint64_t)L.epoch << 2) | (inc ? LB_ST_INC : LB_ST_AGG);
+                    // (if tile q publishes too, both words are right: an AGG landing after its
+                    // INC only lengthens later look-backs)
+                    __hip_atomic_store(&L.w[8 + sbase + q], wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicAdd(L.fails, 1u);
+                }
             }
         }
         const bool term = !valid || (wv & 3) == LB_ST_INC;
