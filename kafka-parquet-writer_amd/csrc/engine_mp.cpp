@@ -404,6 +404,14 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         launch_dba_suffixes(ap, d_pre.as<uint32_t>(), dla.jobs, d_tile_sfx_off.as<uint64_t>(), d_body.as<uint8_t>(), st);
     }
     CK(hipGetLastError());
+    // page metadata (the dictionary descriptors, the page descriptors and their binary statistics'
+    // offsets / lengths) queued now, so they come back with the compression's results in its sync
+    uint64_t *const d_smeta = (uint64_t *)(d_chunks.as<ChunkDesc>() + npg);
+    static thread_local std::vector<uint8_t> md;
+    md.resize(npg * (sizeof(ChunkDesc) + 32));
+    CK(xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st));
+    launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta, nullptr, st);
+    CK(xd2h(md.data(), d_chunks.p, md.size(), st));
     // (no sync here: the page offsets and lengths came back with the layout)
     std::vector<uint64_t> poff(ptab.begin() + 4, ptab.begin() + 4 + P2), plen(ptab.begin() + 4 + P2, ptab.begin() + 4 + 2 * P2);
     std::vector<uint64_t> pcoff(P2), pclen(P2), ppre(P2, 0);
@@ -465,22 +473,15 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         for (int p = 0; p < 2 * npg; p++) { pcoff[p] = poff[p] - ppre[p]; pclen[p] = plen[p] + ppre[p]; }
         pages_dev_ = d_body.as<uint8_t>();
         pages_len_ = body_tot;
+        CK(xsync(st));
     }
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
     // ---------------------------------------------------------------- page metadata
-    CK(xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st));
+    // (read back above, with the compression's sync)
     std::vector<uint64_t> smeta(4 * npg, 0);
-    uint64_t *const d_smeta = (uint64_t *)(d_chunks.as<ChunkDesc>() + npg);
-    launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta, nullptr, st);
-    {   // descriptors + metadata in one copy
-        static thread_local std::vector<uint8_t> md;
-        md.resize(npg * (sizeof(ChunkDesc) + 32));
-        CK(xd2h(md.data(), d_chunks.p, md.size(), st));
-        CK(xsync(st));
-        memcpy(pg.data(), md.data(), npg * sizeof(ChunkDesc));
-        for (auto &C : pg) chunk_stats_derive(C);
-        memcpy(smeta.data(), md.data() + npg * sizeof(ChunkDesc), npg * 32);
-    }
+    memcpy(pg.data(), md.data(), npg * sizeof(ChunkDesc));
+    for (auto &C : pg) chunk_stats_derive(C);
+    memcpy(smeta.data(), md.data() + npg * sizeof(ChunkDesc), npg * 32);
     std::vector<std::string> bmin(npg), bmax(npg);
     {
         uint64_t blob_len = 0;
@@ -490,16 +491,14 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             if (cols[pg[p].col].phys == KPW_BYTE_ARRAY && pg[p].has_minmax) blob_len += smeta[4 * p + 1] + smeta[4 * p + 3];
         }
         // a probe needs the page headers' sizes only: the min / max lengths, and whether min ==
-        // max (write_stats then also writes the deprecated fields), which differing lengths decide
-        bool need_bytes = !probe_;
-        for (int p = 0; p < npg && !need_bytes; p++)
-            if (cols[pg[p].col].phys == KPW_BYTE_ARRAY && pg[p].has_minmax && smeta[4 * p + 1] == smeta[4 * p + 3])
-                need_bytes = true;
-        if (blob_len && !need_bytes) {
+        // max (write_stats then also writes the deprecated fields), which k_stats_gather flags
+        // (bit 63 of the max offset word), so no bytes come back
+        if (blob_len && probe_) {
             for (int p = 0; p < npg; p++)
                 if (cols[pg[p].col].phys == KPW_BYTE_ARRAY && pg[p].has_minmax) {
+                    const bool eq = (smeta[4 * p + 2] >> 63) != 0;
                     bmin[p].assign(smeta[4 * p + 1], 'a');
-                    bmax[p].assign(smeta[4 * p + 3], 'b');
+                    bmax[p].assign(smeta[4 * p + 3], eq ? 'a' : 'b');
                 }
         } else if (blob_len) {
             std::vector<uint8_t> blob(blob_len);

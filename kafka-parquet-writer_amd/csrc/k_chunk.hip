@@ -902,8 +902,10 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_chunk_prep(const ChunkDesc *ch, i
     out[tail_off + KPW_BLOCK + threadIdx.x] = 0;
 }
 
-// Binary statistics: meta[4c..4c+3] = (min offset, min len, max offset, max len) of chunk c
-// (pass 1, blob == nullptr); pass 2 copies the bytes into blob at the running offset.
+// Binary statistics: meta[4c..4c+3] = (min offset, min len, max offset | eq << 63, max len) of
+// chunk c, eq = the min and max values are the same bytes (pass 1, blob == nullptr: what a
+// page-size probe needs for the header sizes); pass 2 copies the bytes into blob at the running
+// offset.
 __global__ void __launch_bounds__(KPW_BLOCK) k_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols,
                                                             const uint8_t *data, uint64_t *meta, uint8_t *blob)
 {
@@ -919,8 +921,12 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_stats_gather(const ChunkDesc *ch,
             bin = col.phys == 6 && C.nn > 0;   // has_minmax
             if (!blob) {
                 if (bin) {
-                    meta[4 * ci] = col.soff[C.smin]; meta[4 * ci + 1] = col.slen[C.smin];
-                    meta[4 * ci + 2] = col.soff[C.smax]; meta[4 * ci + 3] = col.slen[C.smax];
+                    const uint64_t o1 = col.soff[C.smin], o2 = col.soff[C.smax];
+                    const uint32_t l1 = col.slen[C.smin], l2 = col.slen[C.smax];
+                    bool eq = l1 == l2;
+                    for (uint32_t i = 0; eq && i < l1; i++) eq = data[o1 + i] == data[o2 + i];
+                    meta[4 * ci] = o1; meta[4 * ci + 1] = l1;
+                    meta[4 * ci + 2] = o2 | ((uint64_t)eq << 63); meta[4 * ci + 3] = l2;
                 } else {
                     meta[4 * ci] = meta[4 * ci + 1] = meta[4 * ci + 2] = meta[4 * ci + 3] = 0;
                 }
@@ -934,7 +940,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_stats_gather(const ChunkDesc *ch,
         if (ci < nchunks && bin) {
             const uint64_t l1 = meta[4 * ci + 1], l2 = meta[4 * ci + 3];
             for (uint64_t i = 0; i < l1; i++) blob[o + i] = data[meta[4 * ci] + i];
-            for (uint64_t i = 0; i < l2; i++) blob[o + l1 + i] = data[meta[4 * ci + 2] + i];
+            const uint64_t o2 = meta[4 * ci + 2] & ~(1ull << 63);
+            for (uint64_t i = 0; i < l2; i++) blob[o + l1 + i] = data[o2 + i];
         }
         carry += tot;
     }
