@@ -1,6 +1,6 @@
 #!/bin/bash
 # r05bg: the bench line's c5 key with the c5 leg before / after the c4 and bulk_multipage legs
-# (KPW_BENCH_C5_FIRST), alternated twice
+# (KPW_BENCH_C5_FIRST, a temporary bench knob removed after this measurement), alternated twice
 OUT=gpurun_out/r05bg
 mkdir -p $OUT
 B="python bench.py --no-cpu-baseline --no-resident --per-record-records 0 --per-record-64k-records 0 --steps 2 --warmup 1"
