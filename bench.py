@@ -176,15 +176,18 @@ def dist_init(world, local_rank, backend="nccl"):
     return dist
 
 
-def timed_steps(step, steps, warmup, dist=None, sync=lambda: None):
+def timed_steps(step, steps, warmup, dist=None, sync=lambda: None, on_start=None):
     """W untimed warmup steps, then exactly K timed steps bracketed by barrier + device sync
-    on both sides; returns (max-over-ranks elapsed seconds, per-step results)."""
+    on both sides; returns (max-over-ranks elapsed seconds, per-step results).  on_start runs
+    (untimed) right before the timed region."""
     for i in range(warmup):
         step(i)
     sync()
     if dist:
         dist.barrier()
     sync()
+    if on_start:
+        on_start()
     out = []
     t0 = time.perf_counter()
     for i in range(steps):
@@ -207,8 +210,27 @@ def reduce_scalar(x, dist=None, op="sum"):
     return float(t.item())
 
 
+def rank_memory(dist=None, pinned_sets=()):
+    """This rank's host-memory budget (N ranks share a node's host memory): the
+    library's pinned-cache cap (48 GB / LOCAL_WORLD_SIZE unless KPW_PIN_CACHE_GB is set,
+    memcache.cpp), its live and idle pinned bytes, the record sets this rank pinned, and the
+    worst case (sets + live + cap) maxed over ranks.  Reads allocator counters only (no GPU call)."""
+    import kpw
+    from kpw import _lib
+    st = _lib.cache_stats()
+    sets = sum(int(d.nbytes) + int(o.nbytes) for d, o in pinned_sets)
+    budget = sets + st["pin_cache_cap"] + max(0.0, st["pin_live"] - sets)
+    return dict(local_world_size=int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
+                pin_cache_cap_gb=round(st["pin_cache_cap"] / 1e9, 3), dev_cache_cap_gb=round(st["dev_cache_cap"] / 1e9, 3),
+                record_sets_pinned_gb=round(sets / 1e9, 3), pinned_live_gb=round(st["pin_live"] / 1e9, 3),
+                pinned_idle_gb=round(st["pin_idle"] / 1e9, 3),
+                pinned_budget_gb_max_over_ranks=round(reduce_scalar(budget, dist, "max") / 1e9, 3))
+
+
 def write_file(kpw, schema, props, data, offs, device, batch=POLL_BATCH):
-    """One ParquetFile through the drop-in: batches straight from (pinned) host memory."""
+    """One ParquetFile through the drop-in: batches straight from (pinned) host memory.
+    Returns (file size, pipeline stats); the stats carry the host wall of the writer's phases
+    (open, writes, close, stats, free: `phase_*_ms`), so the line shows where a step went."""
     t0 = time.perf_counter()
     pf = kpw.ParquetFile(None, schema, props, device=device)
     L, h = pf._L, pf._h
@@ -226,14 +248,27 @@ def write_file(kpw, schema, props, data, offs, device, batch=POLL_BATCH):
     t2 = time.perf_counter()
     pf.close()
     t3 = time.perf_counter()
-    res = L.kpw_writer_data_size(h), pf.pipeline_stats()   # after close: the file's length
+    size, stats = L.kpw_writer_data_size(h), pf.pipeline_stats()   # after close: the file's length
     t4 = time.perf_counter()
     pf.__del__()   # the writer (and its in-memory file) is released inside the step
+    t5 = time.perf_counter()
+    stats.update(phase_open_ms=(t1 - t0) * 1e3, phase_writes_ms=(t2 - t1) * 1e3, phase_close_ms=(t3 - t2) * 1e3,
+                 phase_stats_ms=(t4 - t3) * 1e3, phase_free_ms=(t5 - t4) * 1e3)
     if os.environ.get("KPW_TRACE") == "1":
         print("[bench] writer: open %.1f ms, writes %.1f ms, close %.1f ms, stats %.1f ms, free %.1f ms" % (
-            (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (t4 - t3) * 1e3, (time.perf_counter() - t4) * 1e3),
+            (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (t4 - t3) * 1e3, (t5 - t4) * 1e3),
             file=sys.stderr, flush=True)
-    return res
+    return size, stats
+
+
+PHASES = ("open", "writes", "close", "stats", "free")
+
+
+def cache_delta(before, after):
+    """Allocator calls and their host ms between two kpw_cache_stats snapshots."""
+    keys = ("dev_malloc_n", "dev_malloc_ms", "dev_free_n", "dev_free_ms", "pin_malloc_n", "pin_malloc_ms", "pin_free_n",
+            "pin_free_ms", "dev_retry")
+    return {k: round(after.get(k, 0.0) - before.get(k, 0.0), 2) for k in keys}
 
 
 def copy_ceiling(device, nbytes=2 << 30):
@@ -366,8 +401,11 @@ def c5_leg(kpw, device, steps, warmup):
     partitions of the 64-partition topic this GPU owns (seeds 0xC0FFEE05 + p), one concurrent
     kpw_writer per partition on its own thread (KafkaProtoParquetWriter.java:175-179), 125 M Rec8
     records per GPU (15.625 M per partition), SNAPPY, 128 MiB row groups, 500 k poll batches;
-    one step = all 8 files closed.  Same drop-in and timing as the headline."""
+    one step = all 8 files closed.  Same drop-in and timing as the headline.  Reports every
+    step's time, the writers' encode wall and phases, look-back fallbacks and the allocator
+    calls made inside the timed steps (the in-line leg against the standalone one)."""
     import synth
+    from kpw import _lib
     kind, n, wseed, wdesc = WORKLOADS["c5"]
     sschema = synth.SCHEMAS[kind]
     schema = kpw.Schema(sschema.message_name, sschema.columns, sschema.proto_class)
@@ -385,23 +423,88 @@ def c5_leg(kpw, device, steps, warmup):
             except Exception as e:  # noqa: BLE001
                 errs.append(e)
         ts = [threading.Thread(target=one, args=(k,)) for k in range(len(parts))]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
+        t = time.perf_counter()
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join()
         if errs:
             raise errs[0]
-        return sum(size for size, _ in res)
+        return time.perf_counter() - t, res
 
     for _ in range(warmup):
         step()
+    c0 = _lib.cache_stats()
     t0 = time.perf_counter()
-    file_bytes = sum(step() for _ in range(steps))
+    outs = [step() for _ in range(steps)]
     dt = time.perf_counter() - t0
+    c1 = _lib.cache_stats()
+    file_bytes = sum(size for _, res in outs for size, _ in res)
+    sts = [st for _, res in outs for _, st in res]
+    enc = [st.get("worker_encode_wall_ms", 0.0) for st in sts]
     return dict(value=round(nb * steps / dt / 1e9, 4), unit="GB/s", records_per_s=round(steps * per * len(parts) / dt, 1),
-                ms_per_step=round(dt / steps * 1e3, 3), steps=steps, warmup=warmup, records_per_step=per * len(parts),
-                bytes_per_step=nb, file_bytes_per_step=int(file_bytes / steps), writers=len(parts),
-                records_per_writer=per, workload=wdesc + ", 128 MiB row groups, 500 k poll batches")
+                ms_per_step=round(dt / steps * 1e3, 3), step_ms=[round(t * 1e3, 1) for t, _ in outs], steps=steps,
+                warmup=warmup, records_per_step=per * len(parts), bytes_per_step=nb,
+                file_bytes_per_step=int(file_bytes / steps), writers=len(parts), records_per_writer=per,
+                writer_encode_wall_ms=dict(mean=round(float(np.mean(enc)), 2), max=round(float(np.max(enc)), 2)),
+                writer_phase_ms_mean={ph: round(float(np.mean([st["phase_%s_ms" % ph] for st in sts])), 2)
+                                      for ph in PHASES},
+                jobs_per_writer=round(float(np.mean([st.get("jobs", 0.0) for st in sts])), 2),
+                lookback_fallbacks=int(sum(st.get("lookback_fallbacks", 0.0) for st in sts)),
+                allocator_in_timed_steps=cache_delta(c0, c1),
+                hw_queues=os.environ.get("GPU_MAX_HW_QUEUES"),
+                workload=wdesc + ", 128 MiB row groups, 500 k poll batches")
+
+
+def c1_leg(kpw, device, steps=5, threads=1):
+    """BASELINE config 1: 1 M Rec8 records -> ONE UNCOMPRESSED Parquet file
+    (128 MiB row groups and pages), through the GPU writer (pinned host records in, closed
+    in-memory file out; median of `steps` files after one warm-up) and through the CPU oracle
+    (kind "port") on one core and on `threads` cores (one 1 M-record file per thread)."""
+    import synth
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    kind, n, seed = synth.KIND_REC8, 1_000_000, 0xC0FFEE01
+    sschema = synth.SCHEMAS[kind]
+    schema = kpw.Schema(sschema.message_name, sschema.columns, sschema.proto_class)
+    props = kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=kpw.UNCOMPRESSED, page_size=128 * MiB)
+    data, offs = synth.generate(kind, seed, n, alloc=kpw.pinned_empty)
+    nb = int(offs[-1])
+    write_file(kpw, schema, props, data, offs, device)
+    ts = []
+    for _ in range(steps):
+        t = time.perf_counter()
+        write_file(kpw, schema, props, data, offs, device)
+        ts.append(time.perf_counter() - t)
+    gpu_s = float(np.median(ts))
+    oprops = oracle.make_props(codec=oracle.UNCOMPRESSED)
+    hd, ho = np.array(data), np.array(offs)
+    oracle.encode_file(sschema, hd, ho, oprops)
+    one = []
+    for _ in range(3):
+        t = time.perf_counter()
+        oracle.encode_file(sschema, hd, ho, oprops)
+        one.append(time.perf_counter() - t)
+    one_s = float(np.median(one))
+
+    def work():
+        oracle.encode_file(sschema, hd, ho, oprops)
+    th = [threading.Thread(target=work) for _ in range(threads)]
+    t = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    all_s = time.perf_counter() - t
+    return dict(value=round(nb / gpu_s / 1e9, 4), unit="GB/s", records_per_s=round(n / gpu_s, 1),
+                ms_per_file=round(gpu_s * 1e3, 3), records=n, bytes=nb, codec="UNCOMPRESSED",
+                oracle_1core=dict(value=round(nb / one_s / 1e9, 4), records_per_s=round(n / one_s, 1),
+                                  ms_per_file=round(one_s * 1e3, 2), cores=1, kind="port"),
+                oracle_all_cores=dict(value=round(threads * nb / all_s / 1e9, 4),
+                                      records_per_s=round(threads * n / all_s, 1), cores=threads, kind="port",
+                                      sample="%d files of the same 1 M records, one per thread" % threads),
+                workload="C1: 1 M Rec8 records, UNCOMPRESSED, 128 MiB row groups, one file (GPU: median of %d files)"
+                         % steps)
 
 
 def cpu_baseline_per_record(sschema, kind, seed, n, max_file_size, page_size):
@@ -575,7 +678,11 @@ def main():
             raise errs[0]
         return res, set_bytes[i % len(sets)]
 
-    elapsed, outs = timed_steps(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    from kpw import _lib as kpw_lib
+    cs = {}
+    elapsed, outs = timed_steps(step, args.steps, args.warmup, dist, torch.cuda.synchronize,
+                                on_start=lambda: cs.update(before=kpw_lib.cache_stats()))
+    cs["after"] = kpw_lib.cache_stats()
     my_bytes = sum(b for _, b in outs)
     total_bytes = reduce_scalar(my_bytes, dist)
     total_records = reduce_scalar(n * args.steps, dist)
@@ -588,6 +695,9 @@ def main():
             for k, v in st.items():
                 agg[k] = agg.get(k, 0.0) + v
     file_bytes = sum(size for res, _ in outs for size, _ in res)
+
+    # host-memory budget of the ranks sharing this node (a collective: every rank calls it)
+    mem = rank_memory(dist, pinned_sets=[x for ss in sets for x in ss])
 
     resident = None
     if not args.no_resident and args.workload != "c5" and rank == 0:
@@ -646,16 +756,21 @@ def main():
     if args.per_record_64k_records and world == 1:   # 64 KiB pages: a size probe every ~2-3 k records
         per_record_64k = per_record_leg(kpw, schema, sschema, kind, wseed, args.per_record_64k_records, local_rank,
                                         args.per_record_max_file_mb * MiB, 64 * 1024)
-    c4_leg = bulk_mp = c5 = gz = None
+    c4_leg = bulk_mp = c5 = gz = c3_leg = c1 = None
     if args.secondary_steps and world == 1 and args.workload == "c2":
         # the config where encode, not PCIe, sets the pace (C4), and bulk writes with 1 MiB pages
         c4k, c4n, c4seed, _ = WORKLOADS["c4"]
         c4_leg = writer_leg(kpw, c4k, c4seed, c4n, local_rank, args.secondary_steps, 1)
         bulk_mp = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, page_size=MiB,
                              sets=[s[0] for s in sets])
-        c5 = c5_leg(kpw, local_rank, args.secondary_steps, 1)
+        c5 = c5_leg(kpw, local_rank, max(3, args.secondary_steps), 1)
+        # BASELINE config 3 (wide telemetry schema), 10 M records, its own writer line
+        c3k, c3n, c3seed, _ = WORKLOADS["c3"]
+        c3_leg = writer_leg(kpw, c3k, c3seed, c3n, local_rank, max(3, args.secondary_steps), 1)
         # the same C2 records with CompressionCodecName.GZIP (no BASELINE config; K7' k_deflate.hip)
         gz = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, sets=[s[0] for s in sets], codec=kpw.GZIP)
+    if args.secondary_steps and world == 1 and args.workload == "c2" and not args.no_cpu_baseline:
+        c1 = c1_leg(kpw, local_rank, threads=args.cpu_threads or host_threads())   # BASELINE config 1
     cpu = None
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         threads = args.cpu_threads or host_threads()
@@ -692,7 +807,12 @@ def main():
         "file_bytes_per_step": int(file_bytes / max(1, args.steps)),
         "encode_jobs_per_step": round(jobs / args.steps, 2),
         "worker_encode_wall_ms_per_step": round(agg.get("worker_encode_wall_ms", 0) / args.steps, 2),
+        # host wall of each writer phase (write_file), summed over the step's writers
+        "writer_phase_ms_per_step": {ph: round(agg.get("phase_%s_ms" % ph, 0.0) / args.steps, 2) for ph in PHASES},
+        "lookback_fallbacks": int(agg.get("lookback_fallbacks", 0)),
+        "allocator_in_timed_steps": cache_delta(cs.get("before", {}), cs["after"]),
         "stage_ms_per_step": {k: round(v / args.steps, 3) for k, v in stage_ms.items()},
+        "rank_memory": mem,
         "resident_encode": resident,
         "roofline": roof,
         "stage_roofline": stage_roof,
@@ -702,6 +822,8 @@ def main():
         "c4": c4_leg,
         "bulk_multipage": bulk_mp,
         "c5": c5,
+        "c3": c3_leg,
+        "c1": c1,
         "gzip": gz,
         "cpu_baseline": cpu,
     }

@@ -72,10 +72,19 @@ void kpw_host_free(void *p);
 
 /* The library keeps freed HBM and pinned blocks for the next writer (a writer is one file and
  * files rotate; hipFree synchronises the device): up to KPW_DEV_CACHE_GB per device (default 96)
- * and KPW_PIN_CACHE_GB pinned (default 48), read once per process.  This releases every idle
- * block now (e.g. before a co-located consumer or framework allocates).  Thread-safe.  No
+ * and KPW_PIN_CACHE_GB pinned per process (default 48 GB divided by LOCAL_WORLD_SIZE, the ranks
+ * sharing the host), read once per process.  This releases every idle block and idle pooled
+ * stream set now (e.g. before a co-located consumer or framework allocates).  Thread-safe.  No
  * reference counterpart (the JVM writer allocates on the Java heap). */
 void kpw_trim_caches(void);
+
+/* Allocator figures of this process: [0] device cache cap (bytes), [1] pinned cache cap,
+ * [2] device bytes live, [3] device bytes idle in the cache, [4] pinned bytes live, [5] pinned
+ * bytes idle, [6] hipMalloc calls, [7] their host ms, [8] hipFree calls, [9] their ms,
+ * [10] hipHostMalloc calls, [11] ms, [12] hipHostFree calls, [13] ms, [14] device cache hits,
+ * [15] pinned cache hits, [16] hipMalloc failures retried after releasing the idle blocks.
+ * Returns the number of entries written (<= cap).  Diagnostics; no reference counterpart. */
+int kpw_cache_stats(double *out, int cap);
 
 /* The WorkerThread size-rotation loop (KafkaProtoParquetWriter.java:277-285,306-308):
  * writes records in order and stops right after the first one for which
@@ -105,7 +114,9 @@ int64_t kpw_writer_failed_record(const kpw_writer *w); /* -1 if none */
  * bytes, [4] compressed page bytes, [5..14] device milliseconds per stage summed over jobs
  * (HIP events on the encoder's stream, kpw_encoder_stage_times order), [15] encode wall
  * milliseconds of the worker thread, [16] scan look-backs that recomputed a predecessor tile
- * instead of waiting longer (exact either way).  Returns the number of entries written (<= cap). */
+ * instead of waiting longer (exact either way; every look-back scan runs inside the encoders —
+ * the writer's own record-offsets scan is reduce-then-scan and has none).  Returns the number
+ * of entries written (<= cap). */
 int kpw_writer_stats(kpw_writer *w, double *out, int cap);
 const char *kpw_writer_last_error(const kpw_writer *w);
 void kpw_writer_free(kpw_writer *w);

@@ -29,6 +29,25 @@
 //                ISIZE) and packed in page order.
 // (Round 5 before this: one lane per page ran the parse and the bit stream, ~minutes for a
 // 128 MiB page, the reference's default page size.)
+//
+// ATTRIBUTION: the per-block tree code below (smaller, pqdownheap, gen_bitlen, build_tree,
+// gen_codes, scan_tree / send_tree, build_bl_tree and the stored / static / dynamic choice of
+// _tr_flush_block) follows zlib 1.2.11's trees.c closely, names, locals and control flow
+// included: byte identity with zlib needs its exact heap tie-breaks.  This is an ALTERED
+// version (restated as device code for one configuration), not the original.  zlib is
+//   Copyright (C) 1995-2017 Jean-loup Gailly and Mark Adler
+// and distributed under the zlib license:
+//   This software is provided 'as-is', without any express or implied warranty.  In no event
+//   will the authors be held liable for any damages arising from the use of this software.
+//   Permission is granted to anyone to use this software for any purpose, including commercial
+//   applications, and to alter it and redistribute it freely, subject to the following
+//   restrictions:
+//   1. The origin of this software must not be misrepresented; you must not claim that you
+//      wrote the original software.  If you use this software in a product, an acknowledgment
+//      in the product documentation would be appreciated but is not required.
+//   2. Altered source versions must be plainly marked as such, and must not be misrepresented
+//      as being the original software.
+//   3. This notice may not be removed or altered from any source distribution.
 #include "kpw_chunk.h"
 #include "kpw_device.h"
 

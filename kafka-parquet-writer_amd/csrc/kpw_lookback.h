@@ -154,6 +154,11 @@ __device__ __forceinline__ T lb_tile(const LbView &L, uint32_t sbase, uint32_t t
             if (!inc_now) lb_publish(L, sbase + tile, Enc::enc(Op::op(c, agg)), LB_ST_INC);
         }
     }
+    // Published before overwritten: an in-place scan's tile stores its outputs over its inputs
+    // after this barrier, and a fallback that recomputes this tile (lb_lookback) trusts its
+    // inputs only while it still sees no status word.  The agent-scope release fence makes the
+    // publish visible at L2 before any thread of the tile passes the barrier to store.
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     const T c = *slot;
     __syncthreads();

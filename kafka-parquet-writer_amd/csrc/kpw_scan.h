@@ -26,9 +26,10 @@ void launch_plan_prefix(const uint8_t *ev, uint32_t *E8, uint32_t nev, uint64_t 
 // Status words for one single-pass launch over `nwords` tiles x scans (w == nullptr: the
 // scratch could not grow, sc->failed set; the caller skips the launch).
 LbView lb_prepare(SegScratch *sc, uint64_t nwords, hipStream_t s);
-// look-back timeouts counted on this scratch since the previous call, which it clears
-// (kpw_lookback.h; 0 unless a tile waited past the spin bound: the scans' results are then
-// wrong), -1 if unreadable.  Synchronises `s` (the stream the scans ran on).
+// look-back fallbacks counted on this scratch since the previous call, which it clears
+// (kpw_lookback.h: a tile that waited past the spin bound recomputed its predecessor's status;
+// the scans' results stay exact, the count is a health figure), -1 if unreadable.
+// Synchronises `s` (the stream the scans ran on).
 int lb_failures(SegScratch *sc, hipStream_t s);
 
 // Exclusive segmented scan over tile aggregates (same scratch contract).

@@ -1,6 +1,7 @@
 // memcache.cpp — see memcache.h.
 #include "memcache.h"
 
+#include <chrono>
 #include <cstdint>
 #include <cstdlib>
 #include <map>
@@ -18,7 +19,18 @@ size_t cap_gb(const char *env, size_t dflt)
     const long long v = atoll(e);
     return v > 0 ? (size_t)v << 30 : 0;
 }
-// idle memory kept (KPW_DEV_CACHE_GB per device / KPW_PIN_CACHE_GB; 0 = keep nothing idle)
+// Processes sharing this host (torchrun's LOCAL_WORLD_SIZE: one rank per GPU of the node).
+size_t local_ranks()
+{
+    const char *e = getenv("LOCAL_WORLD_SIZE");
+    const long long v = e ? atoll(e) : 1;
+    return v > 1 ? (size_t)v : 1;
+}
+// idle memory kept (KPW_DEV_CACHE_GB per device / KPW_PIN_CACHE_GB; 0 = keep nothing idle).
+// The device cap is per device, and each rank owns its device; pinned memory is the host's, so
+// its default (48 GB) is shared by the ranks of the node: 48 / LOCAL_WORLD_SIZE per process
+// (8 ranks: 6 GB each, on top of each rank's own pinned record batches).  An explicit
+// KPW_PIN_CACHE_GB is per process.
 size_t dev_cache_cap()
 {
     static const size_t v = cap_gb("KPW_DEV_CACHE_GB", 96);
@@ -26,8 +38,17 @@ size_t dev_cache_cap()
 }
 size_t pin_cache_cap()
 {
-    static const size_t v = cap_gb("KPW_PIN_CACHE_GB", 48);
+    static const size_t v = [] {
+        const char *e = getenv("KPW_PIN_CACHE_GB");
+        if (e && *e) return cap_gb("KPW_PIN_CACHE_GB", 48);
+        return (size_t)(48ull << 30) / local_ranks();
+    }();
     return v;
+}
+
+double mono_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 struct Pool {
@@ -50,6 +71,43 @@ std::map<uintptr_t, size_t> g_pin_live;     // live pinned blocks (pin_contains)
 std::map<void *, int> g_dev_of;             // device of every block dev_alloc handed out
                                             // (hipPointerGetAttributes per free cost ~0.3 ms)
 std::vector<Deferred> g_deferred;
+// allocator counters (kpw_cache_stats): calls into the HIP allocator and the host time they took
+struct Counters {
+    double dev_malloc_n = 0, dev_malloc_ms = 0, dev_free_n = 0, dev_free_ms = 0;
+    double pin_malloc_n = 0, pin_malloc_ms = 0, pin_free_n = 0, pin_free_ms = 0;
+    double dev_hits = 0, pin_hits = 0, dev_live = 0, pin_live = 0, dev_retry = 0;
+} g_cnt;
+
+hipError_t timed_malloc(void **q, size_t bytes)
+{
+    const double t = mono_ms();
+    const hipError_t e = hipMalloc(q, bytes);
+    g_cnt.dev_malloc_n++;
+    g_cnt.dev_malloc_ms += mono_ms() - t;
+    return e;
+}
+void timed_free(void *q)
+{
+    const double t = mono_ms();
+    (void)hipFree(q);
+    g_cnt.dev_free_n++;
+    g_cnt.dev_free_ms += mono_ms() - t;
+}
+hipError_t timed_host_malloc(void **q, size_t bytes)
+{
+    const double t = mono_ms();
+    const hipError_t e = hipHostMalloc(q, bytes, hipHostMallocDefault);
+    g_cnt.pin_malloc_n++;
+    g_cnt.pin_malloc_ms += mono_ms() - t;
+    return e;
+}
+void timed_host_free(void *q)
+{
+    const double t = mono_ms();
+    (void)hipHostFree(q);
+    g_cnt.pin_free_n++;
+    g_cnt.pin_free_ms += mono_ms() - t;
+}
 
 // best fit within 2x (and never more than 1 GiB of slack)
 void *take(Pool &p, size_t bytes)
@@ -80,7 +138,7 @@ void trim(Pool &p, size_t keep, FreeFn fn)
 void dev_release(void *b)
 {
     g_dev_of.erase(b);
-    (void)hipFree(b);
+    timed_free(b);
 }
 
 // a block of ours back into its pool (under g_mu)
@@ -88,9 +146,10 @@ void dev_return(void *q, int dev)
 {
     Pool &p = g_dev[dev];
     auto it = p.size_.find(q);
-    if (it == p.size_.end()) { (void)hipFree(q); return; }
+    if (it == p.size_.end()) { timed_free(q); return; }
     p.free_.emplace(it->second, q);
     p.free_bytes += it->second;
+    g_cnt.dev_live -= (double)it->second;
     trim(p, dev_cache_cap(), dev_release);
 }
 
@@ -119,16 +178,22 @@ void *dev_alloc(size_t bytes)
     std::lock_guard<std::mutex> g(g_mu);
     if (!g_deferred.empty()) reap(false);
     Pool &p = g_dev[dev];
-    if (void *q = take(p, bytes)) return q;
+    if (void *q = take(p, bytes)) {
+        g_cnt.dev_hits++;
+        g_cnt.dev_live += (double)p.size_[q];
+        return q;
+    }
     void *q = nullptr;
-    if (hipMalloc(&q, bytes) != hipSuccess) {
+    if (timed_malloc(&q, bytes) != hipSuccess) {
         (void)hipGetLastError();
+        g_cnt.dev_retry++;
         reap(true);
         trim(p, 0, dev_release);   // give the idle blocks back and retry
-        if (hipMalloc(&q, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+        if (timed_malloc(&q, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
     }
     p.size_[q] = bytes;
     g_dev_of[q] = dev;
+    g_cnt.dev_live += (double)bytes;
     return q;
 }
 
@@ -137,7 +202,7 @@ void dev_free(void *q)
     if (!q) return;
     std::lock_guard<std::mutex> g(g_mu);
     auto d = g_dev_of.find(q);
-    if (d == g_dev_of.end()) { (void)hipFree(q); return; }   // not ours
+    if (d == g_dev_of.end()) { timed_free(q); return; }   // not ours
     dev_return(q, d->second);
 }
 
@@ -157,7 +222,7 @@ void dev_free_after(void *q, hipStream_t s)
     if (d == g_dev_of.end()) {   // not ours: a plain free after the stream
         (void)hipEventSynchronize(ev);
         (void)hipEventDestroy(ev);
-        (void)hipFree(q);
+        timed_free(q);
         return;
     }
     g_deferred.push_back(Deferred{q, d->second, ev});
@@ -168,15 +233,17 @@ void *pin_alloc(size_t bytes)
     if (bytes < 4096) bytes = 4096;
     std::lock_guard<std::mutex> g(g_mu);
     void *q = take(g_pin, bytes);
+    if (q) g_cnt.pin_hits++;
     if (!q) {
-        if (hipHostMalloc(&q, bytes, hipHostMallocDefault) != hipSuccess) {
+        if (timed_host_malloc(&q, bytes) != hipSuccess) {
             (void)hipGetLastError();
-            trim(g_pin, 0, [](void *b) { (void)hipHostFree(b); });
-            if (hipHostMalloc(&q, bytes, hipHostMallocDefault) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+            trim(g_pin, 0, timed_host_free);
+            if (timed_host_malloc(&q, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
         }
         g_pin.size_[q] = bytes;
     }
     g_pin_live[(uintptr_t)q] = g_pin.size_[q];
+    g_cnt.pin_live += (double)g_pin.size_[q];
     return q;
 }
 
@@ -187,9 +254,10 @@ void pin_free(void *q)
     auto it = g_pin.size_.find(q);
     if (it == g_pin.size_.end()) return;
     g_pin_live.erase((uintptr_t)q);
+    g_cnt.pin_live -= (double)it->second;
     g_pin.free_.emplace(it->second, q);
     g_pin.free_bytes += it->second;
-    trim(g_pin, pin_cache_cap(), [](void *b) { (void)hipHostFree(b); });
+    trim(g_pin, pin_cache_cap(), timed_host_free);
 }
 
 size_t pin_size(const void *q)
@@ -210,12 +278,32 @@ bool pin_contains(const void *q, size_t n)
     return (uintptr_t)q >= it->first && (uintptr_t)q + n <= it->first + it->second;
 }
 
+void stream_sets_trim();
+
 void trim_caches()
 {
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        reap(true);
+        for (auto &p : g_dev) trim(p, 0, dev_release);
+        trim(g_pin, 0, timed_host_free);
+    }
+    stream_sets_trim();   // idle pooled stream sets too
+}
+
+int cache_stats(double *out, int cap)
+{
+    size_t dev_idle = 0;
     std::lock_guard<std::mutex> g(g_mu);
-    reap(true);
-    for (auto &p : g_dev) trim(p, 0, dev_release);
-    trim(g_pin, 0, [](void *b) { (void)hipHostFree(b); });
+    for (auto &p : g_dev) dev_idle += p.free_bytes;
+    const double v[] = {(double)dev_cache_cap(), (double)pin_cache_cap(), g_cnt.dev_live, (double)dev_idle,
+                        g_cnt.pin_live, (double)g_pin.free_bytes, g_cnt.dev_malloc_n, g_cnt.dev_malloc_ms,
+                        g_cnt.dev_free_n, g_cnt.dev_free_ms, g_cnt.pin_malloc_n, g_cnt.pin_malloc_ms,
+                        g_cnt.pin_free_n, g_cnt.pin_free_ms, g_cnt.dev_hits, g_cnt.pin_hits, g_cnt.dev_retry};
+    const int n = (int)(sizeof(v) / sizeof(v[0]));
+    int k = 0;
+    for (; k < n && k < cap; k++) out[k] = v[k];
+    return k;
 }
 
 // ---------------------------------------------------------------- streams
@@ -258,6 +346,17 @@ hipError_t stream_set_acquire(int n, hipStream_t *s)
     return hipSuccess;
 }
 
+void stream_sets_trim()
+{
+    std::vector<StreamSet> idle;
+    {
+        std::lock_guard<std::mutex> g(g_smu);
+        idle.swap(g_sets);
+    }
+    for (auto &t : idle)
+        for (int k = 0; k < t.n; k++) if (t.s[k]) (void)hipStreamDestroy(t.s[k]);
+}
+
 void stream_set_release(int n, const hipStream_t *s)
 {
     if (n <= 0 || n > 8 || !s[0]) return;
@@ -278,3 +377,4 @@ void stream_set_release(int n, const hipStream_t *s)
 }  // namespace kpw
 
 extern "C" void kpw_trim_caches(void) { kpw::trim_caches(); }
+extern "C" int kpw_cache_stats(double *out, int cap) { return out && cap > 0 ? kpw::cache_stats(out, cap) : 0; }

@@ -10,7 +10,8 @@
 // stream's queued work has passed an event, without a device-wide synchronisation).
 //
 // Idle memory kept: KPW_DEV_CACHE_GB per device (default 96 of 288 GB: C5 runs 8 writers per
-// GPU and re-opens them every file) and KPW_PIN_CACHE_GB of pinned host memory (default 48);
+// GPU and re-opens them every file) and KPW_PIN_CACHE_GB of pinned host memory per process
+// (default 48 GB shared by the node's ranks: 48 / LOCAL_WORLD_SIZE);
 // kpw_trim_caches() (kpw_gpu.h) releases every idle block, e.g. before a co-located consumer
 // allocates.
 #pragma once
@@ -26,7 +27,8 @@ void *pin_alloc(size_t bytes);     // page-locked host memory; nullptr on failur
 void pin_free(void *p);            // nullptr ok
 size_t pin_size(const void *p);    // usable bytes of a pin_alloc block containing p (0 if none)
 bool pin_contains(const void *p, size_t n);   // [p, p+n) inside one live pin_alloc block
-void trim_caches();                // release every idle block (device pools and pinned)
+void trim_caches();                // release every idle block (device pools, pinned, stream sets)
+int cache_stats(double *out, int cap);   // kpw_cache_stats (kpw_gpu.h)
 // Sets of n non-blocking HIP streams of the current device, kept across writers:
 // hipStreamDestroy takes ~2.5 ms (a writer tears down four streams per file, and the reference
 // opens a file per rotation).  A set is created stream after stream and reused whole: HIP gives

@@ -289,6 +289,9 @@ struct kpw_writer {
     uint64_t fill_gen = 0, pr_gen = ~0ull;   // fill buffer generation / the one pr_off describes
     size_t pr_up = 0;                  // boundaries of that generation already on the device
     bool dirty = false;                // records appended since the last PLANNED job (model off)
+    bool size_polled = false;          // getDataSize() was called on the bulk path: later write-path
+                                       // jobs plan their open row group (no lazy jobs), so
+                                       // each later call does not submit a planning job of its own
     bool pending_cut = false;          // an EXACT job may not be in the file yet (lastRowGroupEndPos stale)
     DevBuf probe_off;                  // write_until_full on the bulk path: offsets of staged prefixes
     PinnedBuf probe_h;
@@ -1214,7 +1217,7 @@ static int submit(kpw_writer *w, int kind, int64_t n_exact, bool exact_open = fa
             fprintf(stderr, "[kpw] submit job %llu kind=%d new records=%lld (%.0f MiB) at %.1f ms, %d in flight, %d queued\n",
                     (unsigned long long)w->next_seq, kind, (long long)F.ends.size(), (F.len - F.gap) / 1048576.0,
                     now_ms() - w->t_open, w->inflight, (int)w->q.size());
-        w->q.push_back(Job{f, kind, next, n_exact, w->next_seq++, kind == JOB_PLANNED && !exact_open});
+        w->q.push_back(Job{f, kind, next, n_exact, w->next_seq++, kind == JOB_PLANNED && !exact_open && !w->size_polled});
         w->cv.notify_all();
     }
     if (kind == JOB_PLANNED) w->dirty = false;
@@ -1976,6 +1979,7 @@ extern "C" int64_t kpw_writer_data_size(kpw_writer *w)
             }
             return w->last_rg_end + w->model.buffered();
         }
+        w->size_polled = true;
         if (w->dirty && submit(w, JOB_PLANNED, 0, true)) return -1;   // encode what is staged (completed row groups flushed)
         if (drain(w)) return -1;
         if (observe_failure(w)) return -1;

@@ -155,6 +155,7 @@ def load_library():
     L.kpw_host_free.argtypes = [vp]
     L.kpw_trim_caches.argtypes = []
     L.kpw_trim_caches.restype = None
+    L.kpw_cache_stats.argtypes = [ctypes.POINTER(ctypes.c_double), i32]
     L.kpw_device_alloc.restype = vp
     L.kpw_device_alloc.argtypes = [i32, u64, ctypes.POINTER(i32)]
     L.kpw_device_free.argtypes = [vp]
@@ -170,4 +171,17 @@ EXPORTED = ["kpw_writer_open", "kpw_writer_write", "kpw_writer_write_async", "kp
             "kpw_writer_failed_record", "kpw_writer_last_error", "kpw_writer_free", "kpw_encoder_create",
             "kpw_encoder_destroy", "kpw_encoder_last_error", "kpw_encoder_encode", "kpw_encoder_copy_pages",
             "kpw_encoder_stage_times", "kpw_host_alloc", "kpw_host_free", "kpw_writer_stats", "kpw_trim_caches",
-            "kpw_device_alloc", "kpw_device_free", "kpw_copy_h2d", "kpw_copy_d2h"]
+            "kpw_cache_stats", "kpw_device_alloc", "kpw_device_free", "kpw_copy_h2d", "kpw_copy_d2h"]
+
+
+CACHE_STATS = ["dev_cache_cap", "pin_cache_cap", "dev_live", "dev_idle", "pin_live", "pin_idle", "dev_malloc_n",
+               "dev_malloc_ms", "dev_free_n", "dev_free_ms", "pin_malloc_n", "pin_malloc_ms", "pin_free_n",
+               "pin_free_ms", "dev_hits", "pin_hits", "dev_retry"]
+
+
+def cache_stats():
+    """kpw_cache_stats as a dict (process-wide allocator figures, include/kpw_gpu.h)."""
+    L = load_library()
+    buf = (ctypes.c_double * len(CACHE_STATS))()
+    k = L.kpw_cache_stats(buf, len(CACHE_STATS))
+    return {name: buf[i] for i, name in enumerate(CACHE_STATS[:k])}

@@ -25,6 +25,26 @@
  * own bundled zlib build is parity unpinned (no JVM here); zlib's level-6 output has been
  * stable across 1.2.x.  Input chunking (Java writes a page's rl / dl / values parts
  * separately) does not change zlib's output for Z_NO_FLUSH writes; the whole page is fed at once.
+ *
+ * ATTRIBUTION: the deflate_slow / longest_match restatement and the trees.c routines below
+ * (pqdownheap, gen_bitlen, gen_codes, build_tree, scan_tree, send_tree, build_bl_tree,
+ * compress_block, _tr_flush_block, _tr_stored_block) follow zlib 1.2.11's deflate.c and trees.c
+ * closely, names and control flow included: byte identity with zlib needs its exact heap
+ * tie-breaks and block decisions.  This is an ALTERED version of that code (restated in one
+ * file for a single configuration), not the original.  zlib is
+ *   Copyright (C) 1995-2017 Jean-loup Gailly and Mark Adler
+ * and distributed under the zlib license:
+ *   This software is provided 'as-is', without any express or implied warranty.  In no event
+ *   will the authors be held liable for any damages arising from the use of this software.
+ *   Permission is granted to anyone to use this software for any purpose, including commercial
+ *   applications, and to alter it and redistribute it freely, subject to the following
+ *   restrictions:
+ *   1. The origin of this software must not be misrepresented; you must not claim that you
+ *      wrote the original software.  If you use this software in a product, an acknowledgment
+ *      in the product documentation would be appreciated but is not required.
+ *   2. Altered source versions must be plainly marked as such, and must not be misrepresented
+ *      as being the original software.
+ *   3. This notice may not be removed or altered from any source distribution.
  */
 #include <stdint.h>
 #include <stdlib.h>

@@ -29,8 +29,11 @@ for a in range(0, n, batch):
     if ow is not None:
         st, nw = ow.write_batch(data, offs[a:b + 1])
         assert st == 0 and nw == b - a, (st, nw)
-        got, want = pf.get_data_size(), ow.data_size()
-        assert got == want, (a, got, want)
+        # the first getDataSize comes after three batches, so it finds a lazy job's unknown open
+        # row group; from then on the writer plans every job's open row group (size_polled)
+        if a >= 3 * batch:
+            got, want = pf.get_data_size(), ow.data_size()
+            assert got == want, (a, got, want)
 pf.close()
 fb = pf.file_bytes()
 ob = oracle.encode_file(synth.REC8, data, offs, oprops)

@@ -22,7 +22,8 @@ def _free_port():
 
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    os.environ.pop("KPW_PIN_CACHE_GB", None)
     sys.path.insert(0, ROOT)
     for p in ("synth", "oracle", "kafka-parquet-writer_amd"):
         sys.path.insert(0, os.path.join(ROOT, p))
@@ -43,7 +44,9 @@ def _worker(rank, world, port, q):
 
     elapsed, outs = bench.timed_steps(step, steps=3, warmup=2, dist=dist)
     units = bench.reduce_scalar(100 * (rank + 1), dist)
-    q.put((rank, elapsed, calls, outs, units))
+    # the per-rank host-memory budget bench.py reports at N>1 (library caps, no GPU call)
+    mem = bench.rank_memory(dist, pinned_sets=[(data, offs)])
+    q.put((rank, elapsed, calls, outs, units, mem))
     dist.destroy_process_group()
 
 
@@ -59,12 +62,18 @@ def test_two_rank_timing_and_units():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, e0, c0, o0, u0), (r1, e1, c1, o1, u1) = res
+    (r0, e0, c0, o0, u0, m0), (r1, e1, c1, o1, u1, m1) = res
     assert c0 == c1 == [0, 1, 2, 3, 4]         # warmup 2 + exactly 3 timed steps
     assert o0 == [0, 0, 0] and o1 == [1, 1, 1]
     assert e0 == pytest.approx(e1)             # every rank reports the max over ranks
     assert e0 >= 3 * 0.1 * 0.95                # ... which is the slow rank's time
     assert u0 == u1 == 300                     # whole-job units = sum over ranks
+    # pinned cache cap shared by the node's ranks: 48 GB / LOCAL_WORLD_SIZE per process
+    assert m0["pin_cache_cap_gb"] == m1["pin_cache_cap_gb"] == pytest.approx(48 * 2 ** 30 / 2 / 1e9, rel=1e-3)
+    assert m0["local_world_size"] == 2
+    # every rank's worst-case pinned total: its record sets + the cache cap (max over ranks)
+    assert m0["pinned_budget_gb_max_over_ranks"] == m1["pinned_budget_gb_max_over_ranks"]
+    assert m0["pinned_budget_gb_max_over_ranks"] >= m0["pin_cache_cap_gb"]
 
 
 def test_partition_assignment_disjoint():

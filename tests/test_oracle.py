@@ -85,6 +85,47 @@ def test_deflate_matches_zlib(i):
     assert gzip.decompress(oracle.gzip_compress(data)) == data
 
 
+def test_deflate_matches_zlib_16mib():
+    """A 16 MiB input (hundreds of window slides, ~1000 blocks): text, PLAIN int64, zero runs,
+    incompressible stretches and JSON, interleaved in 1 MiB pieces, byte-identical to zlib."""
+    import gzip
+    rng = np.random.default_rng(16)
+    parts = []
+    ins = _deflate_inputs()
+    for k in range(16):
+        m = k % 4
+        if m == 0:
+            parts.append((ins[12] * 6)[:MiB])
+        elif m == 1:
+            parts.append(np.cumsum(rng.integers(0, 5000, MiB // 8), dtype=np.int64).astype("<i8").tobytes())
+        elif m == 2:
+            parts.append(bytes(MiB // 2) + rng.integers(0, 256, MiB // 2, dtype=np.uint8).tobytes())
+        else:
+            parts.append(rng.integers(0, 7, MiB, dtype=np.uint8).tobytes())
+    data = b"".join(parts)
+    assert len(data) == 16 * MiB
+    member = oracle.gzip_compress(data)
+    assert member == _zlib_gzip_member(data)
+    assert gzip.decompress(member) == data
+
+
+def test_deflate_full_c2_row_group_pages():
+    """Every page of one whole C2 row group (Rec8, seed 0xC0FFEE02, the reference's 128 MiB row
+    groups and pages: the first row group holds 2.08 M records, 50.7 MB of page bytes, its PLAIN
+    int64 pages 16.6 MB each, deflate's window sliding ~500 times per page) deflated by the
+    oracle, byte-identical to zlib's level-6 member.  The pages the GZIP writer compresses are
+    the UNCOMPRESSED file's page bodies (at pageSize = blockSize nothing is flushed before a cut,
+    so the codec moves no cut)."""
+    data, offs = synth.generate(synth.KIND_REC8, 0xC0FFEE02, 2_300_000)
+    fb = oracle.encode_file(synth.REC8, data, offs, oracle.make_props(codec=oracle.UNCOMPRESSED))
+    del data, offs
+    pages = [pg["body"] for pg in pqwalk.pages(fb) if pg["rg"] == 0]
+    assert sum(len(b) for b in pages) > 48 * MiB and max(len(b) for b in pages) > 16 * 10 ** 6
+    assert any(pg["rg"] == 1 for pg in pqwalk.pages(fb))   # row group 0 is complete (cut before the end)
+    for body in pages:
+        assert oracle.gzip_compress(body) == _zlib_gzip_member(body)
+
+
 def _readback(schema, recs, fb):
     tbl = pq.read_table(io.BytesIO(fb))
     assert tbl.num_rows == len(recs)
