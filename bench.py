@@ -267,7 +267,7 @@ PHASES = ("open", "writes", "close", "stats", "free")
 def cache_delta(before, after):
     """Allocator calls and their host ms between two kpw_cache_stats snapshots."""
     keys = ("dev_malloc_n", "dev_malloc_ms", "dev_free_n", "dev_free_ms", "pin_malloc_n", "pin_malloc_ms", "pin_free_n",
-            "pin_free_ms", "dev_retry")
+            "pin_free_ms", "dev_retry", "dev_sync_n", "dev_sync_ms", "gate_admits", "gate_wait_ms")
     return {k: round(after.get(k, 0.0) - before.get(k, 0.0), 2) for k in keys}
 
 

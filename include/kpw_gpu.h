@@ -82,7 +82,10 @@ void kpw_trim_caches(void);
  * [2] device bytes live, [3] device bytes idle in the cache, [4] pinned bytes live, [5] pinned
  * bytes idle, [6] hipMalloc calls, [7] their host ms, [8] hipFree calls, [9] their ms,
  * [10] hipHostMalloc calls, [11] ms, [12] hipHostFree calls, [13] ms, [14] device cache hits,
- * [15] pinned cache hits, [16] hipMalloc failures retried after releasing the idle blocks.
+ * [15] pinned cache hits, [16] hipMalloc failures retried after releasing the idle blocks,
+ * [17] device-wide synchronisations before freeing a grown buffer, [18] their host ms,
+ * [19] writer jobs admitted by the device encode gate (KPW_DEVICE_ENCODES), [20] their host
+ * ms of waiting for admission.
  * Returns the number of entries written (<= cap).  Diagnostics; no reference counterpart. */
 int kpw_cache_stats(double *out, int cap);
 

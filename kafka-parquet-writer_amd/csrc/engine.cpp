@@ -44,7 +44,7 @@ int DevBuf::ensure(size_t bytes)
     if (bytes <= cap && p) return 0;
     if (p) {
         if (tl_order) dev_free_after(p, tl_order);
-        else { (void)hipDeviceSynchronize(); dev_free(p); }
+        else { device_sync_for_free(); dev_free(p); }
         p = nullptr;
         cap = 0;
     }

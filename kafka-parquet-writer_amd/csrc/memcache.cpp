@@ -2,6 +2,7 @@
 #include "memcache.h"
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <map>
@@ -76,7 +77,9 @@ struct Counters {
     double dev_malloc_n = 0, dev_malloc_ms = 0, dev_free_n = 0, dev_free_ms = 0;
     double pin_malloc_n = 0, pin_malloc_ms = 0, pin_free_n = 0, pin_free_ms = 0;
     double dev_hits = 0, pin_hits = 0, dev_live = 0, pin_live = 0, dev_retry = 0;
+    double dev_sync_n = 0, dev_sync_ms = 0;   // device-wide synchronisations of a buffer growth
 } g_cnt;
+double g_gate_wait_ms = 0, g_gate_waits = 0;   // EncodeGate admissions and their host wait (under g_mu)
 
 hipError_t timed_malloc(void **q, size_t bytes)
 {
@@ -280,6 +283,16 @@ bool pin_contains(const void *q, size_t n)
 
 void stream_sets_trim();
 
+void device_sync_for_free()
+{
+    const double t = mono_ms();
+    (void)hipDeviceSynchronize();
+    const double dt = mono_ms() - t;
+    std::lock_guard<std::mutex> g(g_mu);
+    g_cnt.dev_sync_n++;
+    g_cnt.dev_sync_ms += dt;
+}
+
 void trim_caches()
 {
     {
@@ -299,7 +312,8 @@ int cache_stats(double *out, int cap)
     const double v[] = {(double)dev_cache_cap(), (double)pin_cache_cap(), g_cnt.dev_live, (double)dev_idle,
                         g_cnt.pin_live, (double)g_pin.free_bytes, g_cnt.dev_malloc_n, g_cnt.dev_malloc_ms,
                         g_cnt.dev_free_n, g_cnt.dev_free_ms, g_cnt.pin_malloc_n, g_cnt.pin_malloc_ms,
-                        g_cnt.pin_free_n, g_cnt.pin_free_ms, g_cnt.dev_hits, g_cnt.pin_hits, g_cnt.dev_retry};
+                        g_cnt.pin_free_n, g_cnt.pin_free_ms, g_cnt.dev_hits, g_cnt.pin_hits, g_cnt.dev_retry,
+                        g_cnt.dev_sync_n, g_cnt.dev_sync_ms, g_gate_waits, g_gate_wait_ms};
     const int n = (int)(sizeof(v) / sizeof(v[0]));
     int k = 0;
     for (; k < n && k < cap; k++) out[k] = v[k];
@@ -373,6 +387,58 @@ void stream_set_release(int n, const hipStream_t *s)
     }
     for (int k = 0; k < n; k++) if (s[k]) (void)hipStreamDestroy(s[k]);
 }
+
+// ---------------------------------------------------------------- device encode gate
+namespace {
+struct Gate {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t next_ticket = 0, serving = 0;   // FIFO admission
+    int running = 0;
+};
+Gate g_gate[64];
+int gate_cap()
+{
+    static const int v = [] {
+        const char *e = getenv("KPW_DEVICE_ENCODES");
+        const int x = e ? atoi(e) : 2;
+        return x > 0 ? x : 1 << 20;   // 0 or negative: no limit
+    }();
+    return v;
+}
+}  // namespace
+
+EncodeGate::EncodeGate(int device) : dev_(device >= 0 && device < 64 ? device : 0)
+{
+    Gate &G = g_gate[dev_];
+    const double t = mono_ms();
+    std::unique_lock<std::mutex> lk(G.mu);
+    const uint64_t my = G.next_ticket++;
+    G.cv.wait(lk, [&] { return G.serving == my && G.running < gate_cap(); });
+    G.serving++;
+    G.running++;
+    held_ = true;
+    waited_ = mono_ms() - t;
+    G.cv.notify_all();   // the next ticket may be admitted too
+    lk.unlock();
+    std::lock_guard<std::mutex> g(g_mu);
+    g_gate_wait_ms += waited_;
+    g_gate_waits += 1;
+}
+
+void EncodeGate::release()
+{
+    if (!held_) return;
+    Gate &G = g_gate[dev_];
+    {
+        std::lock_guard<std::mutex> g(G.mu);
+        G.running--;
+        held_ = false;
+    }
+    G.cv.notify_all();
+}
+
+EncodeGate::~EncodeGate() { release(); }
 
 }  // namespace kpw
 

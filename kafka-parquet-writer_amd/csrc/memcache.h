@@ -29,6 +29,7 @@ size_t pin_size(const void *p);    // usable bytes of a pin_alloc block containi
 bool pin_contains(const void *p, size_t n);   // [p, p+n) inside one live pin_alloc block
 void trim_caches();                // release every idle block (device pools, pinned, stream sets)
 int cache_stats(double *out, int cap);   // kpw_cache_stats (kpw_gpu.h)
+void device_sync_for_free();       // hipDeviceSynchronize before a plain free, counted (kpw_cache_stats)
 // Sets of n non-blocking HIP streams of the current device, kept across writers:
 // hipStreamDestroy takes ~2.5 ms (a writer tears down four streams per file, and the reference
 // opens a file per rotation).  A set is created stream after stream and reused whole: HIP gives
@@ -38,5 +39,28 @@ int cache_stats(double *out, int cap);   // kpw_cache_stats (kpw_gpu.h)
 // streams (their owner synchronised them) back (KPW_STREAM_POOL=0: created and destroyed).
 hipError_t stream_set_acquire(int n, hipStream_t *s);
 void stream_set_release(int n, const hipStream_t *s);
+
+// Device encode gate: at most KPW_DEVICE_ENCODES (default 2) writer jobs encode on one device at
+// once, admitted in arrival order (tickets).  A writer runs two encode workers, which is what
+// one file needs to keep up with PCIe; eight concurrent writers (C5, KafkaProtoParquetWriter's
+// threadCount) put sixteen encodes on the chip at once, and each then ran 7-8x slower than
+// alone (r06a: a 7 M-record job 107-117 ms against ~12 ms with two in flight) — their kernel
+// chains interleave on shared hardware queues, the segment kernel's persistent grids queue
+// behind each other and the scans' look-backs fall back.  Admitted jobs run as in the
+// single-writer pipeline; the others wait on the host before issuing any device work.
+class EncodeGate {
+public:
+    explicit EncodeGate(int device);   // blocks until admitted
+    ~EncodeGate();                     // releases the slot (idempotent with release())
+    void release();
+    EncodeGate(const EncodeGate &) = delete;
+    EncodeGate &operator=(const EncodeGate &) = delete;
+    double waited_ms() const { return waited_; }
+
+private:
+    int dev_;
+    bool held_ = false;
+    double waited_ = 0;
+};
 
 }  // namespace kpw

@@ -323,7 +323,7 @@ struct kpw_writer {
     int64_t last_rg_end = 0;           // InternalParquetRecordWriter.lastRowGroupEndPos
     int64_t open_buffered = 0;         // open row group's buffered size after the last PLANNED job
     std::atomic<int> n_materialize{0};
-    double t_open = 0, t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0;
+    double t_open = 0, t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0, t_gate = 0;
     double t_probe = 0;          // page-size probes (multi-page per-record path): wall time, count, records
     uint64_t n_probe = 0, probe_recs = 0;
     double stats[17] = {0};            // kpw_writer_stats (job order; read after drain)
@@ -886,6 +886,13 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
         std::unique_lock<std::mutex> lk(w->mu);
         w->cv.wait(lk, [&] { return B.lp_state != 1; });
     }
+    // admitted with the device's other writers' jobs in arrival order (memcache.h EncodeGate);
+    // released once this job's encode has completed, before its turn to append
+    EncodeGate gate(E.device);
+    {
+        std::lock_guard<std::mutex> g(w->mu);
+        w->t_gate += gate.waited_ms();
+    }
     if (int st = materialize(w, B, s)) return plan_fail(st, "stage buffer rebuild failed");
     bool after_invalid;
     {
@@ -961,6 +968,7 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
         // the host size model and the GPU planner restate the same cut: a mismatch is a bug
         return plan_fail(KPW_ERR_DEVICE, "row-group cut of the size model and the GPU planner differ");
     if (hipStreamSynchronize(s) != hipSuccess) return plan_fail(KPW_ERR_DEVICE, "encode sync failed");
+    gate.release();
     {
         std::lock_guard<std::mutex> g(w->mu);
         B.state = BUF_FREE;   // the carried records were copied out before the rest of the encode
@@ -1022,6 +1030,8 @@ static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
         return st;
     };
     if (prev_carry && hipStreamWaitEvent(s, prev_carry, 0) != hipSuccess) return jfail(KPW_ERR_DEVICE, "stream wait failed");
+    EncodeGate gate(E.device);   // (the job's row groups one at a time: the slot is held throughout)
+    w->t_gate += gate.waited_ms();
     if (int st = materialize(w, B, s)) return jfail(st, "stage buffer rebuild failed");
     bool after_invalid;
     {
@@ -2055,10 +2065,10 @@ extern "C" int kpw_writer_close(kpw_writer *w)
         if (trace_on())
             fprintf(stderr, "[kpw] close: entered at %.1f, footer done at %.1f ms\n", t_close - w->t_open, now_ms() - w->t_open);
         if (trace_on())
-            fprintf(stderr, "[kpw] close: worker encode %.1f ms; caller: pinned DMA waits %.1f ms, buffer acquire %.1f ms; "
-                            "worker: page buffer alloc + D2H issue %.1f ms; assembly %.1f ms; buffers rebuilt for "
-                            "a carry %d, gap %.0f MiB\n",
-                    w->t_encode, w->t_dma, w->t_acquire, w->t_d2h_alloc, w->t_asm, w->n_materialize.load(),
+            fprintf(stderr, "[kpw] close: worker encode %.1f ms, encode gate waits %.1f ms; caller: pinned DMA waits %.1f ms, "
+                            "buffer acquire %.1f ms; worker: page buffer alloc + D2H issue %.1f ms; assembly %.1f ms; "
+                            "buffers rebuilt for a carry %d, gap %.0f MiB\n",
+                    w->t_encode, w->t_gate, w->t_dma, w->t_acquire, w->t_d2h_alloc, w->t_asm, w->n_materialize.load(),
                     w->gap_.load() / 1048576.0);
         if (trace_on() && w->n_probe)
             fprintf(stderr, "[kpw] close: %llu page-size probes, %.1f ms (%.3f ms each, %.0f records each)\n",

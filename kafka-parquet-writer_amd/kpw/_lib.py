@@ -176,7 +176,8 @@ EXPORTED = ["kpw_writer_open", "kpw_writer_write", "kpw_writer_write_async", "kp
 
 CACHE_STATS = ["dev_cache_cap", "pin_cache_cap", "dev_live", "dev_idle", "pin_live", "pin_idle", "dev_malloc_n",
                "dev_malloc_ms", "dev_free_n", "dev_free_ms", "pin_malloc_n", "pin_malloc_ms", "pin_free_n",
-               "pin_free_ms", "dev_hits", "pin_hits", "dev_retry"]
+               "pin_free_ms", "dev_hits", "pin_hits", "dev_retry", "dev_sync_n", "dev_sync_ms",
+               "gate_admits", "gate_wait_ms"]
 
 
 def cache_stats():
