@@ -401,8 +401,8 @@ int gate_cap()
 {
     static const int v = [] {
         const char *e = getenv("KPW_DEVICE_ENCODES");
-        const int x = e ? atoi(e) : 2;
-        return x > 0 ? x : 1 << 20;   // 0 or negative: no limit
+        const int x = e ? atoi(e) : 0;
+        return x > 0 ? x : 1 << 20;   // 0 (default) or negative: no limit
     }();
     return v;
 }

@@ -40,14 +40,12 @@ void device_sync_for_free();       // hipDeviceSynchronize before a plain free, 
 hipError_t stream_set_acquire(int n, hipStream_t *s);
 void stream_set_release(int n, const hipStream_t *s);
 
-// Device encode gate: at most KPW_DEVICE_ENCODES (default 2) writer jobs encode on one device at
-// once, admitted in arrival order (tickets).  A writer runs two encode workers, which is what
-// one file needs to keep up with PCIe; eight concurrent writers (C5, KafkaProtoParquetWriter's
-// threadCount) put sixteen encodes on the chip at once, and each then ran 7-8x slower than
-// alone (r06a: a 7 M-record job 107-117 ms against ~12 ms with two in flight) — their kernel
-// chains interleave on shared hardware queues, the segment kernel's persistent grids queue
-// behind each other and the scans' look-backs fall back.  Admitted jobs run as in the
-// single-writer pipeline; the others wait on the host before issuing any device work.
+// Device encode gate: at most KPW_DEVICE_ENCODES writer jobs encode on one device at once,
+// admitted in arrival order (tickets); default 0 = no limit.  Measured on C5 (eight concurrent
+// writers, 16 encode workers; r06b, one box): unlimited 32.5 GB/s, 2 slots 25.4, 3 slots 28.3,
+// 4 slots 28.9 — admitted jobs encode 3.4x faster each, but the chip is fuller with every
+// writer's job in flight (a job's kernel chain alone leaves most CUs idle), so the default
+// stays unlimited.  Kept for deployments that bound per-file latency or share the GPU.
 class EncodeGate {
 public:
     explicit EncodeGate(int device);   // blocks until admitted
