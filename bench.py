@@ -760,13 +760,23 @@ def main():
     if args.secondary_steps and world == 1 and args.workload == "c2":
         # the config where encode, not PCIe, sets the pace (C4), and bulk writes with 1 MiB pages
         c4k, c4n, c4seed, _ = WORKLOADS["c4"]
+        # each secondary leg starts from empty allocator caches (kpw_trim_caches: a fresh process's
+        # state) and warms them in its own untimed steps; otherwise a leg inherits the previous
+        # workload's cached blocks and pays hipMalloc / hipFree for its own sizes in its timed steps
+        # (r06a: C5 after the C4 and multi-page legs made 229 device allocations in 3 timed steps)
+        L0 = kpw.load_library()
+        L0.kpw_trim_caches()
         c4_leg = writer_leg(kpw, c4k, c4seed, c4n, local_rank, args.secondary_steps, 1)
+        L0.kpw_trim_caches()
         bulk_mp = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, page_size=MiB,
                              sets=[s[0] for s in sets])
-        c5 = c5_leg(kpw, local_rank, max(3, args.secondary_steps), 1)
+        L0.kpw_trim_caches()
+        c5 = c5_leg(kpw, local_rank, max(3, args.secondary_steps), 2)
         # BASELINE config 3 (wide telemetry schema), 10 M records, its own writer line
         c3k, c3n, c3seed, _ = WORKLOADS["c3"]
+        L0.kpw_trim_caches()
         c3_leg = writer_leg(kpw, c3k, c3seed, c3n, local_rank, max(3, args.secondary_steps), 1)
+        L0.kpw_trim_caches()
         # the same C2 records with CompressionCodecName.GZIP (no BASELINE config; K7' k_deflate.hip)
         gz = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, sets=[s[0] for s in sets], codec=kpw.GZIP)
     if args.secondary_steps and world == 1 and args.workload == "c2" and not args.no_cpu_baseline:

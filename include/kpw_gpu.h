@@ -71,14 +71,15 @@ void *kpw_host_alloc(uint64_t bytes, int *status);
 void kpw_host_free(void *p);
 
 /* The library keeps freed HBM and pinned blocks for the next writer (a writer is one file and
- * files rotate; hipFree synchronises the device): up to KPW_DEV_CACHE_GB per device (default 96)
- * and KPW_PIN_CACHE_GB pinned per process (default 48 GB divided by LOCAL_WORLD_SIZE, the ranks
+ * files rotate; hipFree synchronises the device): up to KPW_DEV_CACHE_GB per device (default:
+ * 96 GB or the device's peak live bytes, whichever is larger, at most 3/4 of the device) and
+ * KPW_PIN_CACHE_GB pinned per process (default 48 GB divided by LOCAL_WORLD_SIZE, the ranks
  * sharing the host), read once per process.  This releases every idle block and idle pooled
  * stream set now (e.g. before a co-located consumer or framework allocates).  Thread-safe.  No
  * reference counterpart (the JVM writer allocates on the Java heap). */
 void kpw_trim_caches(void);
 
-/* Allocator figures of this process: [0] device cache cap (bytes), [1] pinned cache cap,
+/* Allocator figures of this process: [0] device cache cap (bytes, the current device's), [1] pinned cache cap,
  * [2] device bytes live, [3] device bytes idle in the cache, [4] pinned bytes live, [5] pinned
  * bytes idle, [6] hipMalloc calls, [7] their host ms, [8] hipFree calls, [9] their ms,
  * [10] hipHostMalloc calls, [11] ms, [12] hipHostFree calls, [13] ms, [14] device cache hits,

@@ -4,6 +4,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -37,6 +38,11 @@ size_t dev_cache_cap()
     static const size_t v = cap_gb("KPW_DEV_CACHE_GB", 96);
     return v;
 }
+bool dev_cap_explicit()
+{
+    static const bool v = [] { const char *e = getenv("KPW_DEV_CACHE_GB"); return e && *e; }();
+    return v;
+}
 size_t pin_cache_cap()
 {
     static const size_t v = [] {
@@ -56,6 +62,8 @@ struct Pool {
     std::multimap<size_t, void *> free_;   // size -> block
     std::map<void *, size_t> size_;        // every block this pool allocated (live or free)
     size_t free_bytes = 0;
+    size_t live = 0, peak = 0;             // bytes handed out now / at most (device pools)
+    size_t total = 0;                      // the device's memory (0: not queried yet)
 };
 
 // a block handed back with dev_free_after: it rejoins its pool once `ev` has completed
@@ -145,6 +153,17 @@ void dev_release(void *b)
 }
 
 // a block of ours back into its pool (under g_mu)
+// Idle bytes a device pool keeps: KPW_DEV_CACHE_GB when set; by default at least 96 GB and up
+// to the pool's peak live bytes (capped at 3/4 of the device), so a workload that re-opens the
+// same writers every file (C5: eight writers, ~110 GB live) finds every block again instead of
+// re-allocating the part above a fixed cap each file.
+size_t dev_keep(const Pool &p)
+{
+    if (dev_cap_explicit()) return dev_cache_cap();
+    const size_t lim = p.total ? p.total / 4 * 3 : dev_cache_cap();
+    return std::max(dev_cache_cap(), std::min(p.peak, lim));
+}
+
 void dev_return(void *q, int dev)
 {
     Pool &p = g_dev[dev];
@@ -152,8 +171,9 @@ void dev_return(void *q, int dev)
     if (it == p.size_.end()) { timed_free(q); return; }
     p.free_.emplace(it->second, q);
     p.free_bytes += it->second;
+    p.live -= it->second;
     g_cnt.dev_live -= (double)it->second;
-    trim(p, dev_cache_cap(), dev_release);
+    trim(p, dev_keep(p), dev_release);
 }
 
 // deferred blocks whose event completed rejoin their pools (under g_mu); wait: block on them
@@ -181,9 +201,15 @@ void *dev_alloc(size_t bytes)
     std::lock_guard<std::mutex> g(g_mu);
     if (!g_deferred.empty()) reap(false);
     Pool &p = g_dev[dev];
+    if (!p.total) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) p.total = tot; else (void)hipGetLastError();
+    }
     if (void *q = take(p, bytes)) {
         g_cnt.dev_hits++;
         g_cnt.dev_live += (double)p.size_[q];
+        p.live += p.size_[q];
+        p.peak = std::max(p.peak, p.live);
         return q;
     }
     void *q = nullptr;
@@ -197,6 +223,8 @@ void *dev_alloc(size_t bytes)
     p.size_[q] = bytes;
     g_dev_of[q] = dev;
     g_cnt.dev_live += (double)bytes;
+    p.live += bytes;
+    p.peak = std::max(p.peak, p.live);
     return q;
 }
 
@@ -298,7 +326,7 @@ void trim_caches()
     {
         std::lock_guard<std::mutex> g(g_mu);
         reap(true);
-        for (auto &p : g_dev) trim(p, 0, dev_release);
+        for (auto &p : g_dev) { trim(p, 0, dev_release); p.peak = p.live; }
         trim(g_pin, 0, timed_host_free);
     }
     stream_sets_trim();   // idle pooled stream sets too
@@ -309,7 +337,9 @@ int cache_stats(double *out, int cap)
     size_t dev_idle = 0;
     std::lock_guard<std::mutex> g(g_mu);
     for (auto &p : g_dev) dev_idle += p.free_bytes;
-    const double v[] = {(double)dev_cache_cap(), (double)pin_cache_cap(), g_cnt.dev_live, (double)dev_idle,
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || cur < 0 || cur >= 64) cur = 0;
+    const double v[] = {(double)dev_keep(g_dev[cur]), (double)pin_cache_cap(), g_cnt.dev_live, (double)dev_idle,
                         g_cnt.pin_live, (double)g_pin.free_bytes, g_cnt.dev_malloc_n, g_cnt.dev_malloc_ms,
                         g_cnt.dev_free_n, g_cnt.dev_free_ms, g_cnt.pin_malloc_n, g_cnt.pin_malloc_ms,
                         g_cnt.pin_free_n, g_cnt.pin_free_ms, g_cnt.dev_hits, g_cnt.pin_hits, g_cnt.dev_retry,

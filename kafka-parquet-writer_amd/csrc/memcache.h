@@ -9,9 +9,10 @@
 // or hand it over with dev_free_after(stream) (buffer growth: the block returns once the
 // stream's queued work has passed an event, without a device-wide synchronisation).
 //
-// Idle memory kept: KPW_DEV_CACHE_GB per device (default 96 of 288 GB: C5 runs 8 writers per
-// GPU and re-opens them every file) and KPW_PIN_CACHE_GB of pinned host memory per process
-// (default 48 GB shared by the node's ranks: 48 / LOCAL_WORLD_SIZE);
+// Idle memory kept: KPW_DEV_CACHE_GB per device when set; by default 96 GB or the device pool's
+// peak live bytes, whichever is larger, at most 3/4 of the device (C5 runs 8 writers per GPU,
+// ~110 GB live, and re-opens them every file), and KPW_PIN_CACHE_GB of pinned host memory per
+// process (default 48 GB shared by the node's ranks: 48 / LOCAL_WORLD_SIZE);
 // kpw_trim_caches() (kpw_gpu.h) releases every idle block, e.g. before a co-located consumer
 // allocates.
 #pragma once
