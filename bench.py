@@ -656,7 +656,16 @@ def main():
     log("generated %d x %d records (%.2f GB each) in pinned host memory in %.1fs"
         % (len(sets), n, set_bytes[0] / 1e9, time.perf_counter() - t0))
 
+    step_wall = []
+
     def step(i):
+        t = time.perf_counter()
+        r = step_body(i)
+        if i >= args.warmup:
+            step_wall.append(time.perf_counter() - t)
+        return r
+
+    def step_body(i):
         s = sets[i % len(sets)]
         if len(s) == 1:
             size, st = write_file(kpw, schema, props, s[0][0], s[0][1], local_rank)
@@ -760,6 +769,9 @@ def main():
     if args.secondary_steps and world == 1 and args.workload == "c2":
         # the config where encode, not PCIe, sets the pace (C4), and bulk writes with 1 MiB pages
         c4k, c4n, c4seed, _ = WORKLOADS["c4"]
+        if os.environ.get("KPW_BENCH_C5_FIRST") == "1":   # (measurement knob: the C5 leg before the others)
+            kpw.load_library().kpw_trim_caches()
+            c5 = c5_leg(kpw, local_rank, max(3, args.secondary_steps), 2)
         # each secondary leg starts from empty allocator caches (kpw_trim_caches: a fresh process's
         # state) and warms them in its own untimed steps; otherwise a leg inherits the previous
         # workload's cached blocks and pays hipMalloc / hipFree for its own sizes in its timed steps
@@ -771,7 +783,8 @@ def main():
         bulk_mp = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, page_size=MiB,
                              sets=[s[0] for s in sets])
         L0.kpw_trim_caches()
-        c5 = c5_leg(kpw, local_rank, max(3, args.secondary_steps), 2)
+        if os.environ.get("KPW_BENCH_C5_FIRST") != "1":
+            c5 = c5_leg(kpw, local_rank, max(3, args.secondary_steps), 2)
         # BASELINE config 3 (wide telemetry schema), 10 M records, its own writer line
         c3k, c3n, c3seed, _ = WORKLOADS["c3"]
         L0.kpw_trim_caches()
@@ -814,6 +827,9 @@ def main():
                    "records_per_gpu": n, "bytes_per_gpu_step": set_bytes[0], "files_per_gpu_step": len(sets[0]),
                    "codec": "SNAPPY", "parallelism": "partition-sharded x%d" % world, "numa_node": numa},
         "records_per_s": round(rec_s, 1),
+        # this rank's wall per timed step (host clock around each step; the line's time is the max
+        # over ranks of the whole timed region)
+        "step_ms": [round(x * 1e3, 1) for x in step_wall],
         "file_bytes_per_step": int(file_bytes / max(1, args.steps)),
         "encode_jobs_per_step": round(jobs / args.steps, 2),
         "worker_encode_wall_ms_per_step": round(agg.get("worker_encode_wall_ms", 0) / args.steps, 2),

@@ -385,7 +385,9 @@ int Engine::encode(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, boo
     const int st = encode_impl(d_data, d_off, n, final_flush, next_rg_size, user_stream, out);
     if (st) return st;
     // look-backs that waited past their bound and recomputed the predecessor (kpw_lookback.h):
-    // exact either way, counted for kpw_writer_stats
+    // exact either way, counted for kpw_writer_stats (a page-size probe's engine reports none:
+    // its count is never read, which saves the probe a readback and a host sync)
+    if (probe_) { lb_fallbacks = 0; return KPW_OK; }
     const int lf = lb_failures(&seg_, stream);
     if (lf < 0) return fail(KPW_ERR_DEVICE, "scan status unreadable");
     lb_fallbacks = (uint32_t)lf;
@@ -475,7 +477,12 @@ int Engine::encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     // plans over all n records and learns the verdict with the plan (k_plan copies it), re-planning
     // over the valid prefix in the rare batch that has one; the multi-page path reads it now.
     uint64_t err_idx = ~0ull;
-    const bool optimistic = !mp_;
+    // a page-size probe of the size model's row group: the host model validated every record
+    // (an invalid one never reaches a probe), so the verdict is read back with the probe's last
+    // sync and checked there (probe_mp) instead of costing a sync here
+    const bool model_probe = probe_ && probe_cuts_;
+    probe_err_dev_ = d_err;
+    const bool optimistic = !mp_ || model_probe;
     if (!optimistic) {
         CK(xd2h(&err_idx, d_err, 8, s));
         CK(xsync(s));
@@ -544,9 +551,10 @@ replan:
         launch_plan_fold(d_ev.as<uint8_t>(), ev_stride, pstreams, nstreams, d_raw.as<uint32_t>(), ne,
                          d_qv.as<uint32_t>(), s);
     }
-    launch_plan_prefix(plan ? d_ev.as<uint8_t>() : nullptr, plan ? d_E.as<uint32_t>() : nullptr, plan ? nstreams : 0, ev_stride,
-                       d_raw.as<uint32_t>(), fold ? d_qv.as<uint32_t>() : nullptr, ne, d_P.as<uint64_t>(),
-                       fold ? d_Q.as<uint64_t>() : nullptr, &seg_, s);
+    if (!model_probe)   // (a model probe takes its page cuts from the host: no planner prefixes)
+        launch_plan_prefix(plan ? d_ev.as<uint8_t>() : nullptr, plan ? d_E.as<uint32_t>() : nullptr, plan ? nstreams : 0,
+                           ev_stride, d_raw.as<uint32_t>(), fold ? d_qv.as<uint32_t>() : nullptr, ne, d_P.as<uint64_t>(),
+                           fold ? d_Q.as<uint64_t>() : nullptr, &seg_, s);
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "scan scratch allocation failed");
     if (mp_) return encode_mp(d_data, d_off, n, ne, final_flush, next_rg_size, hc, nwords, ev_stride, out);
     // ---------------------------------------------------------------- A9 plan

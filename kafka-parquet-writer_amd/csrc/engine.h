@@ -226,8 +226,10 @@ private:
     const std::vector<char> *probe_mask_ = nullptr;
     uint64_t probe_token_ = ~0ull;       // open row group of the cached page sizes (~0: none)
     const std::vector<std::vector<int64_t>> *probe_cuts_ = nullptr;   // v1 probe: the caller's page cuts
+    const unsigned long long *probe_err_dev_ = nullptr;   // K1's first-invalid-record word of this encode
     struct CutPage { int64_t end; int64_t bytes; };   // a cut page: end record, header + compressed bytes
     std::vector<std::vector<CutPage>> probe_cache_;   // per column, in page order
+    std::vector<uint32_t> probe_mode_;                // per column: first page satisfied (1) / all PLAIN (2), 0 unknown
     std::vector<int64_t> probe_flushed_;
     int encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                   const std::vector<DevCol> &hc, uint64_t gend_stride, uint64_t ev_stride, BatchOut &out);

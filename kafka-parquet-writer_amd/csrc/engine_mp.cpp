@@ -137,7 +137,8 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         memset(&D, 0, sizeof(D));
         const uint64_t len = (uint64_t)(e - s);
         D.s = s; D.e = e; D.col = c; D.rg = 0;
-        const bool on = !mask || (*mask)[c];   // a probe of a column subset: the others get no pages
+        bool on = !mask || (*mask)[c];   // a probe of a column subset: the others get no pages
+        if (on && k7_from && !v2_ && (size_t)(*k7_from)[c] >= cuts[c].size()) on = false;   // (nothing new cut)
         D.is_dict = cols[c].dict && on ? 1 : 0;
         D.smin = ~0ull; D.smax = 0;
         D.ids_off = ids_off; D.ent_off = ids_off;
@@ -170,15 +171,29 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         D.dl_job = D.id_job = D.bool_job = D.dj0 = -1;
         D.owner = -1;
         D.first_page = (int32_t)pg.size();
+        // a probe (k7_from) encodes only the pages cut since its previous probe of the open row
+        // group: the pages before are cached, the open page after the last cut is not flushed yet
+        // (ColumnChunkPageWriter.getMemSize counts written pages only).  Without the chunk's first
+        // page, its isCompressionSatisfying outcome comes from the probe that encoded it
+        // (probe_mode_: 1 satisfied, 2 every page PLAIN), as in the splice's tail mode.
+        // (v2 encodes every page: a DELTA stream inherits the previous page's stale bit widths)
+        const bool newonly = k7_from && !v2_;
+        const size_t p_from = newonly ? (size_t)(*k7_from)[c] : 0;
+        if (on && newonly && p_from >= cuts[c].size()) on = false;   // nothing new cut in this column
+        if (on && newonly && p_from > 0) {
+            D.tail_mode = probe_mode_.size() > (size_t)c ? probe_mode_[c] : 0u;
+            if (D.tail_mode == 0) return fail(KPW_ERR_STATE, "probe: first page outcome of a cached column unknown");
+        }
         const uint32_t nt = on ? (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H) : 0u;
         dfirst[c] = ndt;
         dcount[c] = nt;
         ddict[c] = D.is_dict;
         ndt += nt;
         if (!on) { D.npages = 0; continue; }
-        // (splice: only the page after the last cut)
-        int64_t q = spec && !cuts[c].empty() ? cuts[c].back() : s;
-        for (size_t i = spec ? cuts[c].size() : 0; i <= cuts[c].size(); i++) {
+        // (splice: only the page after the last cut; probe: only the pages cut since the last probe)
+        int64_t q = spec && !cuts[c].empty() ? cuts[c].back() : (p_from ? cuts[c][p_from - 1] : s);
+        const size_t i_end = newonly ? cuts[c].size() - 1 : cuts[c].size();
+        for (size_t i = spec ? cuts[c].size() : p_from; i <= i_end; i++) {
             const int64_t pe = i < cuts[c].size() ? std::min<int64_t>(cuts[c][i], e) : e;
             if (pe <= q) continue;
             ChunkDesc P;
@@ -396,7 +411,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     if (body_poison()) CK(hipMemsetAsync(d_body.p, 0xAB, body_tot, st));
     ap.body_tail = body_tot;
     launch_mp_dictpage_off(ap.ch, ad.ch, nc, st);
-    launch_dict_page(ad, d_body.as<uint8_t>(), st);
+    if (!k7_from) launch_dict_page(ad, d_body.as<uint8_t>(), st);   // (a probe needs no dictionary page bytes)
     launch_chunk_write(ap, d_jobs.as<RleJob>(), d_body.as<uint8_t>(), st);
     if (!ej.empty()) launch_rle_write(d_jobs.as<RleJob>(), enpt, enet, esc, d_body.as<uint8_t>(), st);
     if (v2_) {
@@ -608,6 +623,8 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
         if (!ok) pcache.clear();
         from[c] = (uint32_t)pcache.size();
     }
+    probe_mode_.resize(nc, 0);
+    for (int c = 0; c < nc; c++) if (from[c] == 0) probe_mode_[c] = 0;
     int rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
     if (rs) return rs;
     probe_npages_.assign(nc, 0);
@@ -615,7 +632,11 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
     for (int c = 0; c < nc; c++) {
         if (probe_mask_ && !(*probe_mask_)[c]) { probe_npages_[c] = -1; probe_flushed_[c] = -1; continue; }
         std::vector<CutPage> &pcache = probe_cache_[c];
-        size_t i = 0;
+        // the chunk's first page encoded in this run: its dictionary outcome for later probes
+        // (k_mp_satisfy: every page PLAIN when it failed isCompressionSatisfying or fell back)
+        if (from[c] == 0 && !pr.cols[c].empty() && !pr.dch.empty() && pr.dch[c].npages > 0)
+            probe_mode_[c] = (!cols[c].dict || pr.pg[pr.dch[c].first_page].fallback) ? 2u : 1u;
+        size_t i = v2_ ? 0 : from[c];   // the run's data pages: the column's pages from[c] on (v2: all)
         for (const PageOut &p : pr.cols[c]) {
             if (p.page_type == KPW_DICTIONARY_PAGE) continue;
             if (i < pc[c].size() && i >= pcache.size())
@@ -627,7 +648,10 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
     }
     out.records_consumed = 0;
     out.open_records = (int64_t)ne;
+    uint64_t err_idx = 0;   // K1's verdict, not read before the probe (encode_impl: model probes)
+    CK(xd2h(&err_idx, probe_err_dev_, 8, st));
     CK(xsync(st));
+    if (err_idx < n) out.invalid_record = (int64_t)err_idx;
     return KPW_OK;
 }
 

@@ -3,5 +3,6 @@
 # warm-up steps, dynamic device cache cap), timed
 OUT=gpurun_out/r06e
 mkdir -p $OUT
-/usr/bin/time -v timeout -k 10 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || exit $?
+timeout -k 10 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; rc=$?; echo "wall $SECONDS s"; [ $rc -eq 0 ] || exit $rc
+# || exit $?
 echo done
