@@ -767,31 +767,40 @@ def main():
                                         args.per_record_max_file_mb * MiB, 64 * 1024)
     c4_leg = bulk_mp = c5 = gz = c3_leg = c1 = None
     if args.secondary_steps and world == 1 and args.workload == "c2":
-        # the config where encode, not PCIe, sets the pace (C4), and bulk writes with 1 MiB pages
-        c4k, c4n, c4seed, _ = WORKLOADS["c4"]
-        if os.environ.get("KPW_BENCH_C5_FIRST") == "1":   # (measurement knob: the C5 leg before the others)
-            kpw.load_library().kpw_trim_caches()
-            c5 = c5_leg(kpw, local_rank, max(3, args.secondary_steps), 2)
-        # each secondary leg starts from empty allocator caches (kpw_trim_caches: a fresh process's
-        # state) and warms them in its own untimed steps; otherwise a leg inherits the previous
-        # workload's cached blocks and pays hipMalloc / hipFree for its own sizes in its timed steps
-        # (r06a: C5 after the C4 and multi-page legs made 229 device allocations in 3 timed steps)
+        # Secondary writer legs, in KPW_BENCH_LEGS order (a measurement knob; default below).  Each
+        # starts from empty allocator caches (kpw_trim_caches: a fresh process's state) and warms
+        # them in its own untimed steps; otherwise a leg inherits the previous workload's cached
+        # blocks and pays hipMalloc / hipFree for its own sizes in its timed steps (r06a: C5 after
+        # the C4 and multi-page legs made 229 device allocations in 3 timed steps).
         L0 = kpw.load_library()
+        legs = {}
+
+        def run_c4():   # the config where encode, not PCIe, sets the pace
+            c4k, c4n, c4seed, _ = WORKLOADS["c4"]
+            return writer_leg(kpw, c4k, c4seed, c4n, local_rank, args.secondary_steps, 1)
+
+        def run_bulk():   # bulk writes with 1 MiB pages inside 128 MiB row groups
+            return writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, page_size=MiB,
+                              sets=[s[0] for s in sets])
+
+        def run_c5():   # BASELINE config 5 at its shape on this GPU
+            return c5_leg(kpw, local_rank, max(3, args.secondary_steps), 2)
+
+        def run_c3():   # BASELINE config 3 (wide telemetry schema), 10 M records, its own writer line
+            c3k, c3n, c3seed, _ = WORKLOADS["c3"]
+            return writer_leg(kpw, c3k, c3seed, c3n, local_rank, max(3, args.secondary_steps), 1)
+
+        def run_gzip():   # the same C2 records with CompressionCodecName.GZIP (no BASELINE config; K7')
+            return writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, sets=[s[0] for s in sets],
+                              codec=kpw.GZIP)
+        runners = {"c4": run_c4, "bulk_multipage": run_bulk, "c5": run_c5, "c3": run_c3, "gzip": run_gzip}
+        order = os.environ.get("KPW_BENCH_LEGS", "c5,c3,c4,bulk_multipage,gzip").split(",")
+        for name in order:
+            if name in runners:
+                L0.kpw_trim_caches()
+                legs[name] = runners[name]()
         L0.kpw_trim_caches()
-        c4_leg = writer_leg(kpw, c4k, c4seed, c4n, local_rank, args.secondary_steps, 1)
-        L0.kpw_trim_caches()
-        bulk_mp = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, page_size=MiB,
-                             sets=[s[0] for s in sets])
-        L0.kpw_trim_caches()
-        if os.environ.get("KPW_BENCH_C5_FIRST") != "1":
-            c5 = c5_leg(kpw, local_rank, max(3, args.secondary_steps), 2)
-        # BASELINE config 3 (wide telemetry schema), 10 M records, its own writer line
-        c3k, c3n, c3seed, _ = WORKLOADS["c3"]
-        L0.kpw_trim_caches()
-        c3_leg = writer_leg(kpw, c3k, c3seed, c3n, local_rank, max(3, args.secondary_steps), 1)
-        L0.kpw_trim_caches()
-        # the same C2 records with CompressionCodecName.GZIP (no BASELINE config; K7' k_deflate.hip)
-        gz = writer_leg(kpw, kind, wseed, n, local_rank, args.secondary_steps, 1, sets=[s[0] for s in sets], codec=kpw.GZIP)
+        c4_leg, bulk_mp, c5, c3_leg, gz = (legs.get(k) for k in ("c4", "bulk_multipage", "c5", "c3", "gzip"))
     if args.secondary_steps and world == 1 and args.workload == "c2" and not args.no_cpu_baseline:
         c1 = c1_leg(kpw, local_rank, threads=args.cpu_threads or host_threads())   # BASELINE config 1
     cpu = None

@@ -230,6 +230,23 @@ private:
     struct CutPage { int64_t end; int64_t bytes; };   // a cut page: end record, header + compressed bytes
     std::vector<std::vector<CutPage>> probe_cache_;   // per column, in page order
     std::vector<uint32_t> probe_mode_;                // per column: first page satisfied (1) / all PLAIN (2), 0 unknown
+    // Probe continuation (v1 page-size probes, engine_mp.cpp): each dictionary column's hash table,
+    // ids and entries stay on the device between the probes of one open row group, so a probe
+    // inserts only the records since the column's previous probe (KPW_PROBE_CONT=0: off).
+    struct ProbeDict {
+        int64_t done = 0;       // records [0, done) inserted
+        uint32_t n = 0;         // entries (in first-occurrence order)
+        uint64_t bytes = 0;     // their dictionaryByteSize
+        bool stopped = false;   // past dictPageSize: later records fall in PLAIN pages, need no ids
+    };
+    std::vector<ProbeDict> pd_;
+    bool pd_on_ = false;        // mp_pipeline runs a continuation probe
+    bool pd_exact_ = false;     // the open row group's string keys are compared byte for byte
+    uint64_t pd_ht_cap_ = 0, pd_ent_cap_ = 0, pd_ids_cap_ = 0;   // per dictionary column: table slots, entries, values
+    std::vector<int32_t> pd_slot_;   // column -> its region in the pd_ buffers (-1: no dictionary)
+    DevBuf pd_ht, pd_ids, pd_ent_rec, pd_ent_boff;
+    int pd_prepare(uint64_t ne);   // buffers for a probe of [0, ne)
+    void pd_reset();
     std::vector<int64_t> probe_flushed_;
     int encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, uint64_t ne, bool final_flush, int64_t T,
                   const std::vector<DevCol> &hc, uint64_t gend_stride, uint64_t ev_stride, BatchOut &out);

@@ -44,6 +44,16 @@ void launch_stats_gather(const ChunkDesc *ch, int nchunks, const DevCol *cols, c
     } while (0)
 #define ENS(buf, bytes) do { if ((buf).ensure(bytes)) return fail(KPW_ERR_NOMEM, "device allocation failed: " #buf); } while (0)
 
+// mp_pipeline: a continuation probe found a string hash collision (probe_mp restarts exact)
+constexpr int kPdRetry = -77;
+
+// KPW_PROBE_CONT=0: every probe re-inserts the open row group's prefix (A/B of the continuation)
+static bool pd_enabled()
+{
+    static const bool on = [] { const char *e = getenv("KPW_PROBE_CONT"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
 // multi-page dictionary insertion round: tiles (of KPW_TILE_P_H records) per chunk and round
 constexpr uint32_t kMpRoundTiles = 64;
 
@@ -126,12 +136,14 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     // row group of 8 columns in the same rounds as before
     uint32_t ndict = 0;
     for (int c = 0; c < nc; c++) ndict += (cols[c].dict && (!mask || (*mask)[c])) ? 1 : 0;
-    const uint32_t round_tiles = std::min<uint32_t>(4 * kMpRoundTiles, std::max<uint32_t>(kMpRoundTiles, 1024 / std::max<uint32_t>(1, ndict)));
+    // (a continuation probe inserts in fixed rounds of kMpRoundTiles: its kept table is sized for one)
+    const uint32_t round_tiles = pd_on_ ? kMpRoundTiles
+                                        : std::min<uint32_t>(4 * kMpRoundTiles, std::max<uint32_t>(kMpRoundTiles, 1024 / std::max<uint32_t>(1, ndict)));
     // rounds double up to round_grow x round_tiles: the stop matters near a chunk's crossing, which
     // the high-cardinality chunks reach in the first rounds; the later, larger rounds cost fewer
     // latency-bound launches (a bulk row group: 23 -> 8 rounds).  The table holds one round more.
     static const uint32_t round_grow = [] { const char *e = getenv("KPW_MP_ROUND_GROW"); const int v = e ? atoi(e) : 4; return (uint32_t)(v > 0 ? v : 1); }();
-    const uint32_t round_max = round_tiles * round_grow;
+    const uint32_t round_max = pd_on_ ? round_tiles : round_tiles * round_grow;
     for (int c = 0; c < nc; c++) {
         ChunkDesc &D = dch[c];
         memset(&D, 0, sizeof(D));
@@ -143,7 +155,16 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         D.smin = ~0ull; D.smax = 0;
         D.ids_off = ids_off; D.ent_off = ids_off;
         if (on && !spec) ids_off += len;
-        if (D.is_dict && spec) {
+        if (D.is_dict && pd_on_) {
+            // continuation probe: the column's table, ids and entries of [0, done) are kept in the
+            // pd_ buffers; only [done, e) is inserted (a dictionary past dictPageSize inserts no more)
+            const ProbeDict &Q = pd_[c];
+            const uint64_t k = (uint64_t)pd_slot_[c];
+            D.ht_cap = (uint32_t)pd_ht_cap_; D.ht_off = k * (pd_ht_cap_ + 1);
+            D.ids_off = k * pd_ids_cap_; D.ent_off = k * pd_ent_cap_;
+            D.dict_n = Q.n; D.dict_bytes = Q.bytes; D.ent_base = Q.n; D.boff_base = Q.bytes;
+            D.tile_skip = Q.stopped ? len : (uint64_t)std::min<int64_t>(Q.done, (int64_t)len);
+        } else if (D.is_dict && spec) {
             // the speculative pass's dictionary (ids, entries, tables) stays where it is; the
             // chunk's pages before its last cut are spec's pages, decided as they were there
             const ChunkDesc &S = spec->dch[c];
@@ -184,7 +205,8 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             D.tail_mode = probe_mode_.size() > (size_t)c ? probe_mode_[c] : 0u;
             if (D.tail_mode == 0) return fail(KPW_ERR_STATE, "probe: first page outcome of a cached column unknown");
         }
-        const uint32_t nt = on ? (uint32_t)std::max<uint64_t>(1, (len + KPW_TILE_P_H - 1) / KPW_TILE_P_H) : 0u;
+        const uint64_t tlen = len - D.tile_skip;   // (a continuation's tiles start at its kept records)
+        const uint32_t nt = on ? (uint32_t)std::max<uint64_t>(1, (tlen + KPW_TILE_P_H - 1) / KPW_TILE_P_H) : 0u;
         dfirst[c] = ndt;
         dcount[c] = nt;
         ddict[c] = D.is_dict;
@@ -289,7 +311,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     uint64_t *const d_pcoff = d_ppre + P2, *const d_pclen = d_pcoff + P2;
     uint32_t *const d_coll = (uint32_t *)(pt + 2);
     std::vector<uint64_t> ptab(4 + 5 * P2);
-    for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = d_ids.p;
+    for (auto &J : ej) if (J.src.kind == 1) J.src.ptr = pd_on_ ? pd_ids.p : d_ids.p;
     DeltaArgs dla{};
     if (v2_) {
         ENS(d_dense, std::max<uint64_t>(1, ids_off) * 8); ENS(d_pre, std::max<uint64_t>(1, ids_off) * 4);
@@ -338,6 +360,13 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ap.tile_smax = d_tile_smax.as<uint64_t>(); ap.tile_cnt = d_tile_cnt.as<uint32_t>(); ap.tile_sz = d_tile_sz.as<uint64_t>();
     ap.ht = d_ht.as<HtSlot>();
     ap.ids = d_ids.as<uint32_t>(); ap.ent_rec = d_ent_rec.as<uint64_t>(); ap.ent_boff = d_ent_boff.as<uint64_t>();
+    if (pd_on_) {   // every dictionary (and so every page's ids) in the kept continuation buffers
+        ap.ht = pd_ht.as<HtSlot>();
+        ap.ids = pd_ids.as<uint32_t>(); ap.ent_rec = pd_ent_rec.as<uint64_t>(); ap.ent_boff = pd_ent_boff.as<uint64_t>();
+        for (int c = 0; c < nc; c++)   // a column's first probe of the open row group: an empty table
+            if (dch[c].is_dict && pd_[c].done == 0 && !pd_[c].stopped && dch[c].npages > 0)
+                CK(hipMemsetAsync(ap.ht + dch[c].ht_off, 0xFF, (pd_ht_cap_ + 1) * sizeof(HtSlot), st));
+    }
     ap.fmask = d_fmask.as<uint8_t>();
     ap.max_dict_bytes = (uint32_t)props.dictionary_page_size;
     ap.data_end = d_off + n; ap.collision = d_coll;
@@ -361,7 +390,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     RleScratch esc{};
     uint64_t body_tot = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
-        ap.exact_strings = ad.exact_strings = attempt;
+        ap.exact_strings = ad.exact_strings = pd_on_ ? (pd_exact_ ? 1 : 0) : attempt;
         CK(xh2d(d_chunks.p, pg.data(), npg * sizeof(ChunkDesc), st));
         CK(xh2d(mp_dch.p, dch.data(), nc * sizeof(ChunkDesc), st));
         if (v2_ && !dj.empty()) CK(xh2d(d_djobs.p, dj.data(), dj.size() * sizeof(DeltaJob), st));
@@ -398,6 +427,9 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         for (int c = 0; c < nc; c++)
             if (dch[c].is_dict && dch[c].overflow) return fail(KPW_ERR_DEVICE, "multi-page dictionary table overflow");
         if (!coll) break;
+        // a continuation's kept tables hold hash keys of earlier probes: the probe restarts the open
+        // row group's dictionaries in exact mode (probe_mp)
+        if (pd_on_) return pd_exact_ ? fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode") : kPdRetry;
         if (attempt == 1) return fail(KPW_ERR_DEVICE, "string dictionary verification failed in exact mode");
         for (int c = 0; c < nc; c++) {   // restore the host descriptors for the exact re-run
             dch[c].nn = 0; dch[c].dict_bytes = 0; dch[c].dict_n = 0; dch[c].fallback = 0; dch[c].overflow = 0;
@@ -603,6 +635,49 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     return KPW_OK;
 }
 
+void Engine::pd_reset()
+{
+    for (ProbeDict &Q : pd_) Q = ProbeDict();
+    pd_exact_ = false;
+}
+
+// The continuation buffers for a probe of [0, ne): per dictionary column a hash table and entry
+// arrays sized for one dictionary (dictPageSize of the smallest entries + 1, plus one insertion
+// round) and one id per record so far (grown by doubling, the kept ids copied).
+int Engine::pd_prepare(uint64_t ne)
+{
+    const int nc = (int)cols.size();
+    if ((int)pd_slot_.size() != nc) {
+        pd_slot_.assign(nc, -1);
+        int k = 0;
+        for (int c = 0; c < nc; c++) if (cols[c].dict) pd_slot_[c] = k++;
+    }
+    uint64_t nd = 0;
+    for (int c = 0; c < nc; c++) nd += pd_slot_[c] >= 0 ? 1 : 0;
+    if (!nd) return KPW_OK;
+    hipStream_t st = stream;
+    if (!pd_ht_cap_) {
+        pd_ent_cap_ = (uint64_t)props.dictionary_page_size / 4 + 1 + (uint64_t)kMpRoundTiles * KPW_TILE_P_H;
+        pd_ht_cap_ = next_pow2_mp(2 * pd_ent_cap_);
+        ENS(pd_ht, nd * (pd_ht_cap_ + 1) * sizeof(HtSlot));
+        ENS(pd_ent_rec, nd * pd_ent_cap_ * 8);
+        ENS(pd_ent_boff, nd * pd_ent_cap_ * 8);
+    }
+    if (ne > pd_ids_cap_) {
+        const uint64_t cap = std::max<uint64_t>(2 * ne, 1u << 16);
+        DevBuf nb;
+        ENS(nb, nd * cap * 4);
+        if (pd_ids_cap_)
+            for (uint64_t k = 0; k < nd; k++)
+                CK(hipMemcpyAsync(nb.as<uint32_t>() + k * cap, pd_ids.as<uint32_t>() + k * pd_ids_cap_, pd_ids_cap_ * 4,
+                                  hipMemcpyDeviceToDevice, st));
+        CK(xsync(st));   // (the old buffer is released when nb goes)
+        pd_ids.swap(nb);
+        pd_ids_cap_ = cap;
+    }
+    return KPW_OK;
+}
+
 // probe_pages: the open row group's prefix [0, ne) with its page cuts `pc` (cuts <= ne, a cut at
 // ne included) -> per probed column the pages cut inside it and their header + compressed
 // bytes, i.e. ColumnChunkPageWriter.getMemSize() after record ne - 1
@@ -620,13 +695,38 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
         std::vector<CutPage> &pcache = probe_cache_[c];
         bool ok = pcache.size() <= pc[c].size();
         for (size_t i = 0; ok && i < pcache.size(); i++) ok = pcache[i].end == pc[c][i];
-        if (!ok) pcache.clear();
+        if (!ok) { pcache.clear(); if (pd_.size() > (size_t)c) pd_[c] = ProbeDict(); }
         from[c] = (uint32_t)pcache.size();
     }
     probe_mode_.resize(nc, 0);
     for (int c = 0; c < nc; c++) if (from[c] == 0) probe_mode_[c] = 0;
+    pd_on_ = pd_enabled() && !v2_;
+    if (pd_on_) {
+        pd_.resize(nc);
+        for (int c = 0; c < nc; c++) if (from[c] == 0) pd_[c] = ProbeDict();   // (its row group's first probe)
+        if (int rs = pd_prepare(ne)) { pd_on_ = false; return rs; }
+    }
     int rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
-    if (rs) return rs;
+    if (rs == kPdRetry) {
+        pd_reset();
+        pd_exact_ = true;
+        rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
+    }
+    if (rs) { pd_on_ = false; pd_reset(); return rs; }
+    if (pd_on_) {   // what the run inserted stays for the next probe of the row group
+        for (int c = 0; c < nc; c++) {
+            const ChunkDesc &D = pr.dch[c];
+            if (!cols[c].dict || D.npages <= 0 || !D.is_dict) continue;
+            ProbeDict &Q = pd_[c];
+            Q.n = D.dict_all;
+            Q.bytes = D.dict_bytes;
+            if (!Q.stopped) {
+                Q.done = (int64_t)ne;
+                Q.stopped = D.stop_tile != 0 || D.dict_bytes > (uint64_t)props.dictionary_page_size;
+            }
+        }
+        pd_on_ = false;
+    }
     probe_npages_.assign(nc, 0);
     probe_flushed_.assign(nc, 0);
     for (int c = 0; c < nc; c++) {
@@ -990,7 +1090,7 @@ int Engine::probe_pages(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
                         const std::vector<std::vector<int64_t>> *cuts)
 {
     if (!mp_) return fail(KPW_ERR_STATE, "probe_pages: single-page regime (no page cuts inside row groups)");
-    if (rg_token != probe_token_ || rg_token == ~0ull) probe_cache_.clear();
+    if (rg_token != probe_token_ || rg_token == ~0ull) { probe_cache_.clear(); pd_reset(); }
     probe_token_ = rg_token;
     probe_cuts_ = v2_ || !cuts || cuts->size() != cols.size() ? nullptr : cuts;
     BatchOut out;

@@ -58,7 +58,7 @@ struct TileRecs {
 __device__ __forceinline__ TileRecs tile_recs(const ChunkDesc &C, const DevCol &col, uint32_t t, const uint32_t *ctile_first, uint32_t ci)
 {
     TileRecs T;
-    T.t0 = (uint64_t)C.s + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P;
+    T.t0 = (uint64_t)C.s + C.tile_skip + (uint64_t)(t - ctile_first[ci]) * KPW_TILE_P;
     T.e = (uint64_t)C.e;
     T.rank0 = col.optional ? pres_rank(col, (uint64_t)C.s) : (uint64_t)C.s;
     return T;
@@ -523,8 +523,8 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_firsts(ChunkDesc *ch, const 
     }
     __syncthreads();
     if (!firsts) return;
-    uint32_t ebase = tile_cnt_off[t];
-    uint64_t bbase = tile_sz_off[t];
+    uint32_t ebase = tile_cnt_off[t] + C.ent_base;   // (a probe continuation numbers after the kept entries)
+    uint64_t bbase = tile_sz_off[t] + C.boff_base;
     const int klast = 31 - __clz(firsts);
     for (int k = 0; k <= klast; k++) {
         for (int w2 = 0; w2 < KPW_BLOCK / 64; w2++) {

@@ -227,7 +227,13 @@ struct ChunkDesc {
     uint32_t tail_mode;            // 0: the chunk's first page is in this run; 1: kept first page, dictionary
                                    // satisfying; 2: kept first page, every page of the chunk PLAIN
     uint32_t tail_dict_n;          // mode 1: dict_n of the last kept dictionary-encoded page (0: none)
-    uint32_t pad_tail;
+    // probe continuation (engine_mp.cpp, a page-size probe's dictionary descriptor): the table,
+    // ids and entries of [s, s + tile_skip) are kept on the device from the previous probes of the
+    // open row group; this run inserts only [s + tile_skip, e), new entries numbered from ent_base
+    // with dictionary-page offsets from boff_base.  0 / 0 / 0 everywhere else.
+    uint32_t ent_base;
+    uint64_t tile_skip;
+    uint64_t boff_base;
 };
 
 // One DELTA_BINARY_PACKED stream (k_delta.hip).
