@@ -379,6 +379,11 @@ hipError_t stream_set_acquire(int n, hipStream_t *s)
                 return hipSuccess;
             }
     }
+    // one set's streams are created back to back (HIP hands hardware queues to streams in creation
+    // order): concurrent writers opening at once (C5) would otherwise interleave their creations,
+    // and a set could get two streams on one queue, serialising its two encode workers
+    static std::mutex create_mu;
+    std::lock_guard<std::mutex> cg(create_mu);
     for (int k = 0; k < n; k++) {
         const hipError_t e = hipStreamCreateWithFlags(&s[k], hipStreamNonBlocking);
         if (e != hipSuccess) {
