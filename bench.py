@@ -845,6 +845,10 @@ def main():
         # host wall of each writer phase (write_file), summed over the step's writers
         "writer_phase_ms_per_step": {ph: round(agg.get("phase_%s_ms" % ph, 0.0) / args.steps, 2) for ph in PHASES},
         "lookback_fallbacks": int(agg.get("lookback_fallbacks", 0)),
+        # the box's PCIe as the writer saw it: record bytes / the span from the first record DMA to
+        # the completion of the last (HIP timing events on the copy stream; one writer per step)
+        "h2d_gbps": (round(my_bytes / (agg["h2d_span_ms"] * 1e-3) / 1e9, 2)
+                     if agg.get("h2d_span_ms") and len(sets[0]) == 1 else None),
         "allocator_in_timed_steps": cache_delta(cs.get("before", {}), cs["after"]),
         "stage_ms_per_step": {k: round(v / args.steps, 3) for k, v in stage_ms.items()},
         "rank_memory": mem,

@@ -119,8 +119,9 @@ int64_t kpw_writer_failed_record(const kpw_writer *w); /* -1 if none */
  * (HIP events on the encoder's stream, kpw_encoder_stage_times order), [15] encode wall
  * milliseconds of the worker thread, [16] scan look-backs that recomputed a predecessor tile
  * instead of waiting longer (exact either way; every look-back scan runs inside the encoders —
- * the writer's own record-offsets scan is reduce-then-scan and has none).  Returns the number
- * of entries written (<= cap). */
+ * the writer's own record-offsets scan is reduce-then-scan and has none), [17] milliseconds from
+ * the file's first record DMA to the completion of its last (the H2D span, after close; 0
+ * before).  Returns the number of entries written (<= cap). */
 int kpw_writer_stats(kpw_writer *w, double *out, int cap);
 const char *kpw_writer_last_error(const kpw_writer *w);
 void kpw_writer_free(kpw_writer *w);

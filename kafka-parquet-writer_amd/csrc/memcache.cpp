@@ -358,6 +358,13 @@ struct StreamSet {
 };
 std::mutex g_smu;
 std::vector<StreamSet> g_sets;   // idle pooled sets
+std::vector<hipStream_t> g_pads;   // pad streams (stream_set_acquire), under g_smu
+int g_live_sets = 0;               // sets handed out and not yet released (under g_smu)
+bool stream_pad_on()
+{
+    static const bool on = [] { const char *e = getenv("KPW_STREAM_PAD"); return !(e && e[0] == '0'); }();
+    return on;
+}
 bool stream_pool_on()
 {
     static const bool on = [] { const char *e = getenv("KPW_STREAM_POOL"); return !(e && e[0] == '0'); }();
@@ -376,6 +383,7 @@ hipError_t stream_set_acquire(int n, hipStream_t *s)
             if (g_sets[i].dev == dev && g_sets[i].n == n) {
                 for (int k = 0; k < n; k++) s[k] = g_sets[i].s[k];
                 g_sets.erase(g_sets.begin() + (long)i);
+                g_live_sets++;
                 return hipSuccess;
             }
     }
@@ -392,18 +400,35 @@ hipError_t stream_set_acquire(int n, hipStream_t *s)
             return e;
         }
     }
+    // HIP hands out its hardware queues round-robin in creation order, so with sets of four
+    // streams on four (or eight) queues every writer's first engine stream lands on the same
+    // queue, and so does every second one: eight concurrent writers' encodes then share two
+    // queues (r06h kernel trace of C5: all engine dispatches on queues 2 and 3).  One pad stream
+    // after each set (kept idle until trim_caches) shifts the next set by one queue, so the
+    // writers' engine streams rotate over the queues (KPW_STREAM_PAD=0: none).
+    hipStream_t pad = nullptr;
+    if (stream_pad_on() && hipStreamCreateWithFlags(&pad, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        pad = nullptr;
+    }
+    std::lock_guard<std::mutex> g(g_smu);
+    if (pad) g_pads.push_back(pad);
+    g_live_sets++;
     return hipSuccess;
 }
 
 void stream_sets_trim()
 {
     std::vector<StreamSet> idle;
+    std::vector<hipStream_t> pads;
     {
         std::lock_guard<std::mutex> g(g_smu);
         idle.swap(g_sets);
+        if (g_live_sets == 0) pads.swap(g_pads);   // (pads only when no set is in use)
     }
     for (auto &t : idle)
         for (int k = 0; k < t.n; k++) if (t.s[k]) (void)hipStreamDestroy(t.s[k]);
+    for (hipStream_t p : pads) (void)hipStreamDestroy(p);
 }
 
 void stream_set_release(int n, const hipStream_t *s)
@@ -411,6 +436,10 @@ void stream_set_release(int n, const hipStream_t *s)
     if (n <= 0 || n > 8 || !s[0]) return;
     int dev = 0;   // (the streams' own device: the caller's current one may differ)
     const bool keep = stream_pool_on() && hipStreamGetDevice(s[0], &dev) == hipSuccess;
+    {
+        std::lock_guard<std::mutex> g(g_smu);
+        g_live_sets--;
+    }
     if (keep) {
         std::lock_guard<std::mutex> g(g_smu);
         if (g_sets.size() < 64) {   // (bounded)

@@ -266,6 +266,10 @@ struct kpw_writer {
     uint64_t slot_used = 0, slot_dev = 0;   // pending bytes in the current slot and their device offset
     hipEvent_t direct_ev = nullptr;
     bool direct_pending = false;       // a DMA from the caller's pinned batch is in flight
+    // the record bytes' H2D span (kpw_writer_stats [17]): timing events on the copy stream before
+    // the first record DMA and after the last one (recorded at close)
+    hipEvent_t h2d_ev[2] = {nullptr, nullptr};
+    int h2d_marks = 0;
     // kpw_writer_write_async: the DMAs of call k may still read the caller's batch until call
     // k+1 returns (call_ev[k & 1] follows them on the copy stream)
     bool async_call = false;
@@ -326,7 +330,7 @@ struct kpw_writer {
     double t_open = 0, t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0, t_gate = 0;
     double t_probe = 0;          // page-size probes (multi-page per-record path): wall time, count, records
     uint64_t n_probe = 0, probe_recs = 0;
-    double stats[17] = {0};            // kpw_writer_stats (job order; read after drain)
+    double stats[18] = {0};            // kpw_writer_stats (job order; read after drain)
 
     ~kpw_writer();
     int init_pipeline(const kpw_schema *schema, const kpw_props *props);
@@ -411,9 +415,16 @@ static int acquire_fill(kpw_writer *w)
 }
 
 // Issue the H2D of the bytes pending in the current slot.
+// the first record DMA of the file: the H2D span starts (kpw_writer_stats [17])
+static void mark_h2d_start(kpw_writer *w)
+{
+    if (w->h2d_marks == 0 && w->h2d_ev[0] && hipEventRecord(w->h2d_ev[0], w->copy_stream) == hipSuccess) w->h2d_marks = 1;
+}
+
 static int flush_slot(kpw_writer *w)
 {
     if (!w->slot_used) return KPW_OK;
+    mark_h2d_start(w);
     const int k = w->cur_slot;
     if (hipMemcpyAsync(w->buf[w->fill].d + w->slot_dev, w->slot[k].p, w->slot_used, hipMemcpyHostToDevice, w->copy_stream) !=
             hipSuccess ||
@@ -432,6 +443,7 @@ static int stage_bytes(kpw_writer *w, const uint8_t *src, uint64_t len, bool all
         // direct DMA from the caller's pinned batch; the caller waits for it (wait_direct)
         // before the write returns, so it may reuse the batch
         if (int st = flush_slot(w)) return st;
+        mark_h2d_start(w);
         if (hipMemcpyAsync(F.d + F.len, src, len, hipMemcpyHostToDevice, w->copy_stream) != hipSuccess ||
             hipEventRecord(w->direct_ev, w->copy_stream) != hipSuccess)
             return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
@@ -1284,6 +1296,8 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
     for (auto &e : fd2h_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     if (hipEventCreateWithFlags(&direct_ev, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
+    for (auto &e : h2d_ev)
+        if (hipEventCreate(&e) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &e : call_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return KPW_ERR_DEVICE;
     for (auto &b : buf)
@@ -1338,6 +1352,7 @@ kpw_writer::~kpw_writer()
         if (b.copied) (void)hipEventDestroy(b.copied);
     }
     for (auto &e : slot_ev) if (e) (void)hipEventDestroy(e);
+    for (auto &e : h2d_ev) if (e) (void)hipEventDestroy(e);
     for (auto &e : fd2h_ev) if (e) (void)hipEventDestroy(e);
     for (auto &W : wk) {
         for (hipEvent_t e : {W.carry_ev, W.enc_done, W.d2h_ev[0], W.d2h_ev[1], W.asm_ev}) if (e) (void)hipEventDestroy(e);
@@ -2058,6 +2073,7 @@ extern "C" int kpw_writer_close(kpw_writer *w)
         if (w->fill >= 0) {
             if (int st = submit(w, JOB_FINAL, 0)) return st;
         }
+        if (w->h2d_marks == 1 && hipEventRecord(w->h2d_ev[1], w->copy_stream) == hipSuccess) w->h2d_marks = 2;
         if (int st = drain(w)) return st;
         int st = w->fw->close();
         if (st) return wfail(w, st, w->fw->error());
@@ -2106,7 +2122,14 @@ extern "C" int kpw_writer_stats(kpw_writer *w, double *out, int cap)
 {
     if (!w || !out || cap <= 0) return 0;
     if (release_batches(w) || drain(w)) return 0;
-    const int n = cap < 17 ? cap : 17;
+    if (w->h2d_marks == 2) {
+        float ms = 0.f;
+        if (hipEventSynchronize(w->h2d_ev[1]) == hipSuccess && hipEventElapsedTime(&ms, w->h2d_ev[0], w->h2d_ev[1]) == hipSuccess)
+            w->stats[17] = ms;
+        else
+            (void)hipGetLastError();
+    }
+    const int n = cap < 18 ? cap : 18;
     for (int i = 0; i < n; i++) out[i] = w->stats[i];
     return n;
 }

@@ -197,11 +197,11 @@ class ParquetFile:
 
     def pipeline_stats(self):
         """kpw_writer_stats: accumulated job / byte counts and per-stage device ms."""
-        arr = (ctypes.c_double * 17)()
-        n = self._L.kpw_writer_stats(self._h, arr, 17)
+        arr = (ctypes.c_double * 18)()
+        n = self._L.kpw_writer_stats(self._h, arr, 18)
         names = ["jobs", "records", "record_bytes", "page_bytes_uncompressed", "page_bytes_compressed",
                  "decode_ms", "plan_ms", "stats_dict_ms", "rle_ms", "layout_plain_write_ms", "compress_ms",
-                 "metadata_ms", "total_ms", "k_decode_ms", "k7_snappy_ms", "worker_encode_wall_ms", "lookback_fallbacks"]
+                 "metadata_ms", "total_ms", "k_decode_ms", "k7_snappy_ms", "worker_encode_wall_ms", "lookback_fallbacks", "h2d_span_ms"]
         return dict(zip(names, list(arr[:n])))
 
     def file_bytes(self):
