@@ -706,13 +706,23 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
         for (int c = 0; c < nc; c++) if (from[c] == 0) pd_[c] = ProbeDict();   // (its row group's first probe)
         if (int rs = pd_prepare(ne)) { pd_on_ = false; return rs; }
     }
+    // K1's verdict, not read before the probe (encode_impl: model probes): queued behind K1 now,
+    // it lands with the pipeline's first sync
+    uint64_t err_idx = 0;
+    CK(xd2h(&err_idx, probe_err_dev_, 8, st));
     int rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
     if (rs == kPdRetry) {
         pd_reset();
         pd_exact_ = true;
         rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
     }
-    if (rs) { pd_on_ = false; pd_reset(); return rs; }
+    if (rs) {   // (the verdict's D2H targets this frame: let it land before returning)
+        (void)hipStreamSynchronize(st);
+        (void)hipGetLastError();
+        pd_on_ = false;
+        pd_reset();
+        return rs;
+    }
     if (pd_on_) {   // what the run inserted stays for the next probe of the row group
         for (int c = 0; c < nc; c++) {
             const ChunkDesc &D = pr.dch[c];
@@ -748,9 +758,7 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
     }
     out.records_consumed = 0;
     out.open_records = (int64_t)ne;
-    uint64_t err_idx = 0;   // K1's verdict, not read before the probe (encode_impl: model probes)
-    CK(xd2h(&err_idx, probe_err_dev_, 8, st));
-    CK(xsync(st));
+    CK(xsync(st));   // (nothing queued after the pipeline's last sync: returns at once)
     if (err_idx < n) out.invalid_record = (int64_t)err_idx;
     return KPW_OK;
 }
