@@ -378,20 +378,33 @@ def writer_leg(kpw, kind, seed, n, device, steps, warmup, page_size=128 * MiB, s
         sets = [synth.generate(kind, seed + 0x1000 * k, n, alloc=kpw.pinned_empty) for k in range(2)]
     codec = kpw.SNAPPY if codec is None else codec
     props = kpw.ParquetProperties(block_size=128 * MiB, compression_codec_name=codec, page_size=page_size)
+    from kpw import _lib
     for i in range(warmup):
         write_file(kpw, schema, props, sets[i % 2][0], sets[i % 2][1], device)
+    c0 = _lib.cache_stats()
     t0 = time.perf_counter()
     nb = 0
     file_bytes = 0
+    step_ms, phases = [], []
     for i in range(steps):
         d, o = sets[(warmup + i) % 2]
-        size, _ = write_file(kpw, schema, props, d, o, device)
+        t = time.perf_counter()
+        size, st = write_file(kpw, schema, props, d, o, device)
+        step_ms.append(round((time.perf_counter() - t) * 1e3, 1))
+        phases.append(st)
         nb += int(o[-1])
         file_bytes += size
     dt = time.perf_counter() - t0
+    c1 = _lib.cache_stats()
     return dict(value=round(nb / dt / 1e9, 4), unit="GB/s", records_per_s=round(steps * (len(sets[0][1]) - 1) / dt, 1),
                 ms_per_step=round(dt / steps * 1e3, 3), steps=steps, warmup=warmup, records_per_step=len(sets[0][1]) - 1,
                 bytes_per_step=int(nb / steps), file_bytes_per_step=int(file_bytes / steps), page_size=page_size,
+                step_ms=step_ms,
+                writer_phase_ms_mean={ph: round(float(np.mean([st["phase_%s_ms" % ph] for st in phases])), 2) for ph in PHASES},
+                h2d_gbps=round(nb / (sum(st.get("h2d_span_ms", 0.0) for st in phases) * 1e-3) / 1e9, 2)
+                if all(st.get("h2d_span_ms") for st in phases) else None,
+                lookback_fallbacks=int(sum(st.get("lookback_fallbacks", 0.0) for st in phases)),
+                allocator_in_timed_steps=cache_delta(c0, c1),
                 workload=sschema.message_name.split(".")[-1] + ", %s, 128 MiB row groups, pageSize %d"
                 % ("GZIP" if codec == kpw.GZIP else "SNAPPY", page_size))
 
