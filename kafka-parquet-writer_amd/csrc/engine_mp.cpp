@@ -778,6 +778,15 @@ static bool lazy_on()
     return on;
 }
 
+// Speculative horizon past the last row group's records, in percent (KPW_MP_HORIZON_PCT, default
+// 25): a larger margin encodes more pages past the cut per pass, a too small one misses the cut
+// and pays a second pass over twice the range
+static int64_t horizon_pct()
+{
+    static const int64_t v = [] { const char *e = getenv("KPW_MP_HORIZON_PCT"); const long long x = e ? atoll(e) : 25; return (int64_t)(x > 0 ? x : 25); }();
+    return v;
+}
+
 // KPW_MP_SPLICE=0: every exact pass re-encodes the whole row group (A/B of the splice)
 static bool splice_on()
 {
@@ -862,7 +871,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
         auto it = g_horizon.find(hkey);
         if (it != g_horizon.end()) mp_last_rg_ = it->second;
     }
-    if (mp_last_rg_ > 0) guess = std::max<int64_t>(guess, mp_last_rg_ + mp_last_rg_ / 4 + 200);
+    if (mp_last_rg_ > 0) guess = std::max<int64_t>(guess, mp_last_rg_ + mp_last_rg_ * horizon_pct() / 100 + 200);
     int64_t s0 = 0;
     std::vector<std::vector<int64_t>> cuts;
     MpRun run;
@@ -1035,7 +1044,7 @@ int Engine::encode_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, 
                 if (rs) return rs;
                 lap(4);
             }
-            guess = std::max<int64_t>(1000, (r - s0) + (r - s0) / 4 + 200);
+            guess = std::max<int64_t>(1000, (r - s0) + (r - s0) * horizon_pct() / 100 + 200);
             mp_last_rg_ = r - s0;
             {
                 std::lock_guard<std::mutex> g(g_horizon_mu);
