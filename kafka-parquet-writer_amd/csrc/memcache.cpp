@@ -403,11 +403,11 @@ hipError_t stream_set_acquire(int n, hipStream_t *s)
     // HIP hands out its hardware queues round-robin in creation order, so with sets of four
     // streams on four (or eight) queues every writer's first engine stream lands on the same
     // queue, and so does every second one: eight concurrent writers' encodes then share two
-    // queues (r06h kernel trace of C5: all engine dispatches on queues 2 and 3).  One pad stream
-    // after each set (kept idle until trim_caches) shifts the next set by one queue, so the
-    // writers' engine streams rotate over the queues (KPW_STREAM_PAD=0: none).
+    // queues (r06h kernel trace of C5: all engine dispatches on queues 2 and 3).  Sets of an odd
+    // number of streams rotate over the queues by themselves; after an even-sized set one pad
+    // stream (kept idle until trim_caches) shifts the next set by one queue (KPW_STREAM_PAD=0: none).
     hipStream_t pad = nullptr;
-    if (stream_pad_on() && hipStreamCreateWithFlags(&pad, hipStreamNonBlocking) != hipSuccess) {
+    if (stream_pad_on() && n % 2 == 0 && hipStreamCreateWithFlags(&pad, hipStreamNonBlocking) != hipSuccess) {
         (void)hipGetLastError();
         pad = nullptr;
     }

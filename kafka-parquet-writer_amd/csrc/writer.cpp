@@ -237,23 +237,25 @@ struct Worker {
     std::thread th;
 };
 
-// The writer's stream set (memcache.h): eng, eng1, copy, d2h.  Declared before the engines, so
-// it is destroyed after them: the streams go back idle (every owner synchronised its own).
+// The writer's stream set (memcache.h): eng, eng1, copy, d2h, eng2.  Declared before the engines,
+// so it is destroyed after them: the streams go back idle (every owner synchronised its own).
+constexpr int kSetStreams = 5;
 struct StreamSetOwner {
-    hipStream_t s[4] = {};
-    ~StreamSetOwner() { if (s[0]) stream_set_release(4, s); }
+    hipStream_t s[kSetStreams] = {};
+    ~StreamSetOwner() { if (s[0]) stream_set_release(kSetStreams, s); }
 };
 
 struct kpw_writer {
-    static constexpr int kBufs = 4;    // two encoding, one queued, one filling
+    static constexpr int kBufs = 5;    // up to three encoding, one queued, one filling
     static constexpr int kSlots = 4;
     static constexpr size_t kSlotBytes = 32ull << 20;
     StreamSetOwner sset;
     Engine eng;                        // worker 0's engine (also the caller's, for write_until_full probes)
     Engine eng1;                       // worker 1's engine
+    Engine eng2;                       // worker 2's engine (KPW_ENCODERS=3)
     int nworkers = 2;
     bool aligned = false;              // HDFS PaddingAlignment: row groups planned one at a time (run_job_aligned)
-    Worker wk[2];
+    Worker wk[3];
     FileWriter *fw = nullptr;
     hipStream_t copy_stream = nullptr;
     StageBuf buf[kBufs];
@@ -1275,7 +1277,7 @@ static uint64_t env_workers()
 {
     const char *e = getenv("KPW_ENCODERS");
     const long v = e ? atol(e) : 2;
-    return v == 1 ? 1 : 2;
+    return v == 1 ? 1 : v >= 3 ? 3 : 2;
 }
 
 int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
@@ -1287,8 +1289,12 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
     if (nworkers > 1) {
         if (int st = eng1.init(eng.device, schema, props)) return st;
     }
+    if (nworkers > 2) {
+        if (int st = eng2.init(eng.device, schema, props)) return st;
+    }
     wk[0].eng = &eng;
     wk[1].eng = &eng1;
+    wk[2].eng = &eng2;
     copy_stream = sset.s[2];
     d2h_stream = sset.s[3];
     for (auto &e : slot_ev)
@@ -1346,6 +1352,7 @@ kpw_writer::~kpw_writer()
     if (d2h_stream) (void)hipStreamSynchronize(d2h_stream);
     if (eng.stream) (void)hipStreamSynchronize(eng.stream);
     if (eng1.stream) (void)hipStreamSynchronize(eng1.stream);
+    if (eng2.stream) (void)hipStreamSynchronize(eng2.stream);
     if (trace_on()) tf[1] = now_ms();
     for (auto &b : buf) {
         dev_free(b.d);
@@ -1392,9 +1399,10 @@ extern "C" kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, con
 {
     try {
         kpw_writer *w = new kpw_writer();
-        int st = hipSetDevice(device) == hipSuccess && stream_set_acquire(4, w->sset.s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
+        int st = hipSetDevice(device) == hipSuccess && stream_set_acquire(kSetStreams, w->sset.s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
         w->eng.given_stream = w->sset.s[0];
         w->eng1.given_stream = w->sset.s[1];
+        w->eng2.given_stream = w->sset.s[4];
         if (!st) st = w->eng.init(device, schema, props);
         if (!st) {
             w->fw = new FileWriter(w->eng.cols, w->eng.message_name, w->eng.proto_class, w->eng.props);
