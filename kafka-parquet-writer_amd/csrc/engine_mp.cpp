@@ -779,11 +779,12 @@ static bool lazy_on()
 }
 
 // Speculative horizon past the last row group's records, in percent (KPW_MP_HORIZON_PCT, default
-// 25): a larger margin encodes more pages past the cut per pass, a too small one misses the cut
-// and pays a second pass over twice the range
+// 12): a larger margin encodes more pages past the cut per pass, a too small one misses the cut
+// and pays a second pass over twice the range (r06l, bulk_multipage, two alternations: 25 %
+// 24.3 / 23.7, 12 % 24.6 / 24.7, 6 % 24.1 / 24.1 GB/s; rounds 4-5 used 25 %)
 static int64_t horizon_pct()
 {
-    static const int64_t v = [] { const char *e = getenv("KPW_MP_HORIZON_PCT"); const long long x = e ? atoll(e) : 25; return (int64_t)(x > 0 ? x : 25); }();
+    static const int64_t v = [] { const char *e = getenv("KPW_MP_HORIZON_PCT"); const long long x = e ? atoll(e) : 12; return (int64_t)(x > 0 ? x : 12); }();
     return v;
 }
 
