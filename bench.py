@@ -332,7 +332,7 @@ def cpu_baseline(kind, seed, sample_records, threads, runs=5):
                 records_per_s=round(per * threads / med, 1))
 
 
-def per_record_leg(kpw, schema, sschema, kind, seed, n, device, max_file_size, page_size):
+def per_record_leg(kpw, schema, sschema, kind, seed, n, device, max_file_size, page_size, runs=3):
     """The reference's unchanged WorkerThread loop (KafkaProtoParquetWriter.java:268-285,306-308):
     ONE kpw_writer_write + ONE kpw_writer_data_size per record through the C-ABI (the two
     downcalls a JVM host makes, driven from C: synth/loop.c), rotating files when getDataSize()
@@ -348,21 +348,25 @@ def per_record_leg(kpw, schema, sschema, kind, seed, n, device, max_file_size, p
                           max_file_size)
     pf.close()
     pf.__del__()
-    t0 = time.perf_counter()
-    done = files = 0
-    while done < n:
-        pf = kpw.ParquetFile(None, schema, props, device=device)
-        got, full, st, _ = synth.per_record_loop("kpw", L.kpw_writer_write, L.kpw_writer_data_size, pf._h, data, offs,
-                                                 done, n - done, max_file_size)
-        if st:
-            pf._check(st, "per-record write")
-        pf.close()
-        pf.__del__()
-        files += 1
-        done += got
-    dt = time.perf_counter() - t0
+    walls = []
+    for _ in range(runs):   # the loop over all n records, `runs` times: the median is reported
+        t0 = time.perf_counter()
+        done = files = 0
+        while done < n:
+            pf = kpw.ParquetFile(None, schema, props, device=device)
+            got, full, st, _ = synth.per_record_loop("kpw", L.kpw_writer_write, L.kpw_writer_data_size, pf._h, data, offs,
+                                                     done, n - done, max_file_size)
+            if st:
+                pf._check(st, "per-record write")
+            pf.close()
+            pf.__del__()
+            files += 1
+            done += got
+        walls.append(time.perf_counter() - t0)
+    dt = float(np.median(walls))
     return dict(records=n, bytes=nbytes, records_per_s=round(n / dt, 1), gbps=round(nbytes / dt / 1e9, 4),
-                wall_s=round(dt, 3), files=files, max_file_size=max_file_size, page_size=page_size,
+                wall_s=round(dt, 3), runs_wall_s=[round(w, 3) for w in walls], statistic="median of %d runs" % runs,
+                files=files, max_file_size=max_file_size, page_size=page_size,
                 calls_per_record="1 kpw_writer_write (n=1) + 1 kpw_writer_data_size, from C (synth/loop.c)",
                 reference_sizing_hint_records_per_s=300000)
 
@@ -520,7 +524,7 @@ def c1_leg(kpw, device, steps=5, threads=1):
                          % steps)
 
 
-def cpu_baseline_per_record(sschema, kind, seed, n, max_file_size, page_size):
+def cpu_baseline_per_record(sschema, kind, seed, n, max_file_size, page_size, runs=3):
     """CPU-baseline leg of the per-record loop: the oracle's kpwo_write + kpwo_data_size per
     record on the same records as per_record_leg, one thread (one WorkerThread)."""
     import synth
@@ -529,19 +533,23 @@ def cpu_baseline_per_record(sschema, kind, seed, n, max_file_size, page_size):
     data, offs = synth.generate(kind, seed + 0x77, n)
     OL = oracle.lib()
     oprops = oracle.make_props(block_size=128 * MiB, page_size=page_size, codec=oracle.SNAPPY)
-    t1 = time.perf_counter()
-    done = files = 0
-    while done < n:
-        w = oracle.OracleWriter(sschema, oprops)
-        got, full, st, _ = synth.per_record_loop("oracle", OL.kpwo_write, OL.kpwo_data_size, w._h, data, offs, done,
-                                                 n - done, max_file_size)
-        if st:
-            raise RuntimeError("oracle per-record loop status %d" % st)
-        w.close()
-        files += 1
-        done += got
-    odt = time.perf_counter() - t1
-    return dict(records=n, records_per_s=round(n / odt, 1), wall_s=round(odt, 3), files=files, cores=1, kind="port")
+    walls = []
+    for _ in range(runs):
+        t1 = time.perf_counter()
+        done = files = 0
+        while done < n:
+            w = oracle.OracleWriter(sschema, oprops)
+            got, full, st, _ = synth.per_record_loop("oracle", OL.kpwo_write, OL.kpwo_data_size, w._h, data, offs, done,
+                                                     n - done, max_file_size)
+            if st:
+                raise RuntimeError("oracle per-record loop status %d" % st)
+            w.close()
+            files += 1
+            done += got
+        walls.append(time.perf_counter() - t1)
+    odt = float(np.median(walls))
+    return dict(records=n, records_per_s=round(n / odt, 1), wall_s=round(odt, 3), runs_wall_s=[round(x, 3) for x in walls],
+                statistic="median of %d runs" % runs, files=files, cores=1, kind="port")
 
 
 def bind_to_gpu_numa(device):
