@@ -156,9 +156,13 @@ __device__ __forceinline__ T lb_tile(const LbView &L, uint32_t sbase, uint32_t t
     }
     // Published before overwritten: an in-place scan's tile stores its outputs over its inputs
     // after this barrier, and a fallback that recomputes this tile (lb_lookback) trusts its
-    // inputs only while it still sees no status word.  The agent-scope release fence makes the
-    // publish visible at L2 before any thread of the tile passes the barrier to store.
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // inputs only while it still sees no status word.  The status word is an agent-scope atomic
+    // store (written through to the coherence point), so thread 0 waits for it to complete
+    // (s_waitcnt 0) before the barrier: every output store of the tile is issued after the
+    // publish is visible device-wide.  (An agent-scope release fence does the same plus an L2
+    // write-back of every prior plain store, which no reader needs here: it made the K3
+    // phase / size passes 2.7-4x slower, r06n against r05 profiles.)
+    if (threadIdx.x == 0) __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     const T c = *slot;
     __syncthreads();
