@@ -635,10 +635,18 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     return KPW_OK;
 }
 
+// KPW_PROBE_EXACT=1 (test infrastructure): continuation probes compare string keys byte for byte
+// from a row group's first probe on, the mode a hash collision switches to (tests/pipeline_options_child.py)
+static bool pd_exact_forced()
+{
+    static const bool on = [] { const char *e = getenv("KPW_PROBE_EXACT"); return e && e[0] == '1'; }();
+    return on;
+}
+
 void Engine::pd_reset()
 {
     for (ProbeDict &Q : pd_) Q = ProbeDict();
-    pd_exact_ = false;
+    pd_exact_ = pd_exact_forced();
 }
 
 // The continuation buffers for a probe of [0, ne): per dictionary column a hash table and entry
