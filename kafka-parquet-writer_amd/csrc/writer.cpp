@@ -315,6 +315,8 @@ struct kpw_writer {
     int fatal_st = KPW_OK;             // first failure of the pipeline (sticky)
     std::string fatal_err;
     bool invalid_seen = false;         // a worker found an invalid record (bulk path)
+    bool dev_bound = false;            // hipSetDevice done in this entry call (bind_device)
+    std::atomic<bool> flagged{false};  // fatal_st or invalid_seen set (read without the lock)
     int64_t invalid_global = -1;
     // shared by the workers, used in job order only
     DevBuf carry_store;
@@ -350,6 +352,7 @@ static void set_fatal(kpw_writer *w, int st, const std::string &m)
 {
     std::lock_guard<std::mutex> g(w->mu);
     if (!w->fatal_st) { w->fatal_st = st; w->fatal_err = m; }
+    w->flagged.store(true, std::memory_order_release);
     w->cv.notify_all();
 }
 
@@ -945,9 +948,11 @@ static int run_job(kpw_writer *w, int x, const Job &j, hipEvent_t prev_carry)
         std::lock_guard<std::mutex> g(w->mu);
         if (st) {
             if (!w->fatal_st) { w->fatal_st = st; w->fatal_err = "carry-over copy failed"; }
+            w->flagged.store(true, std::memory_order_release);
         } else if (inv >= 0) {
             w->invalid_seen = true;
             w->invalid_global = inv;
+            w->flagged.store(true, std::memory_order_release);
         }
         w->last_carry_ev = W.carry_ev;
         w->plan_seq = j.seq + 1;
@@ -1128,6 +1133,7 @@ static int run_job_aligned(kpw_writer *w, const Job &j, hipEvent_t prev_carry)
     if (inv >= 0) {
         w->invalid_seen = true;
         w->invalid_global = inv;
+        w->flagged.store(true, std::memory_order_release);
     }
     w->last_carry_ev = W.carry_ev;
     w->plan_seq = j.seq + 1;
@@ -1431,6 +1437,9 @@ extern "C" kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, con
 // the record count: it and everything after it were never written.
 static int observe_failure(kpw_writer *w)
 {
+    // per-record calls (write + getDataSize per record) skip the lock while no worker has
+    // flagged a failure and the caller's own thread recorded none
+    if (!w->flagged.load(std::memory_order_acquire) && w->failed_record < 0) return KPW_OK;
     std::lock_guard<std::mutex> g(w->mu);
     if (w->invalid_seen && w->failed_record < 0) {
         w->failed_record = w->invalid_global;
@@ -1586,6 +1595,17 @@ static int model_pages(kpw_writer *w, size_t m, int &r)
 // slot; an invalid record stops the batch right there (the reference throws at parseFrom,
 // KafkaProtoParquetWriter.java:270-276); a row-group cut hands the fill buffer, which then
 // holds exactly that row group, to the worker.
+// The calling thread's current device, set once per entry call and only when it issues device
+// work: hipSetDevice costs ~70 ns (r06s), more than half of what the per-record loop's write
+// otherwise spends per record.
+static int bind_device(kpw_writer *w)
+{
+    if (w->dev_bound) return KPW_OK;
+    if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
+    w->dev_bound = true;
+    return KPW_OK;
+}
+
 static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *offsets, uint64_t n, int64_t max_file_size,
                           uint64_t *n_accepted, int *full)
 {
@@ -1601,6 +1621,9 @@ static int write_modelled(kpw_writer *w, const uint8_t *data, const uint64_t *of
             rc = KPW_ERR_INVALID_PROTO;
             break;
         }
+        if (r != SizeModel::OK || w->slot_used == 0 || w->slot_used + len > kpw_writer::kSlotBytes ||
+            w->buf[w->fill].len + len + 64 > w->buf[w->fill].cap)
+            if (int st = bind_device(w)) return st;   // a probe, job, slot flush or buffer growth
         if (int st = grow_fill(w, len)) return st;
         if (int st = stage_record(w, rec, len)) return st;
         StageBuf &F = w->buf[w->fill];
@@ -1913,7 +1936,7 @@ static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offse
     if (int st = observe_failure(w)) return st;
     if (w->fill < 0) return wfail(w, KPW_ERR_STATE, "no stage buffer (an earlier failure)");
     if (!n) return KPW_OK;
-    if (hipSetDevice(w->eng.device) != hipSuccess) return wfail(w, KPW_ERR_DEVICE, "hipSetDevice failed");
+    w->dev_bound = false;
     if (w->model_ok) {
         // write_until_full is record-at-a-time where the bulk search is not exact (multi-page
         // chunks: a page cut can shrink the buffered size inside a row group; HDFS alignment:
@@ -1922,9 +1945,13 @@ static int write_entry(kpw_writer *w, const uint8_t *data, const uint64_t *offse
         const bool bulk_search = !w->model.multi_page() && !w->aligned;
         const bool modelled = (max_file_size >= 0 && !bulk_search) || n <= model_max_batch();
         if (!modelled) w->model_on = false;
-        else if (!w->model_on)
+        else if (!w->model_on) {
+            if (int st = bind_device(w)) return st;
             if (int st = model_resync(w)) return st;
+        }
     }
+    if (!w->model_on)
+        if (int st = bind_device(w)) return st;
     int rc;
     if (w->model_on) {
         rc = write_modelled(w, data, offsets, n, max_file_size, n_accepted, full);
