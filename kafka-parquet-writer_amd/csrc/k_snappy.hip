@@ -690,7 +690,8 @@ void launch_snappy(const SnappyArgs &a, hipStream_t s)
         // A launch of few fragments (a page-size probe's cut pages) is latency-bound: one wave
         // per fragment takes ~40 us per 64 KiB where a segment-parallel workgroup takes ~10, so
         // they all go to the segment kernel first (the same bytes either way)
-        const bool few = a.nfrags <= 64;
+        static const uint32_t few_max = [] { const char *e = getenv("KPW_SNAPPY_FEW"); return e ? (uint32_t)atoi(e) : 64u; }();
+        const bool few = a.nfrags <= few_max;
         SnappyArgs v = a;
         v.v_budget = vbudget;
         if (!few) hipLaunchKernelGGL(k_snappy_v, dim3(a.nfrags), dim3(64), 0, s, v);

@@ -21,8 +21,10 @@
  *   /tmp/segp -f pages.bin   (pages from dump_any.py): per page rounds, and a rounds histogram
  *
  * Options (environment):
- *   GPUF=1   every lookup reads the previous round's inserted set, as k_snappy_seg does (default:
- *            a lane's lookups inside its own segment see its live insertions of this parse)
+ *   GPUF=1   every lookup reads the previous round's inserted set (k_snappy_seg before round 6);
+ *            default: a lane's lookups inside its own segment see its live insertions of this parse
+ *   GPUF=2   k_snappy_seg's live lookup (live_lookup: in-segment links with key-equality bits,
+ *            CHAINCAP steps, undecided -> the previous round's candidate)
  *   MODE=4   in-round forwarding, bounded: after the Jacobi parse, every lane whose entry differs
  *            from the forwarded exit of its left neighbours re-parses once in the same round
  *   MODE=1/2 in-round forwarding, unbounded (Gauss-Seidel: lanes re-parse left to right until
@@ -88,6 +90,57 @@ typedef struct {
 
 static int bit(const uint64_t *bm, uint32_t q) { return (bm[q >> 6] >> (q & 63)) & 1; }
 
+/* GPUF=2: k_snappy_seg's live lookup.  creg(x) = the previous round's candidate with its key
+ * check (cand[x]: a position, or NOMATCH); links = the previous same-hash position inside x's
+ * segment with a key-equality bit; walk them to the nearest own-inserted position, or to the
+ * segment's first same-hash position, whose cand[] lies before the segment; an undecided key
+ * comparison or a chain past CHAINCAP steps falls back to creg(x) (both agree at the fixed point) */
+#define NOMATCH 0xffffffffu
+static int CHAINCAP = 8;
+static uint64_t st_live, st_linked, st_steps, st_fallback;
+static uint32_t creg(const Frag *F, uint32_t x)
+{
+    uint32_t c = F->prev[x];
+    while (c && !bit(F->iprev, c)) c = F->prev[c];
+    return ld32(F->in + x) == ld32(F->in + c) ? c : NOMATCH;
+}
+/* GPUF=3: only the nearest same-hash position at distance d in LIVE_D (bit d-1) is looked at:
+ * inserted -> decided by key equality; otherwise the previous round's candidate */
+static int LIVE_D = 1;
+static uint32_t live_short(const Frag *F, uint32_t x, uint32_t sk, uint64_t own)
+{
+    const uint32_t c = creg(F, x);
+    const uint32_t q = F->prev[x];
+    if (!q || q < sk || x - q > 8 || !((LIVE_D >> (x - q - 1)) & 1)) return c;
+    if (!((own >> (q - sk)) & 1)) return c;
+    return ld32(F->in + x) == ld32(F->in + q) ? q : NOMATCH;
+}
+static uint32_t live_lookup(const Frag *F, uint32_t x, uint32_t sk, uint64_t own)
+{
+    if (GPUF == 3) return live_short(F, x, sk, own);
+    const uint32_t c = creg(F, x);
+    uint32_t q = F->prev[x];
+    st_live++;
+    if (!q || q < sk) return c;                      /* no link: hasl bit clear */
+    st_linked++;
+    int rel = ld32(F->in + x) == ld32(F->in + q);    /* 1 EQ, 0 NE */
+    for (int s = 0; s < CHAINCAP; s++) {
+        st_steps++;
+        if ((own >> (q - sk)) & 1) return rel ? q : NOMATCH;
+        const uint32_t q2 = F->prev[q];
+        if (!q2 || q2 < sk) {
+            const uint32_t co = creg(F, q);
+            if (rel) return co;
+            return co != NOMATCH ? NOMATCH : c;
+        }
+        const int eq = ld32(F->in + q) == ld32(F->in + q2);
+        if (rel) rel = eq;
+        else if (!eq) return c;
+        q = q2;
+    }
+    return c;
+}
+
 static void lane_parse(const Frag *F, uint32_t k, St st, Lane *L)
 {
     const uint32_t sk = k * SEG, sk1 = sk + SEG;
@@ -100,19 +153,31 @@ static void lane_parse(const Frag *F, uint32_t k, St st, Lane *L)
         if (st.mode == M_P) {
             const uint32_t ipe = st.ip;
             INSERT(ipe - 1);
+            if (GPUF >= 2) {
+                c = live_lookup(F, ipe, sk, L->own); L->lookups++;
+                INSERT(ipe);
+                if (c == NOMATCH) { St y = {M_S, ipe + 1, 32, ipe}; st = y; continue; }
+            } else {
             c = F->prev[ipe]; L->lookups++;
             { int h = 0; while (c && !INS(c)) { c = F->prev[c]; L->hops++; if (++h > HOPCAP) { L->aborted = 1; goto out; } } }
             INSERT(ipe);
             if (ld32(F->in + ipe) != ld32(F->in + c)) { St y = {M_S, ipe + 1, 32, ipe}; st = y; continue; }
+            }
             base = ipe; ne = ipe;
         } else {
             const uint32_t ip = st.ip;
             const uint32_t next_ip = ip + (st.skip >> 5);
             if (next_ip > F->ip_limit) { St t = {M_T, 0, 0, st.ne}; st = t; break; }
+            if (GPUF >= 2) {
+                c = live_lookup(F, ip, sk, L->own); L->lookups++;
+                INSERT(ip);
+                if (c == NOMATCH) { st.ip = next_ip; st.skip++; continue; }
+            } else {
             c = F->prev[ip]; L->lookups++;
             { int h = 0; while (c && !INS(c)) { c = F->prev[c]; L->hops++; if (++h > HOPCAP) { L->aborted = 1; goto out; } } }
             INSERT(ip);
             if (ld32(F->in + ip) != ld32(F->in + c)) { st.ip = next_ip; st.skip++; continue; }
+            }
             base = ip; ne = st.ne;
         }
         /* match: FindMatchLength(c+4, base+4, n) */
@@ -331,6 +396,7 @@ static int file_mode(const char *path)
     }
     printf("frags %ld mismatches %d nonconverged %ld; rounds histogram:", frags, bad, fail);
     for (int i = 0; i <= MAXIT; i++) if (hist[i]) printf(" %d:%ld", i, hist[i]);
+    if (GPUF == 2) printf("\nlive lookups %llu, linked %.4f, chain steps per linked %.2f", (unsigned long long)st_live, st_live ? (double)st_linked / st_live : 0.0, st_linked ? (double)st_steps / st_linked : 0.0);
     printf("\ncost/frag %.1f reparses/frag %.1f maxchain-sum/frag %.1f\n", (double)stat_cost / frags, (double)stat_reparse/frags, (double)stat_chain/frags);
     return bad != 0;
 }
@@ -339,6 +405,8 @@ int main(int argc, char **argv)
 {
     if (getenv("HOPCAP")) HOPCAP = atoi(getenv("HOPCAP"));
     if (getenv("MODE")) MODE = atoi(getenv("MODE")); if (getenv("TRACE")) TRACE = atoi(getenv("TRACE")); if (getenv("GPUF")) GPUF = atoi(getenv("GPUF"));
+    if (getenv("CHAINCAP")) CHAINCAP = atoi(getenv("CHAINCAP"));
+    if (getenv("LIVE_D")) LIVE_D = atoi(getenv("LIVE_D"));
     if (argc > 2 && !strcmp(argv[1], "-f")) return file_mode(argv[2]);
     const char *kinds[] = {"ts", "price", "user_id", "random", "zeros", "key16", "json", "defl", "mixed", "sparse"};
     static uint8_t page[65536 + 4096], o1[200000], o2[200000];
