@@ -449,8 +449,10 @@ static int stage_bytes(kpw_writer *w, const uint8_t *src, uint64_t len, bool all
         // before the write returns, so it may reuse the batch
         if (int st = flush_slot(w)) return st;
         mark_h2d_start(w);
+        // (an async call's DMAs are marked once, by call_ev at its end: every marker on the copy
+        // stream costs the SDMA queue ~1 % of a 31 MB batch, tests/microbench/h2d_streams.hip)
         if (hipMemcpyAsync(F.d + F.len, src, len, hipMemcpyHostToDevice, w->copy_stream) != hipSuccess ||
-            hipEventRecord(w->direct_ev, w->copy_stream) != hipSuccess)
+            (!w->async_call && hipEventRecord(w->direct_ev, w->copy_stream) != hipSuccess))
             return wfail(w, KPW_ERR_DEVICE, "H2D of a pinned batch failed");
         w->direct_pending = true;
         F.len += len;
