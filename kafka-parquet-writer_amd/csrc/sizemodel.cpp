@@ -35,6 +35,10 @@ uint32_t varint_len(uint32_t v)
 // CodedInputStream.readRawVarint64: at most 10 bytes
 inline bool varint64(const uint8_t *d, uint64_t &pos, uint64_t end, uint64_t &out)
 {
+    if (pos < end && d[pos] < 0x80) {   // one byte: tags and small values
+        out = d[pos++];
+        return true;
+    }
     uint64_t r = 0;
     for (int i = 0; i < 10; i++) {
         if (pos >= end) return false;
@@ -43,6 +47,27 @@ inline bool varint64(const uint8_t *d, uint64_t &pos, uint64_t end, uint64_t &ou
         if (!(b & 0x80)) { out = r; return true; }
     }
     return false;
+}
+
+// varint64 where 8 bytes can be read: the terminating byte found in one word (no per-byte
+// branch: a 6-byte ts varint was 6 dependent compare-and-branch steps); longer ones and the
+// last bytes of a record take varint64
+inline bool varint64w(const uint8_t *d, uint64_t &pos, uint64_t end, uint64_t &out)
+{
+    if (end - pos >= 8) {
+        uint64_t w;
+        std::memcpy(&w, d + pos, 8);
+        const uint64_t stop = ~w & 0x8080808080808080ull;
+        if (stop) {
+            const uint32_t nb = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
+            uint64_t v = 0;
+            for (uint32_t i = 0; i < nb; i++) v |= ((w >> (8 * i)) & 0x7f) << (7 * i);
+            out = v;
+            pos += nb;
+            return true;
+        }
+    }
+    return varint64(d, pos, end, out);
 }
 
 // skipField for an unknown field whose tag was read (k_decode.hip skip_field rules)
@@ -98,20 +123,18 @@ bool skip_field(const uint8_t *d, uint64_t &pos, uint64_t end, uint32_t tag)
 // RunLengthBitPackingHybridEncoder.writeInt (bit width 1), sizes only
 void RleCount::write(uint32_t v)
 {
-    if (v == prev) {
-        ++rc;
-        if (rc >= 8) return;                      // extends the RLE run
-    } else {
-        if (rc >= 8) {                            // writeRleRun: endPreviousBitPackedRun + header + value
-            hdr_open = false;
-            groups = 0;
-            out += varint_len((uint32_t)rc << 1) + 1;
-            rc = 0;
-            nbuf = 0;
-        }
-        rc = 1;
-        prev = v;
+    // (written so that a random 0/1 stream costs no mispredicted branch on v == prev: the
+    // repeat count is a select, and only the rare run ends and group ends branch)
+    const bool same = v == prev;
+    if (!same && rc >= 8) {                       // writeRleRun: endPreviousBitPackedRun + header + value
+        hdr_open = false;
+        groups = 0;
+        out += varint_len((uint32_t)rc << 1) + 1;
+        nbuf = 0;
     }
+    rc = same ? rc + 1 : 1;
+    prev = v;
+    if (same && rc >= 8) return;                  // extends the RLE run
     if (++nbuf == 8) {                            // writeOrAppendBitPackedRun
         if (groups >= 63) { hdr_open = false; groups = 0; }
         if (!hdr_open) { out += 1; hdr_open = true; }
@@ -142,6 +165,8 @@ bool SizeModel::init(const std::vector<ColInfo> &cols, const kpw_props &p)
     next_rg_size_ = p.block_size;
     fmap_.assign(FMAP_SIZE, -1);
     cols_.clear();
+    wire_.clear();
+    nreq_ = 0;
     for (size_t c = 0; c < cols.size(); c++) {
         Col k;
         k.field_number = cols[c].field_number;
@@ -150,9 +175,12 @@ bool SizeModel::init(const std::vector<ColInfo> &cols, const kpw_props &p)
         k.optional = cols[c].optional;
         k.vsize = cols[c].vsize;
         cols_.push_back(k);
+        wire_.push_back(Wire{(uint32_t)cols[c].wire_type, (uint32_t)cols[c].vsize, cols[c].optional ? 0u : 1u});
+        nreq_ += cols[c].optional ? 0u : 1u;
         if (cols[c].field_number < FMAP_SIZE) fmap_[cols[c].field_number] = (int16_t)c;
     }
-    seen_.assign(cols_.size(), 0);
+    seen_.assign(cols_.size(), 0u);
+    gen_ = 0;
     raw_.assign(cols_.size(), 0);
     bval_.assign(cols_.size(), 0);
     reset_store();
@@ -185,10 +213,22 @@ void SizeModel::restart(int64_t next_rg_size)
     next_rg_size_ = next_rg_size;
 }
 
-// parser.parseFrom(record.value()) validity + presence + raw sizes (K1's rules)
+// parser.parseFrom(record.value()) validity + presence + raw sizes (K1's rules).  Presence is
+// the record's generation number in seen_ (no clear per record); the required columns are
+// counted as they first appear.
 bool SizeModel::scan(const uint8_t *d, uint64_t len)
 {
-    std::memset(seen_.data(), 0, seen_.size());
+    if (++gen_ == 0) {   // wrapped: stale generations could match again
+        std::fill(seen_.begin(), seen_.end(), 0u);
+        gen_ = 1;
+    }
+    const uint32_t gen = gen_;
+    uint32_t *seen = seen_.data();
+    uint32_t *raw = raw_.data();
+    uint8_t *bval = bval_.data();
+    const int16_t *fmap = fmap_.data();
+    const Wire *wire = wire_.data();
+    uint32_t nreq = 0;
     uint64_t pos = 0;
     const uint64_t end = len;
     while (pos < end) {
@@ -197,34 +237,35 @@ bool SizeModel::scan(const uint8_t *d, uint64_t len)
         const uint32_t tag = (uint32_t)t64, fno = tag >> 3, wt = tag & 7;
         if (fno == 0) return false;
         int c = -1;
-        if (fno < (uint32_t)FMAP_SIZE) c = fmap_[fno];
+        if (fno < (uint32_t)FMAP_SIZE) c = fmap[fno];
         else
             for (size_t k = 0; k < cols_.size(); k++)
                 if ((uint32_t)cols_[k].field_number == fno) { c = (int)k; break; }
-        if (c < 0 || (uint32_t)cols_[c].wire_type != wt) {
+        if (c < 0 || wire[c].wire_type != wt) {
             if (!skip_field(d, pos, end, tag)) return false;
             continue;
         }
         uint64_t v;
         switch (wt) {
         case 0:
-            if (!varint64(d, pos, end, v)) return false;
-            raw_[c] = (uint32_t)cols_[c].vsize;
-            bval_[c] = v != 0;   // CodedInputStream.readBool
+            if (!varint64w(d, pos, end, v)) return false;
+            raw[c] = wire[c].vsize;
+            bval[c] = v != 0;   // CodedInputStream.readBool
             break;
-        case 1: if (end - pos < 8) return false; pos += 8; raw_[c] = 8; break;
-        case 5: if (end - pos < 4) return false; pos += 4; raw_[c] = 4; break;
+        case 1: if (end - pos < 8) return false; pos += 8; raw[c] = 8; break;
+        case 5: if (end - pos < 4) return false; pos += 4; raw[c] = 4; break;
         default:   // 2: length-delimited (BYTE_ARRAY: 4-byte length + bytes)
-            if (!varint64(d, pos, end, v) || (int32_t)(uint32_t)v < 0 || end - pos < (uint32_t)v) return false;
+            if (!varint64w(d, pos, end, v) || (int32_t)(uint32_t)v < 0 || end - pos < (uint32_t)v) return false;
             pos += (uint32_t)v;
-            raw_[c] = 4 + (uint32_t)v;
+            raw[c] = 4 + (uint32_t)v;
             break;
         }
-        seen_[c] = 1;
+        if (seen[c] != gen) {
+            seen[c] = gen;
+            nreq += wire[c].required;
+        }
     }
-    for (size_t c = 0; c < cols_.size(); c++)
-        if (!seen_[c] && !cols_[c].optional) return false;   // isInitialized: missing required field
-    return true;
+    return nreq == nreq_;   // isInitialized: every required field present
 }
 
 int64_t SizeModel::buffered() const
@@ -238,15 +279,14 @@ int SizeModel::add(const uint8_t *rec, uint64_t len)
 {
     if (!scan(rec, len)) return INVALID;
     bool cut = false;
+    const uint32_t gen = gen_;
     for (size_t c = 0; c < cols_.size(); c++) {
         Col &k = cols_[c];
-        const bool present = seen_[c] != 0;
+        const bool present = seen_[c] == gen;
         if (k.optional) k.dl.write(present ? 1u : 0u);
-        if (present) {
-            if (k.phys != KPW_BOOLEAN) k.data += raw_[c];
-            else if (v2_) k.bv.write(bval_[c]);
-            else k.data += 1;
-        }
+        if (k.phys != KPW_BOOLEAN) k.data += present ? raw_[c] : 0u;   // (a select: presence is random)
+        else if (!v2_) k.data += present ? 1 : 0;
+        else if (present) k.bv.write(bval_[c]);
         ++k.value_count;
         if (v2_) continue;   // ColumnWriteStoreV2 checks the store after the record
         // ColumnWriterV1.accountForValueWritten

@@ -97,7 +97,13 @@ private:
     void reset_store();
     std::vector<Col> cols_;
     std::vector<int16_t> fmap_;             // field number (< 1024) -> column
-    std::vector<uint8_t> seen_;
+    struct Wire {                           // what the scan reads per column, packed
+        uint32_t wire_type, vsize, required;
+    };
+    std::vector<Wire> wire_;
+    uint32_t nreq_ = 0;                     // required columns
+    std::vector<uint32_t> seen_;            // == gen_: present in the record being scanned
+    uint32_t gen_ = 0;
     std::vector<uint32_t> raw_;
     std::vector<uint8_t> bval_;             // BOOLEAN columns: the record's value (last occurrence)
     bool multi_ = false, v2_ = false;
