@@ -237,16 +237,21 @@ struct Worker {
     std::thread th;
 };
 
-// The writer's stream set (memcache.h): eng, eng1, copy, d2h, eng2.  Declared before the engines,
-// so it is destroyed after them: the streams go back idle (every owner synchronised its own).
+// The writer's stream set (memcache.h): eng, eng1, copy, d2h, and eng2 with three encode workers
+// only.  Declared before the engines, so it is destroyed after them: the streams go back idle
+// (every owner synchronised its own).  A fifth stream and a fifth stage buffer for the default two
+// workers cost the bulk multi-page line 23.0-23.4 -> 19.8-21.3 GB/s (r06bm, same box: the writer
+// ran ahead into more queued jobs and the close grew 62 -> 162 ms), so both follow the count.
 constexpr int kSetStreams = 5;
 struct StreamSetOwner {
     hipStream_t s[kSetStreams] = {};
-    ~StreamSetOwner() { if (s[0]) stream_set_release(kSetStreams, s); }
+    int n = 0;
+    ~StreamSetOwner() { if (s[0]) stream_set_release(n, s); }
 };
 
 struct kpw_writer {
-    static constexpr int kBufs = 5;    // up to three encoding, one queued, one filling
+    static constexpr int kBufs = 5;    // up to three encoding, one queued, one filling (nbufs in use)
+    int nbufs = 4;                     // 5 with three workers
     static constexpr int kSlots = 4;
     static constexpr size_t kSlotBytes = 32ull << 20;
     StreamSetOwner sset;
@@ -386,7 +391,7 @@ static int acquire_fill(kpw_writer *w)
     {
         std::unique_lock<std::mutex> lk(w->mu);
         for (;;) {
-            for (int i = 0; i < kpw_writer::kBufs; i++)   // (not while a worker still reads its lengths)
+            for (int i = 0; i < w->nbufs; i++)   // (not while a worker still reads its lengths)
                 if (w->buf[i].state == BUF_FREE && w->buf[i].lp_state != 1) { k = i; break; }
             if (k >= 0 || w->fatal_st) break;
             w->cv.wait(lk);
@@ -1294,6 +1299,7 @@ int kpw_writer::init_pipeline(const kpw_schema *schema, const kpw_props *props)
     nworkers = (int)env_workers();
     aligned = props->dfs_block_size > 0 && props->max_padding_size > 0;
     if (aligned) nworkers = 1;   // each row group's limit follows the file position after the one before
+    nbufs = nworkers >= 3 ? 5 : 4;
     if (nworkers > 1) {
         if (int st = eng1.init(eng.device, schema, props)) return st;
     }
@@ -1407,10 +1413,12 @@ extern "C" kpw_writer *kpw_writer_open(int device, const kpw_schema *schema, con
 {
     try {
         kpw_writer *w = new kpw_writer();
-        int st = hipSetDevice(device) == hipSuccess && stream_set_acquire(kSetStreams, w->sset.s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
+        const int ns = env_workers() >= 3 ? 5 : 4;
+        int st = hipSetDevice(device) == hipSuccess && stream_set_acquire(ns, w->sset.s) == hipSuccess ? KPW_OK : KPW_ERR_DEVICE;
+        if (!st) w->sset.n = ns;
         w->eng.given_stream = w->sset.s[0];
         w->eng1.given_stream = w->sset.s[1];
-        w->eng2.given_stream = w->sset.s[4];
+        w->eng2.given_stream = w->sset.s[4];   // (null with four streams: eng2 is not used)
         if (!st) st = w->eng.init(device, schema, props);
         if (!st) {
             w->fw = new FileWriter(w->eng.cols, w->eng.message_name, w->eng.proto_class, w->eng.props);
