@@ -385,6 +385,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     ad.dict_order = d_dorder.as<uint32_t>(); ad.ndict_tiles = ndict_tiles;
     ad.mp_round_end = rend.data(); ad.mp_nrounds = (uint32_t)rlen.size(); ad.mp_round_len = rlen.data();
     ad.mp_dict_limit = (uint32_t)props.dictionary_page_size;
+    ad.dict_wide = probe_ ? 1u : 0u;
 
     uint32_t enpt = 0, enet = 0;
     RleScratch esc{};

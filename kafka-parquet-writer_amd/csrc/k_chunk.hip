@@ -316,11 +316,16 @@ __device__ __forceinline__ int64_t global_insert(ChunkDesc &C, HtSlot *tab, uint
 constexpr uint32_t LDS_T = 2048;
 constexpr uint32_t LDS_PROBES = 32;
 
-__global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
-                                                           const uint32_t *order, const uint32_t *ctile_chunk, const uint32_t *ctile_first,
-                                                           HtSlot *ht, uint32_t *slotof, uint32_t max_dict_bytes,
-                                                           int exact, const uint64_t *data_end_p)
+// BT threads per tile (KPW_BLOCK, or 1024 for a page-size probe: its few tiles are a chain of
+// dependent global atomics per thread, 2048 / BT of them)
+template <int BT>
+__global__ void __launch_bounds__(BT) k_dict_insert(ChunkDesc *ch, const DevCol *cols, const uint8_t *data,
+                                                    const uint32_t *order, const uint32_t *ctile_chunk, const uint32_t *ctile_first,
+                                                    HtSlot *ht, uint32_t *slotof, uint32_t max_dict_bytes,
+                                                    int exact, const uint64_t *data_end_p)
 {
+    constexpr int NK = KPW_TILE_P / BT;   // records per thread
+    static_assert(NK * BT == KPW_TILE_P && KPW_TILE_P <= LDS_T, "tile / block shape");
     __shared__ uint64_t lkey[LDS_T];
     __shared__ uint32_t lmin[LDS_T];   // phase 1: first rank per key; phase 2 on: its global slot
     __shared__ uint16_t lrec[LDS_T];   // first record of the key, relative to the tile (28 KiB per block in all)
@@ -339,22 +344,23 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     if (C.stop_tile && t - ctile_first[ci] >= C.stop_tile) return;   // multi-page: past dictPageSize
     const DevCol col = cols[C.col];   // by value: not reloaded after stores
     const TileRecs T = tile_recs(C, col, t, ctile_first, ci);
+    if (T.t0 >= T.e) return;   // past the chunk's records (a probe round's fixed tile count)
     const uint32_t cap = C.ht_cap;
     HtSlot *tab = ht + C.ht_off;
     // BYTE_ARRAY keys: the 64-bit hash computed by K1 (verified byte-for-byte afterwards in
     // k_dict_ids); `exact` re-runs with byte comparisons after a detected hash collision
     // (then the LDS stage is skipped: every value goes straight to the global table).
     const bool is_bin = col.phys == 6 && exact;
-    for (uint32_t i = threadIdx.x; i < LDS_T; i += KPW_BLOCK) { lkey[i] = HT_EMPTY; lmin[i] = 0xffffffffu; }
+    for (uint32_t i = threadIdx.x; i < LDS_T; i += BT) { lkey[i] = HT_EMPTY; lmin[i] = 0xffffffffu; }
     if (threadIdx.x == 0) { acc_n = 0; acc_b = 0; }
     __syncthreads();
-    int32_t li[8];
-    uint64_t keyv[8];
-    uint32_t rk[8];
+    int32_t li[NK];
+    uint64_t keyv[NK];
+    uint32_t rk[NK];
     // phase 1: LDS dedup
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < NK; k++) {
         li[k] = -2;  // not present
-        const uint64_t r = T.rec(k);
+        const uint64_t r = (T.t0 + (uint64_t)k * BT + threadIdx.x);
         if (r >= T.e) continue;
         if (!present_at(col, r)) continue;
         uint64_t key;
@@ -384,7 +390,7 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
     }
     __syncthreads();
     // phase 2: one global insert per distinct key of the tile
-    for (uint32_t i = threadIdx.x; i < LDS_T; i += KPW_BLOCK) {
+    for (uint32_t i = threadIdx.x; i < LDS_T; i += BT) {
         const uint64_t key = lkey[i];
         if (key == HT_EMPTY) continue;
         const uint64_t r = T.t0 + lrec[i];
@@ -406,9 +412,9 @@ __global__ void __launch_bounds__(KPW_BLOCK) k_dict_insert(ChunkDesc *ch, const 
         if (nb > max_dict_bytes) __hip_atomic_store(&C.fallback, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // phase 3: slots for every value (LDS hit or direct global insert)
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < NK; k++) {
         if (li[k] == -2) continue;
-        const uint64_t r = T.rec(k);
+        const uint64_t r = (T.t0 + (uint64_t)k * BT + threadIdx.x);
         int64_t g;
         if (li[k] >= 0) {
             g = lmin[li[k]] == 0xffffffffu ? -1 : (int64_t)lmin[li[k]];
@@ -983,13 +989,16 @@ void launch_dict(const ChunkArgs &a, RleJob *jobs, hipStream_t s)
             if (j)
                 hipLaunchKernelGGL(k_mp_dict_stop, dim3((a.nchunks + 63) / 64), dim3(64), 0, s, a.ch, a.nchunks,
                                    a.mp_round_end[j - 1], a.mp_dict_limit);
-            if (cnt)
-                hipLaunchKernelGGL(k_dict_insert, dim3(cnt), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order + o,
+            if (cnt && a.dict_wide)
+                hipLaunchKernelGGL(k_dict_insert<1024>, dim3(cnt), dim3(1024), 0, s, a.ch, a.cols, a.data, a.dict_order + o,
+                                   a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
+            else if (cnt)
+                hipLaunchKernelGGL(k_dict_insert<KPW_BLOCK>, dim3(cnt), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order + o,
                                    a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
             o += cnt;
         }
     } else if (a.ndict_tiles) {
-        hipLaunchKernelGGL(k_dict_insert, dim3(a.ndict_tiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order,
+        hipLaunchKernelGGL(k_dict_insert<KPW_BLOCK>, dim3(a.ndict_tiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.data, a.dict_order,
                            a.ctile_chunk, a.ctile_first, a.ht, a.ids, a.max_dict_bytes, a.exact_strings, a.data_end);
     }
     hipLaunchKernelGGL(k_dict_firsts, dim3(a.nctiles), dim3(KPW_BLOCK), 0, s, a.ch, a.cols, a.ctile_chunk, a.ctile_first,

@@ -62,7 +62,7 @@ struct ChunkArgs {
     uint32_t mp_nrounds;
     const uint32_t *mp_round_len;
     uint32_t mp_dict_limit;
-    uint32_t pad_mp;
+    uint32_t dict_wide;            // K2 insertion with 1024-thread tiles (page-size probes: few tiles)
     SegScratch *seg;               // the handle's segmented-scan scratch
 };
 
