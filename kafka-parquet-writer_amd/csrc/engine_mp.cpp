@@ -305,7 +305,9 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     // page table as in Engine::encode: totals, collision flags, then per page slot its offset,
     // length, level prefix, compressed offset and length
     const size_t P2 = 2 * (size_t)npg;
-    ENS(d_ptab, (4 + 5 * P2) * 8);
+    // (+ room behind it for the dictionary and page descriptors: the compression's sync reads all
+    // three back with one copy)
+    ENS(d_ptab, (4 + 5 * P2) * 8 + nc * sizeof(ChunkDesc) + npg * (sizeof(ChunkDesc) + 32));
     uint64_t *const pt = d_ptab.as<uint64_t>();
     uint64_t *const d_poff = pt + 4, *const d_plen = d_poff + P2, *const d_ppre = d_plen + P2;
     uint64_t *const d_pcoff = d_ppre + P2, *const d_pclen = d_pcoff + P2;
@@ -420,13 +422,12 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         launch_layout(ap, d_jobs.as<RleJob>(), d_poff, d_plen, pt, st);
         CK(hipGetLastError());
         CK(xd2h(ptab.data(), pt, (4 + (v2_ ? 3 : 2) * P2) * 8, st));   // totals, flags, offsets, lengths (v2: prefixes)
-        CK(xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st));
+        // (the dictionary descriptors come back with the compression's sync: a D2H into pageable
+        // memory holds the host until the stream reaches it, an idle gap before every later launch)
         CK(xsync(st));
         body_tot = ptab[0];
         const uint32_t coll = (uint32_t)ptab[2];
         if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
-        for (int c = 0; c < nc; c++)
-            if (dch[c].is_dict && dch[c].overflow) return fail(KPW_ERR_DEVICE, "multi-page dictionary table overflow");
         if (!coll) break;
         // a continuation's kept tables hold hash keys of earlier probes: the probe restarts the open
         // row group's dictionaries in exact mode (probe_mp)
@@ -457,10 +458,14 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     uint64_t *const d_smeta = (uint64_t *)(d_chunks.as<ChunkDesc>() + npg);
     static thread_local std::vector<uint8_t> md;
     md.resize(npg * (sizeof(ChunkDesc) + 32));
-    CK(xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st));
     launch_stats_gather(d_chunks.as<ChunkDesc>(), npg, d_cols.as<DevCol>(), d_data, d_smeta, nullptr, st);
-    CK(xd2h(md.data(), d_chunks.p, md.size(), st));
-    // (no sync here: the page offsets and lengths came back with the layout)
+    // their readback is queued behind the compression's launches (queue_meta), so the host issues
+    // K7 without waiting for the stream; no sync here: the page offsets and lengths came back with
+    // the layout
+    auto queue_meta = [&]() -> hipError_t {
+        hipError_t e = xd2h(dch.data(), mp_dch.p, nc * sizeof(ChunkDesc), st);
+        return e != hipSuccess ? e : xd2h(md.data(), d_chunks.p, md.size(), st);
+    };
     std::vector<uint64_t> poff(ptab.begin() + 4, ptab.begin() + 4 + P2), plen(ptab.begin() + 4 + P2, ptab.begin() + 4 + 2 * P2);
     std::vector<uint64_t> pcoff(P2), pclen(P2), ppre(P2, 0);
     if (v2_) ppre.assign(ptab.begin() + 4 + 2 * P2, ptab.begin() + 4 + 3 * P2);
@@ -492,8 +497,21 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         launch_snappy(sa, st);
         launch_snappy_finish(sa, (const uint32_t *)kt[2], st);
         CK(hipGetLastError());
-        CK(xd2h(ptab.data(), pt, (4 + 5 * P2) * 8, st));   // compressed total, offsets, lengths
-        CK(xsync(st));
+        {   // compressed total, offsets, lengths + the descriptors, gathered on the device (copies
+            // that do not hold the host) and read back at once: each D2H into pageable memory
+            // holds the host ~17 us before it can issue the next (r06bt probe trace)
+            const size_t pb = (4 + 5 * P2) * 8, db = nc * sizeof(ChunkDesc);
+            uint8_t *const rb = (uint8_t *)pt;
+            CK(hipMemcpyAsync(rb + pb, mp_dch.p, db, hipMemcpyDeviceToDevice, st));
+            CK(hipMemcpyAsync(rb + pb + db, d_chunks.p, md.size(), hipMemcpyDeviceToDevice, st));
+            static thread_local std::vector<uint8_t> rbh;
+            rbh.resize(pb + db + md.size());
+            CK(xd2h(rbh.data(), rb, rbh.size(), st));
+            CK(xsync(st));
+            memcpy(ptab.data(), rbh.data(), pb);
+            memcpy(dch.data(), rbh.data() + pb, db);
+            memcpy(md.data(), rbh.data() + pb + db, md.size());
+        }
         const uint64_t ctot = ptab[1];
         pcoff.assign(ptab.begin() + 4 + 3 * P2, ptab.begin() + 4 + 4 * P2);
         pclen.assign(ptab.begin() + 4 + 4 * P2, ptab.begin() + 4 + 5 * P2);
@@ -510,6 +528,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         if (int rs = gzip_pages(d_body.as<uint8_t>(), body_tot, d_poff, v2_ ? d_ppre : nullptr, poff, plen, on, d_pcoff,
                                 d_pclen, pt + 1, pt + 3, st))
             return rs;
+        CK(queue_meta());
         CK(xd2h(ptab.data(), pt, (4 + 5 * P2) * 8, st));   // compressed total, overflow, offsets, lengths
         CK(xsync(st));
         if (ptab[3]) return fail(KPW_ERR_DEVICE, "gzip member overflowed its scratch slot");
@@ -521,9 +540,12 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
         for (int p = 0; p < 2 * npg; p++) { pcoff[p] = poff[p] - ppre[p]; pclen[p] = plen[p] + ppre[p]; }
         pages_dev_ = d_body.as<uint8_t>();
         pages_len_ = body_tot;
+        CK(queue_meta());
         CK(xsync(st));
     }
     if (seg_failed_reset()) return fail(KPW_ERR_NOMEM, "segmented scan scratch allocation failed");
+    for (int c = 0; c < nc; c++)
+        if (dch[c].is_dict && dch[c].overflow) return fail(KPW_ERR_DEVICE, "multi-page dictionary table overflow");
     // ---------------------------------------------------------------- page metadata
     // (read back above, with the compression's sync)
     std::vector<uint64_t> smeta(4 * npg, 0);
