@@ -227,6 +227,11 @@ private:
     uint64_t probe_token_ = ~0ull;       // open row group of the cached page sizes (~0: none)
     const std::vector<std::vector<int64_t>> *probe_cuts_ = nullptr;   // v1 probe: the caller's page cuts
     const unsigned long long *probe_err_dev_ = nullptr;   // K1's first-invalid-record word of this encode
+    // an 8-byte device word mp_pipeline reads back with its last (compression) copy, so the
+    // caller needs no readback of its own: source, value, whether it was read
+    const void *rb_extra_src_ = nullptr;
+    uint64_t rb_extra_val_ = 0;
+    bool rb_extra_done_ = false;
     struct CutPage { int64_t end; int64_t bytes; };   // a cut page: end record, header + compressed bytes
     std::vector<std::vector<CutPage>> probe_cache_;   // per column, in page order
     std::vector<uint32_t> probe_mode_;                // per column: first page satisfied (1) / all PLAIN (2), 0 unknown

@@ -307,7 +307,7 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
     const size_t P2 = 2 * (size_t)npg;
     // (+ room behind it for the dictionary and page descriptors: the compression's sync reads all
     // three back with one copy)
-    ENS(d_ptab, (4 + 5 * P2) * 8 + nc * sizeof(ChunkDesc) + npg * (sizeof(ChunkDesc) + 32));
+    ENS(d_ptab, (4 + 5 * P2) * 8 + nc * sizeof(ChunkDesc) + npg * (sizeof(ChunkDesc) + 32) + 8);
     uint64_t *const pt = d_ptab.as<uint64_t>();
     uint64_t *const d_poff = pt + 4, *const d_plen = d_poff + P2, *const d_ppre = d_plen + P2;
     uint64_t *const d_pcoff = d_ppre + P2, *const d_pclen = d_pcoff + P2;
@@ -504,13 +504,16 @@ int Engine::mp_pipeline(const uint8_t *d_data, const uint64_t *d_off, uint64_t n
             uint8_t *const rb = (uint8_t *)pt;
             CK(hipMemcpyAsync(rb + pb, mp_dch.p, db, hipMemcpyDeviceToDevice, st));
             CK(hipMemcpyAsync(rb + pb + db, d_chunks.p, md.size(), hipMemcpyDeviceToDevice, st));
+            const size_t xb = rb_extra_src_ ? 8 : 0;   // + the caller's word (probe_mp: K1's verdict)
+            if (xb) CK(hipMemcpyAsync(rb + pb + db + md.size(), rb_extra_src_, 8, hipMemcpyDeviceToDevice, st));
             static thread_local std::vector<uint8_t> rbh;
-            rbh.resize(pb + db + md.size());
+            rbh.resize(pb + db + md.size() + xb);
             CK(xd2h(rbh.data(), rb, rbh.size(), st));
             CK(xsync(st));
             memcpy(ptab.data(), rbh.data(), pb);
             memcpy(dch.data(), rbh.data() + pb, db);
             memcpy(md.data(), rbh.data() + pb + db, md.size());
+            if (xb) { memcpy(&rb_extra_val_, rbh.data() + pb + db + md.size(), 8); rb_extra_done_ = true; }
         }
         const uint64_t ctot = ptab[1];
         pcoff.assign(ptab.begin() + 4 + 3 * P2, ptab.begin() + 4 + 4 * P2);
@@ -737,22 +740,29 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
         for (int c = 0; c < nc; c++) if (from[c] == 0) pd_[c] = ProbeDict();   // (its row group's first probe)
         if (int rs = pd_prepare(ne)) { pd_on_ = false; return rs; }
     }
-    // K1's verdict, not read before the probe (encode_impl: model probes): queued behind K1 now,
-    // it lands with the pipeline's first sync
-    uint64_t err_idx = 0;
-    CK(xd2h(&err_idx, probe_err_dev_, 8, st));
+    // K1's verdict, not read before the probe (encode_impl: model probes): the pipeline reads it
+    // back with its last copy (a D2H of its own into pageable memory would hold the host until
+    // K1 and the presence scans finish, before the pipeline's host setup: r06bt trace)
+    rb_extra_src_ = probe_err_dev_;
+    rb_extra_done_ = false;
     int rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
     if (rs == kPdRetry) {
         pd_reset();
         pd_exact_ = true;
         rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
     }
-    if (rs) {   // (the verdict's D2H targets this frame: let it land before returning)
+    rb_extra_src_ = nullptr;
+    if (rs) {
         (void)hipStreamSynchronize(st);
         (void)hipGetLastError();
         pd_on_ = false;
         pd_reset();
         return rs;
+    }
+    uint64_t err_idx = rb_extra_val_;
+    if (!rb_extra_done_) {   // (GZIP / uncompressed pipelines: read it now)
+        CK(xd2h(&err_idx, probe_err_dev_, 8, st));
+        CK(xsync(st));
     }
     if (pd_on_) {   // what the run inserted stays for the next probe of the row group
         for (int c = 0; c < nc; c++) {
