@@ -11,6 +11,9 @@ for p in ("", "synth", "kafka-parquet-writer_amd"):
 import kpw  # noqa: E402
 import synth  # noqa: E402
 
+if os.environ.get("PR_SPIN") == "1":   # spin-wait synchronisation (hipDeviceScheduleSpin) before any HIP use
+    import ctypes
+    assert ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(1) == 0
 n, page = int(sys.argv[1]), int(sys.argv[2])
 block = int(sys.argv[3]) if len(sys.argv) > 3 else 128 << 20
 s = synth.REC8
