@@ -150,6 +150,9 @@ public:
     hipStream_t given_stream = nullptr;   // set before init: the engine's stream (the owner's to release)
     float stage_ms[10] = {0};   // 0-7 stages, 8 k_decode, 9 K7 (k_snappy_v, k_snappy_seg, k_snappy_s_rest)
     uint32_t lb_fallbacks = 0;  // look-backs of the last encode that recomputed a predecessor (kpw_lookback.h)
+    // page-size probes, host wall per phase (ms, summed): encode entry -> probe_mp (K1 and its
+    // launches), the multi-page pipeline, after it (page headers, caches)
+    double probe_t[3] = {0, 0, 0};
 
 private:
     int encode_impl(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, bool final_flush, int64_t next_rg_size,

@@ -745,6 +745,9 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
     // K1 and the presence scans finish, before the pipeline's host setup: r06bt trace)
     rb_extra_src_ = probe_err_dev_;
     rb_extra_done_ = false;
+    auto ms_now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double tq0 = ms_now();
+    probe_t[0] += tq0 - t_encode_in_;
     int rs = mp_pipeline(d_data, d_off, n, hc, 0, (int64_t)ne, pc, pr, probe_mask_, &from);
     if (rs == kPdRetry) {
         pd_reset();
@@ -759,6 +762,8 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
         pd_reset();
         return rs;
     }
+    const double tq1 = ms_now();
+    probe_t[1] += tq1 - tq0;
     uint64_t err_idx = rb_extra_val_;
     if (!rb_extra_done_) {   // (GZIP / uncompressed pipelines: read it now)
         CK(xd2h(&err_idx, probe_err_dev_, 8, st));
@@ -801,6 +806,7 @@ int Engine::probe_mp(const uint8_t *d_data, const uint64_t *d_off, uint64_t n, u
     out.open_records = (int64_t)ne;
     CK(xsync(st));   // (nothing queued after the pipeline's last sync: returns at once)
     if (err_idx < n) out.invalid_record = (int64_t)err_idx;
+    probe_t[2] += ms_now() - tq1;
     return KPW_OK;
 }
 

@@ -338,6 +338,7 @@ struct kpw_writer {
     std::atomic<int> n_materialize{0};
     double t_open = 0, t_encode = 0, t_dma = 0, t_acquire = 0, t_asm = 0, t_d2h_alloc = 0, t_turn = 0, t_gate = 0;
     double t_probe = 0;          // page-size probes (multi-page per-record path): wall time, count, records
+    double t_probe_pre = 0;      // their staging flush + offsets upload before the probe
     uint64_t n_probe = 0, probe_recs = 0;
     double stats[18] = {0};            // kpw_writer_stats (job order; read after drain)
 
@@ -1548,6 +1549,7 @@ static uint64_t boundary_at(const StageBuf &B, size_t i)
 // materialises its carried ones in place first).
 static int probe_flushed(kpw_writer *w, size_t m, std::vector<int32_t> &np, std::vector<int64_t> &fl)
 {
+    const double tp0 = trace_on() ? now_ms() : 0.0;
     StageBuf &F = w->buf[w->fill];
     Engine &P = w->peng;
     StreamOrder order(P.stream);
@@ -1579,7 +1581,7 @@ static int probe_flushed(kpw_writer *w, size_t m, std::vector<int32_t> &np, std:
     const double tp = trace_on() ? now_ms() : 0.0;
     if (int st = P.probe_pages(F.d, w->pr_off.as<uint64_t>(), m, np, fl, &mask, w->fill_gen, &cuts))
         return wfail(w, st, P.error());
-    if (trace_on()) { w->t_probe += now_ms() - tp; w->n_probe++; w->probe_recs += m; }
+    if (trace_on()) { w->t_probe += now_ms() - tp; w->t_probe_pre += tp - tp0; w->n_probe++; w->probe_recs += m; }
     return KPW_OK;
 }
 
@@ -2132,8 +2134,11 @@ extern "C" int kpw_writer_close(kpw_writer *w)
                     w->t_encode, w->t_gate, w->t_dma, w->t_acquire, w->t_d2h_alloc, w->t_asm, w->n_materialize.load(),
                     w->gap_.load() / 1048576.0);
         if (trace_on() && w->n_probe)
-            fprintf(stderr, "[kpw] close: %llu page-size probes, %.1f ms (%.3f ms each, %.0f records each)\n",
-                    (unsigned long long)w->n_probe, w->t_probe, w->t_probe / w->n_probe, (double)w->probe_recs / w->n_probe);
+            fprintf(stderr, "[kpw] close: %llu page-size probes, %.1f ms (%.3f ms each, %.0f records each); per probe: "
+                            "staging + offsets %.3f, encode entry to pipeline %.3f, pipeline %.3f, after %.3f ms\n",
+                    (unsigned long long)w->n_probe, w->t_probe, w->t_probe / w->n_probe, (double)w->probe_recs / w->n_probe,
+                    w->t_probe_pre / w->n_probe, w->peng.probe_t[0] / w->n_probe, w->peng.probe_t[1] / w->n_probe,
+                    w->peng.probe_t[2] / w->n_probe);
         return KPW_OK;
     } catch (...) {
         set_fatal(w, KPW_ERR_DEVICE, "close failed");
